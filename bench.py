@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""bench.py — Mpixels/s of the forward+inverse block-DCT pipeline @ Q=50 4:2:0 (+PSNR vs reference).
+
+Workload (BASELINE.json configs[1]): 1920x1080 uniform-random RGB frames, Q=50,
+4:2:0, prefilter ON, through the fused HIP kernels (k_fwd: RGB -> int16
+coefficients; k_inv: coefficients -> RGB).  One step = one pass over a batch of
+`--frames` device-resident 1080p frames per GPU (default 64, the size of the
+reference's cfg4 batch sweep); inputs are generated on the device before the
+timed region.  Multi-GPU: one process per GPU (torchrun), frames shard across
+ranks with no data-path collective (weak scaling); RCCL is used only for the
+barrier and the max-over-ranks time.
+
+Prints ONE JSON line (rank 0).  The roofline object describes the dominant
+kernel (longer average launch) with ALGORITHMIC bytes: k_fwd reads 3 B/px RGB and
+writes 2*S B/px int16 coefficients, k_inv the reverse (S = coefficients per
+pixel, 1.5037 at 1080p 4:2:0).  Launch durations come from torch.cuda.Events on
+the stream the kernels run on.  `traffic` (HBM bytes/launch from rocprofv3 PMC)
+is read from profiles/pmc_traffic.json when it matches this configuration.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, 'jpeg-dsp-studio_amd')
+for _p in (PKG, ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--frames', type=int, default=64, help='1080p frames per GPU per step')
+    ap.add_argument('--height', type=int, default=1080)
+    ap.add_argument('--width', type=int, default=1920)
+    ap.add_argument('--quality', type=int, default=50)
+    ap.add_argument('--mode', default='4:2:0')
+    ap.add_argument('--prefilter', type=int, default=1)
+    ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-parity', action='store_true')
+    return ap.parse_args()
+
+
+def cpu_baseline(frames_host, quality, mode, pf, budget_s):
+    """The oracle (vectorised NumPy/SciPy restatement) on the host, 1 thread,
+    on a bounded sample of the same workload (whole 1080p frames)."""
+    from oracle import cpu_ref
+    t0 = time.perf_counter()
+    n = 0
+    while n < len(frames_host):
+        cpu_ref.compress_reconstruct(frames_host[n], quality, 8, mode, pf, metrics=False)
+        n += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    h, w = frames_host.shape[1:3]
+    return {'value': round(n * h * w / dt / 1e6, 4), 'unit': 'Mpixels/s', 'cores': 1, 'kind': 'port',
+            'sample': f'{n} x {w}x{h} frames (Q{quality} {mode} prefilter={bool(pf)}) through oracle/cpu_ref.py '
+                      f'compress_reconstruct without SSIM, {dt:.1f} s, 1 thread'}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    from jds import _abi, codec
+    from engines.quantizer import scale_quant_matrix
+    from utils.constants import JPEG_LUMA_Q50
+
+    B, H, W = args.frames, args.height, args.width
+    qt = scale_quant_matrix(JPEG_LUMA_Q50, args.quality)
+    prm = _abi.make_params(args.quality, qt, args.mode, bool(args.prefilter), codec.gaussian_kernel3())
+    plan = _abi.Plan(_abi.context(local), [prm] * B, H, W)
+    geo = plan.geometry
+    cpf = geo.coeffs_per_frame
+
+    # device-resident synthetic frames (uniform random RGB), distinct per rank
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
+    rgb = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=gen)
+    out = torch.empty_like(rgb)
+    coeffs = torch.empty((B, cpf), dtype=torch.int16, device=dev)
+    stats = torch.zeros((B, _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        plan.run(rgb.data_ptr(), out.data_ptr(), coeffs.data_ptr(), stats.data_ptr(), _abi.RUN_FWD, sp)
+        if ev is not None:
+            ev[1].record(stream)
+        plan.run(rgb.data_ptr(), out.data_ptr(), coeffs.data_ptr(), stats.data_ptr(), _abi.RUN_INV, sp)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    t_fwd = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    t_inv = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    px_per_step = B * H * W
+    value = world * px_per_step * args.steps / elapsed / 1e6
+    S = cpf / (H * W)
+    bytes_fwd = px_per_step * 3 + B * cpf * 2
+    bytes_inv = B * cpf * 2 + px_per_step * 3
+    dom = 'k_fwd' if t_fwd >= t_inv else 'k_inv'
+    t_dom = max(t_fwd, t_inv)
+    achieved = (bytes_fwd if dom == 'k_fwd' else bytes_inv) / (t_dom * 1e-3) / 1e9
+    kname = f'k_fwd<{ {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[args.mode] },{"true" if args.prefilter else "false"}>' \
+        if dom == 'k_fwd' else f'k_inv<{ {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[args.mode] }>'
+    traffic = None
+    tf = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(tf):
+        try:
+            rec = json.load(open(tf))
+            key = f'{W}x{H}_q{args.quality}_{args.mode}_pf{int(bool(args.prefilter))}_b{B}'
+            traffic = rec.get(key, {}).get(dom)
+        except Exception:
+            traffic = None
+
+    result = {
+        'metric': 'Mpixels/s forward+inverse pipeline @ Q=50 4:2:0; PSNR vs ref',
+        'value': round(value, 2),
+        'unit': 'Mpixels/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f64',
+        'data': 'synthetic (uniform random RGB generated on device)',
+        'config': {'workload': f'{W}x{H} RGB, Q={args.quality}, {args.mode}, prefilter={"on" if args.prefilter else "off"} '
+                               f'(BASELINE configs[1])',
+                   'frames_per_gpu_per_step': B, 'global_batch_frames': B * world,
+                   'parallelism': f'frame-shard x{world}'},
+        'roofline': {'bound': 'hbm', 'kernel': kname, 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                     'algorithmic_bytes_per_launch': bytes_fwd if dom == 'k_fwd' else bytes_inv,
+                     'avg_launch_ms': round(t_dom, 4)},
+        'kernels_ms': {'k_fwd': round(t_fwd, 4), 'k_inv': round(t_inv, 4)},
+        'pipeline_roofline_frac': round(value / world * 1e6 * (6 + 2 * S) / (HBM_PEAK_GBS * 1e9), 4),
+    }
+
+    if rank == 0 and not args.no_parity:
+        # PSNR / bytes vs the reference restatement on frame 0 (outside the timed region)
+        from oracle import cpu_ref
+        f0 = rgb[0].cpu().numpy()
+        ref = cpu_ref.compress_reconstruct(f0, args.quality, 8, args.mode, bool(args.prefilter), metrics=False)
+        rec0, cf0 = out[0].cpu().numpy(), coeffs[0].cpu().numpy()
+        mse = np.mean((f0.astype(np.float64) - rec0) ** 2)
+        mse_ref = np.mean((f0.astype(np.float64) - ref['reconstructed']) ** 2)
+        result['parity'] = {'frame': 0, 'coeff_mismatch': int(np.sum(cf0 != ref['coeffs'])),
+                            'recon_mismatch_bytes': int(np.sum(rec0 != ref['reconstructed'])),
+                            'psnr_rgb': float(10 * np.log10(255 ** 2 / mse)),
+                            'dpsnr_rgb_vs_ref': float(10 * np.log10(255 ** 2 / mse) - 10 * np.log10(255 ** 2 / mse_ref))}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        n = max(1, min(B, 64))
+        host = rgb[:n].cpu().numpy()
+        result['cpu_baseline'] = cpu_baseline(host, args.quality, args.mode, bool(args.prefilter),
+                                              args.cpu_baseline_seconds)
+    else:
+        result['cpu_baseline'] = None
+    plan.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,163 @@
+/* jds.h — C-ABI of the MI355X-native JPEG-DSP-Studio block-DCT codec path.
+ *
+ * The reference (Xneonz0/JPEG-DSP-Studio) is pure Python and has no FFI; its
+ * boundary is the Python function engines.pipeline.compress_reconstruct
+ * (engines/pipeline.py:17-21) plus the per-stage functions re-exported by
+ * engines/__init__.py:10-27.  This library is what sits UNDER that boundary:
+ * the drop-in Python package (jpeg-dsp-studio_amd/engines) binds these entry
+ * points with ctypes (jpeg-dsp-studio_amd/jds/_abi.py).
+ *
+ * Conventions: plain pointers and sizes, no torch/HIP types in signatures
+ * (streams are passed as void*).  Every int-returning function returns
+ * JDS_OK (0) or a negative code; jds_last_error() holds a thread-local message.
+ * All GPU work is hand-written HIP for gfx950; there is no CPU fallback.
+ */
+#ifndef JDS_H
+#define JDS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JDS_ABI_VERSION 1
+
+#define JDS_OK       0
+#define JDS_EINVAL  (-1)  /* bad argument                    -> ValueError   */
+#define JDS_ENOTSUP (-2)  /* e.g. block_size != 8, odd size  -> ValueError   */
+#define JDS_EHIP    (-3)  /* HIP runtime / device failure     -> RuntimeError */
+#define JDS_ENOMEM  (-4)  /* device allocation failed         -> RuntimeError */
+
+/* subsampling modes: models/compression_params.py:13 ('4:4:4','4:2:2','4:2:0') */
+#define JDS_SS_444 0
+#define JDS_SS_422 1
+#define JDS_SS_420 2
+
+/* jds_plan_run flags */
+#define JDS_RUN_SSE 1u  /* fill sse_rgb / sse_y (PSNR); the inverse kernel re-reads the input */
+#define JDS_RUN_FWD 2u  /* forward phase only (stats reset + k_fwd); with neither FWD nor INV: both */
+#define JDS_RUN_INV 4u  /* inverse phase only (k_inv + finalize); needs the forward's coeffs/stats */
+
+typedef struct jds_ctx jds_ctx;    /* one per (thread, device): owns a HIP stream + scratch */
+typedef struct jds_plan jds_plan;  /* fixed geometry + per-frame quant tables, device-resident */
+
+/* Per-frame parameters.  Mirrors CompressionParams (models/compression_params.py:7-20);
+ * the tables are computed on the host exactly as the reference does. */
+typedef struct {
+  int32_t block_size;  /* only 8 is supported (the reference crashes otherwise, engines/quantizer.py:24) */
+  int32_t quality;     /* 1..100 (informational; the table below is authoritative) */
+  int32_t subsampling; /* JDS_SS_* */
+  int32_t prefilter;   /* 0/1; ignored for 4:4:4 (engines/color_space.py:34-35) */
+  double qtable[64];   /* scale_quant_matrix(JPEG_LUMA_Q50, quality) (engines/quantizer.py:7-19) */
+  double gauss[3];     /* cv2.getGaussianKernel(3, 0.75) taps (engines/color_space.py:39-40) */
+} jds_params;
+
+/* Per-frame statistics, all exact integers except sse_y.
+ * estimate_bitrate_no_entropy (utils/metrics.py:51-92), histogram
+ * (engines/pipeline.py:123-124) and the PSNR sums (utils/metrics.py:11,20). */
+typedef struct {
+  uint64_t nonzero;             /* count of q != 0 */
+  uint64_t total_coeffs;        /* all_quantized_coeffs.size */
+  uint64_t magnitude_bits;      /* sum over q != 0 of ceil(log2(|q|+1)) + 1 */
+  uint64_t block_overhead_bits; /* 2 * ceil(H/8) * ceil(W/8) (luma grid only) */
+  uint64_t hist[50];            /* np.histogram(q, bins=50, range=(-100, 100))[0] */
+  uint64_t sse_rgb;             /* sum (orig - rec)^2 over H*W*3 uint8 samples (JDS_RUN_SSE) */
+  double sse_y;                 /* sum (Y(orig) - Y(rec))^2, Y = .299R+.587G+.114B (JDS_RUN_SSE) */
+  uint64_t pixels;              /* H * W */
+  double fwd_ms, inv_ms;        /* host path only: forward / inverse kernel time (hipEvents) */
+  double ssim[4];               /* host path only: SSIM of R, G, B and of Y (utils/metrics.py:12-21) */
+  double mse_y;                 /* host path only: NumPy-order mean of (Y(orig) - Y(rec))^2 */
+  uint64_t reserved[2];
+} jds_frame_stats;
+
+typedef struct {
+  int64_t H, W;
+  int64_t chroma_h, chroma_w;        /* after subsampling, before padding */
+  int64_t y_blocks_y, y_blocks_x;    /* padded luma block grid */
+  int64_t c_blocks_y, c_blocks_x;    /* padded chroma block grid (per plane) */
+  int64_t coeffs_per_frame;          /* 64 * (Y blocks + 2 * chroma blocks) */
+  int64_t cb_offset, cr_offset;      /* coefficient offsets of the Cb / Cr planes */
+  int32_t tiles, threads_fwd, threads_inv, reserved;
+} jds_geometry;
+
+/* IntermediateData.selected_block_* (engines/pipeline.py:128-151) */
+typedef struct {
+  double original[64], shifted[64], dct[64];
+  int16_t quantized[64];
+  double dequantized[64], reconstructed[64];
+} jds_selected_block;
+
+int jds_abi_version(void);
+const char* jds_last_error(void);
+int jds_device_count(int* n);
+
+/* Geometry of one frame (host only, no device access). */
+int jds_geometry_of(const jds_params* p, int64_t H, int64_t W, jds_geometry* out);
+
+int jds_ctx_create(int device, jds_ctx** out);
+void jds_ctx_destroy(jds_ctx* ctx);
+
+/* Device-resident batch path (bench, batch sweep).  n_frames frames of the same
+ * HxW share one subsampling/prefilter setting; params[i] gives frame i's table.
+ * Buffers are device pointers: rgb (n*H*W*3 u8), rgb_out (same), coeffs
+ * (n * coeffs_per_frame int16, reference layout: Y blocks, Cb blocks, Cr blocks,
+ * raster order, each block row-major), stats (n entries, overwritten).
+ * stream: a hipStream_t (NULL = the context's own stream).  Asynchronous. */
+int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n_frames, int64_t H, int64_t W,
+                    jds_plan** out);
+int jds_plan_run(jds_plan* plan, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs,
+                 jds_frame_stats* stats, uint32_t flags, void* stream);
+int jds_plan_geometry(const jds_plan* plan, jds_geometry* out);
+void jds_plan_destroy(jds_plan* plan);
+
+/* Host-buffer path: the drop-in for engines.pipeline.compress_reconstruct
+ * (engines/pipeline.py:17-167).  Synchronous.  rgb: HxWx3 u8, C-contiguous.
+ * Outputs (caller-allocated, all but rgb_out/stats nullable):
+ *   rgb_out       HxWx3 u8   reconstructed_image            (:95)
+ *   coeffs        coeffs_per_frame int16  all_quantized_coeffs (:99)
+ *   error_map_y   HxW f64    |Y - Y_rec|                     (:119-120)
+ *   error_map_rgb HxW f64    mean_c |rgb - rgb_rec_f|        (:121)
+ *   sel           selected luma block (sel_by, sel_bx) arrays (:128-151);
+ *                 *sel_valid set to 1 if the index is inside the padded grid. */
+int jds_compress_reconstruct(jds_ctx* ctx, const jds_params* p, const uint8_t* rgb, int64_t H,
+                             int64_t W, uint8_t* rgb_out, int16_t* coeffs, jds_frame_stats* stats,
+                             double* error_map_y, double* error_map_rgb, int32_t sel_by,
+                             int32_t sel_bx, jds_selected_block* sel, int32_t* sel_valid);
+
+/* PSNR / SSIM of two HxWx3 uint8 host images on the GPU (utils/metrics.py:9-28):
+ * out[0..3] = SSIM of R, G, B, Y; out[4] = MSE of Y; out[5] = MSE of RGB.
+ * Bit-identical to skimage + scipy.ndimage + NumPy reductions.  H, W >= 7. */
+int jds_psnr_ssim(jds_ctx* ctx, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out);
+
+/* Per-stage functions of the engines.* API (engines/__init__.py:10-27), on host
+ * fp64 arrays staged through the context's device memory.  Synchronous.
+ *   rgb_to_ycbcr / ycbcr_to_rgb: n_pixels x 3 (engines/color_space.py:8-24)
+ *   subsample: cb, cr HxW -> (H/2 or H) x W/2; mode JDS_SS_422 / JDS_SS_420;
+ *              gauss = 3 prefilter taps (engines/color_space.py:27-53)
+ *   upsample : h x w -> H x W, bilinear (nearest != 0: INTER_NEAREST) (:56-66)
+ *   block_dct: n 8x8 blocks; op 0 dct2, 1 idct2, 2 encode_block, 3 decode_block
+ *              (engines/dct_engine.py:7-27)
+ *   quantize : n values (n % 64 == 0, 8x8-periodic table); dequant = 0:
+ *              f64 -> int16 round-half-even of c/Q; 1: int16 -> f64 q*Q
+ *              (engines/quantizer.py:22-29) */
+int jds_stage_rgb_to_ycbcr(jds_ctx* ctx, const double* rgb, double* ycc, int64_t n_pixels);
+int jds_stage_ycbcr_to_rgb(jds_ctx* ctx, const double* ycc, double* rgb, int64_t n_pixels);
+int jds_stage_subsample(jds_ctx* ctx, const double* cb, const double* cr, int64_t H, int64_t W, int32_t mode,
+                        int32_t prefilter, const double* gauss, double* cb_out, double* cr_out);
+int jds_stage_upsample(jds_ctx* ctx, const double* in, int64_t h, int64_t w, int64_t H, int64_t W,
+                       int32_t nearest, double* out);
+int jds_stage_block_dct(jds_ctx* ctx, const double* in, double* out, int64_t n_blocks, int32_t op);
+int jds_stage_quantize(jds_ctx* ctx, const void* in, const double* qtable, void* out, int64_t n,
+                       int32_t dequant);
+
+/* Test-only: evaluate the device DCT expressions (jds_dct8.hpp) on the host so
+ * the CPU test suite can pin them against SciPy without a GPU.  Not used by
+ * any product path.  in/out: n blocks of 8x8 f64; inverse: 0 = dctn, 1 = idctn. */
+int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t inverse);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* JDS_H */

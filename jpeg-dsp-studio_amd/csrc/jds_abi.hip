@@ -1,0 +1,570 @@
+// jds_abi.hip — the C-ABI (include/jds.h): contexts, plans, host-buffer path.
+//
+// Host side only orchestrates: geometry, quant-table upload, buffer
+// management and launches.  All per-pixel / per-coefficient arithmetic runs
+// in the HIP kernels of jds_codec.hip; there is no CPU fallback.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+
+#include "jds_dct8.hpp"
+#include "jds_internal.hpp"
+
+namespace jds {
+hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
+                        int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
+                        double* part, bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel,
+                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases);
+hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, double c1, double c2,
+                            double* scratch_planes, double* scratch_smap, double* scratch_chunks, double* out,
+                            hipStream_t s);
+hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
+hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse, hipStream_t s);
+hipError_t stage_subsample(const double* in, double* tmp, double* tmp2, double* out, int H, int W, int sy,
+                           int prefilter, const double* k, hipStream_t s);
+hipError_t stage_resize(const double* in, int h, int w, double* out, int H, int W, int nearest, hipStream_t s);
+hipError_t stage_block(const double* in, double* out, long long n, int op, hipStream_t s);
+hipError_t stage_quant(const void* in, const double* q, void* out, long long n, int dequant, hipStream_t s);
+}
+
+// skimage: C1 = (K1 * R) ** 2, C2 = (K2 * R) ** 2 with R = data_range = 255
+static const double SSIM_C1 = (0.01 * 255) * (0.01 * 255);
+static const double SSIM_C2 = (0.03 * 255) * (0.03 * 255);
+
+using namespace jds;
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(e_ == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "%s: %s (%s:%d)", #expr, \
+                  hipGetErrorString(e_), __FILE__, __LINE__);                               \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+    if (e == hipSuccess) n = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct jds_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  // host-path scratch
+  DevBuf rgb, out, coeffs, stats, part, fq, gk, erry, errrgb, sel;
+  DevBuf ss_planes, ss_map, ss_chunks, ss_out, img_a, img_b;
+  DevBuf st[5];  // per-stage API staging
+};
+
+// SSIM scratch in the context; returns the device pointer of 5 result doubles
+static int run_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int H, int W, double* dres) {
+  const size_t n = (size_t)H * W;
+  HIP_TRY(c->ss_planes.ensure(5 * n * sizeof(double)));
+  HIP_TRY(c->ss_map.ensure((size_t)(H - 6) * (W - 6) * sizeof(double)));
+  HIP_TRY(c->ss_chunks.ensure(((n + 8191) / 8192 + 1) * sizeof(double)));
+  HIP_TRY(launch_psnr_ssim(a, b, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_planes.p, (double*)c->ss_map.p,
+                           (double*)c->ss_chunks.p, dres, c->stream));
+  return JDS_OK;
+}
+
+struct jds_plan {
+  jds_ctx* ctx = nullptr;
+  int n = 0, mode = 0;
+  bool pf = false;
+  Geo g{};
+  DevBuf fq, gk, part;
+};
+
+// ------------------------------------------------------------- geometry --
+
+static int make_geo(const jds_params* p, int64_t H, int64_t W, Geo* g, int* mode_out, bool* pf_out) {
+  if (!p || !g) return fail(JDS_EINVAL, "null argument");
+  if (p->block_size != 8)
+    return fail(JDS_ENOTSUP, "operands could not be broadcast together with shapes (%d,%d) (8,8) ",
+                p->block_size, p->block_size);
+  if (p->subsampling < JDS_SS_444 || p->subsampling > JDS_SS_420)
+    return fail(JDS_EINVAL, "Unknown subsampling mode: %d", p->subsampling);
+  if (H < 1 || W < 1 || H > 65536 || W > 65536 || H * W > (int64_t)1 << 28)
+    return fail(JDS_EINVAL, "unsupported image size %lldx%lld", (long long)H, (long long)W);
+  const int mode = p->subsampling;
+  const int sy = mode == JDS_SS_420 ? 2 : 1, sx = mode == JDS_SS_444 ? 1 : 2;
+  if ((sy == 2 && (H % 2)) || (sx == 2 && (W % 2)))
+    return fail(JDS_ENOTSUP,
+                "odd image size %lldx%lld with chroma subsampling needs cv2's fractional INTER_AREA "
+                "path, which is not implemented",
+                (long long)H, (long long)W);
+  Geo& G = *g;
+  memset(&G, 0, sizeof G);
+  G.H = (int)H;
+  G.W = (int)W;
+  G.hc = (int)(H / sy);
+  G.wc = (int)(W / sx);
+  G.nby = (int)((H + 7) / 8);
+  G.nbx = (int)((W + 7) / 8);
+  G.ncy = (G.hc + 7) / 8;
+  G.ncx = (G.wc + 7) / 8;
+  int MY, MX;
+  switch (mode) {
+    case JDS_SS_420: MY = Cfg<M420>::MY; MX = Cfg<M420>::MX; break;
+    case JDS_SS_422: MY = Cfg<M422>::MY; MX = Cfg<M422>::MX; break;
+    default: MY = Cfg<M444>::MY; MX = Cfg<M444>::MX; break;
+  }
+  G.nmy = mode == JDS_SS_444 ? G.nby : G.ncy;
+  G.nmx = mode == JDS_SS_444 ? G.nbx : G.ncx;
+  G.tiles_y = (G.nmy + MY - 1) / MY;
+  G.tiles_x = (G.nmx + MX - 1) / MX;
+  G.ty_off = G.tiles_y * MY - G.nmy;
+  G.tx_off = G.tiles_x * MX - G.nmx;
+  const long long yb = (long long)G.nby * G.nbx, cb = (long long)G.ncy * G.ncx;
+  G.cpf = 64 * (yb + 2 * cb);
+  G.off_cb = 64 * yb;
+  G.off_cr = 64 * (yb + cb);
+  // cv2.resize: inv_scale = dst/src, scale = 1/inv_scale
+  G.up_sy = 1.0 / ((double)H / (double)G.hc);
+  G.up_sx = 1.0 / ((double)W / (double)G.wc);
+  if (mode_out) *mode_out = mode;
+  if (pf_out) *pf_out = mode != JDS_SS_444 && p->prefilter != 0;
+  return JDS_OK;
+}
+
+static void fill_geometry(const Geo& G, int mode, jds_geometry* o) {
+  o->H = G.H;
+  o->W = G.W;
+  o->chroma_h = G.hc;
+  o->chroma_w = G.wc;
+  o->y_blocks_y = G.nby;
+  o->y_blocks_x = G.nbx;
+  o->c_blocks_y = G.ncy;
+  o->c_blocks_x = G.ncx;
+  o->coeffs_per_frame = G.cpf;
+  o->cb_offset = G.off_cb;
+  o->cr_offset = G.off_cr;
+  o->tiles = G.tiles_y * G.tiles_x;
+  o->threads_fwd = mode == JDS_SS_420 ? Cfg<M420>::TF : mode == JDS_SS_422 ? Cfg<M422>::TF : Cfg<M444>::TF;
+  o->threads_inv = Cfg<M420>::TI;
+  o->reserved = 0;
+}
+
+static void make_fq(const jds_params* p, FrameQ* q) {
+  for (int i = 0; i < 64; ++i) {
+    q->q[i] = p->qtable[i];
+    q->q16[i] = 16.0 * p->qtable[i];  // exact
+  }
+}
+
+static int check_tables(const jds_params* p) {
+  for (int i = 0; i < 64; ++i)
+    if (!(p->qtable[i] >= 1.0 && p->qtable[i] <= 255.0))
+      return fail(JDS_EINVAL, "qtable[%d] = %g outside [1, 255]", i, p->qtable[i]);
+  return JDS_OK;
+}
+
+// ------------------------------------------------------------------ ABI --
+
+extern "C" {
+
+int jds_abi_version(void) { return JDS_ABI_VERSION; }
+
+const char* jds_last_error(void) { return g_err; }
+
+int jds_device_count(int* n) {
+  if (!n) return fail(JDS_EINVAL, "null argument");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    return fail(JDS_EHIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *n = c;
+  return JDS_OK;
+}
+
+int jds_geometry_of(const jds_params* p, int64_t H, int64_t W, jds_geometry* out) {
+  Geo g;
+  int mode;
+  int rc = make_geo(p, H, W, &g, &mode, nullptr);
+  if (rc) return rc;
+  if (!out) return fail(JDS_EINVAL, "null argument");
+  fill_geometry(g, mode, out);
+  return JDS_OK;
+}
+
+int jds_ctx_create(int device, jds_ctx** out) {
+  if (!out) return fail(JDS_EINVAL, "null argument");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(JDS_EINVAL, "device %d out of range (%d devices)", device, n);
+  HIP_TRY(hipSetDevice(device));
+  jds_ctx* c = new (std::nothrow) jds_ctx();
+  if (!c) return fail(JDS_ENOMEM, "host allocation failed");
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(JDS_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  for (int i = 0; i < 3; ++i) {
+    if ((e = hipEventCreate(&c->ev[i])) != hipSuccess) {
+      jds_ctx_destroy(c);
+      return fail(JDS_EHIP, "hipEventCreate: %s", hipGetErrorString(e));
+    }
+  }
+  *out = c;
+  return JDS_OK;
+}
+
+void jds_ctx_destroy(jds_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  DevBuf* bufs[] = {&c->rgb,     &c->out,    &c->coeffs,    &c->stats,  &c->part,  &c->fq,   &c->gk,  &c->erry,
+                    &c->errrgb,  &c->sel,    &c->ss_planes, &c->ss_map, &c->ss_chunks, &c->ss_out, &c->img_a, &c->img_b};
+  for (DevBuf* b : bufs) b->release();
+  for (DevBuf& b : c->st) b.release();
+  for (hipEvent_t e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n, int64_t H, int64_t W, jds_plan** out) {
+  if (!ctx || !params || !out || n < 1) return fail(JDS_EINVAL, "bad argument");
+  Geo g;
+  int mode;
+  bool pf;
+  int rc = make_geo(params, H, W, &g, &mode, &pf);
+  if (rc) return rc;
+  FrameQ* hq = (FrameQ*)malloc(sizeof(FrameQ) * (size_t)n);
+  if (!hq) return fail(JDS_ENOMEM, "host allocation failed");
+  for (int i = 0; i < n; ++i) {
+    if (params[i].subsampling != params[0].subsampling || params[i].block_size != params[0].block_size ||
+        (params[i].prefilter != 0) != (params[0].prefilter != 0)) {
+      free(hq);
+      return fail(JDS_EINVAL, "all frames of a plan must share subsampling / prefilter / block size");
+    }
+    if ((rc = check_tables(params + i))) {
+      free(hq);
+      return rc;
+    }
+    make_fq(params + i, hq + i);
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  jds_plan* p = new (std::nothrow) jds_plan();
+  if (!p) {
+    free(hq);
+    return fail(JDS_ENOMEM, "host allocation failed");
+  }
+  p->ctx = ctx;
+  p->n = n;
+  p->mode = mode;
+  p->pf = pf;
+  p->g = g;
+  hipError_t e;
+  if ((e = p->fq.ensure(sizeof(FrameQ) * n)) != hipSuccess || (e = p->gk.ensure(3 * sizeof(double))) != hipSuccess ||
+      (e = p->part.ensure(sizeof(double) * (size_t)n * g.tiles_y * g.tiles_x)) != hipSuccess ||
+      (e = hipMemcpy(p->fq.p, hq, sizeof(FrameQ) * n, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(p->gk.p, params[0].gauss, 3 * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess) {
+    free(hq);
+    p->fq.release();
+    p->gk.release();
+    p->part.release();
+    delete p;
+    return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
+  }
+  free(hq);
+  *out = p;
+  return JDS_OK;
+}
+
+int jds_plan_geometry(const jds_plan* p, jds_geometry* out) {
+  if (!p || !out) return fail(JDS_EINVAL, "null argument");
+  fill_geometry(p->g, p->mode, out);
+  return JDS_OK;
+}
+
+int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs, jds_frame_stats* stats,
+                 uint32_t flags, void* stream) {
+  if (!p || !rgb || !rgb_out || !coeffs || !stats) return fail(JDS_EINVAL, "null argument");
+  hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+  int phases = (flags & JDS_RUN_FWD ? 1 : 0) | (flags & JDS_RUN_INV ? 2 : 0);
+  if (!phases) phases = 3;
+  if (phases & 1) HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
+  HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
+                       (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
+                       nullptr, nullptr, 0, s, nullptr, phases));
+  return JDS_OK;
+}
+
+void jds_plan_destroy(jds_plan* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->ctx->device);
+  (void)hipStreamSynchronize(p->ctx->stream);
+  p->fq.release();
+  p->gk.release();
+  p->part.release();
+  delete p;
+}
+
+int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* rgb, int64_t H, int64_t W,
+                             uint8_t* rgb_out, int16_t* coeffs, jds_frame_stats* stats, double* error_map_y,
+                             double* error_map_rgb, int32_t sel_by, int32_t sel_bx, jds_selected_block* sel,
+                             int32_t* sel_valid) {
+  if (!c || !prm || !rgb || !rgb_out || !stats) return fail(JDS_EINVAL, "null argument");
+  if ((error_map_y == nullptr) != (error_map_rgb == nullptr))
+    return fail(JDS_EINVAL, "error_map_y and error_map_rgb must be requested together");
+  Geo g;
+  int mode;
+  bool pf;
+  int rc = make_geo(prm, H, W, &g, &mode, &pf);
+  if (rc) return rc;
+  if ((rc = check_tables(prm))) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t npx = (size_t)H * (size_t)W, nimg = npx * 3, ncf = (size_t)g.cpf;
+  const int tiles = g.tiles_y * g.tiles_x;
+  HIP_TRY(c->rgb.ensure(nimg));
+  HIP_TRY(c->out.ensure(nimg));
+  HIP_TRY(c->coeffs.ensure(ncf * sizeof(int16_t)));
+  HIP_TRY(c->stats.ensure(sizeof(jds_frame_stats)));
+  HIP_TRY(c->part.ensure(sizeof(double) * tiles));
+  HIP_TRY(c->fq.ensure(sizeof(FrameQ)));
+  HIP_TRY(c->gk.ensure(3 * sizeof(double)));
+  const bool maps = error_map_y != nullptr;
+  if (maps) {
+    HIP_TRY(c->erry.ensure(npx * sizeof(double)));
+    HIP_TRY(c->errrgb.ensure(npx * sizeof(double)));
+  }
+  // selected luma block (pipeline.py:132-138): index into the padded grid
+  int sel_blk = -1;
+  if (sel) {
+    const long long bpr = g.nbx;
+    const long long ti = (long long)sel_by * bpr + sel_bx;
+    const long long nyb = (long long)g.nby * g.nbx;
+    if (ti >= 0 && ti < nyb) sel_blk = (int)ti;
+    if (sel_valid) *sel_valid = sel_blk >= 0;
+    if (sel_blk >= 0) HIP_TRY(c->sel.ensure(sizeof(jds_selected_block)));
+  }
+  FrameQ hq;
+  make_fq(prm, &hq);
+  hipStream_t s = c->stream;
+  HIP_TRY(hipMemcpyAsync(c->fq.p, &hq, sizeof hq, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->gk.p, prm->gauss, 3 * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->rgb.p, rgb, nimg, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(jds_frame_stats), s));
+  jds_selected_block* dsel = sel_blk >= 0 ? (jds_selected_block*)c->sel.p : nullptr;
+  HIP_TRY(launch_codec(mode, pf, g, 1, (const uint8_t*)c->rgb.p, (uint8_t*)c->out.p, (int16_t*)c->coeffs.p,
+                       (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
+                       (double*)c->part.p, true, maps ? (double*)c->erry.p : nullptr,
+                       maps ? (double*)c->errrgb.p : nullptr, dsel, sel_blk, s, c->ev, 3));
+  HIP_TRY(hipMemcpyAsync(rgb_out, c->out.p, nimg, hipMemcpyDeviceToHost, s));
+  if (coeffs) HIP_TRY(hipMemcpyAsync(coeffs, c->coeffs.p, ncf * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+  if (maps) {
+    HIP_TRY(hipMemcpyAsync(error_map_y, c->erry.p, npx * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(error_map_rgb, c->errrgb.p, npx * sizeof(double), hipMemcpyDeviceToHost, s));
+  }
+  if (H >= 7 && W >= 7) {
+    jds_frame_stats* dst = (jds_frame_stats*)c->stats.p;
+    if ((rc = run_ssim(c, (const uint8_t*)c->rgb.p, (const uint8_t*)c->out.p, (int)H, (int)W, &dst->ssim[0])))
+      return rc;
+  }
+  if (dsel) HIP_TRY(hipMemcpyAsync(sel, dsel, sizeof(jds_selected_block), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(stats, c->stats.p, sizeof(jds_frame_stats), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (!(H >= 7 && W >= 7)) {
+    for (int i = 0; i < 4; ++i) stats->ssim[i] = __builtin_nan("");
+    stats->mse_y = __builtin_nan("");
+  }
+  float t0 = 0.f, t1 = 0.f;
+  HIP_TRY(hipEventElapsedTime(&t0, c->ev[0], c->ev[1]));
+  HIP_TRY(hipEventElapsedTime(&t1, c->ev[1], c->ev[2]));
+  stats->fwd_ms = t0;
+  stats->inv_ms = t1;
+  return JDS_OK;
+}
+
+int jds_psnr_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out) {
+  if (!c || !a || !b || !out) return fail(JDS_EINVAL, "null argument");
+  if (H < 7 || W < 7)
+    return fail(JDS_EINVAL,
+                "win_size exceeds image extent. Either ensure that your images are at least 7x7; or pass "
+                "win_size explicitly in the function call, with an odd value less than or equal to the "
+                "smaller side of your images. If your images are multichannel (with color channels), set "
+                "channel_axis to the axis number corresponding to the channels.");
+  if (H * W > (int64_t)1 << 28) return fail(JDS_EINVAL, "image too large");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t nb = (size_t)H * W * 3;
+  HIP_TRY(c->img_a.ensure(nb));
+  HIP_TRY(c->img_b.ensure(nb));
+  HIP_TRY(c->ss_out.ensure(5 * sizeof(double) + sizeof(unsigned long long)));
+  hipStream_t s = c->stream;
+  HIP_TRY(hipMemcpyAsync(c->img_a.p, a, nb, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->img_b.p, b, nb, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(c->ss_out.p, 0, 5 * sizeof(double) + sizeof(unsigned long long), s));
+  double* dres = (double*)c->ss_out.p;
+  unsigned long long* dsse = (unsigned long long*)(dres + 5);
+  int rc = run_ssim(c, (const uint8_t*)c->img_a.p, (const uint8_t*)c->img_b.p, (int)H, (int)W, dres);
+  if (rc) return rc;
+  HIP_TRY(launch_sse_u8((const uint8_t*)c->img_a.p, (const uint8_t*)c->img_b.p, (long long)nb, dsse, s));
+  double res[5];
+  unsigned long long sse = 0;
+  HIP_TRY(hipMemcpyAsync(res, dres, sizeof res, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&sse, dsse, sizeof sse, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int i = 0; i < 5; ++i) out[i] = res[i];
+  out[5] = (double)sse / (double)nb;  // exact: integer sum, one division (np.mean)
+  return JDS_OK;
+}
+
+// ----------------------------------------------------- per-stage API --
+
+static int stage_io(jds_ctx* c, int idx, const void* host, size_t bytes, void** dev) {
+  HIP_TRY(c->st[idx].ensure(bytes));
+  if (host) HIP_TRY(hipMemcpyAsync(c->st[idx].p, host, bytes, hipMemcpyHostToDevice, c->stream));
+  *dev = c->st[idx].p;
+  return JDS_OK;
+}
+
+static int stage_out(jds_ctx* c, void* host, const void* dev, size_t bytes) {
+  HIP_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return JDS_OK;
+}
+
+static int stage_rgb(jds_ctx* c, const double* in, double* out, int64_t n, int inverse) {
+  if (!c || !in || !out || n < 0) return fail(JDS_EINVAL, "bad argument");
+  if (n == 0) return JDS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  void *di, *dout;
+  int rc;
+  const size_t b = (size_t)n * 3 * sizeof(double);
+  if ((rc = stage_io(c, 0, in, b, &di)) || (rc = stage_io(c, 1, nullptr, b, &dout))) return rc;
+  HIP_TRY(stage_rgb_ycc((const double*)di, (double*)dout, n, inverse, c->stream));
+  return stage_out(c, out, dout, b);
+}
+
+int jds_stage_rgb_to_ycbcr(jds_ctx* c, const double* rgb, double* ycc, int64_t n_pixels) {
+  return stage_rgb(c, rgb, ycc, n_pixels, 0);
+}
+
+int jds_stage_ycbcr_to_rgb(jds_ctx* c, const double* ycc, double* rgb, int64_t n_pixels) {
+  return stage_rgb(c, ycc, rgb, n_pixels, 1);
+}
+
+int jds_stage_subsample(jds_ctx* c, const double* cb, const double* cr, int64_t H, int64_t W, int32_t mode,
+                        int32_t prefilter, const double* gauss, double* cb_out, double* cr_out) {
+  if (!c || !cb || !cr || !cb_out || !cr_out || !gauss || H < 1 || W < 1) return fail(JDS_EINVAL, "bad argument");
+  if (mode != JDS_SS_422 && mode != JDS_SS_420) return fail(JDS_EINVAL, "Unknown subsampling mode: %d", mode);
+  const int sy = mode == JDS_SS_420 ? 2 : 1;
+  if ((W % 2) || (sy == 2 && (H % 2)))
+    return fail(JDS_ENOTSUP, "odd plane size needs cv2's fractional INTER_AREA path (not implemented)");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)H * W, bi = n * sizeof(double), bo = (n / (2 * sy)) * sizeof(double);
+  void *din, *t1, *t2, *dout;
+  int rc;
+  if ((rc = stage_io(c, 1, nullptr, bi, &t1)) || (rc = stage_io(c, 2, nullptr, bi, &t2)) ||
+      (rc = stage_io(c, 3, nullptr, bo, &dout)))
+    return rc;
+  const double* planes[2] = {cb, cr};
+  double* outs[2] = {cb_out, cr_out};
+  for (int p = 0; p < 2; ++p) {
+    if ((rc = stage_io(c, 0, planes[p], bi, &din))) return rc;
+    HIP_TRY(stage_subsample((const double*)din, (double*)t1, (double*)t2, (double*)dout, (int)H, (int)W, sy,
+                            prefilter, gauss, c->stream));
+    if ((rc = stage_out(c, outs[p], dout, bo))) return rc;
+  }
+  return JDS_OK;
+}
+
+int jds_stage_upsample(jds_ctx* c, const double* in, int64_t h, int64_t w, int64_t H, int64_t W, int32_t nearest,
+                       double* out) {
+  if (!c || !in || !out || h < 1 || w < 1 || H < 1 || W < 1) return fail(JDS_EINVAL, "bad argument");
+  HIP_TRY(hipSetDevice(c->device));
+  void *din, *dout;
+  int rc;
+  if ((rc = stage_io(c, 0, in, (size_t)h * w * sizeof(double), &din)) ||
+      (rc = stage_io(c, 1, nullptr, (size_t)H * W * sizeof(double), &dout)))
+    return rc;
+  HIP_TRY(stage_resize((const double*)din, (int)h, (int)w, (double*)dout, (int)H, (int)W, nearest, c->stream));
+  return stage_out(c, out, dout, (size_t)H * W * sizeof(double));
+}
+
+int jds_stage_block_dct(jds_ctx* c, const double* in, double* out, int64_t n_blocks, int32_t op) {
+  if (!c || !in || !out || n_blocks < 0 || op < 0 || op > 3) return fail(JDS_EINVAL, "bad argument");
+  if (n_blocks == 0) return JDS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t b = (size_t)n_blocks * 64 * sizeof(double);
+  void *din, *dout;
+  int rc;
+  if ((rc = stage_io(c, 0, in, b, &din)) || (rc = stage_io(c, 1, nullptr, b, &dout))) return rc;
+  HIP_TRY(stage_block((const double*)din, (double*)dout, n_blocks, op, c->stream));
+  return stage_out(c, out, dout, b);
+}
+
+int jds_stage_quantize(jds_ctx* c, const void* in, const double* qtable, void* out, int64_t n, int32_t dequant) {
+  if (!c || !in || !qtable || !out || n < 0 || (n % 64)) return fail(JDS_EINVAL, "bad argument");
+  if (n == 0) return JDS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bi = (size_t)n * (dequant ? sizeof(int16_t) : sizeof(double));
+  const size_t bo = (size_t)n * (dequant ? sizeof(double) : sizeof(int16_t));
+  void *din, *dq, *dout;
+  int rc;
+  if ((rc = stage_io(c, 0, in, bi, &din)) || (rc = stage_io(c, 4, qtable, 64 * sizeof(double), &dq)) ||
+      (rc = stage_io(c, 1, nullptr, bo, &dout)))
+    return rc;
+  HIP_TRY(stage_quant(din, (const double*)dq, dout, n, dequant, c->stream));
+  return stage_out(c, out, dout, bo);
+}
+
+int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t inverse) {
+  if (!in || !out || n < 0) return fail(JDS_EINVAL, "bad argument");
+  for (int64_t b = 0; b < n; ++b) {
+    double t[64];
+    memcpy(t, in + 64 * b, sizeof t);
+    for (int col = 0; col < 8; ++col) {  // axis 0 first
+      double* c = t + col;
+      if (inverse)
+        dct3_line(c[0], c[8], c[16], c[24], c[32], c[40], c[48], c[56]);
+      else
+        dct2_line(c[0], c[8], c[16], c[24], c[32], c[40], c[48], c[56]);
+    }
+    for (int r = 0; r < 8; ++r) {
+      double* c = t + 8 * r;
+      if (inverse)
+        dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
+      else
+        dct2_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
+    }
+    for (int i = 0; i < 64; ++i) out[64 * b + i] = t[i] * 0.0625;  // pocketfft fct = 1/16
+  }
+  return JDS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,57 @@
+// jds_internal.hpp — types shared by the HIP kernels and the host-side C-ABI.
+#pragma once
+#include <stdint.h>
+
+#include "jds.h"
+
+namespace jds {
+
+enum Mode : int { M444 = JDS_SS_444, M422 = JDS_SS_422, M420 = JDS_SS_420 };
+
+// Frame geometry.  Tiles are laid on the MCU grid aligned to the BOTTOM-RIGHT
+// corner (phantom MCUs at the top/left of the first tile row/column), so the
+// block row/column that carries reflect padding always shares its tile with
+// the previous block row/column it reflects into (np.pad 'reflect' reaches at
+// most 7 samples back: engines/block_processor.py:10-13).
+struct Geo {
+  int H, W;          // image
+  int hc, wc;        // chroma plane after subsampling (before padding)
+  int nby, nbx;      // padded luma block grid
+  int ncy, ncx;      // padded chroma block grid (per plane)
+  int nmy, nmx;      // MCU grid
+  int tiles_y, tiles_x, ty_off, tx_off;
+  long long cpf;     // coefficients per frame
+  long long off_cb, off_cr;
+  double up_sy, up_sx;  // cv2.resize scale (src/dst) of the chroma upsample
+};
+
+// Per-frame quantiser: q16 = 16*Q (pocketfft's first-axis fct = 1/16 folded in), q = Q.
+struct FrameQ {
+  double q16[64];
+  double q[64];
+};
+
+// Tile configuration per subsampling mode.
+template <int MODE>
+struct Cfg {
+  static constexpr int SY = (MODE == M420) ? 2 : 1;   // chroma subsampling (rows)
+  static constexpr int SX = (MODE == M444) ? 1 : 2;   // chroma subsampling (cols)
+  static constexpr int MH = 8 * SY, MW = 8 * SX;      // MCU size in pixels
+  static constexpr int TH = (MODE == M444) ? 16 : 32; // tile size in pixels
+  static constexpr int TW = 64;
+  static constexpr int MY = TH / MH, MX = TW / MW;    // MCUs per tile
+  static constexpr int YBR = TH / 8, YBC = TW / 8;    // luma blocks per tile
+  static constexpr int CBR = TH / MH, CBC = TW / MW;  // chroma blocks per plane per tile
+  static constexpr int NYB = YBR * YBC, NCB = CBR * CBC;
+  static constexpr int NB = NYB + 2 * NCB;
+  static constexpr int TF = NB * 8;                   // forward threads: one per block line
+  // inverse: chroma blocks including the 1-block ring the bilinear upsample reaches into
+  static constexpr int RY = (SY == 2) ? 1 : 0, RX = (SX == 2) ? 1 : 0;
+  static constexpr int RBR = CBR + 2 * RY, RBC = CBC + 2 * RX;
+  static constexpr int NRB = RBR * RBC;               // per plane
+  static constexpr int CWR = 8 * CBR + 2 * RY;        // chroma sample window kept in LDS
+  static constexpr int CWC = 8 * CBC + 2 * RX;
+  static constexpr int TI = 384;                      // inverse threads
+};
+
+}  // namespace jds
