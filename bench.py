@@ -100,7 +100,9 @@ def main():
     out = torch.empty_like(rgb)
     coeffs = torch.empty((B, cpf), dtype=torch.int16, device=dev)
     stats = torch.zeros((B, _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # a real (non-null) stream: kernels and events both go here
+    torch.cuda.synchronize(dev)  # inputs were produced on the default stream
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
     def step(ev=None):

@@ -97,13 +97,14 @@ int jds_geometry_of(const jds_params* p, int64_t H, int64_t W, jds_geometry* out
 
 int jds_ctx_create(int device, jds_ctx** out);
 void jds_ctx_destroy(jds_ctx* ctx);
+void* jds_ctx_stream(jds_ctx* ctx);  /* the context's own hipStream_t */
 
 /* Device-resident batch path (bench, batch sweep).  n_frames frames of the same
  * HxW share one subsampling/prefilter setting; params[i] gives frame i's table.
  * Buffers are device pointers: rgb (n*H*W*3 u8), rgb_out (same), coeffs
  * (n * coeffs_per_frame int16, reference layout: Y blocks, Cb blocks, Cr blocks,
  * raster order, each block row-major), stats (n entries, overwritten).
- * stream: a hipStream_t (NULL = the context's own stream).  Asynchronous. */
+ * stream: a hipStream_t (NULL = the HIP null stream).  Asynchronous. */
 int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n_frames, int64_t H, int64_t W,
                     jds_plan** out);
 int jds_plan_run(jds_plan* plan, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs,

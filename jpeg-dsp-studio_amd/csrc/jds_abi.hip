@@ -208,6 +208,8 @@ int jds_device_count(int* n) {
   return JDS_OK;
 }
 
+void* jds_ctx_stream(jds_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
 int jds_geometry_of(const jds_params* p, int64_t H, int64_t W, jds_geometry* out) {
   Geo g;
   int mode;
@@ -314,7 +316,7 @@ int jds_plan_geometry(const jds_plan* p, jds_geometry* out) {
 int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs, jds_frame_stats* stats,
                  uint32_t flags, void* stream) {
   if (!p || !rgb || !rgb_out || !coeffs || !stats) return fail(JDS_EINVAL, "null argument");
-  hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+  hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (torch's default stream)
   int phases = (flags & JDS_RUN_FWD ? 1 : 0) | (flags & JDS_RUN_INV ? 2 : 0);
   if (!phases) phases = 3;
   if (phases & 1) HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));

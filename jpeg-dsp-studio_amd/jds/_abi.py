@@ -73,6 +73,7 @@ _SIGS = {
     'jds_geometry_of': (C.c_int, [C.POINTER(Params), C.c_int64, C.c_int64, C.POINTER(Geometry)]),
     'jds_ctx_create': (C.c_int, [C.c_int, C.POINTER(_P)]),
     'jds_ctx_destroy': (None, [_P]),
+    'jds_ctx_stream': (_P, [_P]),
     'jds_plan_create': (C.c_int, [_P, C.POINTER(Params), C.c_int, C.c_int64, C.c_int64, C.POINTER(_P)]),
     'jds_plan_run': (C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
     'jds_plan_geometry': (C.c_int, [_P, C.POINTER(Geometry)]),
@@ -221,6 +222,9 @@ class Plan:
 
     def run(self, rgb_dev: int, out_dev: int, coeffs_dev: int, stats_dev: int, flags: int = 0,
             stream: int | None = None):
+        """stream: a hipStream_t handle (0 = the null stream); None = the context's stream."""
+        if stream is None:
+            stream = lib().jds_ctx_stream(self.ctx.handle)
         check(lib().jds_plan_run(self.handle, rgb_dev, out_dev, coeffs_dev, stats_dev, flags, stream))
 
     def close(self):
