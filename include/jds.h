@@ -38,6 +38,7 @@ extern "C" {
 #define JDS_RUN_SSE 1u  /* fill sse_rgb / sse_y (PSNR); the inverse kernel re-reads the input */
 #define JDS_RUN_FWD 2u  /* forward phase only (stats reset + k_fwd); with neither FWD nor INV: both */
 #define JDS_RUN_INV 4u  /* inverse phase only (k_inv + finalize); needs the forward's coeffs/stats */
+#define JDS_RUN_EXACT 8u /* all-fp64 kernels (default: certified fp32 + exact fp64 fix-up, same results) */
 
 typedef struct jds_ctx jds_ctx;    /* one per (thread, device): owns a HIP stream + scratch */
 typedef struct jds_plan jds_plan;  /* fixed geometry + per-frame quant tables, device-resident */
@@ -110,6 +111,8 @@ int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n_frames, int64_
 int jds_plan_run(jds_plan* plan, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs,
                  jds_frame_stats* stats, uint32_t flags, void* stream);
 int jds_plan_geometry(const jds_plan* plan, jds_geometry* out);
+/* Entries the last run's fix-up lists received: [0] forward blocks, [1] inverse pixels. */
+int jds_plan_fix_counts(const jds_plan* plan, uint32_t* counts);
 void jds_plan_destroy(jds_plan* plan);
 
 /* Host-buffer path: the drop-in for engines.pipeline.compress_reconstruct

@@ -24,6 +24,11 @@ hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, do
                             double* scratch_planes, double* scratch_smap, double* scratch_chunks, double* out,
                             hipStream_t s);
 hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
+hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
+                           const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
+                           jds_frame_stats* st, uint2* fixlist, unsigned* fixcount, hipStream_t s);
+void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
+size_t fast_q_size();
 hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse, hipStream_t s);
 hipError_t stage_subsample(const double* in, double* tmp, double* tmp2, double* out, int H, int W, int sy,
                            int prefilter, const double* k, hipStream_t s);
@@ -102,6 +107,8 @@ struct jds_plan {
   bool pf = false;
   Geo g{};
   DevBuf fq, gk, part;
+  // fast path: fp32 tables, fix-up lists and counters
+  DevBuf fq32, gk32, fixlist, counters;
 };
 
 // ------------------------------------------------------------- geometry --
@@ -303,7 +310,36 @@ int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n, int64_t H, in
     return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
   }
   free(hq);
+  {
+    const size_t fqs = fast_q_size();
+    char* h32 = (char*)malloc(fqs * (size_t)n);
+    if (!h32) {
+      jds_plan_destroy(p);
+      return fail(JDS_ENOMEM, "host allocation failed");
+    }
+    for (int i = 0; i < n; ++i) {
+      float* f = (float*)(h32 + fqs * i);
+      fast_fwd_thresholds(params[i].qtable, mode, pf, params[i].gauss, f, f + 64);
+    }
+    const float gk32[3] = {(float)params[0].gauss[0], (float)params[0].gauss[1], (float)params[0].gauss[2]};
+    const size_t nblk = (size_t)n * (size_t)(g.cpf / 64);
+    if ((e = p->fq32.ensure(fqs * n)) != hipSuccess || (e = p->gk32.ensure(sizeof gk32)) != hipSuccess ||
+        (e = p->fixlist.ensure(8 * nblk)) != hipSuccess || (e = p->counters.ensure(64)) != hipSuccess ||
+        (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess) {
+      free(h32);
+      jds_plan_destroy(p);
+      return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
+    }
+    free(h32);
+  }
   *out = p;
+  return JDS_OK;
+}
+
+int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
+  if (!p || !counts) return fail(JDS_EINVAL, "null argument");
+  HIP_TRY(hipMemcpy(counts, p->counters.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return JDS_OK;
 }
 
@@ -319,10 +355,23 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (torch's default stream)
   int phases = (flags & JDS_RUN_FWD ? 1 : 0) | (flags & JDS_RUN_INV ? 2 : 0);
   if (!phases) phases = 3;
-  if (phases & 1) HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
-  HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
-                       (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
-                       nullptr, nullptr, 0, s, nullptr, phases));
+  const bool exact = (flags & JDS_RUN_EXACT) != 0;
+  if (phases & 1) {
+    HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
+    HIP_TRY(hipMemsetAsync(p->counters.p, 0, 64, s));
+    if (exact)
+      HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
+                           (const double*)p->gk.p, stats, (double*)p->part.p, false, nullptr, nullptr, nullptr, 0,
+                           s, nullptr, 1));
+    else
+      HIP_TRY(launch_fast_fwd(p->mode, p->pf, p->g, p->n, rgb, coeffs, (const FrameQ*)p->fq.p, p->fq32.p,
+                              (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint2*)p->fixlist.p,
+                              (unsigned*)p->counters.p, s));
+  }
+  if (phases & 2)
+    HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
+                         (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
+                         nullptr, nullptr, 0, s, nullptr, 2));
   return JDS_OK;
 }
 
@@ -333,6 +382,10 @@ void jds_plan_destroy(jds_plan* p) {
   p->fq.release();
   p->gk.release();
   p->part.release();
+  p->fq32.release();
+  p->gk32.release();
+  p->fixlist.release();
+  p->counters.release();
   delete p;
 }
 

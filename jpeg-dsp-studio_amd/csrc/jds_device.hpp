@@ -1,0 +1,56 @@
+// jds_device.hpp — device helpers shared by the codec kernels (exact fp64
+// restatements of the reference's per-sample arithmetic and index maps).
+#pragma once
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace jds {
+
+
+// np.pad(mode='reflect') source index for i >= 0 (engines/block_processor.py:13)
+__device__ __forceinline__ int reflect_pad(int i, int n) {
+  if (i < n) return i;
+  if (n == 1) return 0;
+  const int p = 2 * (n - 1);
+  i %= p;
+  return i >= n ? p - i : i;
+}
+
+// cv2 BORDER_REFLECT_101 for any i (GaussianBlur default border)
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  const int p = 2 * (n - 1);
+  i = i < 0 ? -i : i;
+  i %= p;
+  return i >= n ? p - i : i;
+}
+
+// engines/color_space.py:8-14 — each product rounded, sums left to right
+__device__ __forceinline__ double luma(double R, double G, double B) {
+  return 0.299 * R + 0.587 * G + 0.114 * B;
+}
+__device__ __forceinline__ double chroma_b(double R, double G, double B) {
+  return -0.168736 * R - 0.331264 * G + 0.5 * B + 128.0;
+}
+__device__ __forceinline__ double chroma_r(double R, double G, double B) {
+  return 0.5 * R - 0.418688 * G - 0.081312 * B + 128.0;
+}
+
+__device__ __forceinline__ void unpack(uint32_t v, double& R, double& G, double& B) {
+  R = (double)(v & 255u);
+  G = (double)((v >> 8) & 255u);
+  B = (double)(v >> 16);
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T clampi(T v, T lo, T hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+}  // namespace jds

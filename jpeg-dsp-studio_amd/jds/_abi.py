@@ -23,7 +23,7 @@ LIB_PATH = os.path.join(_HERE, 'libjds.so')
 JDS_OK, JDS_EINVAL, JDS_ENOTSUP, JDS_EHIP, JDS_ENOMEM = 0, -1, -2, -3, -4
 SS_444, SS_422, SS_420 = 0, 1, 2
 MODE_CODES = {'4:4:4': SS_444, '4:2:2': SS_422, '4:2:0': SS_420}
-RUN_SSE, RUN_FWD, RUN_INV = 1, 2, 4
+RUN_SSE, RUN_FWD, RUN_INV, RUN_EXACT = 1, 2, 4, 8
 
 
 class Params(C.Structure):
@@ -77,6 +77,7 @@ _SIGS = {
     'jds_plan_create': (C.c_int, [_P, C.POINTER(Params), C.c_int, C.c_int64, C.c_int64, C.POINTER(_P)]),
     'jds_plan_run': (C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
     'jds_plan_geometry': (C.c_int, [_P, C.POINTER(Geometry)]),
+    'jds_plan_fix_counts': (C.c_int, [_P, _P]),
     'jds_plan_destroy': (None, [_P]),
     'jds_compress_reconstruct': (C.c_int, [_P, C.POINTER(Params), _P, C.c_int64, C.c_int64, _P, _P,
                                            C.POINTER(FrameStats), _P, _P, C.c_int32, C.c_int32,
@@ -226,6 +227,12 @@ class Plan:
         if stream is None:
             stream = lib().jds_ctx_stream(self.ctx.handle)
         check(lib().jds_plan_run(self.handle, rgb_dev, out_dev, coeffs_dev, stats_dev, flags, stream))
+
+    def fix_counts(self):
+        """[forward blocks, inverse pixels] sent to the exact fp64 fix-up by the last run."""
+        c = np.zeros(2, np.uint32)
+        check(lib().jds_plan_fix_counts(self.handle, c.ctypes.data))
+        return c
 
     def close(self):
         if self.handle:

@@ -157,3 +157,55 @@ def test_4k_420_full_size_bit_exact():
     ref = cpu_ref.compress_reconstruct(img, 50, 8, '4:2:0', False, metrics=False)
     assert np.array_equal(inter.all_quantized_coeffs, ref['coeffs'])
     assert np.array_equal(res.reconstructed_image, ref['reconstructed'])
+
+
+def _plan_run(frames, qs, mode, pf, flags):
+    import torch
+    from jds import _abi, codec
+    H, W = frames.shape[1:3]
+    params = [_abi.make_params(q, cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q), mode, pf,
+                               codec.gaussian_kernel3()) for q in qs]
+    plan = _abi.Plan(_abi.context(0), params, H, W)
+    dev = torch.device('cuda:0')
+    rgb = torch.from_numpy(np.ascontiguousarray(frames)).to(dev)
+    out = torch.empty_like(rgb)
+    cf = torch.empty((len(qs), plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+    st = torch.zeros((len(qs), _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), flags, 0)
+    torch.cuda.synchronize()
+    fix = plan.fix_counts()
+    plan.close()
+    return out.cpu().numpy(), cf.cpu().numpy(), st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(-1), fix
+
+
+@pytest.mark.parametrize('h,w,mode,pf', [(1080, 1920, '4:2:0', True), (720, 1280, '4:2:2', True),
+                                          (256, 384, '4:4:4', False), (130, 98, '4:2:0', False),
+                                          (64, 48, '4:2:2', False)])
+def test_fast_path_equals_exact_path_and_oracle(h, w, mode, pf):
+    """Certified fp32 + fp64 fix-up (default) == all-fp64 kernels == oracle, bit for bit."""
+    from jds import _abi
+    qs = [5, 50, 95, 100]
+    frames = np.stack([cpu_ref.random_image(h, w, 300 + i) for i in range(len(qs))])
+    o_fast, c_fast, s_fast, fix = _plan_run(frames, qs, mode, pf, _abi.RUN_SSE)
+    o_ex, c_ex, s_ex, _ = _plan_run(frames, qs, mode, pf, _abi.RUN_SSE | _abi.RUN_EXACT)
+    assert np.array_equal(c_fast, c_ex)
+    assert np.array_equal(o_fast, o_ex)
+    for f in ('nonzero', 'magnitude_bits', 'hist', 'sse_rgb', 'total_coeffs'):
+        assert np.array_equal(s_fast[f], s_ex[f]), f
+    ref = cpu_ref.compress_reconstruct(frames[1], 50, 8, mode, pf, metrics=False)
+    assert np.array_equal(c_fast[1], ref['coeffs'])
+    assert fix[0] < 0.05 * len(qs) * c_fast.shape[1] / 64  # fix-up stays rare on random data
+
+
+def test_fast_path_resolves_exact_ties_through_fixup():
+    """Flat planes put DC/Q exactly on k + 1/2 (pocketfft's rounding decides): every
+    such block must go through the fp64 fix-up and match the reference."""
+    from jds import _abi
+    frames = np.stack([np.full((32, 48, 3), v, np.uint8) for v in (127, 129, 131, 133)])
+    qs = [50] * 4
+    o, c, s, fix = _plan_run(frames, qs, '4:2:0', True, 0)
+    assert fix[0] > 0
+    for i, v in enumerate((127, 129, 131, 133)):
+        g = golden()[f'flat{v}_q50_420_pf']
+        assert sha(c[i]) == g['sha_coeffs'] and sha(o[i]) == g['sha_recon']
