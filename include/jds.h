@@ -69,7 +69,8 @@ typedef struct {
   double fwd_ms, inv_ms;        /* host path only: forward / inverse kernel time (hipEvents) */
   double ssim[4];               /* host path only: SSIM of R, G, B and of Y (utils/metrics.py:12-21) */
   double mse_y;                 /* host path only: NumPy-order mean of (Y(orig) - Y(rec))^2 */
-  uint64_t reserved[2];
+  double magnitude_bits_f32;    /* host path only: magnitude_bits as NumPy's float32 np.sum yields it */
+  uint64_t reserved[1];
 } jds_frame_stats;
 
 typedef struct {

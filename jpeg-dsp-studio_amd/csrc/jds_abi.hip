@@ -24,6 +24,8 @@ hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, do
                             double* scratch_planes, double* scratch_smap, double* scratch_chunks, double* out,
                             hipStream_t s);
 hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
+hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* chunk_sum, int max_chunks,
+                          double* out, hipStream_t s);
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
                            jds_frame_stats* st, uint2* fixlist, unsigned* fixcount, hipStream_t s);
@@ -88,6 +90,7 @@ struct jds_ctx {
   DevBuf rgb, out, coeffs, stats, part, fq, gk, erry, errrgb, sel;
   DevBuf ss_planes, ss_map, ss_chunks, ss_out, img_a, img_b;
   DevBuf st[5];  // per-stage API staging
+  DevBuf chunks;
 };
 
 // SSIM scratch in the context; returns the device pointer of 5 result doubles
@@ -259,6 +262,7 @@ void jds_ctx_destroy(jds_ctx* c) {
                     &c->errrgb,  &c->sel,    &c->ss_planes, &c->ss_map, &c->ss_chunks, &c->ss_out, &c->img_a, &c->img_b};
   for (DevBuf* b : bufs) b->release();
   for (DevBuf& b : c->st) b.release();
+  c->chunks.release();
   for (hipEvent_t e : c->ev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -444,6 +448,14 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
   if (maps) {
     HIP_TRY(hipMemcpyAsync(error_map_y, c->erry.p, npx * sizeof(double), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(error_map_rgb, c->errrgb.p, npx * sizeof(double), hipMemcpyDeviceToHost, s));
+  }
+  {
+    // NumPy float32 magnitude_bits (utils/metrics.py:77-78)
+    const long long nblk = g.cpf / 64;
+    const int max_chunks = (int)((g.cpf + 8191) / 8192) + 1;
+    HIP_TRY(c->chunks.ensure(sizeof(unsigned) * (size_t)max_chunks));
+    HIP_TRY(launch_mag_f32((const int16_t*)c->coeffs.p, nblk, (unsigned*)c->chunks.p, max_chunks,
+                           &((jds_frame_stats*)c->stats.p)->magnitude_bits_f32, s));
   }
   if (H >= 7 && W >= 7) {
     jds_frame_stats* dst = (jds_frame_stats*)c->stats.p;

@@ -245,6 +245,64 @@ hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsign
   return hipGetLastError();
 }
 
+// utils/metrics.py:77-78 — magnitude_bits = np.sum(np.ceil(np.log2(|nz| + 1)) + 1)
+// over the nonzero coefficients in all_quantized_coeffs order, a float32
+// reduction: NumPy sums 8192-element buffers (exact here: terms are integers
+// <= 12, so a buffer sum < 2^24) and accumulates the buffer sums in float32.
+// One workgroup walks the blocks in order, ranking nonzeros with a block scan.
+__global__ void __launch_bounds__(1024)
+k_mag_f32(const int16_t* __restrict__ coeffs, long long nblocks, unsigned* __restrict__ chunk_sum,
+          int max_chunks, double* __restrict__ out) {
+  __shared__ unsigned s_scan[1024];
+  __shared__ unsigned long long s_base;
+  const int t = threadIdx.x;
+  if (t == 0) s_base = 0;
+  __syncthreads();
+  for (long long b0 = 0; b0 < nblocks; b0 += 1024) {
+    const long long b = b0 + t;
+    unsigned cnt = 0;
+    if (b < nblocks)
+      for (int i = 0; i < 64; ++i) cnt += coeffs[b * 64 + i] != 0;
+    s_scan[t] = cnt;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+      const unsigned v = t >= o ? s_scan[t - o] : 0u;
+      __syncthreads();
+      s_scan[t] += v;
+      __syncthreads();
+    }
+    unsigned long long rank = s_base + s_scan[t] - cnt;
+    if (b < nblocks) {
+      for (int i = 0; i < 64; ++i) {
+        const int q = coeffs[b * 64 + i];
+        if (q) {
+          const int m = q < 0 ? -q : q;
+          const long long ch = (long long)(rank >> 13);
+          if (ch < max_chunks) atomicAdd(&chunk_sum[ch], (unsigned)(33 - __clz(m)));
+          ++rank;
+        }
+      }
+    }
+    __syncthreads();
+    if (t == 1023) s_base += s_scan[1023];
+    __syncthreads();
+  }
+  if (t == 0) {
+    const long long nch = (long long)((s_base + 8191) >> 13);
+    float acc = 0.0f;
+    for (long long k = 0; k < nch && k < max_chunks; ++k) acc = acc + (float)chunk_sum[k];
+    *out = (double)acc;
+  }
+}
+
+hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* chunk_sum, int max_chunks,
+                          double* out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(chunk_sum, 0, sizeof(unsigned) * (size_t)max_chunks, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_mag_f32, dim3(1), dim3(1024), 0, s, coeffs, nblocks, chunk_sum, max_chunks, out);
+  return hipGetLastError();
+}
+
 // ssim_out[0..3] = SSIM of R, G, B, Y; ssim_out[4] = MSE of Y (for PSNR-Y)
 hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, double c1, double c2,
                             double* scratch_planes /*5*H*W*/, double* scratch_smap /*(H-6)*(W-6)*/,

@@ -44,7 +44,7 @@ def compress_reconstruct(
             "to the axis number corresponding to the channels.")
 
     ssim = np.ctypeslib.as_array(st.ssim).copy()
-    bitrate = bitrate_from_counts(st.nonzero, st.magnitude_bits, st.total_coeffs, (h, w),
+    bitrate = bitrate_from_counts(st.nonzero, st.magnitude_bits_f32, st.total_coeffs, (h, w),
                                   params.block_size)                        # pipeline.py:100
     result = CompressionResult(
         original_image=image_rgb,

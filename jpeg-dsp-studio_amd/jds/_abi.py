@@ -36,14 +36,15 @@ class FrameStats(C.Structure):
                 ('block_overhead_bits', C.c_uint64), ('hist', C.c_uint64 * 50), ('sse_rgb', C.c_uint64),
                 ('sse_y', C.c_double), ('pixels', C.c_uint64), ('fwd_ms', C.c_double),
                 ('inv_ms', C.c_double), ('ssim', C.c_double * 4), ('mse_y', C.c_double),
-                ('reserved', C.c_uint64 * 2)]
+                ('magnitude_bits_f32', C.c_double), ('reserved', C.c_uint64 * 1)]
 
 
 # the same record as a NumPy dtype, for stats arrays that live in device memory
 STATS_DTYPE = np.dtype([('nonzero', '<u8'), ('total_coeffs', '<u8'), ('magnitude_bits', '<u8'),
                         ('block_overhead_bits', '<u8'), ('hist', '<u8', (50,)), ('sse_rgb', '<u8'),
                         ('sse_y', '<f8'), ('pixels', '<u8'), ('fwd_ms', '<f8'), ('inv_ms', '<f8'),
-                        ('ssim', '<f8', (4,)), ('mse_y', '<f8'), ('reserved', '<u8', (2,))])
+                        ('ssim', '<f8', (4,)), ('mse_y', '<f8'), ('magnitude_bits_f32', '<f8'),
+                        ('reserved', '<u8', (1,))])
 assert STATS_DTYPE.itemsize == C.sizeof(FrameStats)
 
 

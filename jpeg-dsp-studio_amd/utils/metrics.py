@@ -50,15 +50,15 @@ class Timer:
         return result
 
 
-def bitrate_from_counts(nonzero: int, magnitude_bits: int, total_coeffs: int, original_shape: tuple,
+def bitrate_from_counts(nonzero: int, magnitude_bits, total_coeffs: int, original_shape: tuple,
                         block_size: int = 8) -> Dict:
-    """The tail of estimate_bitrate_no_entropy (utils/metrics.py:62-92) from exact counts.
+    """The tail of estimate_bitrate_no_entropy (utils/metrics.py:62-92) from counts.
 
-    The reference sums ceil(log2(|q|+1)) + 1 as float32 (np.log2 of int16);
-    each term is a small integer, so the float32 pairwise sum equals
-    np.float32(exact) while it stays below 2**24.  Evaluating the same
-    expression with that scalar reproduces the reference's NumPy-version-
-    dependent promotion (float32 under NumPy >= 2, float64 under 1.x)."""
+    The reference sums ceil(log2(|q|+1)) + 1 as float32 (np.log2 of int16):
+    `magnitude_bits` is that float32 sum (the GPU reproduces NumPy's buffered
+    float32 reduction; below 2**24 it equals the exact integer).  Evaluating
+    the reference's expression with that np.float32 scalar reproduces its
+    NumPy-version-dependent promotion (float32 under NumPy >= 2, float64 under 1.x)."""
     h, w = original_shape
     num_pixels = h * w
     original_bits = num_pixels * 3 * 8

@@ -9,7 +9,7 @@ ok() { case "$1" in 0|1) return 0;; *) echo "stopping: rc=$1"; exit "$1";; esac;
 STAGE="${1:-all}"
 
 if [ "$STAGE" = all ] || [ "$STAGE" = tests ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest-gpu rc=$rc"; tail -5 gpurun_out/pytest_gpu.log; ok $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
   rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; ok $rc
