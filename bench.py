@@ -129,7 +129,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    t_fwd = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    t_fwd = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps  # k_fwd32 + its exact fix-up
     t_inv = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -178,6 +178,7 @@ def main():
                      'algorithmic_bytes_per_launch': bytes_fwd if dom == 'k_fwd' else bytes_inv,
                      'avg_launch_ms': round(t_dom, 4)},
         'kernels_ms': {'k_fwd': round(t_fwd, 4), 'k_inv': round(t_inv, 4)},
+        'fixups_last_step': dict(zip(('fwd_blocks', 'inv_pixels'), [int(v) for v in plan.fix_counts()])),
         'pipeline_roofline_frac': round(value / world * 1e6 * (6 + 2 * S) / (HBM_PEAK_GBS * 1e9), 4),
     }
 
