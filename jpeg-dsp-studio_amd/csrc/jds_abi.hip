@@ -375,7 +375,7 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
-                         nullptr, nullptr, 0, s, nullptr, 2));
+                         nullptr, nullptr, 0, s, nullptr, exact ? 6 : 2));
   return JDS_OK;
 }
 

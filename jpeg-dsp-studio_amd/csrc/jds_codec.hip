@@ -573,7 +573,15 @@ static hipError_t launch_inv_t(const Geo& g, int n, const int16_t* coeffs, const
   return hipGetLastError();
 }
 
-// phases: bit 0 = forward (k_fwd), bit 1 = inverse (k_inv + finalize)
+int inv_tiles(int mode, int H, int W);
+hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
+                       const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y,
+                       double* err_rgb, hipStream_t s);
+hipError_t launch_sel_recon(const int16_t* coeffs, const FrameQ* fq, jds_selected_block* sel, int sel_blk,
+                            hipStream_t s);
+
+// phases: bit 0 = forward (k_fwd), bit 1 = inverse (k_inv2 + finalize),
+//         bit 2 = use the original one-block-ring k_inv for the inverse
 hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                         int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
                         double* part, bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel,
@@ -598,7 +606,11 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
     if (e != hipSuccess || (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess)) return e;
   }
   if (phases & 2) {
-    switch (mode) {
+    int tiles = g.tiles_y * g.tiles_x;
+    if (!(phases & 4)) {  // jds_inv.hip (default); bit 2 selects the original k_inv
+      e = launch_inv2(mode, g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, s);
+      tiles = inv_tiles(mode, g.H, g.W);
+    } else switch (mode) {
       case M420:
         e = launch_inv_t<M420>(g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, sel, sel_blk, s);
         break;
@@ -613,8 +625,9 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
     if (sel) {
       hipLaunchKernelGGL(k_sel_dequant, dim3(1), dim3(64), 0, s, coeffs, fq, sel, sel_blk);
       if ((e = hipGetLastError()) != hipSuccess) return e;
+      if (!(phases & 4) && (e = launch_sel_recon(coeffs, fq, sel, sel_blk, s)) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, g.tiles_y * g.tiles_x,
+    hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, tiles,
                        (int)(rin != nullptr));
     e = hipGetLastError();
   }

@@ -1,0 +1,393 @@
+// jds_inv.hip — the inverse half of the codec path on gfx950:
+// int16 coefficients -> dequantize -> 2-D IDCT -> clip -> chroma upsample ->
+// YCbCr->RGB -> clip -> truncate -> uint8 RGB.  Reference:
+// engines/pipeline.py:77-95 (dequantize, idct_2d, merge_blocks, upsample_chroma,
+// ycbcr_to_rgb, clip/astype) with quantizer.py:27-29, dct_engine.py:17-27,
+// color_space.py:17-24 and :63-65.  Every operation is fp64 in the
+// reference's order (pocketfft DCT-III butterflies, cv2 INTER_LINEAR taps,
+// NumPy colour expressions), FP contraction off: bytes are bit-identical.
+//
+// Work decomposition (one workgroup per TH x TW pixel tile, tiles laid from the
+// top-left corner):
+//   1. chroma, one plane at a time: the tile's chroma blocks plus the ring the
+//      bilinear upsample reaches into.  Column (axis-0) passes run one thread
+//      per block column, straight from the int16 coefficients in HBM/L2 into
+//      an fp64 transpose buffer; row (axis-1) passes run only for the block
+//      rows the window needs (a top/bottom ring block contributes one row), and
+//      land in an fp64 LDS chroma window.
+//   2. luma, NT/8 blocks per round: the same column pass, then each thread
+//      owns one 8-pixel block row: row IDCT -> Y in registers, chroma taps from
+//      the LDS window, colour, clip, truncate, one 24-byte store.
+// Y never goes through LDS.  The upsample shares products between
+// neighbouring pixels (same IEEE operations, same results).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "jds_dct8.hpp"
+#include "jds_device.hpp"
+#include "jds_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace jds {
+
+template <int MODE>
+struct Inv {
+  static constexpr int SY = Cfg<MODE>::SY, SX = Cfg<MODE>::SX;
+  static constexpr int TH = (MODE == M420) ? 64 : 32;
+  static constexpr int TW = (MODE == M444) ? 64 : 128;
+  static constexpr int NT = (MODE == M444) ? 256 : 512;
+  static constexpr int RY = (SY == 2) ? 1 : 0, RX = (SX == 2) ? 1 : 0;
+  static constexpr int YBC = TW / 8, NYB = (TH / 8) * YBC;
+  static constexpr int RB = NT / 8;                                        // luma blocks per round
+  static constexpr int CBR = TH / (8 * SY) + 2 * RY, CBC = TW / (8 * SX) + 2 * RX;  // chroma blocks incl. ring
+  static constexpr int NCB = CBR * CBC;                                    // per plane
+  static constexpr int CWR = TH / SY + 2 * RY, CWC = TW / SX + 2 * RX;     // chroma sample window
+  static constexpr int NROW = (CBR - 2 * RY) * CBC * 8 + 2 * RY * CBC;     // chroma row tasks per plane
+  static constexpr int MB = NCB > RB ? NCB : RB;                           // transpose-buffer blocks
+  static constexpr int WPE = (MODE == M444) ? 3 : 4;                       // 2 or 3 workgroups per CU
+  static_assert(NCB * 8 <= NT && NROW <= NT && NYB % RB == 0, "one round per chroma plane");
+};
+
+constexpr int MS = 72;  // doubles per block in the transpose buffer (64 + 8: conflict-free column writes)
+
+// Dequantize (quantizer.py:27-29) and IDCT column v of a block (axis 0 first,
+// dct_engine.py:12-14) into dst[r*8 + v].
+__device__ __forceinline__ void idct_col(const int16_t* __restrict__ blk, const double* __restrict__ q, int v,
+                                         double* __restrict__ dst) {
+  double c[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) c[r] = (double)blk[r * 8 + v] * q[r * 8 + v];
+  dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) dst[r * 8 + v] = c[r];
+}
+
+// Row u of a column-transformed block: axis-1 IDCT, fct 1/16, +128, clip
+// (dct_engine.py:23-27).
+__device__ __forceinline__ void idct_row(const double* __restrict__ src, int u, double (&c)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c[k] = src[u * 8 + k];
+  dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const double s = c[k] * 0.0625 + 128.0;
+    c[k] = fmin(fmax(s, 0.0), 255.0);
+  }
+}
+
+// One plane's upsampled chroma at 8 consecutive pixels of one output row (cv2
+// INTER_LINEAR, color_space.py:63-65; or the co-sited sample without
+// subsampling): horizontal taps on chroma rows wr0 (and wr1), then the
+// vertical blend.  Horizontal subsampling implies an even width (the C-ABI
+// rejects odd ones), so the scale is exactly 1/2: pixel 2m reads
+// (s[m-1], s[m]) with weights (1/4, 3/4) and pixel 2m+1 reads (s[m], s[m+1])
+// with (3/4, 1/4), so each product serves two pixels.
+template <int MODE>
+__device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo& g, int x0, int cwx0, int wr0,
+                                        int wr1, double b0, double b1, double (&C)[8]) {
+  using I = Inv<MODE>;
+  if constexpr (I::SX == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) C[k] = cw[wr0 * I::CWC + x0 + k - cwx0];
+  } else {
+    const int c0 = x0 / 2 - 1 - cwx0;
+    double h0[8];
+#pragma unroll
+    for (int rr = 0; rr < (I::SY == 2 ? 2 : 1); ++rr) {
+      const double* s = &cw[(rr ? wr1 : wr0) * I::CWC + c0];
+      double q25[6], q75[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        q25[j] = s[j] * 0.25;
+        q75[j] = s[j] * 0.75;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double e = q25[i] + q75[i + 1], o = q75[i + 1] + q25[i + 2];
+        if (rr == 0) {
+          h0[2 * i] = e;
+          h0[2 * i + 1] = o;
+        } else {
+          C[2 * i] = h0[2 * i] * b0 + e * b1;
+          C[2 * i + 1] = h0[2 * i + 1] * b0 + o * b1;
+        }
+      }
+    }
+    if constexpr (I::SY == 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) C[k] = h0[k];
+    }
+    // cv2's clamped taps at the two edge pixels: x = 0 has sx = -1 -> (s[0], 1.0,
+    // s[1], 0.0) and x = W-1 has sx = wc-1 -> copy; both equal s[edge] exactly
+    // (samples are finite and >= 0)
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int kl = side == 0 ? (x0 == 0 ? 0 : -1) : (g.W - 1 - x0 < 8 ? g.W - 1 - x0 : -1);
+      if (kl >= 0) {
+        const int e = (side == 0 ? 0 : g.wc - 1) - cwx0;
+        const double v0 = cw[wr0 * I::CWC + e];
+        double v = v0;
+        if constexpr (I::SY == 2) v = v0 * b0 + cw[wr1 * I::CWC + e] * b1;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k == kl) C[k] = v;
+      }
+    }
+  }
+}
+
+// XTRA: 0 = RGB only, 1 = + exact integer SSE and luma SSE partials,
+//       2 = + IntermediateData error maps (pipeline.py:117-122)
+template <int MODE, int XTRA>
+__global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(Inv<MODE>::WPE)))
+k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+       const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
+       double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb) {
+  using I = Inv<MODE>;
+  __shared__ __attribute__((aligned(16))) double s_mid[I::MB * MS];
+  __shared__ __attribute__((aligned(16))) double s_cw[2][I::CWR * I::CWC];
+  __shared__ double s_q[64];
+  __shared__ double s_red[I::NT / 64];
+  __shared__ unsigned long long s_sse;
+
+  const int tid = threadIdx.x, lv = tid & 7, lb = tid >> 3;
+  const int frame = blockIdx.y, tile = blockIdx.x;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int Y0 = ty * I::TH, X0 = tx * I::TW;
+  const int16_t* cf = coeffs + (size_t)frame * g.cpf;
+  if (tid < 64) s_q[tid] = fq[frame].q[tid];
+  if (XTRA && tid == 0) s_sse = 0ull;
+  __syncthreads();
+
+  // ---- 1. chroma window ----------------------------------------------------
+  const int cby0 = Y0 / (8 * I::SY) - I::RY, cbx0 = X0 / (8 * I::SX) - I::RX;
+  const int cwy0 = Y0 / I::SY - I::RY, cwx0 = X0 / I::SX - I::RX;
+#pragma unroll 1
+  for (int p = 0; p < 2; ++p) {
+    const int16_t* cp = cf + (p == 0 ? g.off_cb : g.off_cr);
+    if (tid < I::NCB * 8) {
+      const int i = lb / I::CBC, j = lb - i * I::CBC;
+      const int by = cby0 + i, bx = cbx0 + j;
+      if (by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx)
+        idct_col(cp + ((long long)by * g.ncx + bx) * 64, s_q, lv, s_mid + lb * MS);
+    }
+    __syncthreads();
+    if (tid < I::NROW) {
+      int i, j, u;
+      constexpr int FULL = (I::CBR - 2 * I::RY) * I::CBC * 8;
+      if (tid < FULL) {
+        i = I::RY + tid / (I::CBC * 8);
+        const int rem = tid - (i - I::RY) * (I::CBC * 8);
+        j = rem >> 3;
+        u = rem & 7;
+      } else {  // top ring contributes its last row, bottom ring its first
+        const int e = tid - FULL;
+        const bool top = e < I::CBC;
+        i = top ? 0 : I::CBR - 1;
+        j = top ? e : e - I::CBC;
+        u = top ? 7 : 0;
+      }
+      const int by = cby0 + i, bx = cbx0 + j;
+      if (by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx) {
+        double c[8];
+        idct_row(s_mid + (i * I::CBC + j) * MS, u, c);
+        double* w = &s_cw[p][(by * 8 + u - cwy0) * I::CWC];
+        const int wc0 = bx * 8 - cwx0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k];
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- 2. luma rounds: IDCT, upsample, colour, store --------------------------
+  const bool want_in = XTRA > 0;
+  unsigned long long sse = 0ull;
+  double ssy = 0.0;
+  const uint8_t* in_f = want_in ? rgb_in + (size_t)frame * g.H * g.W * 3 : nullptr;
+  uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
+#pragma unroll 1
+  for (int r = 0; r < I::NYB / I::RB; ++r) {
+    const int blk = r * I::RB + lb;
+    const int bi = blk / I::YBC, bj = blk - bi * I::YBC;
+    const int by = Y0 / 8 + bi, bx = X0 / 8 + bj;
+    const bool bvalid = by < g.nby && bx < g.nbx;
+    if (bvalid) idct_col(cf + ((long long)by * g.nbx + bx) * 64, s_q, lv, s_mid + lb * MS);
+    __syncthreads();
+    const int y = by * 8 + lv, x0 = bx * 8;
+    if (bvalid && y < g.H && x0 < g.W) {
+      double Yv[8];
+      idct_row(s_mid + lb * MS, lv, Yv);
+      // chroma rows (cv2 INTER_LINEAR: rows clamped, weights kept)
+      int wr0, wr1 = 0;
+      double b0 = 1.0, b1 = 0.0;
+      if constexpr (I::SY == 2) {
+        float fy = (float)((y + 0.5) * g.up_sy - 0.5);
+        const int sy = (int)floorf(fy);
+        fy -= (float)sy;
+        b0 = (double)(1.f - fy);
+        b1 = (double)fy;
+        wr0 = clampi(clampi(sy, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+        wr1 = clampi(clampi(sy + 1, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+      } else {
+        wr0 = y - cwy0;
+      }
+      // color_space.py:17-24 in NumPy's order, one chroma plane at a time to
+      // bound register pressure: B and G's Cb term first, then R and G.
+      uint32_t pk[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+      double Rc[8], Gc[8], Bc[8];
+      {
+        // one chroma plane at a time to bound register pressure: B and G's Cb
+        // term first, then R and G (same expressions, same order)
+        double C[8], Gt[8];
+        chroma8<MODE>(s_cw[0], g, x0, cwx0, wr0, wr1, b0, b1, C);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const double B = fmin(fmax(Yv[k] + 1.772 * (C[k] - 128.0), 0.0), 255.0);
+          Gt[k] = Yv[k] - 0.344136 * (C[k] - 128.0);
+          Bc[k] = B;
+          const int b = 3 * k + 2;
+          pk[b >> 2] |= (uint32_t)(int)B << (8 * (b & 3));
+        }
+        chroma8<MODE>(s_cw[1], g, x0, cwx0, wr0, wr1, b0, b1, C);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const double R = fmin(fmax(Yv[k] + 1.402 * (C[k] - 128.0), 0.0), 255.0);
+          const double G = fmin(fmax(Gt[k] - 0.714136 * (C[k] - 128.0), 0.0), 255.0);
+          Rc[k] = R;
+          Gc[k] = G;
+          const int b = 3 * k;
+          pk[b >> 2] |= (uint32_t)(int)R << (8 * (b & 3));
+          pk[(b + 1) >> 2] |= (uint32_t)(int)G << (8 * ((b + 1) & 3));
+        }
+      }
+      const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
+      uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
+      if (nx == 8 && ((((uintptr_t)o) & 7u) == 0)) {
+        uint2* o2 = reinterpret_cast<uint2*>(o);
+        o2[0] = make_uint2(pk[0], pk[1]);
+        o2[1] = make_uint2(pk[2], pk[3]);
+        o2[2] = make_uint2(pk[4], pk[5]);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 24; ++b)
+          if (b < 3 * nx) o[b] = (uint8_t)(pk[b >> 2] >> (8 * (b & 3)));
+      }
+      if constexpr (XTRA > 0) {
+        const uint8_t* src = in_f + ((size_t)y * g.W + x0) * 3;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (k < nx) {
+            const int o0 = src[3 * k], o1 = src[3 * k + 1], o2 = src[3 * k + 2];
+            const int b = 3 * k;
+            const int ur = (pk[b >> 2] >> (8 * (b & 3))) & 255, ug = (pk[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 255,
+                      ub = (pk[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 255;
+            const int d0 = o0 - ur, d1 = o1 - ug, d2 = o2 - ub;
+            sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
+            const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
+            const double yo = luma(R0, G0, B0);
+            const double yr = luma((double)ur, (double)ug, (double)ub);
+            const double dy = yo - yr;
+            ssy = ssy + dy * dy;
+            if constexpr (XTRA > 1) {
+              const size_t pix = (size_t)y * g.W + x0 + k;
+              err_y[pix] = fabs(yo - Yv[k]);                                                    // pipeline.py:120
+              err_rgb[pix] = ((fabs(R0 - Rc[k]) + fabs(G0 - Gc[k])) + fabs(B0 - Bc[k])) / 3.0;  // pipeline.py:121
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  if constexpr (XTRA > 0) {
+    unsigned long long s = sse;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((tid & 63) == 0) atomicAdd(&s_sse, s);
+    double d = ssy;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d = d + __shfl_xor(d, o, 64);
+    if ((tid & 63) == 0) s_red[tid >> 6] = d;
+    __syncthreads();
+    if (tid == 0) {
+      double a = 0.0;
+      for (int i = 0; i < I::NT / 64; ++i) a = a + s_red[i];
+      sse_y_part[(size_t)frame * gridDim.x + tile] = a;
+      atomicAdd((unsigned long long*)&st[frame].sse_rgb, s_sse);
+    }
+  }
+}
+
+// IntermediateData.selected_block_reconstructed (pipeline.py:132-138): the
+// clipped luma IDCT of one block (frame 0).
+__global__ void __launch_bounds__(64) k_sel_recon(const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+                                                  jds_selected_block* sel, int sel_blk) {
+  __shared__ __attribute__((aligned(16))) double s[MS];
+  const int t = threadIdx.x;
+  if (t < 8) {
+    idct_col(coeffs + (long long)sel_blk * 64, fq[0].q, t, s);
+  }
+  __syncthreads();
+  if (t < 8) {
+    double c[8];
+    idct_row(s, t, c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sel->reconstructed[t * 8 + k] = c[k];
+  }
+}
+
+// ------------------------------------------------------------ launchers --
+
+template <int MODE>
+static int inv_tiles_t(int H, int W, int* tx) {
+  const int ty = (H + Inv<MODE>::TH - 1) / Inv<MODE>::TH;
+  *tx = (W + Inv<MODE>::TW - 1) / Inv<MODE>::TW;
+  return ty * *tx;
+}
+
+int inv_tiles(int mode, int H, int W) {
+  int tx;
+  return mode == M420 ? inv_tiles_t<M420>(H, W, &tx)
+                      : (mode == M422 ? inv_tiles_t<M422>(H, W, &tx) : inv_tiles_t<M444>(H, W, &tx));
+}
+
+template <int MODE>
+static hipError_t inv2_t(const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq, const uint8_t* rgb_in,
+                         uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y, double* err_rgb,
+                         hipStream_t s) {
+  int tx;
+  const int tiles = inv_tiles_t<MODE>(g.H, g.W, &tx);
+  const dim3 grid(tiles, n), blk(Inv<MODE>::NT);
+  if (err_y)
+    hipLaunchKernelGGL((k_inv2<MODE, 2>), grid, blk, 0, s, g, tx, coeffs, fq, rgb_in, rgb_out, st, part, err_y,
+                       err_rgb);
+  else if (rgb_in)
+    hipLaunchKernelGGL((k_inv2<MODE, 1>), grid, blk, 0, s, g, tx, coeffs, fq, rgb_in, rgb_out, st, part, nullptr,
+                       nullptr);
+  else
+    hipLaunchKernelGGL((k_inv2<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, nullptr,
+                       nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
+                       const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y,
+                       double* err_rgb, hipStream_t s) {
+  switch (mode) {
+    case M420: return inv2_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s);
+    case M422: return inv2_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s);
+    default: return inv2_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s);
+  }
+}
+
+hipError_t launch_sel_recon(const int16_t* coeffs, const FrameQ* fq, jds_selected_block* sel, int sel_blk,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(k_sel_recon, dim3(1), dim3(64), 0, s, coeffs, fq, sel, sel_blk);
+  return hipGetLastError();
+}
+
+}  // namespace jds
