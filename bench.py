@@ -167,7 +167,7 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'f64',
+        'dtype': 'f32+f64',  # forward: fp32 certified + fp64 fix-up; inverse: fp64 (u8 in/out, int16 coefficients)
         'data': 'synthetic (uniform random RGB generated on device)',
         'config': {'workload': f'{W}x{H} RGB, Q={args.quality}, {args.mode}, prefilter={"on" if args.prefilter else "off"} '
                                f'(BASELINE configs[1])',

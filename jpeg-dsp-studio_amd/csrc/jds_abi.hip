@@ -28,7 +28,7 @@ hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* ch
                           double* out, hipStream_t s);
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
-                           jds_frame_stats* st, uint2* fixlist, unsigned* fixcount, hipStream_t s);
+                           jds_frame_stats* st, uint2* fixlist, unsigned* fixcount, hipStream_t s, const Side* side);
 void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
 size_t fast_q_size();
 hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse, hipStream_t s);
@@ -112,6 +112,7 @@ struct jds_plan {
   DevBuf fq, gk, part;
   // fast path: fp32 tables, fix-up lists and counters
   DevBuf fq32, gk32, fixlist, counters;
+  Side side;  // border tiles run beside interior tiles
 };
 
 // ------------------------------------------------------------- geometry --
@@ -337,6 +338,12 @@ int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n, int64_t H, in
     }
     free(h32);
   }
+  if ((e = hipStreamCreateWithFlags(&p->side.stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&p->side.fork, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&p->side.join, hipEventDisableTiming)) != hipSuccess) {
+    jds_plan_destroy(p);
+    return fail(JDS_EHIP, "plan stream: %s", hipGetErrorString(e));
+  }
   *out = p;
   return JDS_OK;
 }
@@ -370,7 +377,7 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
     else
       HIP_TRY(launch_fast_fwd(p->mode, p->pf, p->g, p->n, rgb, coeffs, (const FrameQ*)p->fq.p, p->fq32.p,
                               (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint2*)p->fixlist.p,
-                              (unsigned*)p->counters.p, s));
+                              (unsigned*)p->counters.p, s, &p->side));
   }
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
@@ -390,6 +397,9 @@ void jds_plan_destroy(jds_plan* p) {
   p->gk32.release();
   p->fixlist.release();
   p->counters.release();
+  if (p->side.stream) (void)hipStreamDestroy(p->side.stream);
+  if (p->side.fork) (void)hipEventDestroy(p->side.fork);
+  if (p->side.join) (void)hipEventDestroy(p->side.join);
   delete p;
 }
 

@@ -78,170 +78,319 @@ struct FastQ {
 
 constexpr int BS32 = 68;  // floats per 8x8 block in LDS
 
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[6], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255u; }
+
+// LDS carve-up (in floats).  General tiles stage the packed RGB window (+ the
+// fp32 chroma planes of the window with the prefilter); interior tiles stage
+// fp32 planes only.  The block transpose buffer aliases the planes.
 template <int MODE, bool PF>
+struct FwdLds {
+  using C = Cfg<MODE>;
+  static constexpr int WR = C::TH + 2, WC = C::TW + 2, WN = WR * WC;
+  static constexpr bool CPLANE = (MODE != M444) && PF;
+  static constexpr int BLK_F = C::NB * BS32;
+  static constexpr int GPL_F = CPLANE ? 2 * WN : 0;
+  static constexpr int GEN_F = WN + (GPL_F > BLK_F ? GPL_F : BLK_F);
+  static constexpr int CR = CPLANE ? WR : C::TH;  // interior chroma rows (row-filtered incl. ring rows)
+  static constexpr int IPL_F = C::TH * C::TW + 2 * CR * C::TW;
+  static constexpr int INT_F = IPL_F > BLK_F ? IPL_F : BLK_F;
+  static constexpr int F = GEN_F > INT_F ? GEN_F : INT_F;
+  static_assert((WN * 4) % 16 == 0, "plane alignment");
+};
+
+// Forward throughput kernel: one workgroup per tile, one thread per (block,
+// line).  Tiles whose RGB window (+1 px ring) lies inside the image with no
+// padding (`split` and not on the border ring of tiles) take the interior
+// staging: one thread per 8-pixel row segment loads 24 B with three 8-byte
+// loads, converts colour in registers and applies the prefilter's row pass
+// with its neighbours from adjacent lanes.  Border tiles take the general
+// staging (packed-RGB LDS window with BORDER_REFLECT_101 and np.pad reflect
+// index maps).  Both produce the same fp32 operation sequence per sample, so
+// one set of certified bounds covers them.
+template <int MODE, bool PF, bool INTERIOR>
 __global__ void __launch_bounds__(Cfg<MODE>::TF)
 k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
         const FastQ* __restrict__ fq, const float* __restrict__ gk32, jds_frame_stats* __restrict__ st,
-        uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount) {
+        uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int border) {
   using C = Cfg<MODE>;
-  constexpr int WR = C::TH + 2, WC = C::TW + 2, WN = WR * WC;
-  constexpr bool CPLANE = (MODE != M444) && PF;
-  constexpr int PLANE_F = CPLANE ? 2 * WN : 0;
-  constexpr int BLK_F = C::NB * BS32;
-  constexpr int U_F = PLANE_F > BLK_F ? PLANE_F : BLK_F;
+  using L = FwdLds<MODE, PF>;
+  constexpr int WR = L::WR, WC = L::WC, WN = L::WN;
+  constexpr bool CPLANE = L::CPLANE;
+  constexpr int TH = C::TH, TW = C::TW, SEG = TW / 8;
 
-  __shared__ uint32_t s_rgb[WN];
-  __shared__ __attribute__((aligned(16))) float s_u[U_F];
+  __shared__ __attribute__((aligned(16))) float s_raw[INTERIOR ? L::INT_F : L::GEN_F];
   __shared__ float s_rq[64], s_thr[2][64];
   __shared__ unsigned s_hist[50];
-  __shared__ int s_acc[2];
+  __shared__ unsigned s_acc[2];
 
   const int tid = threadIdx.x;
   const int frame = blockIdx.y;
-  const int ty = blockIdx.x / g.tiles_x, tx = blockIdx.x - ty * g.tiles_x;
+  int ty, tx;
+  if (INTERIOR) {  // tiles 1..tiles-2 in both directions
+    ty = 1 + (int)blockIdx.x / (g.tiles_x - 2);
+    tx = 1 + (int)blockIdx.x % (g.tiles_x - 2);
+  } else if (border) {  // the ring of border tiles only
+    const int e = blockIdx.x;
+    if (e < 2 * g.tiles_x) {
+      ty = e < g.tiles_x ? 0 : g.tiles_y - 1;
+      tx = e < g.tiles_x ? e : e - g.tiles_x;
+    } else {
+      ty = 1 + ((e - 2 * g.tiles_x) >> 1);
+      tx = (e & 1) ? g.tiles_x - 1 : 0;
+    }
+  } else {
+    ty = blockIdx.x / g.tiles_x;
+    tx = blockIdx.x - ty * g.tiles_x;
+  }
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
   const int y0 = m0y * C::MH, x0 = m0x * C::MW;
   const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
 
-  // 1. stage the RGB window (+1 px ring, BORDER_REFLECT_101 outside the image)
-  const bool interior = y0 - 1 >= 0 && x0 - 1 >= 0 && y0 + C::TH + 1 <= g.H && x0 + C::TW + 1 <= g.W;
-  if (interior) {
-    for (int i = tid; i < WN; i += C::TF) {
-      const int r = i / WC, c = i - r * WC;
-      const uint8_t* p = img + ((size_t)(y0 - 1 + r) * g.W + (x0 - 1 + c)) * 3;
-      s_rgb[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
-    }
-  } else {
-    for (int i = tid; i < WN; i += C::TF) {
-      const int r = i / WC, c = i - r * WC;
-      const int yy = reflect101(y0 - 1 + r, g.H), xx = reflect101(x0 - 1 + c, g.W);
-      const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
-      s_rgb[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
-    }
-  }
   if (tid < 64) {
     s_rq[tid] = fq[frame].rq[tid];
     s_thr[0][tid] = fq[frame].thr[0][tid];
     s_thr[1][tid] = fq[frame].thr[1][tid];
   }
   if (tid < 50) s_hist[tid] = 0u;
-  if (tid < 2) s_acc[tid] = 0;
-  __syncthreads();
+  if (tid < 2) s_acc[tid] = 0u;
 
-  // 2. fp32 chroma planes + Gaussian row pass
-  if constexpr (CPLANE) {
-    float* s_cb = s_u;
-    float* s_cr = s_u + WN;
-    for (int i = tid; i < WN; i += C::TF) {
-      float R, G, B;
-      unpack32(s_rgb[i], R, G, B);
-      s_cb[i] = cb32(R, G, B);
-      s_cr[i] = cr32(R, G, B);
-    }
-    __syncthreads();
-    constexpr int NRP = WR * (WC - 2);
-    constexpr int PER = (NRP + C::TF - 1) / C::TF;
-    const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
-    float tb[PER], tr[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int i = tid + j * C::TF;
-      if (i < NRP) {
-        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
-        const float* b = s_cb + r * WC + c;
-        const float* q = s_cr + r * WC + c;
-        tb[j] = fmaf(k2, b[1], fmaf(k1, b[0], k0 * b[-1]));
-        tr[j] = fmaf(k2, q[1], fmaf(k1, q[0], k0 * q[-1]));
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int i = tid + j * C::TF;
-      if (i < NRP) {
-        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
-        s_cb[r * WC + c] = tb[j];
-        s_cr[r * WC + c] = tr[j];
-      }
-    }
-    __syncthreads();
-  }
-
-  // 3. one block column per thread, DCT along axis 0
+  // the thread's block column
   const int blk = tid >> 3, line = tid & 7;
-  int plane, gy, gx;
+  int plane, by_t, bx_t;
   if (blk < C::NYB) {
     plane = 0;
-    gy = m0y * C::SY + blk / C::YBC;
-    gx = m0x * C::SX + blk % C::YBC;
+    by_t = blk / C::YBC;
+    bx_t = blk % C::YBC;
   } else {
     const int bi = (blk - C::NYB) % C::NCB;
     plane = 1 + (blk - C::NYB) / C::NCB;
-    gy = m0y + bi / C::CBC;
-    gx = m0x + bi % C::CBC;
+    by_t = bi / C::CBC;
+    bx_t = bi % C::CBC;
   }
+  const int gy = plane == 0 ? m0y * C::SY + by_t : m0y + by_t;
+  const int gx = plane == 0 ? m0x * C::SX + bx_t : m0x + bx_t;
   const int nby = plane ? g.ncy : g.nby, nbx = plane ? g.ncx : g.nbx;
-  const bool valid = gy >= 0 && gx >= 0 && gy < nby && gx < nbx;
+  const bool valid = INTERIOR || (gy >= 0 && gx >= 0 && gy < nby && gx < nbx);
   const int bidx = gy * nbx + gx;
-
+  const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
   float v[8];
-  if (valid) {
-    if (plane == 0 || MODE == M444) {
-      const int sx = reflect_pad(gx * 8 + line, g.W) - x0 + 1;
+  float* s_blkbase;
+
+  if constexpr (INTERIOR) {
+    // ---- interior staging: fp32 planes straight from 8-byte loads ----
+    float* s_y = s_raw;
+    float* s_cb = s_raw + TH * TW;
+    float* s_cr = s_cb + L::CR * TW;
+    s_blkbase = s_raw;
+    if (tid < WR * SEG) {
+      const int r = tid / SEG, c = tid % SEG;
+      if (CPLANE || (r >= 1 && r <= TH)) {  // uniform per row (lane groups of SEG)
+        const uint8_t* p = img + ((size_t)(y0 - 1 + r) * g.W + x0 + 8 * c) * 3;
+        const uint2* p2 = reinterpret_cast<const uint2*>(p);
+        const uint2 a = p2[0], b = p2[1], d = p2[2];
+        const uint32_t w[6] = {a.x, a.y, b.x, b.y, d.x, d.y};
+        float cb[8], cr[8], yy[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int sy = reflect_pad(gy * 8 + i, g.H) - y0 + 1;
-        float R, G, B;
-        unpack32(s_rgb[sy * WC + sx], R, G, B);
-        v[i] = (plane == 0 ? luma32(R, G, B) : (plane == 1 ? cb32(R, G, B) : cr32(R, G, B))) - 128.0f;
-      }
-    } else {
-      const float* s_pl = s_u + (plane == 1 ? 0 : WN);
-      const float k0 = gk32[0], k1 = gk32[1];
-      const int sc = reflect_pad(gx * 8 + line, g.wc);
-      const int wc0 = C::SX * sc - x0 + 1;
+        for (int k = 0; k < 8; ++k) {
+          const float R = (float)byte_at(w, 3 * k), G = (float)byte_at(w, 3 * k + 1), B = (float)byte_at(w, 3 * k + 2);
+          yy[k] = luma32(R, G, B) - 128.0f;
+          cb[k] = cb32(R, G, B);
+          cr[k] = cr32(R, G, B);
+        }
+        if (r >= 1 && r <= TH) {
+          float4* dy = reinterpret_cast<float4*>(s_y + (r - 1) * TW + 8 * c);
+          dy[0] = make_float4(yy[0], yy[1], yy[2], yy[3]);
+          dy[1] = make_float4(yy[4], yy[5], yy[6], yy[7]);
+        }
+        float ob[8], orr[8];
+        if constexpr (CPLANE) {
+          float lb = __shfl_up(cb[7], 1, SEG), lr = __shfl_up(cr[7], 1, SEG);
+          float rb = __shfl_down(cb[0], 1, SEG), rr = __shfl_down(cr[0], 1, SEG);
+          if (c == 0) {
+            const float R = p[-3], G = p[-2], B = p[-1];
+            lb = cb32(R, G, B);
+            lr = cr32(R, G, B);
+          }
+          if (c == SEG - 1) {
+            const float R = p[24], G = p[25], B = p[26];
+            rb = cb32(R, G, B);
+            rr = cr32(R, G, B);
+          }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int sr = reflect_pad(gy * 8 + i, g.hc);
-        const int wr0 = C::SY * sr - y0 + 1;
-        float s[C::SY][2];
+          for (int k = 0; k < 8; ++k) {
+            const float bl = k == 0 ? lb : cb[k - 1], br = k == 7 ? rb : cb[k + 1];
+            const float ql = k == 0 ? lr : cr[k - 1], qr = k == 7 ? rr : cr[k + 1];
+            ob[k] = fmaf(k2, br, fmaf(k1, cb[k], k0 * bl));
+            orr[k] = fmaf(k2, qr, fmaf(k1, cr[k], k0 * ql));
+          }
+        } else {
 #pragma unroll
-        for (int a = 0; a < C::SY; ++a) {
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const int w = (wr0 + a) * WC + wc0 + b;
-            if constexpr (CPLANE) {
-              s[a][b] = fmaf(k0, s_pl[w + WC] + s_pl[w - WC], k1 * s_pl[w]);
-            } else {
-              float R, G, B;
-              unpack32(s_rgb[w], R, G, B);
-              s[a][b] = plane == 1 ? cb32(R, G, B) : cr32(R, G, B);
-            }
+          for (int k = 0; k < 8; ++k) {
+            ob[k] = cb[k];
+            orr[k] = cr[k];
           }
         }
-        if constexpr (C::SY == 2)
-          v[i] = (((s[0][0] + s[0][1]) + s[1][0]) + s[1][1]) * 0.25f - 128.0f;
-        else
-          v[i] = (s[0][0] + s[0][1]) * 0.5f - 128.0f;
+        if (CPLANE || (r >= 1 && r <= TH)) {
+          const int pr = CPLANE ? r : r - 1;
+          float4* db = reinterpret_cast<float4*>(s_cb + pr * TW + 8 * c);
+          float4* dr = reinterpret_cast<float4*>(s_cr + pr * TW + 8 * c);
+          db[0] = make_float4(ob[0], ob[1], ob[2], ob[3]);
+          db[1] = make_float4(ob[4], ob[5], ob[6], ob[7]);
+          dr[0] = make_float4(orr[0], orr[1], orr[2], orr[3]);
+          dr[1] = make_float4(orr[4], orr[5], orr[6], orr[7]);
+        }
+      }
+    }
+    __syncthreads();
+    if (plane == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = s_y[(by_t * 8 + i) * TW + bx_t * 8 + line];
+    } else {
+      const float* P = plane == 1 ? s_cb : s_cr;
+      const int cc = bx_t * 8 + line;
+      if constexpr (MODE == M444) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = P[(by_t * 8 + i) * TW + cc] - 128.0f;
+      } else {
+        const int xc = 2 * cc;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int pr = C::SY * (by_t * 8 + i);
+          float s[C::SY][2];
+#pragma unroll
+          for (int a = 0; a < C::SY; ++a) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              if constexpr (CPLANE) {
+                const int w = (pr + a + 1) * TW + xc + b;
+                s[a][b] = fmaf(k0, P[w + TW] + P[w - TW], k1 * P[w]);
+              } else {
+                s[a][b] = P[(pr + a) * TW + xc + b];
+              }
+            }
+          }
+          if constexpr (C::SY == 2)
+            v[i] = (((s[0][0] + s[0][1]) + s[1][0]) + s[1][1]) * 0.25f - 128.0f;
+          else
+            v[i] = (s[0][0] + s[0][1]) * 0.5f - 128.0f;
+        }
       }
     }
     fdct8_f32(v);
+  } else {
+    // ---- general staging: packed RGB window with reflect index maps ----
+    uint32_t* s_rgb = reinterpret_cast<uint32_t*>(s_raw);
+    float* s_u = s_raw + WN;
+    s_blkbase = s_u;
+    const bool inside = y0 - 1 >= 0 && x0 - 1 >= 0 && y0 + TH + 1 <= g.H && x0 + TW + 1 <= g.W;
+    for (int i = tid; i < WN; i += C::TF) {
+      const int r = i / WC, c = i - r * WC;
+      const int yy = inside ? y0 - 1 + r : reflect101(y0 - 1 + r, g.H);
+      const int xx = inside ? x0 - 1 + c : reflect101(x0 - 1 + c, g.W);
+      const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
+      s_rgb[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+    }
+    __syncthreads();
+    if constexpr (CPLANE) {
+      float* s_cb = s_u;
+      float* s_cr = s_u + WN;
+      for (int i = tid; i < WN; i += C::TF) {
+        float R, G, B;
+        unpack32(s_rgb[i], R, G, B);
+        s_cb[i] = cb32(R, G, B);
+        s_cr[i] = cr32(R, G, B);
+      }
+      __syncthreads();
+      constexpr int NRP = WR * (WC - 2);
+      constexpr int PER = (NRP + C::TF - 1) / C::TF;
+      float tb[PER], tr[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int i = tid + j * C::TF;
+        if (i < NRP) {
+          const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
+          const float* b = s_cb + r * WC + c;
+          const float* q = s_cr + r * WC + c;
+          tb[j] = fmaf(k2, b[1], fmaf(k1, b[0], k0 * b[-1]));
+          tr[j] = fmaf(k2, q[1], fmaf(k1, q[0], k0 * q[-1]));
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int i = tid + j * C::TF;
+        if (i < NRP) {
+          const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
+          s_cb[r * WC + c] = tb[j];
+          s_cr[r * WC + c] = tr[j];
+        }
+      }
+      __syncthreads();
+    }
+    if (valid) {
+      if (plane == 0 || MODE == M444) {
+        const int sx = reflect_pad(gx * 8 + line, g.W) - x0 + 1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int sy = reflect_pad(gy * 8 + i, g.H) - y0 + 1;
+          float R, G, B;
+          unpack32(s_rgb[sy * WC + sx], R, G, B);
+          v[i] = (plane == 0 ? luma32(R, G, B) : (plane == 1 ? cb32(R, G, B) : cr32(R, G, B))) - 128.0f;
+        }
+      } else {
+        const float* s_pl = s_u + (plane == 1 ? 0 : WN);
+        const int sc = reflect_pad(gx * 8 + line, g.wc);
+        const int wc0 = C::SX * sc - x0 + 1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int sr = reflect_pad(gy * 8 + i, g.hc);
+          const int wr0 = C::SY * sr - y0 + 1;
+          float s[C::SY][2];
+#pragma unroll
+          for (int a = 0; a < C::SY; ++a) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              const int w = (wr0 + a) * WC + wc0 + b;
+              if constexpr (CPLANE) {
+                s[a][b] = fmaf(k0, s_pl[w + WC] + s_pl[w - WC], k1 * s_pl[w]);
+              } else {
+                float R, G, B;
+                unpack32(s_rgb[w], R, G, B);
+                s[a][b] = plane == 1 ? cb32(R, G, B) : cr32(R, G, B);
+              }
+            }
+          }
+          if constexpr (C::SY == 2)
+            v[i] = (((s[0][0] + s[0][1]) + s[1][0]) + s[1][1]) * 0.25f - 128.0f;
+          else
+            v[i] = (s[0][0] + s[0][1]) * 0.5f - 128.0f;
+        }
+      }
+      fdct8_f32(v);
+    }
   }
-  if constexpr (CPLANE) __syncthreads();  // block buffer aliases the chroma planes
-  float* s_blk = s_u + blk * BS32;
+  __syncthreads();  // the block buffer aliases the staging planes
+  float* s_blk = s_blkbase + blk * BS32;
   if (valid) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) s_blk[i * 8 + line] = v[i];
   }
   __syncthreads();
 
-  // 4. DCT along axis 1, certified quantisation, store
-  int nz = 0, mb = 0;
-  bool flag = false;
-  if (valid) {
+  // DCT along axis 1, certified quantisation, statistics, store.  Statistics
+  // without branches: nonzero counts from ballots, magnitude bits from the
+  // binary exponent of the rounded quotient (frexp: 0 -> 0, |q| -> bit length),
+  // histogram bins 22..29 (q in [-12, 19], zeros included and removed after the
+  // wave sum) in eight 4-bit counters per lane; only rarer bins take an LDS
+  // atomic.
+  // (Every lane runs the loop so the ballots stay wave-wide; lanes of padding
+  // blocks outside the grid are masked to zero and store nothing.)
+  unsigned mb = 0u, hn = 0u, nzw = 0u;
+  unsigned long long fm = 0ull;
+  {
     const int u = line;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = s_blk[u * 8 + k];
+    for (int k = 0; k < 8; ++k) v[k] = valid ? s_blk[u * 8 + k] : 0.0f;
     fdct8_f32(v);
     const float* thr = s_thr[plane ? 1 : 0] + u * 8;
     int q[8];
@@ -249,16 +398,16 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
     for (int k = 0; k < 8; ++k) {
       const float t = v[k] * s_rq[u * 8 + k];
       const float r = rintf(t);
-      const float margin = fmaf(fabsf(t), 0x1p-22f, thr[k]);
-      flag |= (0.5f - fabsf(t - r)) <= margin;
+      fm |= __ballot(valid && (0.5f - fabsf(t - r)) <= fmaf(fabsf(t), 0x1p-22f, thr[k]));
       q[k] = (int)r;
-      const int m = q[k] < 0 ? -q[k] : q[k];
-      if (m) {
-        ++nz;
-        mb += 33 - __clz(m);
-        if (q[k] >= -100 && q[k] <= 100) atomicAdd(&s_hist[q[k] == 100 ? 49 : (q[k] + 100) >> 2], 1u);
-      }
+      nzw += __popcll(__ballot(r != 0.0f));
+      mb += (unsigned)__builtin_amdgcn_frexp_expf(r);
+      const unsigned o = (unsigned)(q[k] + 12);
+      hn += o < 32u ? 1u << (o & ~3u) : 0u;
+      if (o >= 32u && (unsigned)(q[k] + 100) <= 200u) atomicAdd(&s_hist[q[k] == 100 ? 49 : (q[k] + 100) >> 2], 1u);
     }
+    if (!valid) hn = 0u;
+    if (valid) {
     const long long off = (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
                           (long long)bidx * 64 + u * 8;
     uint4 pk;
@@ -267,17 +416,27 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
     pk.z = (uint32_t)(uint16_t)q[4] | ((uint32_t)(uint16_t)q[5] << 16);
     pk.w = (uint32_t)(uint16_t)q[6] | ((uint32_t)(uint16_t)q[7] << 16);
     *reinterpret_cast<uint4*>(coeffs + off) = pk;
+    }
   }
-  const unsigned long long fm = __ballot(flag);
   if (valid && line == 0 && ((fm >> ((tid & 63) & ~7)) & 0xffull)) {
     const unsigned slot = atomicAdd(fixcount, 1u);
     fixlist[slot] = make_uint2((unsigned)frame, ((unsigned)plane << 24) | (unsigned)bidx);
   }
-  nz = wave_sum(nz);
-  mb = wave_sum(mb);
+  // widen the nibbles to 16-bit fields: (22|26), (24|28), (23|27), (25|29)
+  const unsigned e = hn & 0x0f0f0f0fu, o = (hn >> 4) & 0x0f0f0f0fu;
+  const unsigned w0 = __reduce_add_sync(~0ull, e & 0x00ff00ffu), w1 = __reduce_add_sync(~0ull, (e >> 8) & 0x00ff00ffu);
+  const unsigned w2 = __reduce_add_sync(~0ull, o & 0x00ff00ffu), w3 = __reduce_add_sync(~0ull, (o >> 8) & 0x00ff00ffu);
+  const unsigned wmb = __reduce_add_sync(~0ull, mb);
+  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
   if ((tid & 63) == 0) {
-    atomicAdd(&s_acc[0], nz);
-    atomicAdd(&s_acc[1], mb);
+    atomicAdd(&s_acc[0], nzw);
+    atomicAdd(&s_acc[1], wmb + nzw);  // magnitude bits = bit length + 1 per nonzero
+    const unsigned zeros = 8u * nvalid - nzw;
+    const unsigned c[8] = {w0 & 0xffffu, w2 & 0xffffu, w1 & 0xffffu, (w3 & 0xffffu) - zeros,
+                           w0 >> 16,     w2 >> 16,     w1 >> 16,     w3 >> 16};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (c[j]) atomicAdd(&s_hist[22 + j], c[j]);
   }
   __syncthreads();
   jds_frame_stats* fs = st + frame;
@@ -332,41 +491,42 @@ __device__ double sample64(const uint8_t* img, const Geo& g, int plane, int pr, 
     return (s[0][0] + s[0][1]) * 0.5;
 }
 
-// 64 threads = 8 listed blocks x 8 lines; grid-strides over the fix list
+// One listed block per 64-thread workgroup iteration (grid-strides over the
+// fix list): every thread forms one sample exactly, then 8 threads run the
+// column and row transforms, requantize and correct the statistics.
 template <int MODE, bool PF>
 __global__ void __launch_bounds__(64)
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
           const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount) {
-  __shared__ double s_blk[8][BS32];
-  const int tid = threadIdx.x, lb = tid >> 3, line = tid & 7;
+  __shared__ double s_b[64];
+  const int t = threadIdx.x;
   const unsigned count = *fixcount;
   const double k[3] = {gk[0], gk[1], gk[2]};
-  for (unsigned base = blockIdx.x * 8u; base < count; base += gridDim.x * 8u) {
-    const unsigned e = base + lb;
-    const bool ok = e < count;
-    int frame = 0, plane = 0, bidx = 0, gy = 0, gx = 0;
+  for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
+    const uint2 ent = fixlist[e];
+    const int frame = (int)ent.x;
+    const int plane = (int)(ent.y >> 24);
+    const int bidx = (int)(ent.y & 0xffffffu);
+    const int nbx = plane ? g.ncx : g.nbx;
+    const int gy = bidx / nbx, gx = bidx - gy * nbx;
+    const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
+    const int i = t >> 3, j = t & 7;
+    s_b[t] = sample64<MODE, PF>(img, g, plane, gy * 8 + i, gx * 8 + j, k) - 128.0;
+    __syncthreads();
     double v[8];
-    if (ok) {
-      const uint2 ent = fixlist[e];
-      frame = (int)ent.x;
-      plane = (int)(ent.y >> 24);
-      bidx = (int)(ent.y & 0xffffffu);
-      const int nbx = plane ? g.ncx : g.nbx;
-      gy = bidx / nbx;
-      gx = bidx - gy * nbx;
-      const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
-#pragma unroll 1
-      for (int i = 0; i < 8; ++i) v[i] = sample64<MODE, PF>(img, g, plane, gy * 8 + i, gx * 8 + line, k) - 128.0;
+    if (t < 8) {  // axis 0, column t
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = s_b[r * 8 + t];
       dct2_line(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) s_blk[lb][i * 8 + line] = v[i];
+      for (int r = 0; r < 8; ++r) s_b[r * 8 + t] = v[r];
     }
     __syncthreads();
-    if (ok) {
-      const int u = line;
+    if (t < 8) {  // axis 1, row u = t; requantize and correct the stats
+      const int u = t;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) v[c] = s_blk[lb][u * 8 + c];
+      for (int c = 0; c < 8; ++c) v[c] = s_b[u * 8 + c];
       dct2_line(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
       const long long off = (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
                             (long long)bidx * 64 + u * 8;
@@ -410,29 +570,52 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
 template <int MODE, bool PF>
 static hipError_t fast_fwd_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
                              const FastQ* fq32, const double* gk, const float* gk32, jds_frame_stats* st,
-                             uint2* fixlist, unsigned* fixcount, hipStream_t s) {
-  hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(g.tiles_y * g.tiles_x, n), dim3(Cfg<MODE>::TF), 0, s, g, rgb, coeffs,
-                     fq32, gk32, st, fixlist, fixcount);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(1024), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
+                             uint2* fixlist, unsigned* fixcount, hipStream_t s, const Side* side) {
+  using C = Cfg<MODE>;
+  // Interior tiles (window + ring inside the image, no padding, 8-byte rows)
+  // take k_fwd32<.., true>; the border ring of tiles runs beside it on the
+  // side stream when there is one.
+  const int yl = ((g.tiles_y - 2) * C::MY - g.ty_off) * C::MH, xl = ((g.tiles_x - 2) * C::MX - g.tx_off) * C::MW;
+  const bool split = g.tiles_y >= 3 && g.tiles_x >= 3 && (g.W % 8) == 0 && (C::MY - g.ty_off) * C::MH >= 1 &&
+                     (C::MX - g.tx_off) * C::MW >= 1 && yl + C::TH + 1 <= g.H && xl + C::TW + 1 <= g.W;
+  hipError_t e;
+  if (split) {
+    const bool fork = side && side->stream;
+    hipStream_t sb = fork ? side->stream : s;
+    if (fork && ((e = hipEventRecord(side->fork, s)) != hipSuccess ||
+                 (e = hipStreamWaitEvent(sb, side->fork, 0)) != hipSuccess))
+      return e;
+    hipLaunchKernelGGL((k_fwd32<MODE, PF, false>), dim3(2 * g.tiles_x + 2 * (g.tiles_y - 2), n), dim3(C::TF), 0, sb,
+                       g, rgb, coeffs, fq32, gk32, st, fixlist, fixcount, 1);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (fork && (e = hipEventRecord(side->join, sb)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_fwd32<MODE, PF, true>), dim3((g.tiles_y - 2) * (g.tiles_x - 2), n), dim3(C::TF), 0, s, g,
+                       rgb, coeffs, fq32, gk32, st, fixlist, fixcount, 0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (fork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
+  } else {
+    hipLaunchKernelGGL((k_fwd32<MODE, PF, false>), dim3(g.tiles_y * g.tiles_x, n), dim3(C::TF), 0, s, g, rgb,
+                       coeffs, fq32, gk32, st, fixlist, fixcount, 0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(4096), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                      fixcount);
   return hipGetLastError();
 }
 
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
-                           jds_frame_stats* st, uint2* fixlist, unsigned* fixcount, hipStream_t s) {
+                           jds_frame_stats* st, uint2* fixlist, unsigned* fixcount, hipStream_t s, const Side* side) {
   const FastQ* f = (const FastQ*)fq32;
   switch (mode) {
     case M420:
-      return pf ? fast_fwd_t<M420, true>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s)
-                : fast_fwd_t<M420, false>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s);
+      return pf ? fast_fwd_t<M420, true>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s, side)
+                : fast_fwd_t<M420, false>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s, side);
     case M422:
-      return pf ? fast_fwd_t<M422, true>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s)
-                : fast_fwd_t<M422, false>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s);
+      return pf ? fast_fwd_t<M422, true>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s, side)
+                : fast_fwd_t<M422, false>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s, side);
     default:
-      return fast_fwd_t<M444, false>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s);
+      return fast_fwd_t<M444, false>(g, n, rgb, coeffs, fq, f, gk, gk32, st, fixlist, fixcount, s, side);
   }
 }
 

@@ -1,5 +1,6 @@
 // jds_internal.hpp — types shared by the HIP kernels and the host-side C-ABI.
 #pragma once
+#include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
 #include "jds.h"
@@ -23,6 +24,13 @@ struct Geo {
   long long cpf;     // coefficients per frame
   long long off_cb, off_cr;
   double up_sy, up_sx;  // cv2.resize scale (src/dst) of the chroma upsample
+};
+
+// A second stream with fork/join events: lets a plan run independent launches
+// (border tiles beside interior tiles) concurrently.  All null = serial.
+struct Side {
+  hipStream_t stream = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
 };
 
 // Per-frame quantiser: q16 = 16*Q (pocketfft's first-axis fct = 1/16 folded in), q = Q.

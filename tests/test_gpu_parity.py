@@ -181,7 +181,9 @@ def _plan_run(frames, qs, mode, pf, flags):
 
 @pytest.mark.parametrize('h,w,mode,pf', [(1080, 1920, '4:2:0', True), (720, 1280, '4:2:2', True),
                                           (256, 384, '4:4:4', False), (130, 98, '4:2:0', False),
-                                          (64, 48, '4:2:2', False)])
+                                          (64, 48, '4:2:2', False), (360, 648, '4:2:0', False),
+                                          (200, 328, '4:2:2', True), (184, 260, '4:4:4', False),
+                                          (226, 516, '4:2:0', True), (98, 196, '4:2:2', False)])
 def test_fast_path_equals_exact_path_and_oracle(h, w, mode, pf):
     """Certified fp32 + fp64 fix-up (default) == all-fp64 kernels == oracle, bit for bit."""
     from jds import _abi
@@ -195,7 +197,7 @@ def test_fast_path_equals_exact_path_and_oracle(h, w, mode, pf):
         assert np.array_equal(s_fast[f], s_ex[f]), f
     ref = cpu_ref.compress_reconstruct(frames[1], 50, 8, mode, pf, metrics=False)
     assert np.array_equal(c_fast[1], ref['coeffs'])
-    assert fix[0] < 0.05 * len(qs) * c_fast.shape[1] / 64  # fix-up stays rare on random data
+    assert fix[0] < 0.10 * len(qs) * c_fast.shape[1] / 64  # fix-up stays rare on random data (Q=100 is the worst)
 
 
 def test_fast_path_resolves_exact_ties_through_fixup():
