@@ -28,7 +28,8 @@ hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* ch
                           double* out, hipStream_t s);
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
-                           jds_frame_stats* st, uint2* fixlist, unsigned* fixcount, hipStream_t s, const Side* side);
+                           jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* fixcount, hipStream_t s,
+                           const Side* side);
 void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
 size_t fast_q_size();
 hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse, hipStream_t s);
@@ -111,7 +112,7 @@ struct jds_plan {
   Geo g{};
   DevBuf fq, gk, part;
   // fast path: fp32 tables, fix-up lists and counters
-  DevBuf fq32, gk32, fixlist, counters;
+  DevBuf fq32, gk32, fixlist, counters, part32;  // part32: per-tile forward statistics
   Side side;  // border tiles run beside interior tiles
 };
 
@@ -330,6 +331,7 @@ int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n, int64_t H, in
     const size_t nblk = (size_t)n * (size_t)(g.cpf / 64);
     if ((e = p->fq32.ensure(fqs * n)) != hipSuccess || (e = p->gk32.ensure(sizeof gk32)) != hipSuccess ||
         (e = p->fixlist.ensure(8 * nblk)) != hipSuccess || (e = p->counters.ensure(64)) != hipSuccess ||
+        (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * g.tiles_y * g.tiles_x)) != hipSuccess ||
         (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess) {
       free(h32);
@@ -376,8 +378,8 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
                            s, nullptr, 1));
     else
       HIP_TRY(launch_fast_fwd(p->mode, p->pf, p->g, p->n, rgb, coeffs, (const FrameQ*)p->fq.p, p->fq32.p,
-                              (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint2*)p->fixlist.p,
-                              (unsigned*)p->counters.p, s, &p->side));
+                              (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint32_t*)p->part32.p,
+                              (uint2*)p->fixlist.p, (unsigned*)p->counters.p, s, &p->side));
   }
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
@@ -397,6 +399,7 @@ void jds_plan_destroy(jds_plan* p) {
   p->gk32.release();
   p->fixlist.release();
   p->counters.release();
+  p->part32.release();
   if (p->side.stream) (void)hipStreamDestroy(p->side.stream);
   if (p->side.fork) (void)hipEventDestroy(p->side.fork);
   if (p->side.join) (void)hipEventDestroy(p->side.join);

@@ -533,7 +533,58 @@ __global__ void k_sel_dequant(const int16_t* __restrict__ coeffs, const FrameQ* 
   if (i < 64) sel->dequantized[i] = (double)coeffs[(long long)sel_blk * 64 + i] * fq[0].q[i];
 }
 
-// Per-frame constants, histogram zero bin, deterministic luma-SSE sum.
+// Sum of the forward kernels' per-tile statistics partials (nonzero, magnitude
+// bits, hist[50] as u32 per tile) into the frame stats: 8 groups x 64 lanes
+// per workgroup, 64 tiles per workgroup, one u64 atomic per statistic.
+__global__ void __launch_bounds__(512) k_fwd_reduce(jds_frame_stats* st, const uint32_t* __restrict__ part, int ptiles) {
+  __shared__ unsigned long long s_sum[8][64];
+  const int f = blockIdx.y, j = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int t0 = blockIdx.x * 64 + grp * 8;
+  unsigned long long a = 0ull;
+  if (j < 52) {
+    unsigned v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = t0 + i < ptiles ? part[((size_t)f * ptiles + t0 + i) * 52 + j] : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a += v[i];
+  }
+  s_sum[grp][j] = a;
+  __syncthreads();
+  if (threadIdx.x < 52) {
+    unsigned long long b = 0ull;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b += s_sum[i][threadIdx.x];
+    jds_frame_stats* s = st + f;
+    unsigned long long* dst = threadIdx.x == 0 ? (unsigned long long*)&s->nonzero
+                              : threadIdx.x == 1 ? (unsigned long long*)&s->magnitude_bits
+                                                 : (unsigned long long*)&s->hist[threadIdx.x - 2];
+    if (b) atomicAdd(dst, b);
+  }
+}
+
+// End of the forward phase: per-frame constants and the histogram's zero bin.
+__global__ void k_fwd_finish(const Geo g, jds_frame_stats* st) {
+  const int f = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  jds_frame_stats* s = st + f;
+  s->total_coeffs = (uint64_t)g.cpf;
+  s->block_overhead_bits = 2ull * (uint64_t)g.nby * (uint64_t)g.nbx;
+  s->pixels = (uint64_t)g.H * (uint64_t)g.W;
+  s->hist[25] += (uint64_t)g.cpf - s->nonzero;  // zeros fall in bin 25 ([0, 4))
+}
+
+hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uint32_t* part, int ptiles,
+                             hipStream_t s) {
+  if (part) {
+    hipLaunchKernelGGL(k_fwd_reduce, dim3((ptiles + 63) / 64, n), dim3(512), 0, s, st, part, ptiles);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_fwd_finish, dim3(n), dim3(64), 0, s, g, st);
+  return hipGetLastError();
+}
+
+// Per-frame constants and the deterministic luma-SSE sum (inverse phase).
 __global__ void k_finalize(const Geo g, jds_frame_stats* st, const double* __restrict__ sse_y_part,
                            int tiles, int with_sse) {
   const int f = blockIdx.x;
@@ -542,7 +593,6 @@ __global__ void k_finalize(const Geo g, jds_frame_stats* st, const double* __res
   s->total_coeffs = (uint64_t)g.cpf;
   s->block_overhead_bits = 2ull * (uint64_t)g.nby * (uint64_t)g.nbx;
   s->pixels = (uint64_t)g.H * (uint64_t)g.W;
-  s->hist[25] += (uint64_t)g.cpf - s->nonzero;  // zeros fall in bin 25 ([0, 4))
   if (with_sse) {
     double a = 0.0;
     for (int t = 0; t < tiles; ++t) a = a + sse_y_part[(size_t)f * tiles + t];
@@ -603,6 +653,7 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
         e = launch_fwd_t<M444, false>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s);
         break;
     }
+    if (e == hipSuccess) e = launch_fwd_finish(g, n, st, nullptr, 0, s);
     if (e != hipSuccess || (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess)) return e;
   }
   if (phases & 2) {

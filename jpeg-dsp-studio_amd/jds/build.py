@@ -40,7 +40,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return LIB
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    cmd = [HIPCC, '-std=c++17', '-O3', f'--offload-arch={ARCH}', '-fPIC', '-shared',
+    cmd = [HIPCC, '-std=c++17', '-O3', f'--offload-arch={ARCH}', '-fPIC', '-shared', '-fno-slp-vectorize',
            '-ffp-contract=off', '-Wall', '-Wno-unused-function', f'-I{INCLUDE}', f'-I{CSRC}',
            '-o', LIB + '.tmp'] + srcs
     if verbose:
