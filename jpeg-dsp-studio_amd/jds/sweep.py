@@ -1,0 +1,111 @@
+"""Quality sweeps: the GUI's BatchSweepWorker (reference gui/worker.py:39-74) and
+the frame-sharded multi-GPU sweep of BASELINE cfg4 (64 frames x Q in
+{5,10,20,50,80,95}).
+
+* ``quality_sweep`` mirrors BatchSweepWorker.run: one ``compress_reconstruct``
+  per quality in ``range(start, end + 1, step)``, returning ``[(q, result)]``.
+* ``sweep_device`` runs (frame, Q) items as ONE device-resident plan on one
+  GPU (frames replicated per quality on the device) and returns per-item
+  statistics: nonzero count, exact magnitude bits, histogram, integer SSE.
+* ``distributed_sweep`` shards frames across the ranks of an initialised
+  ``torch.distributed`` group (one process per GPU, no data-path collective)
+  and gathers the per-item statistics to every rank with one
+  ``all_gather_object`` -- the only exchange the path has.
+"""
+from __future__ import annotations
+
+from typing import Callable, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+
+def quality_sweep(image: np.ndarray, base_params, quality_start: int = 10, quality_end: int = 90,
+                  quality_step: int = 10, progress: Optional[Callable[[int, int], None]] = None):
+    """BatchSweepWorker.run (gui/worker.py:55-74) without Qt: [(quality, CompressionResult)]."""
+    from engines.pipeline import compress_reconstruct
+    from models.compression_params import CompressionParams
+    qualities = list(range(quality_start, quality_end + 1, quality_step))
+    results = []
+    for i, quality in enumerate(qualities):
+        params = CompressionParams(block_size=base_params.block_size, quality=quality,
+                                   subsampling_mode=base_params.subsampling_mode,
+                                   use_prefilter=base_params.use_prefilter)
+        result, _ = compress_reconstruct(image, params)
+        results.append((quality, result))
+        if progress is not None:
+            progress(i + 1, len(qualities))
+    return results
+
+
+def shard(n: int, rank: int, world: int) -> range:
+    """Contiguous, balanced share of n items for `rank` of `world` (first n % world ranks get one more)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f'bad rank {rank} of world {world}')
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return range(lo, lo + base + (1 if rank < extra else 0))
+
+
+def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilter: bool = True,
+                 device: int = 0) -> List[dict]:
+    """All (frame, quality) items of `frames` (uint8 [F, H, W, 3], NumPy or a torch
+    tensor on the device) through one device-resident plan.  Items are ordered
+    frame-major.  Returns one dict per item."""
+    import torch
+    from jds import _abi, codec
+    from engines.quantizer import scale_quant_matrix
+    from utils.constants import JPEG_LUMA_Q50
+    from utils.metrics import bitrate_from_counts
+
+    dev = torch.device('cuda', device)
+    fr = frames if isinstance(frames, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frames))
+    fr = fr.to(dev)
+    F, H, W = int(fr.shape[0]), int(fr.shape[1]), int(fr.shape[2])
+    qs = [int(q) for q in qualities]
+    gk = codec.gaussian_kernel3()
+    params = [_abi.make_params(q, scale_quant_matrix(JPEG_LUMA_Q50, q), mode, prefilter, gk)
+              for _ in range(F) for q in qs]
+    plan = _abi.Plan(_abi.context(device), params, H, W)
+    try:
+        rgb = fr.repeat_interleave(len(qs), dim=0).contiguous()
+        out = torch.empty_like(rgb)
+        cf = torch.empty((len(params), plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+        st = torch.zeros((len(params), _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), _abi.RUN_SSE, 0)
+        torch.cuda.synchronize(dev)
+        stats = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(-1)
+    finally:
+        plan.close()
+    items = []
+    for i, s in enumerate(stats):
+        f, q = divmod(i, len(qs))
+        br = bitrate_from_counts(int(s['nonzero']), float(s['magnitude_bits']), int(s['total_coeffs']), (H, W), 8)
+        mse = float(s['sse_rgb']) / (H * W * 3)
+        items.append({'frame': f, 'quality': qs[q], 'nonzero': int(s['nonzero']),
+                      'magnitude_bits': int(s['magnitude_bits']), 'total_coeffs': int(s['total_coeffs']),
+                      'hist': s['hist'].astype(np.int64), 'sse_rgb': int(s['sse_rgb']),
+                      'psnr_rgb': float('inf') if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse)),
+                      'bpp': br['bpp'], 'compression_ratio': br['compression_ratio']})
+    return items
+
+
+def distributed_sweep(n_frames: int, qualities: Sequence[int],
+                      compute: Callable[[range, Sequence[int]], List[dict]],
+                      group=None) -> List[dict]:
+    """Frame-shard a sweep over the ranks of the initialised torch.distributed
+    group: rank r computes `compute(frames_of_r, qualities)` (its items in
+    frame-major order, each dict carrying a global 'frame'), then one
+    all_gather_object gives every rank the whole list in global item order."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    mine = shard(n_frames, rank, world)
+    local = compute(mine, list(qualities))
+    if world == 1:
+        return local
+    parts: List[Optional[List[dict]]] = [None] * world
+    dist.all_gather_object(parts, local, group=group)
+    items = [it for p in parts for it in p]
+    items.sort(key=lambda it: (it['frame'], list(qualities).index(it['quality'])))
+    return items

@@ -211,3 +211,31 @@ def test_fast_path_resolves_exact_ties_through_fixup():
     for i, v in enumerate((127, 129, 131, 133)):
         g = golden()[f'flat{v}_q50_420_pf']
         assert sha(c[i]) == g['sha_coeffs'] and sha(o[i]) == g['sha_recon']
+
+
+def test_sweep_device_matches_oracle():
+    """cfg4-style sweep: (frame, Q) items through one device-resident plan."""
+    from jds.sweep import sweep_device
+    frames = np.stack([cpu_ref.random_image(96, 160, s) for s in (1, 2)])
+    qs = [10, 50, 95]
+    items = sweep_device(frames, qs, '4:2:0', True)
+    assert [(it['frame'], it['quality']) for it in items] == [(f, q) for f in range(2) for q in qs]
+    for it in items:
+        f = frames[it['frame']]
+        ref = cpu_ref.compress_reconstruct(f, it['quality'], 8, '4:2:0', True, metrics=False)
+        assert it['nonzero'] == ref['bitrate']['nonzero_count']
+        assert np.array_equal(it['hist'], ref['hist'])
+        assert it['sse_rgb'] == int(((f.astype(np.int64) - ref['reconstructed']) ** 2).sum())
+
+
+def test_quality_sweep_matches_per_call_reference():
+    """BatchSweepWorker.run (gui/worker.py:55-74) semantics."""
+    from jds.sweep import quality_sweep
+    from models.compression_params import CompressionParams
+    img = cpu_ref.random_image(64, 96, 4)
+    res = quality_sweep(img, CompressionParams(quality=50, subsampling_mode='4:2:2', use_prefilter=True), 20, 80, 30)
+    assert [q for q, _ in res] == [20, 50, 80]
+    for q, r in res:
+        ref = cpu_ref.compress_reconstruct(img, q, 8, '4:2:2', True, metrics=True)
+        assert np.array_equal(r.reconstructed_image, ref['reconstructed'])
+        assert (r.psnr_rgb, r.ssim_y) == (ref['metrics']['psnr_rgb'], ref['metrics']['ssim_y'])
