@@ -176,7 +176,7 @@ template <int MODE, bool PF>
 __global__ void __launch_bounds__(Cfg<MODE>::TF)
 k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
         const FastQ* __restrict__ fq, const float* __restrict__ gk32, uint32_t* __restrict__ part,
-        uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int border) {
+        uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int border, const int4 rect) {
   using C = Cfg<MODE>;
   constexpr int WR = C::TH + 2, WC = C::TW + 2, WN = WR * WC;
   constexpr bool CPLANE = (MODE != M444) && PF;
@@ -194,14 +194,24 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   const int tid = threadIdx.x;
   const int frame = blockIdx.y;
   int ty, tx;
-  if (border) {  // the ring of border tiles only (k_fwd32i takes the interior)
-    const int e = blockIdx.x;
-    if (e < 2 * g.tiles_x) {
-      ty = e < g.tiles_x ? 0 : g.tiles_y - 1;
-      tx = e < g.tiles_x ? e : e - g.tiles_x;
+  if (border) {  // tiles outside the interior rectangle rect = (ty_lo, ty_hi, tx_lo, tx_hi) only
+    int e = blockIdx.x;
+    const int top = rect.x * g.tiles_x, bottom = (g.tiles_y - 1 - rect.y) * g.tiles_x;
+    const int rows = rect.y - rect.x + 1, left = rect.z * rows;
+    if (e < top) {
+      ty = e / g.tiles_x;
+      tx = e - ty * g.tiles_x;
+    } else if ((e -= top) < bottom) {
+      ty = rect.y + 1 + e / g.tiles_x;
+      tx = e - (ty - rect.y - 1) * g.tiles_x;
+    } else if ((e -= bottom) < left) {
+      ty = rect.x + e / rect.z;
+      tx = e - (ty - rect.x) * rect.z;
     } else {
-      ty = 1 + ((e - 2 * g.tiles_x) >> 1);
-      tx = (e & 1) ? g.tiles_x - 1 : 0;
+      e -= left;
+      const int nr = g.tiles_x - 1 - rect.w;
+      ty = rect.x + e / nr;
+      tx = rect.w + 1 + e - (ty - rect.x) * nr;
     }
   } else {
     ty = blockIdx.x / g.tiles_x;
@@ -377,7 +387,7 @@ template <int MODE, bool PF>
 __global__ void __launch_bounds__(Cfg<MODE>::TF)
 k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
          const FastQ* __restrict__ fq, const float* __restrict__ gk32, uint32_t* __restrict__ part,
-         uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount) {
+         uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int4 rect) {
   using C = Cfg<MODE>;
   constexpr int TH = C::TH, TW = C::TW, WR = TH + 2, SEG = TW / 8;
   constexpr bool SUB = MODE != M444;
@@ -392,8 +402,8 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   __shared__ unsigned s_st[NSTAT];
 
   const int tid = threadIdx.x, frame = blockIdx.y;
-  const int itx = g.tiles_x - 2;
-  const int ty = 1 + (int)blockIdx.x / itx, tx = 1 + (int)blockIdx.x % itx;
+  const int ncol = rect.w - rect.z + 1;
+  const int ty = rect.x + (int)blockIdx.x / ncol, tx = rect.z + (int)blockIdx.x % ncol;
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
   const int y0 = m0y * C::MH, x0 = m0x * C::MW;
   const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
@@ -412,11 +422,16 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   if (tid < WR * SEG) {
     const int r = tid / SEG, c = tid % SEG;
     if (CPLANE || (r >= 1 && r <= TH)) {  // uniform per row (lane groups of SEG)
-      const uint8_t* p = img + ((size_t)(y0 - 1 + r) * g.W + x0 + 8 * c) * 3;
+      // the tile lies inside the image; only the 1-px ring may leave it:
+      // BORDER_REFLECT_101 maps row -1 to 1 and row H to H-2 (columns below)
+      int yrow = y0 - 1 + r;
+      yrow = yrow < 0 ? -yrow : (yrow >= g.H ? 2 * g.H - 2 - yrow : yrow);
+      const uint8_t* p = img + ((size_t)yrow * g.W + x0 + 8 * c) * 3;
       const uint2* p2 = reinterpret_cast<const uint2*>(p);
+      const bool left_edge = x0 == 0, right_edge = x0 + TW == g.W;
 #ifndef JDS_PROBE_NOLOAD
       const uint2 a = p2[0], b = p2[1], d = p2[2];
-      const uint2 ring = CPLANE ? p2[c == 0 ? -1 : 3] : make_uint2(0u, 0u);
+      const uint2 ring = CPLANE ? p2[c == 0 ? (left_edge ? 0 : -1) : (right_edge ? 0 : 3)] : make_uint2(0u, 0u);
 #else  // tools/probe: synthetic bytes instead of the loads
       const uint32_t hsh = (uint32_t)(tid + 977 * blockIdx.x) * 2654435761u;
       const uint2 a = make_uint2(hsh, hsh ^ 0x5bd1e995u), b = make_uint2(hsh * 3u, hsh + 17u), d = make_uint2(~hsh, hsh >> 3);
@@ -457,15 +472,15 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       } else if constexpr (CPLANE) {
         float lb = __shfl_up(cb[7], 1, SEG), lr = __shfl_up(cr[7], 1, SEG);
         float rb = __shfl_down(cb[0], 1, SEG), rr = __shfl_down(cr[0], 1, SEG);
-        if (c == 0) {  // bytes 5..7 of the 8 before the segment
+        if (c == 0) {  // bytes 5..7 of the 8 before the segment; pixel 1 at the image edge
           const float R = (float)((ring.y >> 8) & 255u), G = (float)((ring.y >> 16) & 255u), B = (float)(ring.y >> 24);
-          lb = cb32(R, G, B);
-          lr = cr32(R, G, B);
+          lb = left_edge ? cb[1] : cb32(R, G, B);
+          lr = left_edge ? cr[1] : cr32(R, G, B);
         }
-        if (c == SEG - 1) {  // bytes 0..2 of the 8 after the segment
+        if (c == SEG - 1) {  // bytes 0..2 of the 8 after the segment; pixel W-2 at the image edge
           const float R = (float)(ring.x & 255u), G = (float)((ring.x >> 8) & 255u), B = (float)((ring.x >> 16) & 255u);
-          rb = cb32(R, G, B);
-          rr = cr32(R, G, B);
+          rb = right_edge ? cb[6] : cb32(R, G, B);
+          rr = right_edge ? cr[6] : cr32(R, G, B);
         }
         float ob[8], orr[8];
 #pragma unroll
@@ -727,30 +742,36 @@ static hipError_t fast_fwd_t(const Geo& g, int n, const uint8_t* rgb, int16_t* c
                              const FastQ* fq32, const double* gk, const float* gk32, jds_frame_stats* st,
                              uint32_t* part, uint2* fixlist, unsigned* fixcount, hipStream_t s, const Side* side) {
   using C = Cfg<MODE>;
-  // Interior tiles (window + ring inside the image, no padding, 8-byte rows)
-  // take k_fwd32i; the border ring of tiles runs in k_fwd32 beside it on the
-  // side stream when there is one.
-  const int yl = ((g.tiles_y - 2) * C::MY - g.ty_off) * C::MH, xl = ((g.tiles_x - 2) * C::MX - g.tx_off) * C::MW;
-  const bool split = g.tiles_y >= 3 && g.tiles_x >= 3 && (g.W % 8) == 0 && (C::MY - g.ty_off) * C::MH >= 1 &&
-                     (C::MX - g.tx_off) * C::MW >= 1 && yl + C::TH + 1 <= g.H && xl + C::TW + 1 <= g.W;
+  // Tiles lying wholly inside the image (no padding blocks, no phantom MCUs;
+  // only the 1-px ring may reflect) form a rectangle of tile indices and take
+  // k_fwd32i; the rest run in k_fwd32 beside it on the side stream.
+  int4 rect;
+  rect.x = (g.ty_off * C::MH > 0) ? 1 : 0;                           // first tile row with y0 >= 0
+  rect.y = (g.H / C::MH + g.ty_off) / C::MY - 1;                     // last tile row with y0 + TH <= H
+  rect.z = (g.tx_off * C::MW > 0) ? 1 : 0;
+  rect.w = (g.W / C::MW + g.tx_off) / C::MX - 1;
+  const bool split = (g.W % 8) == 0 && g.H >= 2 && g.W >= 2 && rect.y >= rect.x && rect.w >= rect.z;
   hipError_t e;
   if (split) {
-    const bool fork = side && side->stream;
+    const int nin = (rect.y - rect.x + 1) * (rect.w - rect.z + 1), nout = g.tiles_y * g.tiles_x - nin;
+    const bool fork = side && side->stream && nout > 0;
     hipStream_t sb = fork ? side->stream : s;
     if (fork && ((e = hipEventRecord(side->fork, s)) != hipSuccess ||
                  (e = hipStreamWaitEvent(sb, side->fork, 0)) != hipSuccess))
       return e;
-    hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(2 * g.tiles_x + 2 * (g.tiles_y - 2), n), dim3(C::TF), 0, sb, g,
-                       rgb, coeffs, fq32, gk32, part, fixlist, fixcount, 1);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (nout > 0) {
+      hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(nout, n), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32, part,
+                         fixlist, fixcount, 1, rect);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (fork && (e = hipEventRecord(side->join, sb)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_fwd32i<MODE, PF>), dim3((g.tiles_y - 2) * (g.tiles_x - 2), n), dim3(C::TF), 0, s, g, rgb,
-                       coeffs, fq32, gk32, part, fixlist, fixcount);
+    hipLaunchKernelGGL((k_fwd32i<MODE, PF>), dim3(nin, n), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32, part,
+                       fixlist, fixcount, rect);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (fork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
   } else {
     hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(g.tiles_y * g.tiles_x, n), dim3(C::TF), 0, s, g, rgb, coeffs, fq32,
-                       gk32, part, fixlist, fixcount, 0);
+                       gk32, part, fixlist, fixcount, 0, rect);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(4096), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,

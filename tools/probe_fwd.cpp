@@ -56,10 +56,14 @@ int main(int argc, char** argv) {
     printf("%-28s %9.1f us\n", name, ms * 1000 / R);
   };
   using C = Cfg<M420>;
-  const dim3 gi((g.tiles_y - 2) * (g.tiles_x - 2), n), gb(2 * g.tiles_x + 2 * (g.tiles_y - 2), n), ga(g.tiles_y * g.tiles_x, n);
-  time_it("fwd32 interior", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt); });
-  time_it("fwd32 border", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32<M420, true>), gb, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 1); });
-  time_it("fwd32 general, all tiles", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32<M420, true>), ga, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 0); });
+  int4 rect;
+  rect.x = (g.ty_off * C::MH > 0) ? 1 : 0; rect.y = (g.H / C::MH + g.ty_off) / C::MY - 1;
+  rect.z = (g.tx_off * C::MW > 0) ? 1 : 0; rect.w = (g.W / C::MW + g.tx_off) / C::MX - 1;
+  const int nin = (rect.y - rect.x + 1) * (rect.w - rect.z + 1);
+  const dim3 gi(nin, n), gb(g.tiles_y * g.tiles_x - nin, n), ga(g.tiles_y * g.tiles_x, n);
+  time_it("fwd32 interior", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, rect); });
+  time_it("fwd32 border", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32<M420, true>), gb, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 1, rect); });
+  time_it("fwd32 general, all tiles", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32<M420, true>), ga, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 0, rect); });
   time_it("inv2", [&] { launch_inv2(M420, g, n, cf, fq, nullptr, out, st, nullptr, nullptr, nullptr, 0); });
   {
     hipStream_t s1, s2;
@@ -67,7 +71,7 @@ int main(int argc, char** argv) {
     hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
     auto both = [&](bool conc) {
       hipStream_t sa = s1, sb = conc ? s2 : s1;
-      hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, sa, g, rgb, cf, fq32, gk32, part, fl, cnt);
+      hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, sa, g, rgb, cf, fq32, gk32, part, fl, cnt, rect);
       launch_inv2(M420, g, n, cf, fq, nullptr, out, st, nullptr, nullptr, nullptr, sb);
     };
     for (int conc = 0; conc < 2; ++conc) {
@@ -83,8 +87,8 @@ int main(int argc, char** argv) {
   }
   {
     unsigned hc = 0; hipMemset(cnt, 0, 64);
-    hipLaunchKernelGGL((k_fwd32<M420, true>), gb, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 1);
-    hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt);
+    hipLaunchKernelGGL((k_fwd32<M420, true>), gb, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 1, rect);
+    hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, rect);
     hipMemcpy(&hc, cnt, 4, hipMemcpyDeviceToHost);
     printf("flagged blocks (64 frames): %u\n", hc);
   }
