@@ -666,7 +666,12 @@ __global__ void __launch_bounds__(64)
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
           const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount) {
+  constexpr bool CPLANE = (MODE != M444) && PF;
+  constexpr int SY = Cfg<MODE>::SY;
+  constexpr int WRR = 8 * SY + 2, WCC = 18;  // prefilter source window of one chroma block
   __shared__ double s_b[64];
+  __shared__ double s_w[CPLANE ? WRR * WCC : 1];         // fp64 chroma of the window
+  __shared__ double s_rf[CPLANE ? WRR * (WCC - 2) : 1];  // after the row pass
   const int t = threadIdx.x;
   const unsigned count = *fixcount;
   const double k[3] = {gk[0], gk[1], gk[2]};
@@ -679,7 +684,44 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     const int gy = bidx / nbx, gx = bidx - gy * nbx;
     const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
     const int i = t >> 3, j = t & 7;
-    s_b[t] = sample64<MODE, PF>(img, g, plane, gy * 8 + i, gx * 8 + j, k) - 128.0;
+    // prefiltered chroma of a block away from every edge: stage the source
+    // window once (colour, then the row pass, in LDS), same fp64 operations
+    const int wy0 = SY * 8 * gy - 1, wx0 = 16 * gx - 1;
+    const bool staged = CPLANE && plane != 0 && gy * 8 + 8 <= g.hc && gx * 8 + 8 <= g.wc && wy0 >= 0 &&
+                        wx0 >= 0 && wy0 + WRR <= g.H && wx0 + WCC <= g.W;
+    if (staged) {  // uniform per workgroup
+      for (int q = t; q < WRR * WCC; q += 64) {
+        const int r = q / WCC, c = q - r * WCC;
+        s_w[q] = px_chroma64(img, g, wy0 + r, wx0 + c, plane);
+      }
+      __syncthreads();
+      for (int q = t; q < WRR * (WCC - 2); q += 64) {
+        const int r = q / (WCC - 2), c = q - r * (WCC - 2) + 1;
+        const double* w = s_w + r * WCC + c;
+        double a = k[0] * w[-1];
+        a = a + k[1] * w[0];
+        s_rf[q] = a + k[2] * w[1];
+      }
+      __syncthreads();
+      double sm[SY][2];
+#pragma unroll
+      for (int a = 0; a < SY; ++a) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const double* f = s_rf + (SY * i + a + 1) * (WCC - 2) + 2 * j + b;  // window row of pixel row
+          const double d = k[1] * f[0] + 0.0;
+          sm[a][b] = d + k[0] * (f[WCC - 2] + f[-(WCC - 2)]);
+        }
+      }
+      double v;
+      if constexpr (SY == 2)
+        v = (((sm[0][0] + sm[0][1]) + sm[1][0]) + sm[1][1]) * 0.25;
+      else
+        v = (sm[0][0] + sm[0][1]) * 0.5;
+      s_b[t] = v - 128.0;
+    } else {
+      s_b[t] = sample64<MODE, PF>(img, g, plane, gy * 8 + i, gx * 8 + j, k) - 128.0;
+    }
     __syncthreads();
     double v[8];
     if (t < 8) {  // axis 0, column t
