@@ -58,6 +58,11 @@ __device__ __forceinline__ void fdct8_f32(float (&x)[8]) {
 __device__ __forceinline__ float luma32(float R, float G, float B) {
   return fmaf(0.114f, B, fmaf(0.587f, G, 0.299f * R));
 }
+// luma - 128 with the level shift folded into the chain: three roundings of
+// magnitude <= 128 instead of luma32's, inside fwd_input_error's luma bound
+__device__ __forceinline__ float luma32m(float R, float G, float B) {
+  return fmaf(0.114f, B, fmaf(0.587f, G, fmaf(0.299f, R, -128.0f)));
+}
 __device__ __forceinline__ float cb32(float R, float G, float B) {
   return fmaf(-0.168736f, R, fmaf(-0.331264f, G, fmaf(0.5f, B, 128.0f)));
 }
@@ -73,7 +78,7 @@ __device__ __forceinline__ void unpack32(uint32_t v, float& R, float& G, float& 
 
 struct FastQ {
   float rq[64];      // fp32(1/Q)
-  float thr[2][64];  // certification margins in quotient units: [0] luma, [1] chroma
+  float thr[2][64];  // certification limits on |t - rint(t)| (0.5 - margin): [0] luma, [1] chroma
 };
 
 constexpr int BS32 = 72;  // floats per 8x8 block in LDS (column writes conflict-free)
@@ -101,19 +106,24 @@ __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8]
   for (int k = 0; k < 8; ++k) {
     const float t = v[k] * rq[k];
     const float r = rintf(t);
-    ls.nflag += (0.5f - fabsf(t - r)) <= fmaf(fabsf(t), 0x1p-22f, thr[k]) ? 1u : 0u;
+    // |t - r| is exact (Sterbenz); thr[k] holds 0.5 - E/Q - slack, rounded down
+    ls.nflag += fabsf(t - r) >= fmaf(fabsf(t), -0x1p-22f, thr[k]) ? 1u : 0u;
     q[k] = (int)r;
     ls.nz += r != 0.0f ? 1u : 0u;
     ls.mb += (unsigned)__builtin_amdgcn_frexp_expf(r);
     const unsigned o = (unsigned)(q[k] + 12);
-    ls.hn += o < 32u ? 1u << (o & ~3u) : 0u;
+    ls.hn += 1u << (o & 28u);  // bins 22..29; a rare q lands in some nibble and is taken back below
     nrare += o >= 32u ? 1u : 0u;
   }
-  if (nrare != 0u && valid) {
+  if (nrare != 0u) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if ((unsigned)(q[k] + 12) >= 32u && (unsigned)(q[k] + 100) <= 200u)
-        atomicAdd(&s_st[2 + (q[k] == 100 ? 49 : (q[k] + 100) >> 2)], 1u);
+    for (int k = 0; k < 8; ++k) {
+      const unsigned o = (unsigned)(q[k] + 12);
+      if (o >= 32u) {
+        ls.hn -= 1u << (o & 28u);
+        if (valid && (unsigned)(q[k] + 100) <= 200u) atomicAdd(&s_st[2 + (q[k] == 100 ? 49 : (q[k] + 100) >> 2)], 1u);
+      }
+    }
   }
 }
 
@@ -377,8 +387,9 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
 //      adjacent lanes (4:4:4: the chroma row DCTs too);
 //   2. luma threads (one per block column) run the column DCT (axis 0),
 //      quantise and store, while chroma threads (one per block row) form their
-//      samples (vertical filter + area average) and run the chroma row DCT;
-//   3. chroma threads run the column DCT, quantise and store.
+//      samples (vertical filter + area average), run the chroma row DCT and
+//      then, as the block's column threads, the column DCT, quantise and store
+//      (the 8 threads of a block are lanes of one wave: no barrier between).
 // Quantised columns turn into 16-byte rows through an int16 transpose in the
 // block's own (already consumed) LDS region: the 8 lanes of a block belong to
 // one wave, whose LDS operations execute in order, so no barrier is needed.
@@ -442,7 +453,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float R = (float)byte_at(w, 3 * k), G = (float)byte_at(w, 3 * k + 1), B = (float)byte_at(w, 3 * k + 2);
-        yy[k] = luma32(R, G, B) - 128.0f;
+        yy[k] = luma32m(R, G, B);
         cb[k] = cb32(R, G, B);
         cr[k] = cr32(R, G, B);
       }
@@ -603,9 +614,10 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       float4* d4 = reinterpret_cast<float4*>(s_cd + (blk - C::NYB) * BS32 + i * 8);
       d4[0] = make_float4(v[0], v[1], v[2], v[3]);
       d4[1] = make_float4(v[4], v[5], v[6], v[7]);
+      // the block's 8 row tasks are lanes of this wave: its columns follow
+      // without a workgroup barrier (LDS operations of a wave execute in order)
+      column(s_cd + (blk - C::NYB) * BS32, 8, plane);
     }
-    __syncthreads();
-    if (plane != 0) column(s_cd + (blk - C::NYB) * BS32, 8, plane);
   } else {
     float* P = plane == 0 ? s_y : (plane == 1 ? s_cb : s_cr);
     column(P + by_t * 8 * TW + bx_t * 8, TW, plane);
@@ -916,7 +928,12 @@ void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, f
         const double e2l = E2[k][l] > E2[l][k] ? E2[k][l] : E2[l][k];
         const double E = e2l * (1 + 1e-5) + 1e-9;
         const double t = E / Q[k * 8 + l] * (1 + 1e-5) + 1e-7;
-        thr[p * 64 + k * 8 + l] = (float)t * (1.0f + 0x1p-20f);
+        // stored as the certification limit on |t - rint(t)|: 0.5 - t - 2^-23
+        // (covers the fp32 rounding of the in-kernel fma), rounded down
+        const double lim = 0.5 - t * (1 + 0x1p-20) - 0x1p-23;
+        float f = (float)lim;
+        if ((double)f > lim) f = nextafterf(f, 0.0f);
+        thr[p * 64 + k * 8 + l] = f;
       }
     }
   }

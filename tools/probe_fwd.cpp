@@ -91,6 +91,16 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, rect);
     hipMemcpy(&hc, cnt, 4, hipMemcpyDeviceToHost);
     printf("flagged blocks (64 frames): %u\n", hc);
+    std::vector<uint2> hl(hc);
+    hipMemcpy(hl.data(), fl, 8 * (size_t)hc, hipMemcpyDeviceToHost);
+    unsigned byplane[3] = {0, 0, 0};
+    for (auto& e : hl) byplane[(e.y >> 24) & 3]++;
+    printf("  by plane: Y %u  Cb %u  Cr %u\n", byplane[0], byplane[1], byplane[2]);
+    for (int p = 0; p < 2; ++p) {
+      printf("  thr[%d] (x1e4):", p);
+      for (int i = 0; i < 64; i += 9) printf(" %.3f", hq.thr[p][i] * 1e4);
+      printf("\n");
+    }
   }
   printf("done\n");
   return 0;
