@@ -52,7 +52,10 @@ struct Inv {
 constexpr int MS = 72;  // doubles per block in the transpose buffer (64 + 8: conflict-free column writes)
 
 // Dequantize (quantizer.py:27-29) and IDCT column v of a block (axis 0 first,
-// dct_engine.py:12-14) into dst[r*8 + v].
+// dct_engine.py:12-14) into dst[r*8 + v].  `q` holds Q/16: q*Q is an exact
+// integer and scaling by 2^-4 commutes exactly with every rounding of the
+// transform (no subnormals arise), so IDCT(q*Q/16) == IDCT(q*Q)/16 bit for bit
+// and pocketfft's fct = 1/16 costs nothing later.
 __device__ __forceinline__ void idct_col(const int16_t* __restrict__ blk, const double* __restrict__ q, int v,
                                          double* __restrict__ dst) {
   double c[8];
@@ -71,7 +74,7 @@ __device__ __forceinline__ void idct_row(const double* __restrict__ src, int u, 
   dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const double s = c[k] * 0.0625 + 128.0;
+    const double s = c[k] + 128.0;  // the fct 1/16 rides on the prescaled quantiser (exact)
     c[k] = fmin(fmax(s, 0.0), 255.0);
   }
 }
@@ -83,6 +86,13 @@ __device__ __forceinline__ void idct_row(const double* __restrict__ src, int u, 
 // rejects odd ones), so the scale is exactly 1/2: pixel 2m reads
 // (s[m-1], s[m]) with weights (1/4, 3/4) and pixel 2m+1 reads (s[m], s[m+1])
 // with (3/4, 1/4), so each product serves two pixels.
+// cv2's vertical blend r0*b0 + r1*b1 for an exact 2x upsample, where
+// {b0, b1} = {1/4, 3/4}: the quarter product is exact, so one fma reproduces
+// the two roundings of the reference.
+__device__ __forceinline__ double vblend(double r0, double r1, double b0) {
+  return b0 == 0.25 ? fma(r0, 0.25, r1 * 0.75) : fma(r1, 0.25, r0 * 0.75);
+}
+
 template <int MODE>
 __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo& g, int x0, int cwx0, int wr0,
                                         int wr1, double b0, double b1, double (&C)[8]) {
@@ -96,21 +106,19 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
 #pragma unroll
     for (int rr = 0; rr < (I::SY == 2 ? 2 : 1); ++rr) {
       const double* s = &cw[(rr ? wr1 : wr0) * I::CWC + c0];
-      double q25[6], q75[6];
+      // s*0.25 is exact, so fl(s0*0.25 + fl(s1*0.75)) == fma(s0, 0.25, fl(s1*0.75))
+      double q75[6];
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        q25[j] = s[j] * 0.25;
-        q75[j] = s[j] * 0.75;
-      }
+      for (int j = 1; j < 5; ++j) q75[j] = s[j] * 0.75;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const double e = q25[i] + q75[i + 1], o = q75[i + 1] + q25[i + 2];
+        const double e = fma(s[i], 0.25, q75[i + 1]), o = fma(s[i + 2], 0.25, q75[i + 1]);
         if (rr == 0) {
           h0[2 * i] = e;
           h0[2 * i + 1] = o;
         } else {
-          C[2 * i] = h0[2 * i] * b0 + e * b1;
-          C[2 * i + 1] = h0[2 * i + 1] * b0 + o * b1;
+          C[2 * i] = vblend(h0[2 * i], e, b0);
+          C[2 * i + 1] = vblend(h0[2 * i + 1], o, b0);
         }
       }
     }
@@ -128,7 +136,7 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
         const int e = (side == 0 ? 0 : g.wc - 1) - cwx0;
         const double v0 = cw[wr0 * I::CWC + e];
         double v = v0;
-        if constexpr (I::SY == 2) v = v0 * b0 + cw[wr1 * I::CWC + e] * b1;
+        if constexpr (I::SY == 2) v = vblend(v0, cw[wr1 * I::CWC + e], b0);
 #pragma unroll
         for (int k = 0; k < 8; ++k)
           if (k == kl) C[k] = v;
@@ -156,7 +164,7 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int Y0 = ty * I::TH, X0 = tx * I::TW;
   const int16_t* cf = coeffs + (size_t)frame * g.cpf;
-  if (tid < 64) s_q[tid] = fq[frame].q[tid];
+  if (tid < 64) s_q[tid] = fq[frame].q[tid] * 0.0625;  // Q/16, exact
   if (XTRA && tid == 0) s_sse = 0ull;
   __syncthreads();
 
@@ -242,25 +250,29 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
         // one chroma plane at a time to bound register pressure: B and G's Cb
         // term first, then R and G (same expressions, same order)
         double C[8], Gt[8];
+        // floor(clip(v, 0, 255)) == clamp(trunc(v), 0, 255) for |v| < 2^31:
+        // one conversion and integer min/max instead of two fp64 ops
         chroma8<MODE>(s_cw[0], g, x0, cwx0, wr0, wr1, b0, b1, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const double B = fmin(fmax(Yv[k] + 1.772 * (C[k] - 128.0), 0.0), 255.0);
+          const double B = Yv[k] + 1.772 * (C[k] - 128.0);
           Gt[k] = Yv[k] - 0.344136 * (C[k] - 128.0);
-          Bc[k] = B;
+          if constexpr (XTRA > 1) Bc[k] = fmin(fmax(B, 0.0), 255.0);
           const int b = 3 * k + 2;
-          pk[b >> 2] |= (uint32_t)(int)B << (8 * (b & 3));
+          pk[b >> 2] |= (uint32_t)clampi((int)B, 0, 255) << (8 * (b & 3));
         }
         chroma8<MODE>(s_cw[1], g, x0, cwx0, wr0, wr1, b0, b1, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const double R = fmin(fmax(Yv[k] + 1.402 * (C[k] - 128.0), 0.0), 255.0);
-          const double G = fmin(fmax(Gt[k] - 0.714136 * (C[k] - 128.0), 0.0), 255.0);
-          Rc[k] = R;
-          Gc[k] = G;
+          const double R = Yv[k] + 1.402 * (C[k] - 128.0);
+          const double G = Gt[k] - 0.714136 * (C[k] - 128.0);
+          if constexpr (XTRA > 1) {
+            Rc[k] = fmin(fmax(R, 0.0), 255.0);
+            Gc[k] = fmin(fmax(G, 0.0), 255.0);
+          }
           const int b = 3 * k;
-          pk[b >> 2] |= (uint32_t)(int)R << (8 * (b & 3));
-          pk[(b + 1) >> 2] |= (uint32_t)(int)G << (8 * ((b + 1) & 3));
+          pk[b >> 2] |= (uint32_t)clampi((int)R, 0, 255) << (8 * (b & 3));
+          pk[(b + 1) >> 2] |= (uint32_t)clampi((int)G, 0, 255) << (8 * ((b + 1) & 3));
         }
       }
       const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
@@ -329,7 +341,10 @@ __global__ void __launch_bounds__(64) k_sel_recon(const int16_t* __restrict__ co
   __shared__ __attribute__((aligned(16))) double s[MS];
   const int t = threadIdx.x;
   if (t < 8) {
-    idct_col(coeffs + (long long)sel_blk * 64, fq[0].q, t, s);
+    double qs[64];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) qs[r * 8 + t] = fq[0].q[r * 8 + t] * 0.0625;
+    idct_col(coeffs + (long long)sel_blk * 64, qs, t, s);
   }
   __syncthreads();
   if (t < 8) {
