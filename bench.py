@@ -2,8 +2,9 @@
 """bench.py — Mpixels/s of the forward+inverse block-DCT pipeline @ Q=50 4:2:0 (+PSNR vs reference).
 
 Workload (BASELINE.json configs[1]): 1920x1080 uniform-random RGB frames, Q=50,
-4:2:0, prefilter ON, through the fused HIP kernels (k_fwd: RGB -> int16
-coefficients; k_inv: coefficients -> RGB).  One step = one pass over a batch of
+4:2:0, prefilter ON, through the fused HIP kernels (forward phase: k_fwd32i /
+k_fwd32 / k_fix_fwd, RGB -> int16 coefficients + statistics; inverse phase:
+k_inv2, coefficients -> RGB).  One step = one pass over a batch of
 `--frames` device-resident 1080p frames per GPU (default 64, the size of the
 reference's cfg4 batch sweep); inputs are generated on the device before the
 timed region.  Multi-GPU: one process per GPU (torchrun), frames shard across
@@ -144,8 +145,10 @@ def main():
     dom = 'k_fwd' if t_fwd >= t_inv else 'k_inv'
     t_dom = max(t_fwd, t_inv)
     achieved = (bytes_fwd if dom == 'k_fwd' else bytes_inv) / (t_dom * 1e-3) / 1e9
-    kname = f'k_fwd<{ {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[args.mode] },{"true" if args.prefilter else "false"}>' \
-        if dom == 'k_fwd' else f'k_inv<{ {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[args.mode] }>'
+    mcode = {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[args.mode]
+    pfs = 'true' if (args.prefilter and mcode != 0) else 'false'
+    kname = (f'k_fwd32i<{mcode},{pfs}> + k_fwd32<{mcode},{pfs}> (border tiles) + k_fix_fwd'
+             if dom == 'k_fwd' else f'k_inv2<{mcode},0>')
     traffic = None
     tf = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tf):
