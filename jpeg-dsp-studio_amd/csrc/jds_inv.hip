@@ -171,6 +171,7 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
   // ---- 1. chroma window ----------------------------------------------------
   const int cby0 = Y0 / (8 * I::SY) - I::RY, cbx0 = X0 / (8 * I::SX) - I::RX;
   const int cwy0 = Y0 / I::SY - I::RY, cwx0 = X0 / I::SX - I::RX;
+#ifndef JDS_PROBE_NOCHROMA  // tools/probe: skip the chroma window
 #pragma unroll 1
   for (int p = 0; p < 2; ++p) {
     const int16_t* cp = cf + (p == 0 ? g.off_cb : g.off_cr);
@@ -210,6 +211,7 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
     __syncthreads();
   }
 
+#endif
   // ---- 2. luma rounds: IDCT, upsample, colour, store --------------------------
   const bool want_in = XTRA > 0;
   unsigned long long sse = 0ull;
@@ -252,7 +254,11 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
         double C[8], Gt[8];
         // floor(clip(v, 0, 255)) == clamp(trunc(v), 0, 255) for |v| < 2^31:
         // one conversion and integer min/max instead of two fp64 ops
+#ifndef JDS_PROBE_NOUPS
         chroma8<MODE>(s_cw[0], g, x0, cwx0, wr0, wr1, b0, b1, C);
+#else
+        for (int k = 0; k < 8; ++k) C[k] = Yv[k] * 0.5;
+#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const double B = Yv[k] + 1.772 * (C[k] - 128.0);
@@ -261,7 +267,11 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
           const int b = 3 * k + 2;
           pk[b >> 2] |= (uint32_t)clampi((int)B, 0, 255) << (8 * (b & 3));
         }
+#ifndef JDS_PROBE_NOUPS
         chroma8<MODE>(s_cw[1], g, x0, cwx0, wr0, wr1, b0, b1, C);
+#else
+        for (int k = 0; k < 8; ++k) C[k] = Yv[k] * 0.25;
+#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const double R = Yv[k] + 1.402 * (C[k] - 128.0);
