@@ -9,15 +9,17 @@
 //
 // Work decomposition (one workgroup per TH x TW pixel tile, tiles laid from the
 // top-left corner):
-//   1. chroma, one plane at a time: the tile's chroma blocks plus the ring the
+//   1. chroma, both planes: the tile's chroma blocks plus the ring the
 //      bilinear upsample reaches into.  Column (axis-0) passes run one thread
 //      per block column, straight from the int16 coefficients in HBM/L2 into
-//      an fp64 transpose buffer; row (axis-1) passes run only for the block
-//      rows the window needs (a top/bottom ring block contributes one row), and
-//      land in an fp64 LDS chroma window.
+//      an fp64 transpose buffer; row (axis-1) passes run on the same 8 threads
+//      (lanes of one wave: no barrier) for the block rows the window needs (a
+//      top/bottom ring block contributes one row), into an fp64 LDS window.
+//      One workgroup barrier completes the window.
 //   2. luma, NT/8 blocks per round: the same column pass, then each thread
 //      owns one 8-pixel block row: row IDCT -> Y in registers, chroma taps from
-//      the LDS window, colour, clip, truncate, one 24-byte store.
+//      the LDS window, colour, clip, truncate, one 24-byte store.  Again
+//      wave-local: no barriers.
 // Y never goes through LDS.  The upsample shares products between
 // neighbouring pixels (same IEEE operations, same results).
 #include <hip/hip_runtime.h>
@@ -172,45 +174,33 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
   const int cby0 = Y0 / (8 * I::SY) - I::RY, cbx0 = X0 / (8 * I::SX) - I::RX;
   const int cwy0 = Y0 / I::SY - I::RY, cwx0 = X0 / I::SX - I::RX;
 #ifndef JDS_PROBE_NOCHROMA  // tools/probe: skip the chroma window
+  // Each block's column pass and row pass run on the same 8 lanes (one wave),
+  // whose LDS operations execute in order: no workgroup barrier until the
+  // window is complete.  A top (bottom) ring block contributes only its last
+  // (first) row.
+  if (tid < I::NCB * 8) {
+    const int i = lb / I::CBC, j = lb - i * I::CBC;
+    const int by = cby0 + i, bx = cbx0 + j;
+    const bool bvalid = by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx;
+    const bool need = !I::RY || (i == 0 ? lv == 7 : (i == I::CBR - 1 ? lv == 0 : true));
 #pragma unroll 1
-  for (int p = 0; p < 2; ++p) {
-    const int16_t* cp = cf + (p == 0 ? g.off_cb : g.off_cr);
-    if (tid < I::NCB * 8) {
-      const int i = lb / I::CBC, j = lb - i * I::CBC;
-      const int by = cby0 + i, bx = cbx0 + j;
-      if (by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx)
+    for (int p = 0; p < 2; ++p) {
+      const int16_t* cp = cf + (p == 0 ? g.off_cb : g.off_cr);
+      if (bvalid) {
         idct_col(cp + ((long long)by * g.ncx + bx) * 64, s_q, lv, s_mid + lb * MS);
-    }
-    __syncthreads();
-    if (tid < I::NROW) {
-      int i, j, u;
-      constexpr int FULL = (I::CBR - 2 * I::RY) * I::CBC * 8;
-      if (tid < FULL) {
-        i = I::RY + tid / (I::CBC * 8);
-        const int rem = tid - (i - I::RY) * (I::CBC * 8);
-        j = rem >> 3;
-        u = rem & 7;
-      } else {  // top ring contributes its last row, bottom ring its first
-        const int e = tid - FULL;
-        const bool top = e < I::CBC;
-        i = top ? 0 : I::CBR - 1;
-        j = top ? e : e - I::CBC;
-        u = top ? 7 : 0;
-      }
-      const int by = cby0 + i, bx = cbx0 + j;
-      if (by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx) {
-        double c[8];
-        idct_row(s_mid + (i * I::CBC + j) * MS, u, c);
-        double* w = &s_cw[p][(by * 8 + u - cwy0) * I::CWC];
-        const int wc0 = bx * 8 - cwx0;
+        if (need) {
+          double c[8];
+          idct_row(s_mid + lb * MS, lv, c);
+          double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWC];
+          const int wc0 = bx * 8 - cwx0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k];
+          for (int k = 0; k < 8; ++k)
+            if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k];
+        }
       }
     }
-    __syncthreads();
   }
-
+  __syncthreads();
 #endif
   // ---- 2. luma rounds: IDCT, upsample, colour, store --------------------------
   const bool want_in = XTRA > 0;
@@ -225,7 +215,7 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
     const int by = Y0 / 8 + bi, bx = X0 / 8 + bj;
     const bool bvalid = by < g.nby && bx < g.nbx;
     if (bvalid) idct_col(cf + ((long long)by * g.nbx + bx) * 64, s_q, lv, s_mid + lb * MS);
-    __syncthreads();
+    // (the block's row pass reads what its own wave wrote: no barrier)
     const int y = by * 8 + lv, x0 = bx * 8;
     if (bvalid && y < g.H && x0 < g.W) {
       double Yv[8];
@@ -322,7 +312,6 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
         }
       }
     }
-    __syncthreads();
   }
 
   if constexpr (XTRA > 0) {
