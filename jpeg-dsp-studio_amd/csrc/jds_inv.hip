@@ -68,6 +68,27 @@ __device__ __forceinline__ void idct_col(const int16_t* __restrict__ blk, const 
   for (int r = 0; r < 8; ++r) dst[r * 8 + v] = c[r];
 }
 
+// The same with the column's coefficients already loaded (software
+// prefetch: the loads of the next block are issued before this one's math).
+struct Col16 {
+  int16_t q[8];
+};
+__device__ __forceinline__ Col16 load_col(const int16_t* __restrict__ blk, int v, bool ok) {
+  Col16 c;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) c.q[r] = ok ? blk[r * 8 + v] : (int16_t)0;
+  return c;
+}
+__device__ __forceinline__ void idct_col(const Col16& in, const double* __restrict__ q, int v,
+                                         double* __restrict__ dst) {
+  double c[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) c[r] = (double)in.q[r] * q[r * 8 + v];
+  dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) dst[r * 8 + v] = c[r];
+}
+
 // Row u of a column-transformed block: axis-1 IDCT, fct 1/16, +128, clip
 // (dct_engine.py:23-27).
 __device__ __forceinline__ void idct_row(const double* __restrict__ src, int u, double (&c)[8]) {
@@ -140,8 +161,7 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
         double v = v0;
         if constexpr (I::SY == 2) v = vblend(v0, cw[wr1 * I::CWC + e], b0);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k == kl) C[k] = v;
+        for (int k = 0; k < 8; ++k) C[k] = k == kl ? v : C[k];  // selects, not branches
       }
     }
   }
@@ -173,21 +193,38 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
   // ---- 1. chroma window ----------------------------------------------------
   const int cby0 = Y0 / (8 * I::SY) - I::RY, cbx0 = X0 / (8 * I::SX) - I::RX;
   const int cwy0 = Y0 / I::SY - I::RY, cwx0 = X0 / I::SX - I::RX;
-#ifndef JDS_PROBE_NOCHROMA  // tools/probe: skip the chroma window
   // Each block's column pass and row pass run on the same 8 lanes (one wave),
   // whose LDS operations execute in order: no workgroup barrier until the
   // window is complete.  A top (bottom) ring block contributes only its last
   // (first) row.
+  // luma round 0's coefficients are requested before any chroma math
+  auto luma_blk = [&](int r, int& by, int& bx) {
+    const int blk = r * I::RB + lb;
+    const int bi = blk / I::YBC, bj = blk - bi * I::YBC;
+    by = Y0 / 8 + bi;
+    bx = X0 / 8 + bj;
+    return by < g.nby && bx < g.nbx;
+  };
+  Col16 lq;
+  {
+    int by, bx;
+    const bool ok = luma_blk(0, by, bx);
+    lq = load_col(cf + ((long long)by * g.nbx + bx) * 64, lv, ok);
+  }
+#ifndef JDS_PROBE_NOCHROMA  // tools/probe: skip the chroma window
   if (tid < I::NCB * 8) {
     const int i = lb / I::CBC, j = lb - i * I::CBC;
     const int by = cby0 + i, bx = cbx0 + j;
     const bool bvalid = by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx;
     const bool need = !I::RY || (i == 0 ? lv == 7 : (i == I::CBR - 1 ? lv == 0 : true));
+    const long long boff = ((long long)by * g.ncx + bx) * 64;
+    Col16 cq = load_col(cf + g.off_cb + boff, lv, bvalid);
 #pragma unroll 1
     for (int p = 0; p < 2; ++p) {
-      const int16_t* cp = cf + (p == 0 ? g.off_cb : g.off_cr);
+      const Col16 cur = cq;
+      if (p == 0) cq = load_col(cf + g.off_cr + boff, lv, bvalid);  // next plane in flight
       if (bvalid) {
-        idct_col(cp + ((long long)by * g.ncx + bx) * 64, s_q, lv, s_mid + lb * MS);
+        idct_col(cur, s_q, lv, s_mid + lb * MS);
         if (need) {
           double c[8];
           idct_row(s_mid + lb * MS, lv, c);
@@ -210,11 +247,15 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
   uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
 #pragma unroll 1
   for (int r = 0; r < I::NYB / I::RB; ++r) {
-    const int blk = r * I::RB + lb;
-    const int bi = blk / I::YBC, bj = blk - bi * I::YBC;
-    const int by = Y0 / 8 + bi, bx = X0 / 8 + bj;
-    const bool bvalid = by < g.nby && bx < g.nbx;
-    if (bvalid) idct_col(cf + ((long long)by * g.nbx + bx) * 64, s_q, lv, s_mid + lb * MS);
+    int by, bx;
+    const bool bvalid = luma_blk(r, by, bx);
+    const Col16 cur = lq;
+    if (r + 1 < I::NYB / I::RB) {  // next round's coefficients in flight
+      int by1, bx1;
+      const bool ok1 = luma_blk(r + 1, by1, bx1);
+      lq = load_col(cf + ((long long)by1 * g.nbx + bx1) * 64, lv, ok1);
+    }
+    if (bvalid) idct_col(cur, s_q, lv, s_mid + lb * MS);
     // (the block's row pass reads what its own wave wrote: no barrier)
     const int y = by * 8 + lv, x0 = bx * 8;
     if (bvalid && y < g.H && x0 < g.W) {
