@@ -44,6 +44,8 @@ def parse():
     ap.add_argument('--quality', type=int, default=50)
     ap.add_argument('--mode', default='4:2:0')
     ap.add_argument('--prefilter', type=int, default=1)
+    ap.add_argument('--block', type=int, default=8, choices=(8, 16),
+                    help='16 = the configs[4] 16x16 stretch path (jds_b16.hip, exact fp64 kernels)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
@@ -52,21 +54,21 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(frames_host, quality, mode, pf, budget_s):
+def cpu_baseline(frames_host, quality, mode, pf, budget_s, block=8):
     """The oracle (vectorised NumPy/SciPy restatement) on the host, 1 thread,
     on a bounded sample of the same workload (whole 1080p frames)."""
     from oracle import cpu_ref
     t0 = time.perf_counter()
     n = 0
     while n < len(frames_host):
-        cpu_ref.compress_reconstruct(frames_host[n], quality, 8, mode, pf, metrics=False)
+        cpu_ref.compress_reconstruct(frames_host[n], quality, block, mode, pf, metrics=False, stretch=block == 16)
         n += 1
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
     h, w = frames_host.shape[1:3]
     return {'value': round(n * h * w / dt / 1e6, 4), 'unit': 'Mpixels/s', 'cores': 1, 'kind': 'port',
-            'sample': f'{n} x {w}x{h} frames (Q{quality} {mode} prefilter={bool(pf)}) through oracle/cpu_ref.py '
+            'sample': f'{n} x {w}x{h} frames (Q{quality} {mode} prefilter={bool(pf)} {block}x{block}) through oracle/cpu_ref.py '
                       f'compress_reconstruct without SSIM, {dt:.1f} s, 1 thread'}
 
 
@@ -92,7 +94,7 @@ def main():
     B, H, W = args.frames, args.height, args.width
     K = max(1, min(args.chunks, B))
     qt = scale_quant_matrix(JPEG_LUMA_Q50, args.quality)
-    prm = _abi.make_params(args.quality, qt, args.mode, bool(args.prefilter), codec.gaussian_kernel3())
+    prm = _abi.make_params(args.quality, qt, args.mode, bool(args.prefilter), codec.gaussian_kernel3(), args.block)
     # the batch in K chunks (one plan each) so the forward of chunk c+1 runs
     # beside the inverse of chunk c on a second stream
     bounds = [(B * c // K, B * (c + 1) // K) for c in range(K)]
@@ -172,14 +174,18 @@ def main():
     achieved = (bytes_fwd if dom == 'k_fwd' else bytes_inv) / (t_dom * 1e-3) / 1e9
     mcode = {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[args.mode]
     pfs = 'true' if (args.prefilter and mcode != 0) else 'false'
-    kname = (f'k_fwd32i<{mcode},{pfs}> + k_fwd32<{mcode},{pfs}> (border tiles) + k_fix_fwd'
-             if dom == 'k_fwd' else f'k_inv2<{mcode},0>')
+    if args.block == 16:
+        kname = f'k_fwd16<{mcode},{pfs}>' if dom == 'k_fwd' else f'k_chroma16<{mcode}> + k_inv16<{mcode}>'
+    else:
+        kname = (f'k_fwd32i<{mcode},{pfs}> + k_fwd32<{mcode},{pfs}> (border tiles) + k_fix_fwd'
+                 if dom == 'k_fwd' else f'k_inv2<{mcode},0>')
     traffic = None
     tf = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tf):
         try:
             rec = json.load(open(tf))
-            base = f'{W}x{H}_q{args.quality}_{args.mode}_pf{int(bool(args.prefilter))}_b'
+            base = (f'{W}x{H}_q{args.quality}_{args.mode}_pf{int(bool(args.prefilter))}'
+                    + ('_B16' if args.block == 16 else '') + '_b')
             nl = bounds[0][1] - bounds[0][0]  # frames per launch
             if base + str(nl) in rec:
                 traffic = rec[base + str(nl)].get(dom)
@@ -204,8 +210,9 @@ def main():
         'vs_baseline': None,
         'dtype': 'f32+f64',  # forward: fp32 certified + fp64 fix-up; inverse: fp64 (u8 in/out, int16 coefficients)
         'data': 'synthetic (uniform random RGB generated on device)',
-        'config': {'workload': f'{W}x{H} RGB, Q={args.quality}, {args.mode}, prefilter={"on" if args.prefilter else "off"} '
-                               f'(BASELINE configs[1])',
+        'config': {'workload': f'{W}x{H} RGB, Q={args.quality}, {args.mode}, prefilter={"on" if args.prefilter else "off"}, '
+                               f'{args.block}x{args.block} blocks '
+                               + ('(BASELINE configs[1])' if args.block == 8 else '(BASELINE configs[4] stretch)'),
                    'frames_per_gpu_per_step': B, 'global_batch_frames': B * world, 'chunks': K,
                    'parallelism': f'frame-shard x{world}'},
         'roofline': {'bound': 'hbm', 'kernel': kname, 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
@@ -221,7 +228,8 @@ def main():
         # PSNR / bytes vs the reference restatement on frame 0 (outside the timed region)
         from oracle import cpu_ref
         f0 = rgb[0].cpu().numpy()
-        ref = cpu_ref.compress_reconstruct(f0, args.quality, 8, args.mode, bool(args.prefilter), metrics=False)
+        ref = cpu_ref.compress_reconstruct(f0, args.quality, args.block, args.mode, bool(args.prefilter),
+                                           metrics=False, stretch=args.block == 16)
         rec0, cf0 = out[0].cpu().numpy(), coeffs[0].cpu().numpy()
         mse = np.mean((f0.astype(np.float64) - rec0) ** 2)
         mse_ref = np.mean((f0.astype(np.float64) - ref['reconstructed']) ** 2)
@@ -233,7 +241,7 @@ def main():
         n = max(1, min(B, 64))
         host = rgb[:n].cpu().numpy()
         result['cpu_baseline'] = cpu_baseline(host, args.quality, args.mode, bool(args.prefilter),
-                                              args.cpu_baseline_seconds)
+                                              args.cpu_baseline_seconds, args.block)
     else:
         result['cpu_baseline'] = None
     for p_ in plans:

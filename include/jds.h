@@ -21,11 +21,11 @@
 extern "C" {
 #endif
 
-#define JDS_ABI_VERSION 1
+#define JDS_ABI_VERSION 2
 
 #define JDS_OK       0
 #define JDS_EINVAL  (-1)  /* bad argument                    -> ValueError   */
-#define JDS_ENOTSUP (-2)  /* e.g. block_size != 8, odd size  -> ValueError   */
+#define JDS_ENOTSUP (-2)  /* e.g. block_size not 8/16, odd size -> ValueError */
 #define JDS_EHIP    (-3)  /* HIP runtime / device failure     -> RuntimeError */
 #define JDS_ENOMEM  (-4)  /* device allocation failed         -> RuntimeError */
 
@@ -46,7 +46,12 @@ typedef struct jds_plan jds_plan;  /* fixed geometry + per-frame quant tables, d
 /* Per-frame parameters.  Mirrors CompressionParams (models/compression_params.py:7-20);
  * the tables are computed on the host exactly as the reference does. */
 typedef struct {
-  int32_t block_size;  /* only 8 is supported (the reference crashes otherwise, engines/quantizer.py:24) */
+  /* 8: the reference's path.  16: the BASELINE configs[4] stretch the reference
+   * stubs (models/compression_params.py:19-20 accepts it, engines/quantizer.py:24
+   * then fails); its table is np.kron(qtable, ones((2, 2))), i.e.
+   * Q16[u][v] = qtable[(u/2)*8 + v/2] (build decision).  Other values
+   * fail with the reference's broadcast error (JDS_ENOTSUP). */
+  int32_t block_size;
   int32_t quality;     /* 1..100 (informational; the table below is authoritative) */
   int32_t subsampling; /* JDS_SS_* */
   int32_t prefilter;   /* 0/1; ignored for 4:4:4 (engines/color_space.py:34-35) */
@@ -61,7 +66,7 @@ typedef struct {
   uint64_t nonzero;             /* count of q != 0 */
   uint64_t total_coeffs;        /* all_quantized_coeffs.size */
   uint64_t magnitude_bits;      /* sum over q != 0 of ceil(log2(|q|+1)) + 1 */
-  uint64_t block_overhead_bits; /* 2 * ceil(H/8) * ceil(W/8) (luma grid only) */
+  uint64_t block_overhead_bits; /* 2 * ceil(H/B) * ceil(W/B) (luma grid only) */
   uint64_t hist[50];            /* np.histogram(q, bins=50, range=(-100, 100))[0] */
   uint64_t sse_rgb;             /* sum (orig - rec)^2 over H*W*3 uint8 samples (JDS_RUN_SSE) */
   double sse_y;                 /* sum (Y(orig) - Y(rec))^2, Y = .299R+.587G+.114B (JDS_RUN_SSE) */
@@ -78,12 +83,13 @@ typedef struct {
   int64_t chroma_h, chroma_w;        /* after subsampling, before padding */
   int64_t y_blocks_y, y_blocks_x;    /* padded luma block grid */
   int64_t c_blocks_y, c_blocks_x;    /* padded chroma block grid (per plane) */
-  int64_t coeffs_per_frame;          /* 64 * (Y blocks + 2 * chroma blocks) */
+  int64_t coeffs_per_frame;          /* B*B * (Y blocks + 2 * chroma blocks) */
   int64_t cb_offset, cr_offset;      /* coefficient offsets of the Cb / Cr planes */
   int32_t tiles, threads_fwd, threads_inv, reserved;
 } jds_geometry;
 
-/* IntermediateData.selected_block_* (engines/pipeline.py:128-151) */
+/* IntermediateData.selected_block_* (engines/pipeline.py:128-151); 8x8 path only
+ * (with block_size 16, *sel_valid is always 0) */
 typedef struct {
   double original[64], shifted[64], dct[64];
   int16_t quantized[64];
@@ -155,11 +161,20 @@ int jds_stage_upsample(jds_ctx* ctx, const double* in, int64_t h, int64_t w, int
 int jds_stage_block_dct(jds_ctx* ctx, const double* in, double* out, int64_t n_blocks, int32_t op);
 int jds_stage_quantize(jds_ctx* ctx, const void* in, const double* qtable, void* out, int64_t n,
                        int32_t dequant);
+/* The same for 8x8 or 16x16 blocks (block_size 8 / 16; dctn / idctn of a 16x16
+ * block, dct_engine.py:7-27) and for a 64- or 256-entry table broadcast over
+ * n values (quantizer.py:22-29 with a 16x16 table). */
+int jds_stage_block_dct_n(jds_ctx* ctx, const double* in, double* out, int64_t n_blocks, int32_t block_size,
+                          int32_t op);
+int jds_stage_quantize_n(jds_ctx* ctx, const void* in, const double* qtable, int32_t table_len, void* out,
+                         int64_t n, int32_t dequant);
 
 /* Test-only: evaluate the device DCT expressions (jds_dct8.hpp) on the host so
  * the CPU test suite can pin them against SciPy without a GPU.  Not used by
  * any product path.  in/out: n blocks of 8x8 f64; inverse: 0 = dctn, 1 = idctn. */
 int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t inverse);
+/* The same for 16x16 blocks (jds_dct16.hpp). */
+int jds_selftest_dct16x16(const double* in, double* out, int64_t n, int32_t inverse);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,7 @@
 #include <mutex>
 #include <new>
 
+#include "jds_dct16.hpp"
 #include "jds_dct8.hpp"
 #include "jds_internal.hpp"
 
@@ -36,8 +37,14 @@ hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse
 hipError_t stage_subsample(const double* in, double* tmp, double* tmp2, double* out, int H, int W, int sy,
                            int prefilter, const double* k, hipStream_t s);
 hipError_t stage_resize(const double* in, int h, int w, double* out, int H, int W, int nearest, hipStream_t s);
-hipError_t stage_block(const double* in, double* out, long long n, int op, hipStream_t s);
-hipError_t stage_quant(const void* in, const double* q, void* out, long long n, int dequant, hipStream_t s);
+hipError_t stage_block(const double* in, double* out, long long n, int bs, int op, hipStream_t s);
+hipError_t stage_quant(const void* in, const double* q, void* out, long long n, int dequant, int period,
+                       hipStream_t s);
+int tile_dims16(int mode, int* MY, int* MX);
+hipError_t launch_codec16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
+                          int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st, double* part,
+                          double* planes, bool want_sse, double* err_y, double* err_rgb, hipStream_t s,
+                          hipEvent_t* ev, int phases);
 }
 
 // skimage: C1 = (K1 * R) ** 2, C2 = (K2 * R) ** 2 with R = data_range = 255
@@ -92,6 +99,7 @@ struct jds_ctx {
   DevBuf ss_planes, ss_map, ss_chunks, ss_out, img_a, img_b;
   DevBuf st[5];  // per-stage API staging
   DevBuf chunks;
+  DevBuf planes;  // 16x16 path: reconstructed chroma planes
 };
 
 // SSIM scratch in the context; returns the device pointer of 5 result doubles
@@ -114,15 +122,20 @@ struct jds_plan {
   // fast path: fp32 tables, fix-up lists and counters
   DevBuf fq32, gk32, fixlist, counters, part32;  // part32: per-tile forward statistics
   Side side;  // border tiles run beside interior tiles
+  DevBuf planes;  // 16x16 path: reconstructed chroma planes (n x 2 x hc x wc f64)
 };
 
 // ------------------------------------------------------------- geometry --
 
 static int make_geo(const jds_params* p, int64_t H, int64_t W, Geo* g, int* mode_out, bool* pf_out) {
   if (!p || !g) return fail(JDS_EINVAL, "null argument");
-  if (p->block_size != 8)
+  // 8: the reference's path.  16: the configs[4] stretch (jds_b16.hip; table
+  // np.kron(Q8, ones((2,2)))).  Anything else fails the way the reference's
+  // quantizer does (engines/quantizer.py:24).
+  if (p->block_size != 8 && p->block_size != 16)
     return fail(JDS_ENOTSUP, "operands could not be broadcast together with shapes (%d,%d) (8,8) ",
                 p->block_size, p->block_size);
+  const int B = p->block_size;
   if (p->subsampling < JDS_SS_444 || p->subsampling > JDS_SS_420)
     return fail(JDS_EINVAL, "Unknown subsampling mode: %d", p->subsampling);
   if (H < 1 || W < 1 || H > 65536 || W > 65536 || H * W > (int64_t)1 << 28)
@@ -140,12 +153,14 @@ static int make_geo(const jds_params* p, int64_t H, int64_t W, Geo* g, int* mode
   G.W = (int)W;
   G.hc = (int)(H / sy);
   G.wc = (int)(W / sx);
-  G.nby = (int)((H + 7) / 8);
-  G.nbx = (int)((W + 7) / 8);
-  G.ncy = (G.hc + 7) / 8;
-  G.ncx = (G.wc + 7) / 8;
+  G.bs = B;
+  G.nby = (int)((H + B - 1) / B);
+  G.nbx = (int)((W + B - 1) / B);
+  G.ncy = (G.hc + B - 1) / B;
+  G.ncx = (G.wc + B - 1) / B;
   int MY, MX;
-  switch (mode) {
+  if (B == 16) (void)tile_dims16(mode, &MY, &MX);
+  else switch (mode) {
     case JDS_SS_420: MY = Cfg<M420>::MY; MX = Cfg<M420>::MX; break;
     case JDS_SS_422: MY = Cfg<M422>::MY; MX = Cfg<M422>::MX; break;
     default: MY = Cfg<M444>::MY; MX = Cfg<M444>::MX; break;
@@ -157,9 +172,9 @@ static int make_geo(const jds_params* p, int64_t H, int64_t W, Geo* g, int* mode
   G.ty_off = G.tiles_y * MY - G.nmy;
   G.tx_off = G.tiles_x * MX - G.nmx;
   const long long yb = (long long)G.nby * G.nbx, cb = (long long)G.ncy * G.ncx;
-  G.cpf = 64 * (yb + 2 * cb);
-  G.off_cb = 64 * yb;
-  G.off_cr = 64 * (yb + cb);
+  G.cpf = (long long)B * B * (yb + 2 * cb);
+  G.off_cb = (long long)B * B * yb;
+  G.off_cr = (long long)B * B * (yb + cb);
   // cv2.resize: inv_scale = dst/src, scale = 1/inv_scale
   G.up_sy = 1.0 / ((double)H / (double)G.hc);
   G.up_sx = 1.0 / ((double)W / (double)G.wc);
@@ -181,8 +196,14 @@ static void fill_geometry(const Geo& G, int mode, jds_geometry* o) {
   o->cb_offset = G.off_cb;
   o->cr_offset = G.off_cr;
   o->tiles = G.tiles_y * G.tiles_x;
-  o->threads_fwd = mode == JDS_SS_420 ? Cfg<M420>::TF : mode == JDS_SS_422 ? Cfg<M422>::TF : Cfg<M444>::TF;
-  o->threads_inv = Cfg<M420>::TI;
+  if (G.bs == 16) {
+    int my, mx;
+    o->threads_fwd = tile_dims16(mode, &my, &mx);
+    o->threads_inv = 256;
+  } else {
+    o->threads_fwd = mode == JDS_SS_420 ? Cfg<M420>::TF : mode == JDS_SS_422 ? Cfg<M422>::TF : Cfg<M444>::TF;
+    o->threads_inv = Cfg<M420>::TI;
+  }
   o->reserved = 0;
 }
 
@@ -265,6 +286,7 @@ void jds_ctx_destroy(jds_ctx* c) {
   for (DevBuf* b : bufs) b->release();
   for (DevBuf& b : c->st) b.release();
   c->chunks.release();
+  c->planes.release();
   for (hipEvent_t e : c->ev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -316,7 +338,14 @@ int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n, int64_t H, in
     return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
   }
   free(hq);
-  {
+  if (g.bs == 16) {
+    // 16x16 stretch path: exact fp64 kernels only (jds_b16.hip); chroma planes scratch
+    if ((e = p->planes.ensure(sizeof(double) * 2 * (size_t)n * g.hc * g.wc)) != hipSuccess ||
+        (e = p->counters.ensure(64)) != hipSuccess) {
+      jds_plan_destroy(p);
+      return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
+    }
+  } else {
     const size_t fqs = fast_q_size();
     char* h32 = (char*)malloc(fqs * (size_t)n);
     if (!h32) {
@@ -369,6 +398,16 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   int phases = (flags & JDS_RUN_FWD ? 1 : 0) | (flags & JDS_RUN_INV ? 2 : 0);
   if (!phases) phases = 3;
   const bool exact = (flags & JDS_RUN_EXACT) != 0;
+  if (p->g.bs == 16) {
+    if (phases & 1) {
+      HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
+      HIP_TRY(hipMemsetAsync(p->counters.p, 0, 64, s));
+    }
+    HIP_TRY(launch_codec16(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
+                           (const double*)p->gk.p, stats, (double*)p->part.p, (double*)p->planes.p,
+                           (flags & JDS_RUN_SSE) != 0, nullptr, nullptr, s, nullptr, phases));
+    return JDS_OK;
+  }
   if (phases & 1) {
     HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
     HIP_TRY(hipMemsetAsync(p->counters.p, 0, 64, s));
@@ -400,6 +439,7 @@ void jds_plan_destroy(jds_plan* p) {
   p->fixlist.release();
   p->counters.release();
   p->part32.release();
+  p->planes.release();
   if (p->side.stream) (void)hipStreamDestroy(p->side.stream);
   if (p->side.fork) (void)hipEventDestroy(p->side.fork);
   if (p->side.join) (void)hipEventDestroy(p->side.join);
@@ -435,8 +475,11 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
     HIP_TRY(c->errrgb.ensure(npx * sizeof(double)));
   }
   // selected luma block (pipeline.py:132-138): index into the padded grid
+  // (8x8 only: jds_selected_block holds 8x8 arrays; the 16x16 path reports none)
   int sel_blk = -1;
-  if (sel) {
+  if (sel && g.bs == 16) {
+    if (sel_valid) *sel_valid = 0;
+  } else if (sel) {
     const long long bpr = g.nbx;
     const long long ti = (long long)sel_by * bpr + sel_bx;
     const long long nyb = (long long)g.nby * g.nbx;
@@ -452,6 +495,13 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
   HIP_TRY(hipMemcpyAsync(c->rgb.p, rgb, nimg, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(jds_frame_stats), s));
   jds_selected_block* dsel = sel_blk >= 0 ? (jds_selected_block*)c->sel.p : nullptr;
+  if (g.bs == 16) {
+    HIP_TRY(c->planes.ensure(sizeof(double) * 2 * (size_t)g.hc * g.wc));
+    HIP_TRY(launch_codec16(mode, pf, g, 1, (const uint8_t*)c->rgb.p, (uint8_t*)c->out.p, (int16_t*)c->coeffs.p,
+                           (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
+                           (double*)c->part.p, (double*)c->planes.p, true, maps ? (double*)c->erry.p : nullptr,
+                           maps ? (double*)c->errrgb.p : nullptr, s, c->ev, 3));
+  } else
   HIP_TRY(launch_codec(mode, pf, g, 1, (const uint8_t*)c->rgb.p, (uint8_t*)c->out.p, (int16_t*)c->coeffs.p,
                        (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
                        (double*)c->part.p, true, maps ? (double*)c->erry.p : nullptr,
@@ -596,31 +646,44 @@ int jds_stage_upsample(jds_ctx* c, const double* in, int64_t h, int64_t w, int64
   return stage_out(c, out, dout, (size_t)H * W * sizeof(double));
 }
 
-int jds_stage_block_dct(jds_ctx* c, const double* in, double* out, int64_t n_blocks, int32_t op) {
+int jds_stage_block_dct_n(jds_ctx* c, const double* in, double* out, int64_t n_blocks, int32_t block_size,
+                          int32_t op) {
   if (!c || !in || !out || n_blocks < 0 || op < 0 || op > 3) return fail(JDS_EINVAL, "bad argument");
+  if (block_size != 8 && block_size != 16)
+    return fail(JDS_ENOTSUP, "block transforms are 8x8 or 16x16 (got %d)", block_size);
   if (n_blocks == 0) return JDS_OK;
   HIP_TRY(hipSetDevice(c->device));
-  const size_t b = (size_t)n_blocks * 64 * sizeof(double);
+  const size_t b = (size_t)n_blocks * block_size * block_size * sizeof(double);
   void *din, *dout;
   int rc;
   if ((rc = stage_io(c, 0, in, b, &din)) || (rc = stage_io(c, 1, nullptr, b, &dout))) return rc;
-  HIP_TRY(stage_block((const double*)din, (double*)dout, n_blocks, op, c->stream));
+  HIP_TRY(stage_block((const double*)din, (double*)dout, n_blocks, block_size, op, c->stream));
   return stage_out(c, out, dout, b);
 }
 
-int jds_stage_quantize(jds_ctx* c, const void* in, const double* qtable, void* out, int64_t n, int32_t dequant) {
-  if (!c || !in || !qtable || !out || n < 0 || (n % 64)) return fail(JDS_EINVAL, "bad argument");
+int jds_stage_block_dct(jds_ctx* c, const double* in, double* out, int64_t n_blocks, int32_t op) {
+  return jds_stage_block_dct_n(c, in, out, n_blocks, 8, op);
+}
+
+int jds_stage_quantize_n(jds_ctx* c, const void* in, const double* qtable, int32_t table_len, void* out, int64_t n,
+                         int32_t dequant) {
+  if (!c || !in || !qtable || !out || n < 0) return fail(JDS_EINVAL, "bad argument");
+  if ((table_len != 64 && table_len != 256) || (n % table_len)) return fail(JDS_EINVAL, "bad table length");
   if (n == 0) return JDS_OK;
   HIP_TRY(hipSetDevice(c->device));
   const size_t bi = (size_t)n * (dequant ? sizeof(int16_t) : sizeof(double));
   const size_t bo = (size_t)n * (dequant ? sizeof(double) : sizeof(int16_t));
   void *din, *dq, *dout;
   int rc;
-  if ((rc = stage_io(c, 0, in, bi, &din)) || (rc = stage_io(c, 4, qtable, 64 * sizeof(double), &dq)) ||
+  if ((rc = stage_io(c, 0, in, bi, &din)) || (rc = stage_io(c, 4, qtable, table_len * sizeof(double), &dq)) ||
       (rc = stage_io(c, 1, nullptr, bo, &dout)))
     return rc;
-  HIP_TRY(stage_quant(din, (const double*)dq, dout, n, dequant, c->stream));
+  HIP_TRY(stage_quant(din, (const double*)dq, dout, n, dequant, table_len, c->stream));
   return stage_out(c, out, dout, bo);
+}
+
+int jds_stage_quantize(jds_ctx* c, const void* in, const double* qtable, void* out, int64_t n, int32_t dequant) {
+  return jds_stage_quantize_n(c, in, qtable, 64, out, n, dequant);
 }
 
 int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t inverse) {
@@ -643,6 +706,24 @@ int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t invers
         dct2_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
     }
     for (int i = 0; i < 64; ++i) out[64 * b + i] = t[i] * 0.0625;  // pocketfft fct = 1/16
+  }
+  return JDS_OK;
+}
+
+int jds_selftest_dct16x16(const double* in, double* out, int64_t n, int32_t inverse) {
+  if (!in || !out || n < 0) return fail(JDS_EINVAL, "bad argument");
+  for (int64_t b = 0; b < n; ++b) {
+    double t[256], c[16];
+    memcpy(t, in + 256 * b, sizeof t);
+    for (int col = 0; col < 16; ++col) {  // axis 0 first
+      for (int i = 0; i < 16; ++i) c[i] = t[i * 16 + col];
+      if (inverse) dct3_line16(c); else dct2_line16(c);
+      for (int i = 0; i < 16; ++i) t[i * 16 + col] = c[i];
+    }
+    for (int r = 0; r < 16; ++r) {
+      if (inverse) dct3_line16(t + 16 * r); else dct2_line16(t + 16 * r);
+    }
+    for (int i = 0; i < 256; ++i) out[256 * b + i] = t[i] * 0.03125;  // pocketfft fct = 1/32
   }
   return JDS_OK;
 }

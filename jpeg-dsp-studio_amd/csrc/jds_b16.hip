@@ -1,0 +1,556 @@
+// jds_b16.hip — the 16x16 block path (BASELINE configs[4] stretch): the same
+// pipeline as the 8x8 path (engines/pipeline.py:17-167) with block_size = 16,
+// which the reference's validator accepts (models/compression_params.py:19-20)
+// but its quantizer cannot run (engines/quantizer.py:24 broadcasts a 16x16
+// block against the 8x8 table).  Build decision, documented in include/jds.h
+// and DESIGN.md: the 16x16 table is np.kron(Q8, ones((2, 2))), i.e.
+// Q16[u][v] = Q8[u/2][v/2] (same frequency band, same per-pixel noise).
+//
+// All arithmetic is fp64 in the reference's operation order (pocketfft's
+// 16-point transforms restated in jds_dct16.hpp), so coefficients and bytes
+// are bit-identical to the oracle (oracle/cpu_ref.py with block_size=16).
+//
+//   k_fwd16<MODE,PF> : one workgroup per TH x TW tile; RGB (+1 px ring) staged
+//                      in LDS, chroma prefilter row pass in LDS, one thread
+//                      per (block, column): column DCT, LDS exchange, row DCT,
+//                      quantise, 2 x 16-B stores; exact statistics.
+//   k_chroma16<MODE> : dequantise + 16x16 IDCT of every chroma block into
+//                      cropped fp64 chroma planes (scratch in HBM; the 1-sample
+//                      reach of the bilinear upsample then needs no ring
+//                      blocks per tile).
+//   k_inv16<MODE>    : one workgroup per tile: luma IDCT into LDS, bilinear
+//                      chroma from the planes, colour, clip, truncate, 24-B
+//                      stores; SSE / error maps like k_inv.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "jds_dct16.hpp"
+#include "jds_internal.hpp"
+#include "jds_device.hpp"
+
+#pragma clang fp contract(off)
+
+namespace jds {
+
+constexpr int B16 = 16;
+constexpr int BS16 = 264;  // doubles per 16x16 block in LDS (256 + 8 pad)
+
+template <int MODE>
+struct Cfg16 {
+  static constexpr int SY = (MODE == M420) ? 2 : 1;
+  static constexpr int SX = (MODE == M444) ? 1 : 2;
+  static constexpr int MH = 16 * SY, MW = 16 * SX;  // MCU in pixels
+  // two MCU rows / >= two MCU columns per tile: the block row/column carrying
+  // np.pad reflect padding (<= 15 samples) always shares its tile with the
+  // block row/column it reflects into (tiles are bottom-right aligned, Geo)
+  static constexpr int TH = 2 * MH, TW = 64;
+  static constexpr int MY = TH / MH, MX = TW / MW;
+  static constexpr int YBR = TH / 16, YBC = TW / 16;
+  static constexpr int CBR = MY, CBC = MX;
+  static constexpr int NYB = YBR * YBC, NCB = CBR * CBC;
+  static constexpr int NB = NYB + 2 * NCB;
+  static constexpr int TF = NB * 16;  // forward: one thread per block column
+  static constexpr int TI = 256;      // inverse threads
+};
+
+// 32*Q16[u][v] = 32*Q8[u/2][v/2]: pocketfft's first-axis fct = 1/32 folded in (exact)
+__device__ __forceinline__ double q16_of(const double* q8, int u, int v) { return q8[(u >> 1) * 8 + (v >> 1)]; }
+
+// ---------------------------------------------------------------- forward --
+
+template <int MODE, bool PF>
+__global__ void __launch_bounds__(Cfg16<MODE>::TF)
+k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+        const double* __restrict__ gk, jds_frame_stats* __restrict__ st) {
+  using C = Cfg16<MODE>;
+  constexpr int WR = C::TH + 2, WC = C::TW + 2, WN = WR * WC;
+  constexpr bool CPLANE = (MODE != M444) && PF;
+  constexpr int PLANE_D = CPLANE ? 2 * WN : 0;
+  constexpr int BLK_D = C::NB * BS16;
+  constexpr int U_D = PLANE_D > BLK_D ? PLANE_D : BLK_D;
+
+  __shared__ uint32_t s_rgb[WN];
+  __shared__ __attribute__((aligned(16))) double s_u[U_D];
+  __shared__ double s_q32[64];
+  __shared__ unsigned s_hist[50];
+  __shared__ int s_acc[2];
+
+  const int tid = threadIdx.x;
+  const int frame = blockIdx.y;
+  const int ty = blockIdx.x / g.tiles_x, tx = blockIdx.x - ty * g.tiles_x;
+  const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
+  const int y0 = m0y * C::MH, x0 = m0x * C::MW;
+  const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
+
+  for (int i = tid; i < WN; i += C::TF) {
+    const int r = i / WC, c = i - r * WC;
+    const int yy = reflect101(y0 - 1 + r, g.H), xx = reflect101(x0 - 1 + c, g.W);
+    const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
+    s_rgb[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+  }
+  if (tid < 64) s_q32[tid] = 32.0 * fq[frame].q[tid];  // exact
+  if (tid < 50) s_hist[tid] = 0u;
+  if (tid < 2) s_acc[tid] = 0;
+  __syncthreads();
+
+  if constexpr (CPLANE) {  // full-resolution chroma + Gaussian row pass (cv2 RowFilter<double>)
+    double* s_cb = s_u;
+    double* s_cr = s_u + WN;
+    for (int i = tid; i < WN; i += C::TF) {
+      double R, G, B;
+      unpack(s_rgb[i], R, G, B);
+      s_cb[i] = chroma_b(R, G, B);
+      s_cr[i] = chroma_r(R, G, B);
+    }
+    __syncthreads();
+    constexpr int NRP = WR * (WC - 2);
+    constexpr int PER = (NRP + C::TF - 1) / C::TF;
+    const double k0 = gk[0], k1 = gk[1], k2 = gk[2];
+    double tb[PER], tr[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * C::TF;
+      if (i < NRP) {
+        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
+        const double* b = s_cb + r * WC + c;
+        const double* q = s_cr + r * WC + c;
+        double t = k0 * b[-1];
+        t = t + k1 * b[0];
+        tb[j] = t + k2 * b[1];
+        t = k0 * q[-1];
+        t = t + k1 * q[0];
+        tr[j] = t + k2 * q[1];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * C::TF;
+      if (i < NRP) {
+        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
+        s_cb[r * WC + c] = tb[j];
+        s_cr[r * WC + c] = tr[j];
+      }
+    }
+    __syncthreads();
+  }
+
+  // one thread per (block, column)
+  const int blk = tid >> 4, line = tid & 15;
+  int plane, gy, gx;
+  if (blk < C::NYB) {
+    plane = 0;
+    gy = m0y * C::SY + blk / C::YBC;  // an MCU holds SY x SX luma blocks
+    gx = m0x * C::SX + blk % C::YBC;
+  } else {
+    const int bi = (blk - C::NYB) % C::NCB;
+    plane = 1 + (blk - C::NYB) / C::NCB;
+    gy = m0y + bi / C::CBC;
+    gx = m0x + bi % C::CBC;
+  }
+  const int nby = plane ? g.ncy : g.nby, nbx = plane ? g.ncx : g.nbx;
+  const bool valid = gy >= 0 && gx >= 0 && gy < nby && gx < nbx;
+  const int bidx = gy * nbx + gx;
+
+  double v[16];
+  if (valid) {
+    if (plane == 0 || MODE == M444) {
+      const int sx = reflect_pad(gx * 16 + line, g.W) - x0 + 1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int sy = reflect_pad(gy * 16 + i, g.H) - y0 + 1;
+        double R, G, B;
+        unpack(s_rgb[sy * WC + sx], R, G, B);
+        v[i] = plane == 0 ? luma(R, G, B) : (plane == 1 ? chroma_b(R, G, B) : chroma_r(R, G, B));
+      }
+    } else {
+      // INTER_AREA mean of (blurred) full-resolution chroma (color_space.py:38-49)
+      const double* s_pl = s_u + (plane == 1 ? 0 : WN);
+      const double k0 = gk[0], k1 = gk[1];
+      const int sc = reflect_pad(gx * 16 + line, g.wc);
+      const int wc0 = C::SX * sc - x0 + 1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int sr = reflect_pad(gy * 16 + i, g.hc);
+        const int wr0 = C::SY * sr - y0 + 1;
+        double s[C::SY][2];
+#pragma unroll
+        for (int a = 0; a < C::SY; ++a) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int w = (wr0 + a) * WC + wc0 + b;
+            if constexpr (CPLANE) {
+              const double d = k1 * s_pl[w] + 0.0;  // SymmColumnFilter<double>
+              s[a][b] = d + k0 * (s_pl[w + WC] + s_pl[w - WC]);
+            } else {
+              double R, G, B;
+              unpack(s_rgb[w], R, G, B);
+              s[a][b] = plane == 1 ? chroma_b(R, G, B) : chroma_r(R, G, B);
+            }
+          }
+        }
+        if constexpr (C::SY == 2)
+          v[i] = (((s[0][0] + s[0][1]) + s[1][0]) + s[1][1]) * 0.25;
+        else
+          v[i] = (s[0][0] + s[0][1]) * 0.5;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = v[i] - 128.0;  // dct_engine.py:19
+    dct2_line16(v);                                    // axis 0 (columns) first
+  }
+  if constexpr (CPLANE) __syncthreads();  // the block buffer aliases the chroma planes
+  double* s_blk = s_u + blk * BS16;
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s_blk[i * 16 + line] = v[i];
+  }
+  __syncthreads();
+
+  int nz = 0, mb = 0;
+  if (valid) {
+    const int u = line;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = s_blk[u * 16 + k];
+    dct2_line16(v);
+    int q[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      q[k] = (int)__builtin_rint(v[k] / q16_of(s_q32, u, k));  // quantizer.py:22-24
+      const int m = q[k] < 0 ? -q[k] : q[k];
+      if (m) {
+        ++nz;
+        mb += 33 - __clz(m);
+        if (q[k] >= -100 && q[k] <= 100) atomicAdd(&s_hist[q[k] == 100 ? 49 : (q[k] + 100) >> 2], 1u);
+      }
+    }
+    const long long off = (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
+                          (long long)bidx * 256 + u * 16;
+    uint4 pk[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int* qq = q + 8 * h;
+      pk[h].x = (uint32_t)(uint16_t)qq[0] | ((uint32_t)(uint16_t)qq[1] << 16);
+      pk[h].y = (uint32_t)(uint16_t)qq[2] | ((uint32_t)(uint16_t)qq[3] << 16);
+      pk[h].z = (uint32_t)(uint16_t)qq[4] | ((uint32_t)(uint16_t)qq[5] << 16);
+      pk[h].w = (uint32_t)(uint16_t)qq[6] | ((uint32_t)(uint16_t)qq[7] << 16);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(coeffs + off);
+    dst[0] = pk[0];
+    dst[1] = pk[1];
+  }
+  nz = wave_sum(nz);
+  mb = wave_sum(mb);
+  if ((tid & 63) == 0) {
+    atomicAdd(&s_acc[0], nz);
+    atomicAdd(&s_acc[1], mb);
+  }
+  __syncthreads();
+  jds_frame_stats* fs = st + frame;
+  if (tid == 0) {
+    atomicAdd((unsigned long long*)&fs->nonzero, (unsigned long long)s_acc[0]);
+    atomicAdd((unsigned long long*)&fs->magnitude_bits, (unsigned long long)s_acc[1]);
+  }
+  if (tid < 50 && s_hist[tid]) atomicAdd((unsigned long long*)&fs->hist[tid], (unsigned long long)s_hist[tid]);
+}
+
+// ---------------------------------------------------------------- inverse --
+
+// Dequantise + 2-D IDCT (axis 0 first) of one 16x16 block held in LDS by the
+// 16 lanes (line = 0..15) that own it; the same lanes do both passes, so the
+// exchange is wave-local (a block's 16 lanes are in one wave).  Returns the
+// clipped spatial row `line` in r[16] (dct_engine.py:23-27).
+__device__ __forceinline__ void idct16_block(const int16_t* __restrict__ src, const double* __restrict__ q8,
+                                             double* __restrict__ s_b, int line, double* r) {
+  {
+    const uint4* p = reinterpret_cast<const uint4*>(src + line * 16);
+    const uint4 a = p[0], b = p[1];
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int16_t qv = (int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
+      s_b[line * 16 + k] = (double)qv * q16_of(q8, line, k);  // quantizer.py:27-29
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // no LDS access moves across (the exchange is wave-local)
+  double c[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) c[i] = s_b[i * 16 + line];
+  dct3_line16(c);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s_b[i * 16 + line] = c[i];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) c[k] = s_b[line * 16 + k];
+  dct3_line16(c);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const double s = c[k] * 0.03125 + 128.0;  // fct 1/32 (exact), then +128
+    r[k] = fmin(fmax(s, 0.0), 255.0);
+  }
+}
+
+// Every chroma block -> cropped fp64 planes cb/cr (hc x wc each, per frame).
+template <int MODE>
+__global__ void __launch_bounds__(256)
+k_chroma16(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+           double* __restrict__ planes) {
+  __shared__ double s_b[16 * BS16];
+  __shared__ double s_q[64];
+  const int tid = threadIdx.x, frame = blockIdx.y;
+  if (tid < 64) s_q[tid] = fq[frame].q[tid];
+  __syncthreads();
+  const int per_plane = g.ncy * g.ncx;
+  const int b = blockIdx.x * 16 + (tid >> 4), line = tid & 15;
+  if (b >= 2 * per_plane) return;  // whole 16-lane groups leave together
+  const int p = b >= per_plane, bi = b - p * per_plane;
+  const int by = bi / g.ncx, bx = bi - by * g.ncx;
+  const int16_t* src = coeffs + (size_t)frame * g.cpf + (p ? g.off_cr : g.off_cb) + (long long)bi * 256;
+  double r[16];
+  idct16_block(src, s_q, s_b + (tid >> 4) * BS16, line, r);
+  const int y = by * 16 + line;
+  if (y >= g.hc) return;  // crop (pipeline.py:77-82)
+  double* dst = planes + ((size_t)frame * 2 + p) * g.hc * g.wc + (size_t)y * g.wc + bx * 16;
+  const int n = g.wc - bx * 16 < 16 ? g.wc - bx * 16 : 16;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (k < n) dst[k] = r[k];
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(Cfg16<MODE>::TI)
+k_inv16(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+        const double* __restrict__ planes, const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out,
+        jds_frame_stats* __restrict__ st, double* __restrict__ sse_y_part, double* __restrict__ err_y,
+        double* __restrict__ err_rgb) {
+  using C = Cfg16<MODE>;
+  constexpr int NT = C::TI;
+  constexpr int NGRP = NT / 16;  // blocks in flight per round
+  __shared__ double s_b[NGRP * BS16];
+  __shared__ double s_y[C::TH * C::TW];
+  __shared__ double s_q[64];
+  __shared__ double s_red[NT / 64];
+  __shared__ unsigned long long s_sse;
+
+  const int tid = threadIdx.x, frame = blockIdx.y, tile = blockIdx.x;
+  const int ty = tile / g.tiles_x, tx = tile - ty * g.tiles_x;
+  const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
+  const int y0 = m0y * C::MH, x0 = m0x * C::MW;
+  const int16_t* cf = coeffs + (size_t)frame * g.cpf;
+  if (tid < 64) s_q[tid] = fq[frame].q[tid];
+  if (tid == 0) s_sse = 0ull;
+  __syncthreads();
+
+  // luma blocks of the tile -> s_y (rows of phantom / out-of-grid blocks untouched, never read)
+  for (int b0 = 0; b0 < C::NYB; b0 += NGRP) {
+    const int blk = b0 + (tid >> 4), line = tid & 15;
+    if (blk < C::NYB) {
+      const int br = blk / C::YBC, bc = blk - br * C::YBC;
+      const int by = m0y * C::SY + br, bx = m0x * C::SX + bc;
+      if (by >= 0 && bx >= 0 && by < g.nby && bx < g.nbx) {
+        double r[16];
+        idct16_block(cf + ((long long)by * g.nbx + bx) * 256, s_q, s_b + (tid >> 4) * BS16, line, r);
+        double* d = s_y + (br * 16 + line) * C::TW + bc * 16;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = r[k];
+      }
+    }
+  }
+  __syncthreads();
+
+  const bool want_in = rgb_in != nullptr;
+  unsigned long long sse = 0ull;
+  double ssy = 0.0;
+  const uint8_t* in_f = want_in ? rgb_in + (size_t)frame * g.H * g.W * 3 : nullptr;
+  uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
+  const double* pcb = planes + (size_t)frame * 2 * g.hc * g.wc;
+  const double* pcr = pcb + (size_t)g.hc * g.wc;
+  for (int t = tid; t < C::TH * (C::TW / 8); t += NT) {
+    const int r = t / (C::TW / 8), sg = t - r * (C::TW / 8);
+    const int y = y0 + r;
+    if (y < 0 || y >= g.H) continue;
+    int r0 = y, r1 = y;
+    double b0 = 1.0, b1 = 0.0;
+    if constexpr (MODE != M444) {  // cv2 INTER_LINEAR vertical taps (color_space.py:63-65)
+      float fy = (float)((y + 0.5) * g.up_sy - 0.5);
+      const int sy = (int)floorf(fy);
+      fy -= (float)sy;
+      b0 = (double)(1.f - fy);
+      b1 = (double)fy;
+      r0 = clampi(sy, 0, g.hc - 1);
+      r1 = clampi(sy + 1, 0, g.hc - 1);
+    }
+    uint8_t px[24];
+    double ey[8], er[8];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int lx = sg * 8 + k, x = x0 + lx;
+      if (x < 0 || x >= g.W) { ey[k] = er[k] = 0.0; px[3 * k] = px[3 * k + 1] = px[3 * k + 2] = 0; continue; }
+      ++cnt;
+      const double Y = s_y[r * C::TW + lx];
+      double Cb, Cr;
+      if constexpr (MODE == M444) {
+        Cb = pcb[(size_t)y * g.wc + x];
+        Cr = pcr[(size_t)y * g.wc + x];
+      } else {
+        float fx = (float)((x + 0.5) * g.up_sx - 0.5);
+        int sx = (int)floorf(fx);
+        fx -= (float)sx;
+        if (sx < 0) { sx = 0; fx = 0.f; }
+        const bool copy = sx + 1 >= g.wc;
+        if (sx >= g.wc - 1) { sx = g.wc - 1; fx = 0.f; }
+        const double a0 = (double)(1.f - fx), a1 = (double)fx;
+        double hv[2][2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const double* pl = p ? pcr : pcb;
+          const double* s0 = pl + (size_t)r0 * g.wc + sx;
+          const double* s1 = pl + (size_t)r1 * g.wc + sx;
+          if (copy) {
+            hv[p][0] = s0[0] * 1.0;
+            hv[p][1] = s1[0] * 1.0;
+          } else {
+            hv[p][0] = s0[0] * a0 + s0[1] * a1;
+            hv[p][1] = s1[0] * a0 + s1[1] * a1;
+          }
+        }
+        Cb = hv[0][0] * b0 + hv[0][1] * b1;
+        Cr = hv[1][0] * b0 + hv[1][1] * b1;
+      }
+      // engines/color_space.py:17-24, pipeline.py:93-95
+      double R = Y + 1.402 * (Cr - 128.0);
+      double G = Y - 0.344136 * (Cb - 128.0) - 0.714136 * (Cr - 128.0);
+      double B = Y + 1.772 * (Cb - 128.0);
+      R = fmin(fmax(R, 0.0), 255.0);
+      G = fmin(fmax(G, 0.0), 255.0);
+      B = fmin(fmax(B, 0.0), 255.0);
+      const uint8_t ur = (uint8_t)(int)R, ug = (uint8_t)(int)G, ub = (uint8_t)(int)B;
+      px[3 * k] = ur; px[3 * k + 1] = ug; px[3 * k + 2] = ub;
+      if (want_in) {
+        const uint8_t* o = in_f + ((size_t)y * g.W + x) * 3;
+        const int o0 = o[0], o1 = o[1], o2 = o[2];
+        const int d0 = o0 - ur, d1 = o1 - ug, d2 = o2 - ub;
+        sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
+        const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
+        const double yo = luma(R0, G0, B0);
+        const double yr = luma((double)ur, (double)ug, (double)ub);
+        const double dy = yo - yr;
+        ssy = ssy + dy * dy;
+        ey[k] = fabs(yo - Y);                                          // pipeline.py:120
+        er[k] = ((fabs(R0 - R) + fabs(G0 - G)) + fabs(B0 - B)) / 3.0;  // pipeline.py:121
+      }
+    }
+    const int x = x0 + sg * 8;
+    if (cnt == 8 && (((size_t)y * g.W + x) * 3 & 7) == 0) {
+      uint64_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        w0 |= (uint64_t)px[k] << (8 * k);
+        w1 |= (uint64_t)px[8 + k] << (8 * k);
+        w2 |= (uint64_t)px[16 + k] << (8 * k);
+      }
+      uint64_t* o64 = reinterpret_cast<uint64_t*>(out_f + ((size_t)y * g.W + x) * 3);
+      o64[0] = w0; o64[1] = w1; o64[2] = w2;
+    } else {
+      for (int k = 0; k < 8; ++k) {
+        const int xx = x + k;
+        if (xx < 0 || xx >= g.W) continue;
+        uint8_t* q = out_f + ((size_t)y * g.W + xx) * 3;
+        q[0] = px[3 * k]; q[1] = px[3 * k + 1]; q[2] = px[3 * k + 2];
+      }
+    }
+    if (err_y != nullptr) {
+      for (int k = 0; k < 8; ++k) {
+        const int xx = x + k;
+        if (xx < 0 || xx >= g.W) continue;
+        err_y[(size_t)y * g.W + xx] = ey[k];
+        err_rgb[(size_t)y * g.W + xx] = er[k];
+      }
+    }
+  }
+  if (want_in) {
+    unsigned long long s = sse;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((tid & 63) == 0) atomicAdd(&s_sse, s);
+    double d = ssy;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d = d + __shfl_xor(d, o, 64);
+    if ((tid & 63) == 0) s_red[tid >> 6] = d;
+    __syncthreads();
+    if (tid == 0) {
+      double a = 0.0;
+      for (int i = 0; i < NT / 64; ++i) a = a + s_red[i];
+      sse_y_part[(size_t)frame * gridDim.x + tile] = a;
+      atomicAdd((unsigned long long*)&st[frame].sse_rgb, s_sse);
+    }
+  }
+}
+
+// ------------------------------------------------------------ launchers --
+
+hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uint32_t* part, int ptiles,
+                             hipStream_t s);
+hipError_t launch_finalize(const Geo& g, int n, jds_frame_stats* st, const double* part, int tiles, bool with_sse,
+                           hipStream_t s);
+
+int tile_dims16(int mode, int* MY, int* MX) {
+  switch (mode) {
+    case M420: *MY = Cfg16<M420>::MY; *MX = Cfg16<M420>::MX; return Cfg16<M420>::TF;
+    case M422: *MY = Cfg16<M422>::MY; *MX = Cfg16<M422>::MX; return Cfg16<M422>::TF;
+    default: *MY = Cfg16<M444>::MY; *MX = Cfg16<M444>::MX; return Cfg16<M444>::TF;
+  }
+}
+
+template <int MODE>
+static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs,
+                             const FrameQ* fq, const double* gk, jds_frame_stats* st, double* part, double* planes,
+                             bool want_sse, double* err_y, double* err_rgb, hipStream_t s, hipEvent_t* ev,
+                             int phases) {
+  using C = Cfg16<MODE>;
+  const dim3 grid(g.tiles_y * g.tiles_x, n);
+  hipError_t e = hipSuccess;
+  if (phases & 1) {
+    if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
+    if (MODE != M444 && pf)
+      hipLaunchKernelGGL((k_fwd16<MODE, (MODE != M444)>), grid, dim3(C::TF), 0, s, g, rgb, coeffs, fq, gk, st);
+    else
+      hipLaunchKernelGGL((k_fwd16<MODE, false>), grid, dim3(C::TF), 0, s, g, rgb, coeffs, fq, gk, st);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_fwd_finish(g, n, st, nullptr, 0, s)) != hipSuccess) return e;
+    if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
+  }
+  if (phases & 2) {
+    const int cblocks = 2 * g.ncy * g.ncx;
+    hipLaunchKernelGGL((k_chroma16<MODE>), dim3((cblocks + 15) / 16, n), dim3(256), 0, s, g, coeffs, fq, planes);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint8_t* rin = (want_sse || err_y) ? rgb : nullptr;
+    hipLaunchKernelGGL((k_inv16<MODE>), grid, dim3(C::TI), 0, s, g, coeffs, fq, planes, rin, rgb_out, st, part,
+                       err_y, err_rgb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
+    e = launch_finalize(g, n, st, part, g.tiles_y * g.tiles_x, rin != nullptr, s);
+  }
+  return e;
+}
+
+// phases: bit 0 forward, bit 1 inverse (chroma planes + tiles + finalize)
+hipError_t launch_codec16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
+                          int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st, double* part,
+                          double* planes, bool want_sse, double* err_y, double* err_rgb, hipStream_t s,
+                          hipEvent_t* ev, int phases) {
+  switch (mode) {
+    case M420:
+      return launch16_t<M420>(pf, g, n, rgb, rgb_out, coeffs, fq, gk, st, part, planes, want_sse, err_y, err_rgb,
+                              s, ev, phases);
+    case M422:
+      return launch16_t<M422>(pf, g, n, rgb, rgb_out, coeffs, fq, gk, st, part, planes, want_sse, err_y, err_rgb,
+                              s, ev, phases);
+    default:
+      return launch16_t<M444>(false, g, n, rgb, rgb_out, coeffs, fq, gk, st, part, planes, want_sse, err_y,
+                              err_rgb, s, ev, phases);
+  }
+}
+
+}  // namespace jds

@@ -600,6 +600,12 @@ __global__ void k_finalize(const Geo g, jds_frame_stats* st, const double* __res
   }
 }
 
+hipError_t launch_finalize(const Geo& g, int n, jds_frame_stats* st, const double* part, int tiles, bool with_sse,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, tiles, (int)with_sse);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ launchers --
 
 template <int MODE, bool PF>

@@ -24,6 +24,7 @@ struct Geo {
   long long cpf;     // coefficients per frame
   long long off_cb, off_cr;
   double up_sy, up_sx;  // cv2.resize scale (src/dst) of the chroma upsample
+  int bs;               // block size: 8, or 16 (jds_b16.hip)
 };
 
 // A second stream with fork/join events: lets a plan run independent launches

@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "jds_dct8.hpp"
+#include "jds_dct16.hpp"
 #include "jds_internal.hpp"
 
 #pragma clang fp contract(off)
@@ -163,12 +164,51 @@ __global__ void k_stage_block(const double* __restrict__ in, double* __restrict_
   }
 }
 
-// quantize: int16(rint(c / Q)); dequantize: double(q) * Q (Q broadcast per 8x8 position)
+// quantize: int16(rint(c / Q)); dequantize: double(q) * Q (Q broadcast with period 64 or 256)
+// 16x16 blocks (dctn / idctn on a 16x16 block, dct_engine.py:7-27): 16 lanes
+// per block, column pass then row pass; fct = 1/32 on the first axis (exact).
+__global__ void __launch_bounds__(256) k_stage_block16(const double* __restrict__ in, double* __restrict__ out,
+                                                       long long n, int op) {
+  __shared__ double s[16][16 * 16 + 1];
+  const int lb = threadIdx.x >> 4, line = threadIdx.x & 15;
+  const long long b = (long long)blockIdx.x * 16 + lb;
+  const bool ok = b < n;
+  double c[16];
+  if (ok) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c[i] = in[b * 256 + i * 16 + line];  // column `line`
+    if (op == 2) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) c[i] = c[i] - 128.0;
+    }
+    if (op == 0 || op == 2)
+      dct2_line16(c);
+    else
+      dct3_line16(c);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[lb][i * 16 + line] = c[i];
+  }
+  __syncthreads();
+  if (!ok) return;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) c[k] = s[lb][line * 16 + k];  // row `line`
+  if (op == 0 || op == 2)
+    dct2_line16(c);
+  else
+    dct3_line16(c);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    double v = c[k] * 0.03125;
+    if (op == 3) v = fmin(fmax(v + 128.0, 0.0), 255.0);
+    out[b * 256 + line * 16 + k] = v;
+  }
+}
+
 __global__ void k_stage_quant(const void* __restrict__ in, const double* __restrict__ q, void* __restrict__ out,
-                              long long n, int dequant) {
+                              long long n, int dequant, int period) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double qq = q[i & 63];
+  const double qq = q[i & (period - 1)];
   if (dequant)
     ((double*)out)[i] = (double)((const int16_t*)in)[i] * qq;
   else
@@ -206,13 +246,17 @@ hipError_t stage_resize(const double* in, int h, int w, double* out, int H, int 
   return hipGetLastError();
 }
 
-hipError_t stage_block(const double* in, double* out, long long n, int op, hipStream_t s) {
-  hipLaunchKernelGGL(k_stage_block, dim3(nblk(n, 8)), dim3(64), 0, s, in, out, n, op);
+hipError_t stage_block(const double* in, double* out, long long n, int bs, int op, hipStream_t s) {
+  if (bs == 16)
+    hipLaunchKernelGGL(k_stage_block16, dim3(nblk(n, 16)), dim3(256), 0, s, in, out, n, op);
+  else
+    hipLaunchKernelGGL(k_stage_block, dim3(nblk(n, 8)), dim3(64), 0, s, in, out, n, op);
   return hipGetLastError();
 }
 
-hipError_t stage_quant(const void* in, const double* q, void* out, long long n, int dequant, hipStream_t s) {
-  hipLaunchKernelGGL(k_stage_quant, dim3(nblk(n, 256)), dim3(256), 0, s, in, q, out, n, dequant);
+hipError_t stage_quant(const void* in, const double* q, void* out, long long n, int dequant, int period,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_stage_quant, dim3(nblk(n, 256)), dim3(256), 0, s, in, q, out, n, dequant, period);
   return hipGetLastError();
 }
 

@@ -30,6 +30,34 @@ def compress_reconstruct(
     """Run the JPEG-like compression + reconstruction pipeline on the GPU."""
     if params.subsampling_mode not in ('4:4:4', '4:2:2', '4:2:0'):
         raise ValueError(f"Unknown subsampling mode: {params.subsampling_mode}")
+    if params.block_size != 8:
+        # the reference gets as far as quantize(), which broadcasts the BxB block
+        # against the 8x8 table (engines/quantizer.py:24)
+        b = params.block_size
+        raise ValueError(f"operands could not be broadcast together with shapes ({b},{b}) (8,8) ")
+    return _run(image_rgb, params, selected_block_idx)
+
+
+def compress_reconstruct_stretch(
+    image_rgb: np.ndarray,
+    params: CompressionParams,
+    selected_block_idx: Tuple[int, int] = (0, 0)
+) -> Tuple[CompressionResult, IntermediateData]:
+    """The same pipeline with block_size 8 or 16 (BASELINE configs[4] stretch).
+
+    The reference accepts block_size=16 in CompressionParams but cannot run it;
+    here 16x16 blocks use Q16 = np.kron(Q8, ones((2, 2))) (include/jds.h,
+    DESIGN.md) with every other stage unchanged.  IntermediateData's
+    selected_block_* fields are None for 16x16 blocks."""
+    if params.subsampling_mode not in ('4:4:4', '4:2:2', '4:2:0'):
+        raise ValueError(f"Unknown subsampling mode: {params.subsampling_mode}")
+    if params.block_size not in (8, 16):
+        b = params.block_size
+        raise ValueError(f"operands could not be broadcast together with shapes ({b},{b}) (8,8) ")
+    return _run(image_rgb, params, selected_block_idx)
+
+
+def _run(image_rgb, params, selected_block_idx):
     q_matrix = scale_quant_matrix(JPEG_LUMA_Q50, params.quality)           # pipeline.py:43
     raw = compress_reconstruct_raw(image_rgb, params.quality, q_matrix, params.subsampling_mode,
                                    params.use_prefilter, params.block_size, selected_block_idx)

@@ -90,7 +90,10 @@ _SIGS = {
     'jds_stage_upsample': (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int32, _P]),
     'jds_stage_block_dct': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32]),
     'jds_stage_quantize': (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int32]),
+    'jds_stage_block_dct_n': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32]),
+    'jds_stage_quantize_n': (C.c_int, [_P, _P, _P, C.c_int32, _P, C.c_int64, C.c_int32]),
     'jds_selftest_dct8x8': (C.c_int, [_P, _P, C.c_int64, C.c_int32]),
+    'jds_selftest_dct16x16': (C.c_int, [_P, _P, C.c_int64, C.c_int32]),
 }
 _OPTIONAL_SIGS: dict = {}
 
@@ -128,7 +131,7 @@ def lib():
             f = getattr(h, name, None)
             if f is not None:
                 f.restype, f.argtypes = res, args
-        if h.jds_abi_version() != 1:
+        if h.jds_abi_version() != 2:
             raise ImportError('libjds.so ABI version mismatch')
         _lib = h
         return h

@@ -121,25 +121,28 @@ def stage_resize(x: np.ndarray, H: int, W: int, nearest: bool) -> np.ndarray:
 
 
 def stage_block(x: np.ndarray, op: int) -> np.ndarray:
-    """op: 0 dct2, 1 idct2, 2 encode_block, 3 decode_block on (..., 8, 8)."""
+    """op: 0 dct2, 1 idct2, 2 encode_block, 3 decode_block on (..., 8, 8) or (..., 16, 16)."""
     x = _f64(x)
-    if x.shape[-2:] != (8, 8):
-        raise ValueError(f'the MI355X block transform is 8x8 (got {x.shape})')
+    if x.ndim < 2 or x.shape[-2:] not in ((8, 8), (16, 16)):
+        raise ValueError(f'the MI355X block transforms are 8x8 and 16x16 (got {x.shape})')
+    b = x.shape[-1]
     out = np.empty_like(x)
-    check(lib().jds_stage_block_dct(context().handle, x.ctypes.data, out.ctypes.data, x.size // 64, op))
+    check(lib().jds_stage_block_dct_n(context().handle, x.ctypes.data, out.ctypes.data, x.size // (b * b), b, op))
     return out
 
 
 def stage_quant(x: np.ndarray, q: np.ndarray, dequant: bool) -> np.ndarray:
     q = _f64(q)
-    if q.shape != (8, 8) or x.shape[-2:] != (8, 8):
-        raise ValueError(f'operands could not be broadcast together with shapes {x.shape} {q.shape} ')
+    if q.shape not in ((8, 8), (16, 16)) or x.shape[-2:] != q.shape:
+        # NumPy's broadcast error for c / Q (engines/quantizer.py:24)
+        fmt = lambda s: '(' + ','.join(str(d) for d in s) + (',)' if len(s) == 1 else ')')
+        raise ValueError(f'operands could not be broadcast together with shapes {fmt(x.shape)} {fmt(q.shape)} ')
     if dequant:
         x = np.ascontiguousarray(x, dtype=np.int16)
         out = np.empty(x.shape, np.float64)
     else:
         x = _f64(x)
         out = np.empty(x.shape, np.int16)
-    check(lib().jds_stage_quantize(context().handle, x.ctypes.data, q.ctypes.data, out.ctypes.data, x.size,
-                                   1 if dequant else 0))
+    check(lib().jds_stage_quantize_n(context().handle, x.ctypes.data, q.ctypes.data, q.size, out.ctypes.data,
+                                     x.size, 1 if dequant else 0))
     return out

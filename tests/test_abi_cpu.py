@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(L):
     assert not missing, missing
     for n in names:
         assert hasattr(L, n)
-    assert L.jds_abi_version() == 1
+    assert L.jds_abi_version() == 2
 
 
 def test_library_has_gfx950_code_object(L):
@@ -86,12 +86,41 @@ def test_survey_geometry_table(L):
 def test_errors_map_to_reference_exceptions(L):
     from jds import _abi, codec
     q = cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, 50)
-    with pytest.raises(ValueError, match=r'operands could not be broadcast together with shapes \(16,16\) \(8,8\)'):
-        _abi.geometry(_abi.make_params(50, q, '4:2:0', False, codec.gaussian_kernel3(), block_size=16), 64, 64)
+    for b in (4, 32):
+        with pytest.raises(ValueError, match=rf'operands could not be broadcast together with shapes \({b},{b}\) \(8,8\)'):
+            _abi.geometry(_abi.make_params(50, q, '4:2:0', False, codec.gaussian_kernel3(), block_size=b), 64, 64)
+    # 16x16: the configs[4] stretch geometry (B*B coefficients per block)
+    g16 = _abi.geometry(_abi.make_params(50, q, '4:2:0', False, codec.gaussian_kernel3(), block_size=16), 1080, 1920)
+    assert (g16.y_blocks_y, g16.y_blocks_x, g16.c_blocks_y, g16.c_blocks_x) == (68, 120, 34, 60)
+    assert g16.coeffs_per_frame == 256 * (68 * 120 + 2 * 34 * 60)
     with pytest.raises(ValueError, match='odd image size'):
         _abi.geometry(_abi.make_params(50, q, '4:2:0', False, codec.gaussian_kernel3()), 63, 64)
     # 4:4:4 takes any size
     assert _abi.geometry(_abi.make_params(50, q, '4:4:4', False, codec.gaussian_kernel3()), 63, 65).tiles > 0
+
+
+def test_drop_in_rejects_block16_like_the_reference():
+    # the reference validates block_size 16 but its quantizer raises (engines/quantizer.py:24);
+    # the check happens on the host, before any device work
+    from engines.pipeline import compress_reconstruct
+    from models.compression_params import CompressionParams
+    img = np.zeros((32, 32, 3), np.uint8)
+    for b in (4, 16, 32):
+        with pytest.raises(ValueError, match=rf'operands could not be broadcast together with shapes \({b},{b}\) \(8,8\)'):
+            compress_reconstruct(img, CompressionParams(block_size=b))
+
+
+@pytest.mark.parametrize('inverse', [0, 1])
+def test_dct16_expressions_match_scipy(L, inverse):
+    rng = np.random.default_rng(7 + inverse)
+    x = np.concatenate([
+        rng.standard_normal((1500, 16, 16)) * rng.choice([1.0, 100.0, 3000.0], (1500, 1, 1)),
+        rng.integers(-1024, 1024, (1500, 16, 16)).astype(np.float64) * rng.integers(1, 256, (1, 16, 16)),
+    ])
+    out = np.empty_like(x)
+    assert L.jds_selftest_dct16x16(x.ctypes.data, out.ctypes.data, len(x), inverse) == 0
+    f = sfft.idctn if inverse else sfft.dctn
+    assert np.array_equal(out, f(x, type=2, norm='ortho', axes=(1, 2)))
 
 
 def test_gaussian_taps_match_oracle():
