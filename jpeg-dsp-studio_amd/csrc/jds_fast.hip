@@ -82,6 +82,14 @@ struct FastQ {
 };
 
 constexpr int BS32 = 72;  // floats per 8x8 block in LDS (column writes conflict-free)
+
+// k_fwd32i's chroma planes (4:2:x): the 16-B slot f of plane row `row` is
+// stored at slot f ^ csw(row).  The 8 lanes of a chroma block read rows SY
+// apart at the same columns (rows are 256 B = one bank row apart), 4-way
+// conflicting per ds_read_b128 lane group; XOR-ing the slot with the row's
+// sample index mod 4 puts them on 4 different slots (MI355X_MICROARCH.md §LDS).
+template <int SY>
+__device__ __forceinline__ int csw(int row) { return (row / SY) & 3; }
 constexpr int NSTAT = 52; // per-tile statistics: nonzero, magnitude bits, hist[50]
 
 __device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[6], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255u; }
@@ -501,20 +509,22 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
           ob[k] = fmaf(k2, br, fmaf(k1, cb[k], k0 * bl));
           orr[k] = fmaf(k2, qr, fmaf(k1, cr[k], k0 * ql));
         }
-        float4* db = reinterpret_cast<float4*>(s_cb + r * TW + 8 * c);
-        float4* dr = reinterpret_cast<float4*>(s_cr + r * TW + 8 * c);
-        db[0] = make_float4(ob[0], ob[1], ob[2], ob[3]);
-        db[1] = make_float4(ob[4], ob[5], ob[6], ob[7]);
-        dr[0] = make_float4(orr[0], orr[1], orr[2], orr[3]);
-        dr[1] = make_float4(orr[4], orr[5], orr[6], orr[7]);
+        const int hs = csw<C::SY>(r);
+        float4* db = reinterpret_cast<float4*>(s_cb + r * TW);
+        float4* dr = reinterpret_cast<float4*>(s_cr + r * TW);
+        db[(2 * c) ^ hs] = make_float4(ob[0], ob[1], ob[2], ob[3]);
+        db[(2 * c + 1) ^ hs] = make_float4(ob[4], ob[5], ob[6], ob[7]);
+        dr[(2 * c) ^ hs] = make_float4(orr[0], orr[1], orr[2], orr[3]);
+        dr[(2 * c + 1) ^ hs] = make_float4(orr[4], orr[5], orr[6], orr[7]);
       } else {
         if (r >= 1 && r <= TH) {
-          float4* db = reinterpret_cast<float4*>(s_cb + o);
-          float4* dr = reinterpret_cast<float4*>(s_cr + o);
-          db[0] = make_float4(cb[0], cb[1], cb[2], cb[3]);
-          db[1] = make_float4(cb[4], cb[5], cb[6], cb[7]);
-          dr[0] = make_float4(cr[0], cr[1], cr[2], cr[3]);
-          dr[1] = make_float4(cr[4], cr[5], cr[6], cr[7]);
+          const int hs = csw<C::SY>(r - 1);
+          float4* db = reinterpret_cast<float4*>(s_cb + (r - 1) * TW);
+          float4* dr = reinterpret_cast<float4*>(s_cr + (r - 1) * TW);
+          db[(2 * c) ^ hs] = make_float4(cb[0], cb[1], cb[2], cb[3]);
+          db[(2 * c + 1) ^ hs] = make_float4(cb[4], cb[5], cb[6], cb[7]);
+          dr[(2 * c) ^ hs] = make_float4(cr[0], cr[1], cr[2], cr[3]);
+          dr[(2 * c + 1) ^ hs] = make_float4(cr[4], cr[5], cr[6], cr[7]);
         }
       }
     }
@@ -585,8 +595,9 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
         float rows[C::SY + 2][8];
 #pragma unroll
         for (int j = 0; j < (CPLANE ? C::SY + 2 : C::SY); ++j) {
-          const float4* s4 = reinterpret_cast<const float4*>(P + (pr + j) * TW + xc + 8 * h);
-          const float4 x = s4[0], y = s4[1];
+          const int hs = csw<C::SY>(pr + j), f = (xc + 8 * h) >> 2;
+          const float4* s4 = reinterpret_cast<const float4*>(P + (pr + j) * TW);
+          const float4 x = s4[f ^ hs], y = s4[(f + 1) ^ hs];
           rows[j][0] = x.x; rows[j][1] = x.y; rows[j][2] = x.z; rows[j][3] = x.w;
           rows[j][4] = y.x; rows[j][5] = y.y; rows[j][6] = y.z; rows[j][7] = y.w;
         }

@@ -53,6 +53,15 @@ struct Inv {
 
 constexpr int MS = 72;  // doubles per block in the transpose buffer (64 + 8: conflict-free column writes)
 
+// Transpose-buffer slot of element (r, c) of a block: the 16-B pair c/2 of row r
+// is stored at pair (c/2) ^ (r & 3).  Column passes (lane c writes row r) still
+// fill each row's 64 B with two blocks per 16-lane ds_write_b64 group on
+// disjoint banks; row passes (lane r reads row r as 4 x ds_read_b128) then put
+// the 4 lanes of every 16-lane group that share a 64-B window (MS*8 = 576 B
+// shifts blocks by 16 banks) on 4 different 16-B slots: conflict-free instead
+// of 4-way (MI355X_MICROARCH.md §LDS bank rules).
+__device__ __forceinline__ int tslot(int r, int c) { return r * 8 + ((((c >> 1) ^ (r & 3)) << 1) | (c & 1)); }
+
 // Dequantize (quantizer.py:27-29) and IDCT column v of a block (axis 0 first,
 // dct_engine.py:12-14) into dst[r*8 + v].  `q` holds Q/16: q*Q is an exact
 // integer and scaling by 2^-4 commutes exactly with every rounding of the
@@ -65,7 +74,7 @@ __device__ __forceinline__ void idct_col(const int16_t* __restrict__ blk, const 
   for (int r = 0; r < 8; ++r) c[r] = (double)blk[r * 8 + v] * q[r * 8 + v];
   dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) dst[r * 8 + v] = c[r];
+  for (int r = 0; r < 8; ++r) dst[tslot(r, v)] = c[r];
 }
 
 // The same with the column's coefficients already loaded (software
@@ -86,14 +95,19 @@ __device__ __forceinline__ void idct_col(const Col16& in, const double* __restri
   for (int r = 0; r < 8; ++r) c[r] = (double)in.q[r] * q[r * 8 + v];
   dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) dst[r * 8 + v] = c[r];
+  for (int r = 0; r < 8; ++r) dst[tslot(r, v)] = c[r];
 }
 
 // Row u of a column-transformed block: axis-1 IDCT, fct 1/16, +128, clip
 // (dct_engine.py:23-27).
 __device__ __forceinline__ void idct_row(const double* __restrict__ src, int u, double (&c)[8]) {
+  const int sw = u & 3;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) c[k] = src[u * 8 + k];
+  for (int p = 0; p < 4; ++p) {  // pair p of row u (tslot), one 16-B read
+    const double2 d = *reinterpret_cast<const double2*>(src + u * 8 + 2 * (p ^ sw));
+    c[2 * p] = d.x;
+    c[2 * p + 1] = d.y;
+  }
   dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {

@@ -2,6 +2,7 @@
 // build of the HIP sources; JDS_PROBE_* macros strip parts of k_fwd32 to
 // attribute its time.  Prints avg microseconds per launch for 64 1080p frames.
 #include "../jpeg-dsp-studio_amd/csrc/jds_codec.hip"
+#include "../jpeg-dsp-studio_amd/csrc/jds_b16.hip"
 #include "../jpeg-dsp-studio_amd/csrc/jds_inv.hip"
 #include "../jpeg-dsp-studio_amd/csrc/jds_fast.hip"
 #include "../jpeg-dsp-studio_amd/csrc/jds_stages.hip"
