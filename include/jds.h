@@ -169,6 +169,28 @@ int jds_stage_block_dct_n(jds_ctx* ctx, const double* in, double* out, int64_t n
 int jds_stage_quantize_n(jds_ctx* ctx, const void* in, const double* qtable, int32_t table_len, void* out,
                          int64_t n, int32_t dequant);
 
+/* Baseline JPEG entropy coding (the reference only estimates
+ * the size, utils/metrics.py:51-92): coefficients in the reference's layout
+ * (all_quantized_coeffs, engines/pipeline.py:56,99) -> one JFIF file per frame:
+ * SOI, APP0, DQT (the frame's 8x8 table, zigzag order, utils/constants.py:18-27),
+ * SOF0, the T.81 Annex K Huffman tables, three non-interleaved scans (Y, Cb, Cr),
+ * EOI.  Byte-for-byte definition: oracle/jpeg_entropy.py.  8x8 blocks only;
+ * tables must hold integers in [1, 255].
+ *   jds_plan_entropy: device buffers; coeffs as jds_plan_run writes them; frame i's
+ *     file at out + i*out_stride (out_stride >= jds_plan_entropy_capacity), its
+ *     length in lengths[i] (u64, device), and optionally the entropy-coded bits of
+ *     its Y/Cb/Cr scans in scan_bits[3*i..] (before the byte pad).  Asynchronous.
+ *     lengths[i] = 0 marks a frame whose coefficients baseline JPEG cannot code
+ *     (DC difference category > 11 or AC category > 10; the codec path never
+ *     produces those).
+ *   jds_encode_jfif: one frame from host memory (synchronous); *out_len is set even
+ *     when out_cap is too small (then JDS_EINVAL). */
+int jds_plan_entropy_capacity(const jds_plan* plan, int64_t* bytes_per_frame);
+int jds_plan_entropy(jds_plan* plan, const int16_t* coeffs, uint8_t* out, int64_t out_stride, uint64_t* lengths,
+                     uint64_t* scan_bits, void* stream);
+int jds_encode_jfif(jds_ctx* ctx, const jds_params* p, int64_t H, int64_t W, const int16_t* coeffs, uint8_t* out,
+                    int64_t out_cap, int64_t* out_len, uint64_t* scan_bits);
+
 /* Test-only: evaluate the device DCT expressions (jds_dct8.hpp) on the host so
  * the CPU test suite can pin them against SciPy without a GPU.  Not used by
  * any product path.  in/out: n blocks of 8x8 f64; inverse: 0 = dctn, 1 = idctn. */

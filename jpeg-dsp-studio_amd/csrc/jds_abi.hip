@@ -41,6 +41,15 @@ hipError_t stage_block(const double* in, double* out, long long n, int bs, int o
 hipError_t stage_quant(const void* in, const double* q, void* out, long long n, int dequant, int period,
                        hipStream_t s);
 int tile_dims16(int mode, int* MY, int* MX);
+struct EntTab;
+void ent_build_tables(EntTab* t);
+size_t ent_tab_size();
+int ent_header(const double* q, int mode, int H, int W, uint8_t* o);
+long long ent_capacity(const Geo& g);
+void ent_sizes(const Geo& g, int n, size_t* sz);
+hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* const* buf, const uint8_t* hdr_dev,
+                          const void* tab_dev, uint8_t* out, long long stride, unsigned long long* lengths,
+                          unsigned long long* scan_bits, hipStream_t s);
 hipError_t launch_codec16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                           int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st, double* part,
                           double* planes, bool want_sse, double* err_y, double* err_rgb, hipStream_t s,
@@ -100,6 +109,7 @@ struct jds_ctx {
   DevBuf st[5];  // per-stage API staging
   DevBuf chunks;
   DevBuf planes;  // 16x16 path: reconstructed chroma planes
+  DevBuf ent[8], ent_hdr, ent_tab, ent_cf, ent_out, ent_meta;  // entropy coder (jds_encode_jfif)
 };
 
 // SSIM scratch in the context; returns the device pointer of 5 result doubles
@@ -123,6 +133,8 @@ struct jds_plan {
   DevBuf fq32, gk32, fixlist, counters, part32;  // part32: per-tile forward statistics
   Side side;  // border tiles run beside interior tiles
   DevBuf planes;  // 16x16 path: reconstructed chroma planes (n x 2 x hc x wc f64)
+  double* qt = nullptr;  // host copy of the per-frame 8x8 tables (entropy headers)
+  DevBuf ent[8], ent_hdr, ent_tab;  // entropy coder scratch, allocated by the first jds_plan_entropy
 };
 
 // ------------------------------------------------------------- geometry --
@@ -287,6 +299,12 @@ void jds_ctx_destroy(jds_ctx* c) {
   for (DevBuf& b : c->st) b.release();
   c->chunks.release();
   c->planes.release();
+  for (DevBuf& b : c->ent) b.release();
+  c->ent_hdr.release();
+  c->ent_tab.release();
+  c->ent_cf.release();
+  c->ent_out.release();
+  c->ent_meta.release();
   for (hipEvent_t e : c->ev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -322,6 +340,13 @@ int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n, int64_t H, in
   }
   p->ctx = ctx;
   p->n = n;
+  p->qt = (double*)malloc(sizeof(double) * 64 * (size_t)n);
+  if (!p->qt) {
+    free(hq);
+    delete p;
+    return fail(JDS_ENOMEM, "host allocation failed");
+  }
+  for (int i = 0; i < n; ++i) memcpy(p->qt + 64 * i, params[i].qtable, 64 * sizeof(double));
   p->mode = mode;
   p->pf = pf;
   p->g = g;
@@ -440,6 +465,10 @@ void jds_plan_destroy(jds_plan* p) {
   p->counters.release();
   p->part32.release();
   p->planes.release();
+  for (DevBuf& b : p->ent) b.release();
+  p->ent_hdr.release();
+  p->ent_tab.release();
+  free(p->qt);
   if (p->side.stream) (void)hipStreamDestroy(p->side.stream);
   if (p->side.fork) (void)hipEventDestroy(p->side.fork);
   if (p->side.join) (void)hipEventDestroy(p->side.join);
@@ -684,6 +713,101 @@ int jds_stage_quantize_n(jds_ctx* c, const void* in, const double* qtable, int32
 
 int jds_stage_quantize(jds_ctx* c, const void* in, const double* qtable, void* out, int64_t n, int32_t dequant) {
   return jds_stage_quantize_n(c, in, qtable, 64, out, n, dequant);
+}
+
+// ------------------------------------------------------- entropy coding --
+
+// Entropy-coder scratch for n frames of geometry g, plus per-frame JFIF headers
+// built from the 8x8 tables qt (n x 64).
+static int ent_prepare(const Geo& g, int mode, int n, const double* qt, DevBuf* ent, DevBuf& hdr, DevBuf& tab,
+                       hipStream_t s) {
+  if (g.bs != 8) return fail(JDS_ENOTSUP, "JPEG entropy coding needs 8x8 blocks (block_size %d)", g.bs);
+  if (g.H > 65535 || g.W > 65535) return fail(JDS_ENOTSUP, "baseline JPEG is limited to 65535 x 65535");
+  size_t sz[8];
+  ent_sizes(g, n, sz);
+  for (int i = 0; i < 8; ++i)
+    if (i != 6) HIP_TRY(ent[i].ensure(sz[i]));
+  const size_t hl = sz[6] / (size_t)n;
+  uint8_t* h = (uint8_t*)malloc(sz[6]);
+  if (!h) return fail(JDS_ENOMEM, "host allocation failed");
+  for (int i = 0; i < n; ++i) {
+    if (ent_header(qt + 64 * i, mode, g.H, g.W, h + hl * i) != (int)hl) {
+      free(h);
+      return fail(JDS_EINVAL, "frame %d: baseline JPEG needs integer quantisation steps in [1, 255]", i);
+    }
+  }
+  hipError_t e = hdr.ensure(sz[6]);
+  if (e == hipSuccess) e = hipMemcpyAsync(hdr.p, h, sz[6], hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);  // h is freed below
+  free(h);
+  HIP_TRY(e);
+  if (!tab.p) {
+    char t[4096];
+    ent_build_tables((EntTab*)t);
+    HIP_TRY(tab.ensure(ent_tab_size()));
+    HIP_TRY(hipMemcpy(tab.p, t, ent_tab_size(), hipMemcpyHostToDevice));
+  }
+  return JDS_OK;
+}
+
+int jds_plan_entropy_capacity(const jds_plan* p, int64_t* bytes_per_frame) {
+  if (!p || !bytes_per_frame) return fail(JDS_EINVAL, "null argument");
+  if (p->g.bs != 8) return fail(JDS_ENOTSUP, "JPEG entropy coding needs 8x8 blocks (block_size %d)", p->g.bs);
+  *bytes_per_frame = ent_capacity(p->g);
+  return JDS_OK;
+}
+
+int jds_plan_entropy(jds_plan* p, const int16_t* coeffs, uint8_t* out, int64_t out_stride, uint64_t* lengths,
+                     uint64_t* scan_bits, void* stream) {
+  if (!p || !coeffs || !out || !lengths) return fail(JDS_EINVAL, "null argument");
+  if (out_stride < ent_capacity(p->g))
+    return fail(JDS_EINVAL, "out_stride %lld < worst-case file size %lld", (long long)out_stride,
+                (long long)ent_capacity(p->g));
+  HIP_TRY(hipSetDevice(p->ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (!p->ent_hdr.p) {
+    int rc = ent_prepare(p->g, p->mode, p->n, p->qt, p->ent, p->ent_hdr, p->ent_tab, s);
+    if (rc) return rc;
+  }
+  void* bufs[8];
+  for (int i = 0; i < 8; ++i) bufs[i] = p->ent[i].p;
+  HIP_TRY(launch_entropy(p->g, p->n, coeffs, bufs, (const uint8_t*)p->ent_hdr.p, p->ent_tab.p, out, out_stride,
+                         (unsigned long long*)lengths, (unsigned long long*)scan_bits, s));
+  return JDS_OK;
+}
+
+int jds_encode_jfif(jds_ctx* c, const jds_params* prm, int64_t H, int64_t W, const int16_t* coeffs, uint8_t* out,
+                    int64_t out_cap, int64_t* out_len, uint64_t* scan_bits) {
+  if (!c || !prm || !coeffs || !out || !out_len) return fail(JDS_EINVAL, "null argument");
+  Geo g;
+  int mode;
+  int rc = make_geo(prm, H, W, &g, &mode, nullptr);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if ((rc = ent_prepare(g, mode, 1, prm->qtable, c->ent, c->ent_hdr, c->ent_tab, s))) return rc;
+  const long long cap = ent_capacity(g);
+  HIP_TRY(c->ent_cf.ensure((size_t)g.cpf * sizeof(int16_t)));
+  HIP_TRY(c->ent_out.ensure((size_t)cap));
+  HIP_TRY(c->ent_meta.ensure(4 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemcpyAsync(c->ent_cf.p, coeffs, (size_t)g.cpf * sizeof(int16_t), hipMemcpyHostToDevice, s));
+  void* bufs[8];
+  for (int i = 0; i < 8; ++i) bufs[i] = c->ent[i].p;
+  unsigned long long* meta = (unsigned long long*)c->ent_meta.p;
+  HIP_TRY(launch_entropy(g, 1, (const int16_t*)c->ent_cf.p, bufs, (const uint8_t*)c->ent_hdr.p, c->ent_tab.p,
+                         (uint8_t*)c->ent_out.p, cap, meta, meta + 1, s));
+  unsigned long long m[4];
+  HIP_TRY(hipMemcpyAsync(m, meta, sizeof m, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (m[0] == 0)
+    return fail(JDS_EINVAL, "coefficients outside baseline JPEG's range (DC difference category > 11 or "
+                            "AC category > 10)");
+  *out_len = (int64_t)m[0];
+  if (scan_bits)
+    for (int i = 0; i < 3; ++i) scan_bits[i] = m[1 + i];
+  if ((long long)m[0] > out_cap) return fail(JDS_EINVAL, "output buffer too small: %llu bytes needed", m[0]);
+  HIP_TRY(hipMemcpy(out, c->ent_out.p, (size_t)m[0], hipMemcpyDeviceToHost));
+  return JDS_OK;
 }
 
 int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t inverse) {

@@ -1,0 +1,516 @@
+// jds_entropy.hip — baseline JPEG entropy coding of the quantised coefficients
+// (SURVEY.md §8(f)4).  The reference stops at a size estimate
+// (utils/metrics.py:51-92, "no entropy coding") and keeps the zigzag order
+// unused (utils/constants.py:18-27); this turns its all_quantized_coeffs
+// (engines/pipeline.py:56,99) into a standard JFIF file per frame: one
+// quantisation table (all planes use the luma table, pipeline.py:43), the
+// T.81 Annex K standard Huffman tables, three non-interleaved scans (Y, Cb,
+// Cr; a non-interleaved scan's raster block order is exactly the reference's
+// block order).  Byte-for-byte definition: oracle/jpeg_entropy.py.
+//
+// Integer / byte work, HBM-bound by design.  Pipeline per batch of frames:
+//   k_ent_bits   one wave per 8x8 block, one lane per zigzag position: run
+//                lengths from a 64-bit ballot of the nonzero mask, Huffman
+//                code lengths from LDS tables -> bits per block.
+//   scan         exclusive prefix of block bits (hipCUB) -> bit offsets.
+//   k_ent_info   per scan: start offset, bit and byte counts.
+//   k_ent_zero   zero each block's first/last 32-bit word of the packed scan.
+//   k_ent_pack   recompute the lane codes, wave prefix of lane bit counts,
+//                assemble the block's bits in an LDS window (ds_or), plain
+//                stores for interior words, global atomic OR for the two
+//                boundary words it may share with neighbouring blocks.
+//   k_ent_ff     per 1 KiB chunk of a scan: 0xFF bytes (after the 1-bit pad).
+//   scan         exclusive prefix of the 0xFF counts -> stuffed offsets.
+//   k_ent_emit   chunk bytes -> the JFIF at their stuffed offsets (0x00 after
+//                every 0xFF).
+//   k_ent_frame  headers (host-built template: SOI, APP0, DQT, SOF0, DHT),
+//                the three SOS markers, EOI, file length.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+#include <string.h>
+
+#include <initializer_list>
+
+#include "jds_internal.hpp"
+
+namespace jds {
+
+// ------------------------------------------------------------ tables --
+
+// T.81 Annex K.3 (tables K.3 - K.6): BITS[1..16] and HUFFVAL
+static const uint8_t K3_BITS[16] = {0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0};
+static const uint8_t K4_BITS[16] = {0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
+static const uint8_t DC_VALS[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+static const uint8_t K5_BITS[16] = {0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7d};
+static const uint8_t K5_VALS[162] = {
+    0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51, 0x61, 0x07, 0x22, 0x71,
+    0x14, 0x32, 0x81, 0x91, 0xa1, 0x08, 0x23, 0x42, 0xb1, 0xc1, 0x15, 0x52, 0xd1, 0xf0, 0x24, 0x33, 0x62, 0x72,
+    0x82, 0x09, 0x0a, 0x16, 0x17, 0x18, 0x19, 0x1a, 0x25, 0x26, 0x27, 0x28, 0x29, 0x2a, 0x34, 0x35, 0x36, 0x37,
+    0x38, 0x39, 0x3a, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59,
+    0x5a, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a, 0x83,
+    0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9a, 0xa2, 0xa3,
+    0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3,
+    0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe1, 0xe2,
+    0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea, 0xf1, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+static const uint8_t K6_BITS[16] = {0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77};
+static const uint8_t K6_VALS[162] = {
+    0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61, 0x71, 0x13, 0x22,
+    0x32, 0x81, 0x08, 0x14, 0x42, 0x91, 0xa1, 0xb1, 0xc1, 0x09, 0x23, 0x33, 0x52, 0xf0, 0x15, 0x62, 0x72, 0xd1,
+    0x0a, 0x16, 0x24, 0x34, 0xe1, 0x25, 0xf1, 0x17, 0x18, 0x19, 0x1a, 0x26, 0x27, 0x28, 0x29, 0x2a, 0x35, 0x36,
+    0x37, 0x38, 0x39, 0x3a, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58,
+    0x59, 0x5a, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a,
+    0x82, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9a,
+    0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba,
+    0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda,
+    0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+// utils/constants.py:18-27: row-major index of the k-th zigzag coefficient
+static const uint8_t ZZ[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                               12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                               35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                               58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// Code tables as (length << 16 | code): [0] luma, [1] chroma.
+struct EntTab {
+  uint32_t dc[2][16];
+  uint32_t ac[2][256];
+  uint8_t zz[64];
+};
+
+// T.81 Annex C: code lengths and codes in order of increasing length
+static void huff_codes(const uint8_t* bits, const uint8_t* vals, uint32_t* out, int nsym) {
+  for (int i = 0; i < nsym; ++i) out[i] = 0;
+  uint32_t code = 0;
+  int k = 0;
+  for (int len = 1; len <= 16; ++len) {
+    for (int i = 0; i < bits[len - 1]; ++i, ++k) out[vals[k]] = ((uint32_t)len << 16) | code++;
+    code <<= 1;
+  }
+}
+
+void ent_build_tables(EntTab* t) {
+  memset(t, 0, sizeof *t);
+  huff_codes(K3_BITS, DC_VALS, t->dc[0], 16);
+  huff_codes(K4_BITS, DC_VALS, t->dc[1], 16);
+  huff_codes(K5_BITS, K5_VALS, t->ac[0], 256);
+  huff_codes(K6_BITS, K6_VALS, t->ac[1], 256);
+  memcpy(t->zz, ZZ, 64);
+}
+
+size_t ent_tab_size() { return sizeof(EntTab); }
+
+// JFIF header template (oracle/jpeg_entropy.py::jfif_headers): returns its length
+// (ENT_HDR bytes) or -1 if the table is not baseline (integers in [1, 255]).
+constexpr int ENT_HDR = 2 + 18 + 69 + 19 + 2 * (4 + 1 + 16 + 12) + 2 * (4 + 1 + 16 + 162);
+constexpr int ENT_SOS = 10;
+
+int ent_header(const double* q, int mode, int H, int W, uint8_t* o) {
+  int p = 0;
+  auto put = [&](std::initializer_list<int> b) {
+    for (int v : b) o[p++] = (uint8_t)v;
+  };
+  put({0xFF, 0xD8});
+  put({0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0, 1, 1, 0, 0, 1, 0, 1, 0, 0});
+  put({0xFF, 0xDB, 0x00, 0x43, 0x00});
+  for (int k = 0; k < 64; ++k) {
+    const double v = q[ZZ[k]];
+    if (!(v >= 1.0 && v <= 255.0) || v != (double)(int)v) return -1;
+    o[p++] = (uint8_t)(int)v;
+  }
+  const int smp = mode == M420 ? 0x22 : (mode == M422 ? 0x21 : 0x11);
+  put({0xFF, 0xC0, 0x00, 0x11, 0x08, H >> 8, H & 255, W >> 8, W & 255, 3, 1, smp, 0, 2, 0x11, 0, 3, 0x11, 0});
+  const uint8_t* bits[4] = {K3_BITS, K5_BITS, K4_BITS, K6_BITS};
+  const uint8_t* vals[4] = {DC_VALS, K5_VALS, DC_VALS, K6_VALS};
+  const int nv[4] = {12, 162, 12, 162}, id[4] = {0x00, 0x10, 0x01, 0x11};
+  for (int t = 0; t < 4; ++t) {
+    const int len = 3 + 16 + nv[t];
+    put({0xFF, 0xC4, len >> 8, len & 255, id[t]});
+    for (int i = 0; i < 16; ++i) o[p++] = bits[t][i];
+    for (int i = 0; i < nv[t]; ++i) o[p++] = vals[t][i];
+  }
+  return p;
+}
+
+// ------------------------------------------------------------ kernels --
+
+struct EntGeo {
+  int nb;          // blocks per frame (Y + Cb + Cr)
+  int first[4];    // first block of each scan within the frame, first[3] = nb
+  int cap_w[3];    // packed-scan capacity in 32-bit words (worst case 1660 bits per block)
+  long long raw_w; // packed words per frame
+  int chunks;      // 1 KiB chunks per scan (worst-case Y scan)
+  long long hdr;   // header template bytes per frame
+};
+
+__device__ __forceinline__ int scan_of(const EntGeo& e, int b) { return b < e.first[1] ? 0 : (b < e.first[2] ? 1 : 2); }
+
+__device__ __forceinline__ long long raw_base(const EntGeo& e, int frame, int s) {
+  return (long long)frame * e.raw_w + (s == 0 ? 0 : (s == 1 ? e.cap_w[0] : e.cap_w[0] + e.cap_w[1]));
+}
+
+__device__ __forceinline__ void load_tab(const EntTab* __restrict__ g, EntTab* s) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(s);
+  for (int i = threadIdx.x; i < (int)(sizeof(EntTab) / 4); i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+}
+
+// The code of lane k (zigzag position k) of a block: `v` its coefficient,
+// `nzm` the wave's nonzero mask, `diff` the DC difference (lane 0).
+// T.81 F.1.2.1 / F.1.2.2; returns the bit count, the bits right-aligned in *val.
+// Categories above the baseline limits (DC 11, AC 10: values the reference's
+// path cannot produce, but int16 input can hold) are clamped so the output
+// stays within the capacity, and reported through *bad.
+__device__ __forceinline__ int lane_code(int k, int v, uint64_t nzm, int diff, const uint32_t* dct,
+                                         const uint32_t* act, uint64_t* val, bool* bad) {
+  if (k == 0) {
+    const int a = diff < 0 ? -diff : diff;
+    int s = a ? 32 - __clz(a) : 0;
+    *bad = s > 11;
+    s = s > 11 ? 11 : s;
+    const uint32_t e = dct[s];
+    const int mag = (diff < 0 ? diff - 1 : diff) & ((1 << s) - 1);
+    *val = ((uint64_t)(e & 0xFFFFu) << s) | (uint64_t)mag;
+    return (int)(e >> 16) + s;
+  }
+  if (v != 0) {
+    const uint64_t lower = nzm & (((uint64_t)1 << k) - 1) & ~(uint64_t)1;
+    const int p = lower ? 63 - __clzll(lower) : 0;
+    const int r = k - p - 1;
+    const int a = v < 0 ? -v : v;
+    int s = 32 - __clz(a);
+    *bad = s > 10;
+    s = s > 10 ? 10 : s;
+    const uint32_t e = act[((r & 15) << 4) | s], z = act[0xF0];
+    const int zl = (int)(z >> 16), nz = r >> 4;
+    uint64_t acc = 0;
+    for (int i = 0; i < nz; ++i) acc = (acc << zl) | (z & 0xFFFFu);  // ZRL: 16 zeros
+    const int mag = (v < 0 ? v - 1 : v) & ((1 << s) - 1);
+    acc = (acc << (e >> 16)) | (e & 0xFFFFu);
+    *val = (acc << s) | (uint64_t)mag;
+    return nz * zl + (int)(e >> 16) + s;
+  }
+  *bad = false;
+  if (k == 63) {  // coefficient 63 is zero: EOB after the last nonzero (lane 63 comes last)
+    const uint32_t e = act[0x00];
+    *val = e & 0xFFFFu;
+    return (int)(e >> 16);
+  }
+  *val = 0;
+  return 0;
+}
+
+__device__ __forceinline__ int wave_excl_sum(int x, int lane) {
+  int inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  return inc - x;
+}
+
+// Per wave: one block's lane code.  Returns the lane's bit count.
+__device__ __forceinline__ int block_lane(const EntGeo& e, const int16_t* __restrict__ coeffs, long long gb,
+                                          const EntTab* t, int lane, uint64_t* val, bool* bad) {
+  const int frame = (int)(gb / e.nb), b = (int)(gb - (long long)frame * e.nb);
+  const int s = scan_of(e, b);
+  const int16_t* blk = coeffs + gb * 64;
+  const int v = blk[t->zz[lane]];
+  int diff = 0;
+  if (lane == 0) diff = v - (b == e.first[s] ? 0 : (int)blk[-64]);  // DC predictor resets per scan
+  const uint64_t nzm = __ballot(v != 0);
+  const int cls = s == 0 ? 0 : 1;
+  return lane_code(lane, v, nzm, diff, t->dc[cls], t->ac[cls], val, bad);
+}
+
+__global__ void __launch_bounds__(256) k_ent_bits(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
+                                                  const EntTab* __restrict__ gt, unsigned long long* __restrict__ bits,
+                                                  unsigned long long* __restrict__ bad) {
+  __shared__ EntTab t;
+  load_tab(gt, &t);
+  const int lane = threadIdx.x & 63;
+  const long long gb = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gb >= nblk) return;
+  uint64_t val;
+  bool b;
+  int n = block_lane(e, coeffs, gb, &t, lane, &val, &b);
+  if (__ballot(b) && lane == 0) bad[gb / e.nb] = 1ull;  // not baseline-codable: the frame is reported
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+  if (lane == 0) bits[gb] = (unsigned long long)n;
+}
+
+// info[(f*3+s)*2 + 0] = scan start (global bit prefix), [1] = scan bits
+__global__ void k_ent_info(const EntGeo e, int n, const unsigned long long* __restrict__ excl,
+                           unsigned long long* __restrict__ info, unsigned long long* __restrict__ scan_bits) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * 3) return;
+  const int f = i / 3, s = i - f * 3;
+  const unsigned long long a = excl[(long long)f * e.nb + e.first[s]], b = excl[(long long)f * e.nb + e.first[s + 1]];
+  info[2 * i] = a;
+  info[2 * i + 1] = b - a;
+  if (scan_bits) scan_bits[i] = b - a;
+}
+
+__global__ void __launch_bounds__(256) k_ent_zero(const EntGeo e, long long nblk, const unsigned long long* __restrict__ bits,
+                                                  const unsigned long long* __restrict__ excl,
+                                                  const unsigned long long* __restrict__ info, uint32_t* __restrict__ raw) {
+  const long long gb = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gb >= nblk) return;
+  const int f = (int)(gb / e.nb), s = scan_of(e, (int)(gb - (long long)f * e.nb));
+  const unsigned long long rel = excl[gb] - info[2 * (f * 3 + s)];
+  uint32_t* w = raw + raw_base(e, f, s);
+  w[rel >> 5] = 0u;
+  w[(rel + bits[gb] - 1) >> 5] = 0u;
+}
+
+constexpr int ENT_WIN = 64;  // LDS words per block window (max 1660 + 31 bits)
+
+__global__ void __launch_bounds__(256) k_ent_pack(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
+                                                  const EntTab* __restrict__ gt,
+                                                  const unsigned long long* __restrict__ excl,
+                                                  const unsigned long long* __restrict__ info,
+                                                  uint32_t* __restrict__ raw) {
+  __shared__ EntTab t;
+  __shared__ uint32_t s_win[4][ENT_WIN];
+  load_tab(gt, &t);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long gb = (long long)blockIdx.x * 4 + wv;
+  if (gb >= nblk) return;
+  uint32_t* win = s_win[wv];
+  win[lane] = 0u;
+  uint64_t val;
+  bool bad;
+  const int n = block_lane(e, coeffs, gb, &t, lane, &val, &bad);
+  int tot = n;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+  const int loff = wave_excl_sum(n, lane);
+  const int f = (int)(gb / e.nb), s = scan_of(e, (int)(gb - (long long)f * e.nb));
+  const unsigned long long rel = excl[gb] - info[2 * (f * 3 + s)];
+  const int lp = (int)(rel & 31) + loff;  // bit position in the window (0 = MSB of word 0)
+  __builtin_amdgcn_wave_barrier();        // window cleared before any lane ORs into it (one wave: in order)
+  asm volatile("" ::: "memory");
+  if (n) {
+    const int j0 = lp >> 5, j1 = (lp + n - 1) >> 5;
+    for (int j = j0; j <= j1; ++j) {
+      const int sh = lp + n - 32 * (j + 1);
+      const uint32_t piece = sh >= 0 ? (uint32_t)(val >> sh) : (uint32_t)(val << -sh);
+      atomicOr(&win[j], piece);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  const int nw = ((int)(rel & 31) + tot + 31) >> 5;
+  if (lane < nw) {
+    uint32_t* dst = raw + raw_base(e, f, s) + (rel >> 5) + lane;
+    const uint32_t w = __builtin_bswap32(win[lane]);  // bitstream order: MSB first, byte 0 first
+    if (lane == 0 || lane == nw - 1)
+      atomicOr(dst, w);  // may share this word with the neighbouring blocks
+    else
+      *dst = w;
+  }
+}
+
+constexpr int ENT_CH = 1024;  // bytes per stuffing chunk (256 threads x 4)
+
+// byte i of scan (f, s) with the 1-bit pad applied (T.81 F.1.2.3)
+__device__ __forceinline__ uint32_t scan_word(const uint32_t* w, int i4, unsigned long long nbits) {
+  const unsigned long long nbytes = (nbits + 7) >> 3;
+  uint32_t x = w[i4];
+  const unsigned long long last = nbytes - 1;
+  if ((nbits & 7) && (unsigned long long)i4 == (last >> 2)) {
+    const int pad = 8 - (int)(nbits & 7);
+    x |= ((1u << pad) - 1u) << (8 * (int)(last & 3));
+  }
+  return x;
+}
+
+// grid (CG, 3, n): workgroups stride over the chunks a scan actually has (ffc
+// is zeroed beforehand for the rest)
+__global__ void __launch_bounds__(256) k_ent_ff(const EntGeo e, const unsigned long long* __restrict__ info,
+                                                const uint32_t* __restrict__ raw, unsigned long long* __restrict__ ffc) {
+  __shared__ int s_red[2][4];
+  const int s = blockIdx.y, f = blockIdx.z;
+  const unsigned long long nbits = info[2 * (f * 3 + s) + 1], nbytes = (nbits + 7) >> 3;
+  const long long nch = (long long)((nbytes + ENT_CH - 1) / ENT_CH);
+  const uint32_t* w = raw + raw_base(e, f, s);
+  int par = 0;
+  for (long long c = blockIdx.x; c < nch; c += gridDim.x, par ^= 1) {
+    const long long i0 = c * ENT_CH + 4 * threadIdx.x;
+    int cnt = 0;
+    if ((unsigned long long)i0 < nbytes) {
+      const uint32_t x = scan_word(w, (int)(i0 >> 2), nbits);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        cnt += ((unsigned long long)(i0 + k) < nbytes && ((x >> (8 * k)) & 255u) == 255u) ? 1 : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) s_red[par][threadIdx.x >> 6] = cnt;  // double-buffered: one barrier per chunk
+    __syncthreads();
+    if (threadIdx.x == 0)
+      ffc[((long long)f * 3 + s) * e.chunks + c] =
+          (unsigned long long)(s_red[par][0] + s_red[par][1] + s_red[par][2] + s_red[par][3]);
+  }
+}
+
+// output offset of scan s of frame f (after its SOS marker)
+__device__ __forceinline__ long long scan_out(const EntGeo& e, int f, int s, const unsigned long long* info,
+                                              const unsigned long long* ffx) {
+  long long p = e.hdr + ENT_SOS;
+  for (int j = 0; j < s; ++j) {
+    const unsigned long long nb = (info[2 * (f * 3 + j) + 1] + 7) >> 3;
+    const unsigned long long ff = ffx[((long long)f * 3 + j + 1) * e.chunks] - ffx[((long long)f * 3 + j) * e.chunks];
+    p += (long long)(nb + ff) + ENT_SOS;
+  }
+  return p;
+}
+
+__global__ void __launch_bounds__(256) k_ent_emit(const EntGeo e, const unsigned long long* __restrict__ info,
+                                                  const uint32_t* __restrict__ raw,
+                                                  const unsigned long long* __restrict__ ffx, uint8_t* __restrict__ out,
+                                                  long long stride) {
+  __shared__ int s_w[2][4];
+  const int s = blockIdx.y, f = blockIdx.z;
+  const unsigned long long nbits = info[2 * (f * 3 + s) + 1], nbytes = (nbits + 7) >> 3;
+  const long long nch = (long long)((nbytes + ENT_CH - 1) / ENT_CH);
+  const uint32_t* w = raw + raw_base(e, f, s);
+  const long long cidx = ((long long)f * 3 + s) * e.chunks;
+  const long long sbase = scan_out(e, f, s, info, ffx);
+  uint8_t* dst = out + (long long)f * stride;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int par = 0;
+  for (long long c = blockIdx.x; c < nch; c += gridDim.x, par ^= 1) {
+    const long long i0 = c * ENT_CH + 4 * threadIdx.x;
+    uint32_t x = 0;
+    int nv = 0, ff = 0;
+    if ((unsigned long long)i0 < nbytes) {
+      x = scan_word(w, (int)(i0 >> 2), nbits);
+      nv = nbytes - i0 < 4 ? (int)(nbytes - i0) : 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ff += (k < nv && ((x >> (8 * k)) & 255u) == 255u) ? 1 : 0;
+    }
+    // exclusive prefix of ff over the workgroup (double-buffered partials: one barrier per chunk)
+    const int ex = wave_excl_sum(ff, lane);
+    if (lane == 63) s_w[par][wv] = ex + ff;
+    __syncthreads();
+    int base = 0;
+    for (int i = 0; i < wv; ++i) base += s_w[par][i];
+    long long o = sbase + i0 + (long long)(ffx[cidx + c] - ffx[cidx]) + base + ex;
+    for (int k = 0; k < nv; ++k) {
+      const uint8_t b = (uint8_t)(x >> (8 * k));
+      dst[o++] = b;
+      if (b == 0xFF) dst[o++] = 0x00;
+    }
+  }
+}
+
+__global__ void k_ent_frame(const EntGeo e, const uint8_t* __restrict__ hdr, const unsigned long long* __restrict__ info,
+                            const unsigned long long* __restrict__ ffx, uint8_t* __restrict__ out, long long stride,
+                            unsigned long long* __restrict__ lengths, const unsigned long long* __restrict__ bad) {
+  const int f = blockIdx.x;
+  uint8_t* dst = out + (long long)f * stride;
+  for (int i = threadIdx.x; i < e.hdr; i += blockDim.x) dst[i] = hdr[(long long)f * e.hdr + i];
+  if (threadIdx.x < 3) {
+    const int s = threadIdx.x;
+    uint8_t* m = dst + scan_out(e, f, s, info, ffx) - ENT_SOS;
+    const uint8_t sos[ENT_SOS] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(s + 1), (uint8_t)(s == 0 ? 0x00 : 0x11),
+                                  0x00, 0x3F, 0x00};
+    for (int i = 0; i < ENT_SOS; ++i) m[i] = sos[i];
+  }
+  if (threadIdx.x == 0) {
+    // end of the Cr scan = start of a fourth scan minus its SOS
+    const unsigned long long nb = (info[2 * (f * 3 + 2) + 1] + 7) >> 3;
+    const unsigned long long ff = ffx[((long long)f * 3 + 3) * e.chunks] - ffx[((long long)f * 3 + 2) * e.chunks];
+    const long long end = scan_out(e, f, 2, info, ffx) + (long long)(nb + ff);
+    dst[end] = 0xFF;
+    dst[end + 1] = 0xD9;
+    if (lengths) lengths[f] = bad[f] ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
+  }
+}
+
+// ------------------------------------------------------------ driver --
+
+EntGeo ent_geo(const Geo& g) {
+  EntGeo e{};
+  const int ny = g.nby * g.nbx, nc = g.ncy * g.ncx;
+  e.nb = ny + 2 * nc;
+  e.first[0] = 0;
+  e.first[1] = ny;
+  e.first[2] = ny + nc;
+  e.first[3] = e.nb;
+  e.cap_w[0] = (int)(((long long)ny * 1660 + 31) / 32) + 2;
+  e.cap_w[1] = e.cap_w[2] = (int)(((long long)nc * 1660 + 31) / 32) + 2;
+  e.raw_w = (long long)e.cap_w[0] + 2LL * e.cap_w[1];
+  e.chunks = (int)(((long long)e.cap_w[0] * 4 + ENT_CH - 1) / ENT_CH);
+  e.hdr = ENT_HDR;
+  return e;
+}
+
+// worst case file: header + 3 SOS + every scan at 1660 bits per block, all bytes stuffed + EOI
+long long ent_capacity(const Geo& g) {
+  const EntGeo e = ent_geo(g);
+  return e.hdr + 3 * ENT_SOS + 2 * 4 * e.raw_w + 2;
+}
+
+// scratch sizes (bytes): [0] bits, [1] excl, [2] info, [3] raw, [4] ffc, [5] ffx, [6] hdr, [7] cub temp
+void ent_sizes(const Geo& g, int n, size_t* sz) {
+  const EntGeo e = ent_geo(g);
+  const long long nblk = (long long)n * e.nb;
+  const long long nch = (long long)n * 3 * e.chunks;
+  sz[0] = sizeof(unsigned long long) * (nblk + 1);
+  sz[1] = sizeof(unsigned long long) * (nblk + 1);
+  sz[2] = sizeof(unsigned long long) * 7 * n;  // 6 per frame (scan start / bits) + the frame's error flag
+  sz[3] = sizeof(uint32_t) * e.raw_w * n;
+  sz[4] = sizeof(unsigned long long) * (nch + 1);
+  sz[5] = sizeof(unsigned long long) * (nch + 1);
+  sz[6] = (size_t)e.hdr * n;
+  size_t t1 = 0, t2 = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                         (int)(nblk + 1));
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                         (int)(nch + 1));
+  sz[7] = (t1 > t2 ? t1 : t2) + 256;
+}
+
+hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* const* buf, const uint8_t* hdr_dev,
+                          const void* tab_dev, uint8_t* out, long long stride, unsigned long long* lengths,
+                          unsigned long long* scan_bits, hipStream_t s) {
+  const EntGeo e = ent_geo(g);
+  const long long nblk = (long long)n * e.nb;
+  const long long nch = (long long)n * 3 * e.chunks;
+  auto* bits = (unsigned long long*)buf[0];
+  auto* excl = (unsigned long long*)buf[1];
+  auto* info = (unsigned long long*)buf[2];
+  auto* raw = (uint32_t*)buf[3];
+  auto* ffc = (unsigned long long*)buf[4];
+  auto* ffx = (unsigned long long*)buf[5];
+  void* temp = buf[7];
+  size_t sz[8];
+  ent_sizes(g, n, sz);
+  const EntTab* tab = (const EntTab*)tab_dev;
+  hipError_t err;
+  const unsigned gw = (unsigned)((nblk + 3) / 4);
+  unsigned long long* bad = info + 6 * n;
+  if ((err = hipMemsetAsync(bits + nblk, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
+  if ((err = hipMemsetAsync(bad, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) return err;
+  hipLaunchKernelGGL(k_ent_bits, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, bad);
+  if ((err = hipGetLastError()) != hipSuccess) return err;
+  size_t tb = sz[7];
+  if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, bits, excl, (int)(nblk + 1), s)) != hipSuccess) return err;
+  hipLaunchKernelGGL(k_ent_info, dim3((3 * n + 63) / 64), dim3(64), 0, s, e, n, excl, info, scan_bits);
+  hipLaunchKernelGGL(k_ent_zero, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, e, nblk, bits, excl, info, raw);
+  hipLaunchKernelGGL(k_ent_pack, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, excl, info, raw);
+  const dim3 cg(e.chunks < 64 ? e.chunks : 64, 3, n);
+  if ((err = hipMemsetAsync(ffc, 0, sizeof(unsigned long long) * (nch + 1), s)) != hipSuccess) return err;
+  hipLaunchKernelGGL(k_ent_ff, cg, dim3(256), 0, s, e, info, raw, ffc);
+  tb = sz[7];
+  if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, ffc, ffx, (int)(nch + 1), s)) != hipSuccess) return err;
+  hipLaunchKernelGGL(k_ent_emit, cg, dim3(256), 0, s, e, info, raw, ffx, out, stride);
+  hipLaunchKernelGGL(k_ent_frame, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, bad);
+  return hipGetLastError();
+}
+
+}  // namespace jds

@@ -92,6 +92,10 @@ _SIGS = {
     'jds_stage_quantize': (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int32]),
     'jds_stage_block_dct_n': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32]),
     'jds_stage_quantize_n': (C.c_int, [_P, _P, _P, C.c_int32, _P, C.c_int64, C.c_int32]),
+    'jds_plan_entropy_capacity': (C.c_int, [_P, C.POINTER(C.c_int64)]),
+    'jds_plan_entropy': (C.c_int, [_P, _P, _P, C.c_int64, _P, _P, _P]),
+    'jds_encode_jfif': (C.c_int, [_P, C.POINTER(Params), C.c_int64, C.c_int64, _P, _P, C.c_int64,
+                                  C.POINTER(C.c_int64), _P]),
     'jds_selftest_dct8x8': (C.c_int, [_P, _P, C.c_int64, C.c_int32]),
     'jds_selftest_dct16x16': (C.c_int, [_P, _P, C.c_int64, C.c_int32]),
 }

@@ -1,0 +1,122 @@
+"""GPU parity of the JPEG entropy coder (csrc/jds_entropy.hip) against the CPU
+oracle (oracle/jpeg_entropy.py): identical JFIF bytes and scan bit counts, on
+coefficients from the codec path and on synthetic extreme coefficients; the
+GPU file decodes with libjpeg (Pillow)."""
+import io
+
+import numpy as np
+import pytest
+
+from oracle import cpu_ref
+from oracle import jpeg_entropy as je
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module', autouse=True)
+def gpu():
+    from jds import build, _abi
+    build.build()
+    assert _abi.device_count() >= 1, 'no HIP device: the MI355X path has no CPU fallback'
+
+
+def counts(h, w, mode):
+    ny = ((h + 7) // 8) * ((w + 7) // 8)
+    sy, sx = (2, 2) if mode == '4:2:0' else ((1, 2) if mode == '4:2:2' else (1, 1))
+    nc = ((h // sy + 7) // 8) * ((w // sx + 7) // 8)
+    return ny, nc
+
+
+@pytest.mark.parametrize('h,w,mode,q,pf', [
+    (64, 96, '4:2:0', 50, True), (48, 40, '4:2:2', 90, False), (33, 47, '4:4:4', 10, False),
+    (120, 160, '4:2:0', 100, True), (16, 16, '4:2:0', 1, False), (2, 2, '4:2:0', 50, False),
+    (1, 9, '4:4:4', 75, False), (264, 200, '4:2:2', 95, True), (1080, 1920, '4:2:0', 50, True),
+])
+def test_gpu_jfif_matches_oracle(h, w, mode, q, pf):
+    from jds import entropy
+    from jds.codec import compress_reconstruct_raw
+    img = cpu_ref.random_image(h, w, 31 * h + w + q)
+    qt = cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q)
+    raw = compress_reconstruct_raw(img, q, qt, mode, pf, maps=False)
+    ny, nc = counts(h, w, mode)
+    ref, ref_bits = je.encode_jfif(raw['coeffs'], h, w, mode, qt, ny, nc)
+    got, bits = entropy.encode_jfif(raw['coeffs'], h, w, mode, qt)
+    assert bits == ref_bits
+    assert got == ref
+    if h >= 8:
+        from PIL import Image
+        im = np.asarray(Image.open(io.BytesIO(got)).convert('RGB')).astype(np.int64)
+        assert np.abs(im - raw['reconstructed']).max() <= 4
+
+
+def test_gpu_jfif_extreme_coefficients():
+    """Synthetic coefficients at the baseline limits: category-11 DC differences,
+    +-1023 AC, long zero runs (ZRL), coefficient 63 set (no EOB), dense blocks."""
+    from jds import entropy
+    h, w, mode = 96, 128, '4:4:4'
+    ny, nc = counts(h, w, mode)
+    rng = np.random.default_rng(11)
+    blk = np.zeros((ny + 2 * nc, 64), np.int64)
+    blk[:, 0] = rng.choice([1023, -1024, 0, 5], len(blk))
+    zz = je.ZIGZAG
+    kind = rng.integers(0, 5, len(blk))
+    for i in np.flatnonzero(kind == 1):
+        blk[i, zz[63]] = rng.choice([1023, -1023, 1])
+    for i in np.flatnonzero(kind == 2):
+        blk[i, zz[1:]] = rng.integers(-1023, 1024, 63)
+    for i in np.flatnonzero(kind == 3):
+        pos = rng.choice(np.arange(1, 64), 3, replace=False)
+        blk[i, zz[pos]] = rng.integers(-1023, 1024, 3)
+    cf = blk.astype(np.int16).reshape(-1)
+    qt = np.ones((8, 8))
+    ref, ref_bits = je.encode_jfif(cf, h, w, mode, qt, ny, nc)
+    got, bits = entropy.encode_jfif(cf, h, w, mode, qt)
+    assert bits == ref_bits and got == ref
+    assert np.array_equal(je.decode_jfif(got)['coeffs'], cf)
+
+
+def test_gpu_plan_entropy_batch():
+    """Device-resident path: a plan's coefficients -> one file per frame (different Q per frame)."""
+    import torch
+    from jds import _abi, codec, entropy
+    qs = [5, 50, 95]
+    H, W, mode = 360, 648, '4:2:0'
+    frames = np.stack([cpu_ref.random_image(H, W, 200 + s) for s in range(len(qs))])
+    params = [_abi.make_params(q, cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q), mode, True,
+                               codec.gaussian_kernel3()) for q in qs]
+    plan = _abi.Plan(_abi.context(0), params, H, W)
+    ent = entropy.PlanEntropy(plan)
+    dev = torch.device('cuda:0')
+    rgb = torch.from_numpy(frames).to(dev)
+    out = torch.empty_like(rgb)
+    cf = torch.empty((len(qs), plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+    st = torch.zeros((len(qs), _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    files = torch.empty((len(qs), ent.capacity), dtype=torch.uint8, device=dev)
+    lengths = torch.zeros(len(qs), dtype=torch.int64, device=dev)
+    sbits = torch.zeros((len(qs), 3), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), 0, s)
+    ent.run(cf.data_ptr(), files.data_ptr(), ent.capacity, lengths.data_ptr(), sbits.data_ptr(), s)
+    torch.cuda.synchronize()
+    ny, nc = counts(H, W, mode)
+    for i, q in enumerate(qs):
+        ref = cpu_ref.compress_reconstruct(frames[i], q, 8, mode, True, metrics=False)
+        data, bits = je.encode_jfif(ref['coeffs'], H, W, mode, ref['qtable'], ny, nc)
+        n = int(lengths[i])
+        assert files[i, :n].cpu().numpy().tobytes() == data, q
+        assert sbits[i].cpu().tolist() == bits
+    plan.close()
+
+
+def test_gpu_jfif_rejects_non_baseline_coefficients():
+    from jds import entropy
+    h, w, mode = 16, 16, '4:4:4'
+    ny, nc = counts(h, w, mode)
+    cf = np.zeros((ny + 2 * nc) * 64, np.int16)
+    cf[64 * 2 + 5] = 2000  # AC category 11
+    with pytest.raises(ValueError, match='baseline'):
+        entropy.encode_jfif(cf, h, w, mode, np.ones((8, 8)))
+    cf[64 * 2 + 5] = 0
+    cf[64 * 3] = 3000  # DC difference category 12
+    with pytest.raises(ValueError, match='baseline'):
+        entropy.encode_jfif(cf, h, w, mode, np.ones((8, 8)))
