@@ -49,6 +49,8 @@ def parse():
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
+    ap.add_argument('--no-entropy', action='store_true',
+                    help='skip the JPEG entropy-coding measurement (8x8 only, outside the timed region)')
     ap.add_argument('--chunks', type=int, default=1,
                     help='split the batch into this many plans; the forward of chunk c+1 overlaps the inverse of c')
     return ap.parse_args()
@@ -223,6 +225,38 @@ def main():
         'fixups_last_step': {'fwd_blocks': int(sum(int(p_.fix_counts()[0]) for p_ in plans))},
         'pipeline_roofline_frac': round(value / world * 1e6 * (6 + 2 * S) / (HBM_PEAK_GBS * 1e9), 4),
     }
+
+    if not args.no_entropy and args.block == 8 and K == 1:
+        # JPEG entropy coding of the step's coefficients (jds_entropy.hip), timed on
+        # its own after the headline region: files per frame, real bits per pixel
+        from jds import entropy
+        ent = entropy.PlanEntropy(plans[0])
+        files = torch.empty((B, ent.capacity), dtype=torch.uint8, device=dev)
+        lengths = torch.zeros(B, dtype=torch.int64, device=dev)
+        for _ in range(2):
+            ent.run(coeffs.data_ptr(), files.data_ptr(), ent.capacity, lengths.data_ptr(), 0, s_f.cuda_stream)
+        reps = 10
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s_f)
+        for _ in range(reps):
+            ent.run(coeffs.data_ptr(), files.data_ptr(), ent.capacity, lengths.data_ptr(), 0, s_f.cuda_stream)
+        e1.record(s_f)
+        torch.cuda.synchronize(dev)
+        t_ent = e0.elapsed_time(e1) / reps
+        nbytes = int(lengths.sum().item())
+        moved = B * cpf * 2 + nbytes  # algorithmic: coefficients in, files out
+        result['entropy'] = {
+            'kernels': 'k_ent_bits, k_ent_pack, k_ent_ff, k_ent_emit (+ 2 hipCUB scans)', 'ms_per_step': round(t_ent, 4),
+            'Mpixels_per_s': round(px_per_step / (t_ent * 1e-3) / 1e6 * world, 2),
+            'file_bytes_per_frame': round(nbytes / B, 1), 'bpp': round(8 * nbytes / px_per_step, 4),
+            'bpp_estimate_no_entropy': None,
+            'achieved_GBps': round(moved / (t_ent * 1e-3) / 1e9, 2),
+            'frac': round(moved / (t_ent * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        st0 = stats[0].cpu().numpy().view(_abi.STATS_DTYPE)[0]
+        from utils.metrics import bitrate_from_counts
+        result['entropy']['bpp_estimate_no_entropy'] = round(bitrate_from_counts(
+            int(st0['nonzero']), float(st0['magnitude_bits']), int(st0['total_coeffs']), (H, W), 8)['bpp'], 4)
+        del files
 
     if rank == 0 and not args.no_parity:
         # PSNR / bytes vs the reference restatement on frame 0 (outside the timed region)

@@ -32,7 +32,6 @@
 
 namespace jds {
 
-constexpr int B16 = 16;
 constexpr int BS16 = 264;  // doubles per 16x16 block in LDS (256 + 8 pad)
 
 template <int MODE>

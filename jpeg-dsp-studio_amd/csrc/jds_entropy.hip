@@ -9,16 +9,18 @@
 // block order).  Byte-for-byte definition: oracle/jpeg_entropy.py.
 //
 // Integer / byte work, HBM-bound by design.  Pipeline per batch of frames:
-//   k_ent_bits   one wave per 8x8 block, one lane per zigzag position: run
-//                lengths from a 64-bit ballot of the nonzero mask, Huffman
-//                code lengths from LDS tables -> bits per block.
+//   k_ent_bits   one lane per 8x8 block: coefficients in registers, the
+//                zigzag walk unrolled at compile time, Huffman code lengths
+//                from LDS tables -> bits per block.  Coefficients the
+//                baseline tables cannot code are clamped (bounded output)
+//                and flag the frame.
 //   scan         exclusive prefix of block bits (hipCUB) -> bit offsets.
 //   k_ent_info   per scan: start offset, bit and byte counts.
 //   k_ent_zero   zero each block's first/last 32-bit word of the packed scan.
-//   k_ent_pack   recompute the lane codes, wave prefix of lane bit counts,
-//                assemble the block's bits in an LDS window (ds_or), plain
-//                stores for interior words, global atomic OR for the two
-//                boundary words it may share with neighbouring blocks.
+//   k_ent_pack   the same walk, packing MSB-first into 32-bit words from the
+//                block's bit offset: plain stores for the block's own words,
+//                atomic OR for the first / last word it may share with
+//                neighbouring blocks.
 //   k_ent_ff     per 1 KiB chunk of a scan: 0xFF bytes (after the 1-bit pad).
 //   scan         exclusive prefix of the 0xFF counts -> stuffed offsets.
 //   k_ent_emit   chunk bytes -> the JFIF at their stuffed offsets (0x00 after
@@ -158,48 +160,6 @@ __device__ __forceinline__ void load_tab(const EntTab* __restrict__ g, EntTab* s
 // The code of lane k (zigzag position k) of a block: `v` its coefficient,
 // `nzm` the wave's nonzero mask, `diff` the DC difference (lane 0).
 // T.81 F.1.2.1 / F.1.2.2; returns the bit count, the bits right-aligned in *val.
-// Categories above the baseline limits (DC 11, AC 10: values the reference's
-// path cannot produce, but int16 input can hold) are clamped so the output
-// stays within the capacity, and reported through *bad.
-__device__ __forceinline__ int lane_code(int k, int v, uint64_t nzm, int diff, const uint32_t* dct,
-                                         const uint32_t* act, uint64_t* val, bool* bad) {
-  if (k == 0) {
-    const int a = diff < 0 ? -diff : diff;
-    int s = a ? 32 - __clz(a) : 0;
-    *bad = s > 11;
-    s = s > 11 ? 11 : s;
-    const uint32_t e = dct[s];
-    const int mag = (diff < 0 ? diff - 1 : diff) & ((1 << s) - 1);
-    *val = ((uint64_t)(e & 0xFFFFu) << s) | (uint64_t)mag;
-    return (int)(e >> 16) + s;
-  }
-  if (v != 0) {
-    const uint64_t lower = nzm & (((uint64_t)1 << k) - 1) & ~(uint64_t)1;
-    const int p = lower ? 63 - __clzll(lower) : 0;
-    const int r = k - p - 1;
-    const int a = v < 0 ? -v : v;
-    int s = 32 - __clz(a);
-    *bad = s > 10;
-    s = s > 10 ? 10 : s;
-    const uint32_t e = act[((r & 15) << 4) | s], z = act[0xF0];
-    const int zl = (int)(z >> 16), nz = r >> 4;
-    uint64_t acc = 0;
-    for (int i = 0; i < nz; ++i) acc = (acc << zl) | (z & 0xFFFFu);  // ZRL: 16 zeros
-    const int mag = (v < 0 ? v - 1 : v) & ((1 << s) - 1);
-    acc = (acc << (e >> 16)) | (e & 0xFFFFu);
-    *val = (acc << s) | (uint64_t)mag;
-    return nz * zl + (int)(e >> 16) + s;
-  }
-  *bad = false;
-  if (k == 63) {  // coefficient 63 is zero: EOB after the last nonzero (lane 63 comes last)
-    const uint32_t e = act[0x00];
-    *val = e & 0xFFFFu;
-    return (int)(e >> 16);
-  }
-  *val = 0;
-  return 0;
-}
-
 __device__ __forceinline__ int wave_excl_sum(int x, int lane) {
   int inc = x;
 #pragma unroll
@@ -210,35 +170,139 @@ __device__ __forceinline__ int wave_excl_sum(int x, int lane) {
   return inc - x;
 }
 
-// Per wave: one block's lane code.  Returns the lane's bit count.
-__device__ __forceinline__ int block_lane(const EntGeo& e, const int16_t* __restrict__ coeffs, long long gb,
-                                          const EntTab* t, int lane, uint64_t* val, bool* bad) {
-  const int frame = (int)(gb / e.nb), b = (int)(gb - (long long)frame * e.nb);
-  const int s = scan_of(e, b);
-  const int16_t* blk = coeffs + gb * 64;
-  const int v = blk[t->zz[lane]];
-  int diff = 0;
-  if (lane == 0) diff = v - (b == e.first[s] ? 0 : (int)blk[-64]);  // DC predictor resets per scan
-  const uint64_t nzm = __ballot(v != 0);
-  const int cls = s == 0 ? 0 : 1;
-  return lane_code(lane, v, nzm, diff, t->dc[cls], t->ac[cls], val, bad);
+// One LANE per block: its 64 coefficients sit in 32 VGPRs (packed int16
+// pairs) and the zigzag walk is unrolled at compile time, so every register
+// index is a constant; the per-coefficient work is a handful of integer ops
+// under the lane's own "nonzero" mask.  (A wave per block, one lane per
+// coefficient, spent ~400 wave instructions per block on ballots, shuffles
+// and divergent branches.)
+struct BlockRegs {
+  uint32_t w[32];
+};
+
+__device__ __forceinline__ BlockRegs load_block(const int16_t* __restrict__ p) {
+  BlockRegs r;
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 x = q[i];
+    r.w[4 * i] = x.x; r.w[4 * i + 1] = x.y; r.w[4 * i + 2] = x.z; r.w[4 * i + 3] = x.w;
+  }
+  return r;
+}
+
+template <int IDX>
+__device__ __forceinline__ int coef_at(const BlockRegs& r) {
+  return (int)(int16_t)((IDX & 1) ? (r.w[IDX >> 1] >> 16) : (r.w[IDX >> 1] & 0xFFFFu));
+}
+
+// Bit sink: COUNT only counts; otherwise bits are packed MSB-first into 32-bit
+// words starting `n` bits into word *dst.
+//  * global target: the first and the last (partial) word may be shared with
+//    neighbouring blocks -> atomic OR (k_ent_zero cleared them); the words in
+//    between are this block's alone -> plain stores (byte-swapped: stream order).
+//  * LDS target (wave window): every word is OR-ed (ds_or_b32), native order.
+enum SinkMode { SINK_COUNT = 0, SINK_GLOBAL = 1, SINK_LDS = 2 };
+
+template <int MODE>
+struct BitSink {
+  uint64_t acc = 0;
+  int n = 0;
+  int total = 0;
+  uint32_t* dst = nullptr;
+  bool first = true;
+  __device__ __forceinline__ void put(uint32_t v, int len) {
+    total += len;
+    if constexpr (MODE != SINK_COUNT) {
+      acc = (acc << len) | v;
+      n += len;
+      if (n >= 32) {
+        n -= 32;
+        const uint32_t word = (uint32_t)(acc >> n);
+        if constexpr (MODE == SINK_LDS) {
+          atomicOr(dst, word);
+        } else {
+          const uint32_t sw = __builtin_bswap32(word);  // byte 0 of the stream first
+          if (first) atomicOr(dst, sw); else *dst = sw;
+        }
+        first = false;
+        ++dst;
+      }
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if constexpr (MODE == SINK_LDS) {
+      if (n > 0) atomicOr(dst, (uint32_t)(acc << (32 - n)));
+    } else if constexpr (MODE == SINK_GLOBAL) {
+      if (n > 0) atomicOr(dst, __builtin_bswap32((uint32_t)(acc << (32 - n))));
+    }
+  }
+};
+
+constexpr uint8_t ZZC[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+template <int K, int MODE>
+__device__ __forceinline__ void code_ac(const BlockRegs& r, int& last, const uint32_t* act, BitSink<MODE>& o,
+                                        bool& bad) {
+  if constexpr (K < 64) {
+    const int v = coef_at<ZZC[K]>(r);
+    if (v != 0) {
+      const int run = K - last - 1;
+      const uint32_t z = act[0xF0];
+      for (int i = 0; i < (run >> 4); ++i) o.put(z & 0xFFFFu, (int)(z >> 16));  // ZRL: 16 zeros
+      const int a = v < 0 ? -v : v;
+      int s = 32 - __clz(a);
+      bad |= s > 10;
+      s = s > 10 ? 10 : s;
+      const uint32_t e = act[((run & 15) << 4) | s];
+      o.put(e & 0xFFFFu, (int)(e >> 16));
+      o.put((uint32_t)((v < 0 ? v - 1 : v) & ((1 << s) - 1)), s);
+      last = K;
+    }
+    code_ac<K + 1, MODE>(r, last, act, o, bad);
+  }
+}
+
+// T.81 F.1.2 for one block; `pred` = the DC of the previous block of the scan (0 at its start)
+template <int MODE>
+__device__ __forceinline__ void code_block(const BlockRegs& r, int pred, const uint32_t* dct, const uint32_t* act,
+                                           BitSink<MODE>& o, bool& bad) {
+  const int diff = coef_at<0>(r) - pred;
+  const int a = diff < 0 ? -diff : diff;
+  int s = a ? 32 - __clz(a) : 0;
+  bad = s > 11;
+  s = s > 11 ? 11 : s;
+  const uint32_t e = dct[s];
+  o.put(e & 0xFFFFu, (int)(e >> 16));
+  o.put((uint32_t)((diff < 0 ? diff - 1 : diff) & ((1 << s) - 1)), s);
+  int last = 0;
+  code_ac<1, MODE>(r, last, act, o, bad);
+  if (last < 63) {  // EOB
+    const uint32_t eob = act[0x00];
+    o.put(eob & 0xFFFFu, (int)(eob >> 16));
+  }
+  o.finish();
 }
 
 __global__ void __launch_bounds__(256) k_ent_bits(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
                                                   const EntTab* __restrict__ gt, unsigned long long* __restrict__ bits,
                                                   unsigned long long* __restrict__ bad) {
   __shared__ EntTab t;
-  load_tab(gt, &t);
-  const int lane = threadIdx.x & 63;
-  const long long gb = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gb >= nblk) return;
-  uint64_t val;
-  bool b;
-  int n = block_lane(e, coeffs, gb, &t, lane, &val, &b);
-  if (__ballot(b) && lane == 0) bad[gb / e.nb] = 1ull;  // not baseline-codable: the frame is reported
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
-  if (lane == 0) bits[gb] = (unsigned long long)n;
+  load_tab(gt, &t);  // once per workgroup: the grid strides over the blocks
+  for (long long gb = (long long)blockIdx.x * blockDim.x + threadIdx.x; gb < nblk; gb += (long long)gridDim.x * blockDim.x) {
+    const int frame = (int)(gb / e.nb), b = (int)(gb - (long long)frame * e.nb);
+    const int s = scan_of(e, b);
+    const BlockRegs r = load_block(coeffs + gb * 64);
+    const int pred = b == e.first[s] ? 0 : (int)coeffs[(gb - 1) * 64];
+    BitSink<SINK_COUNT> o;
+    bool bd;
+    code_block<SINK_COUNT>(r, pred, t.dc[s ? 1 : 0], t.ac[s ? 1 : 0], o, bd);
+    bits[gb] = (unsigned long long)o.total;
+    if (bd) bad[frame] = 1ull;  // not baseline-codable: the frame is reported
+  }
 }
 
 // info[(f*3+s)*2 + 0] = scan start (global bit prefix), [1] = scan bits
@@ -265,10 +329,18 @@ __global__ void __launch_bounds__(256) k_ent_zero(const EntGeo e, long long nblk
   w[(rel + bits[gb] - 1) >> 5] = 0u;
 }
 
-constexpr int ENT_WIN = 64;  // LDS words per block window (max 1660 + 31 bits)
+
+// One lane per block, 64 consecutive blocks per wave.  Their bits are
+// contiguous within a scan, so the wave assembles them in an LDS window
+// (ds_or: neighbouring lanes share boundary words) and writes the window with
+// coalesced stores; only the window's first and last words, shared with the
+// neighbouring waves, need global atomics.  Waves that straddle a scan
+// boundary or overflow the window write each block straight to global memory.
+constexpr int ENT_WIN = 2048;  // words per wave (64 blocks at <= 1024 bits each)
 
 __global__ void __launch_bounds__(256) k_ent_pack(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
                                                   const EntTab* __restrict__ gt,
+                                                  const unsigned long long* __restrict__ bits,
                                                   const unsigned long long* __restrict__ excl,
                                                   const unsigned long long* __restrict__ info,
                                                   uint32_t* __restrict__ raw) {
@@ -276,40 +348,55 @@ __global__ void __launch_bounds__(256) k_ent_pack(const EntGeo e, long long nblk
   __shared__ uint32_t s_win[4][ENT_WIN];
   load_tab(gt, &t);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long long gb = (long long)blockIdx.x * 4 + wv;
-  if (gb >= nblk) return;
   uint32_t* win = s_win[wv];
-  win[lane] = 0u;
-  uint64_t val;
-  bool bad;
-  const int n = block_lane(e, coeffs, gb, &t, lane, &val, &bad);
-  int tot = n;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-  const int loff = wave_excl_sum(n, lane);
-  const int f = (int)(gb / e.nb), s = scan_of(e, (int)(gb - (long long)f * e.nb));
-  const unsigned long long rel = excl[gb] - info[2 * (f * 3 + s)];
-  const int lp = (int)(rel & 31) + loff;  // bit position in the window (0 = MSB of word 0)
-  __builtin_amdgcn_wave_barrier();        // window cleared before any lane ORs into it (one wave: in order)
-  asm volatile("" ::: "memory");
-  if (n) {
-    const int j0 = lp >> 5, j1 = (lp + n - 1) >> 5;
-    for (int j = j0; j <= j1; ++j) {
-      const int sh = lp + n - 32 * (j + 1);
-      const uint32_t piece = sh >= 0 ? (uint32_t)(val >> sh) : (uint32_t)(val << -sh);
-      atomicOr(&win[j], piece);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long g0 = ((long long)blockIdx.x * 4 + wv) * 64; g0 < nblk; g0 += stride) {
+    const long long gb = g0 + lane;
+    const bool valid = gb < nblk;
+    const long long gl = (nblk - g0 < 64 ? nblk : g0 + 64) - 1;  // last block of the wave
+    const int frame = (int)((valid ? gb : gl) / e.nb), b = (int)((valid ? gb : gl) - (long long)frame * e.nb);
+    const int s = scan_of(e, b);
+    const unsigned long long base = info[2 * (frame * 3 + s)];
+    const unsigned long long rel = (valid ? excl[gb] : excl[gl]) - base;
+    // wave-uniform: one scan, and the window holds the wave's words?
+    const int f0 = (int)(g0 / e.nb), fl = (int)(gl / e.nb);
+    const int s0 = scan_of(e, (int)(g0 - (long long)f0 * e.nb)), sl = scan_of(e, (int)(gl - (long long)fl * e.nb));
+    const unsigned long long rel0 = __shfl(rel, 0, 64);
+    const unsigned long long end = excl[gl] + bits[gl] - base;  // same scan as lane 0 when f0 == fl && s0 == sl
+    const long long w0 = (long long)(rel0 >> 5), nw = (long long)((end + 31) >> 5) - w0;
+    const bool fast = f0 == fl && s0 == sl && nw <= ENT_WIN;
+    BlockRegs r;
+    int pred = 0;
+    if (valid) {
+      r = load_block(coeffs + gb * 64);
+      pred = b == e.first[s] ? 0 : (int)coeffs[(gb - 1) * 64];
     }
-  }
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-  const int nw = ((int)(rel & 31) + tot + 31) >> 5;
-  if (lane < nw) {
-    uint32_t* dst = raw + raw_base(e, f, s) + (rel >> 5) + lane;
-    const uint32_t w = __builtin_bswap32(win[lane]);  // bitstream order: MSB first, byte 0 first
-    if (lane == 0 || lane == nw - 1)
-      atomicOr(dst, w);  // may share this word with the neighbouring blocks
-    else
-      *dst = w;
+    bool bd;
+    if (fast) {
+      for (int i = lane; i < nw; i += 64) win[i] = 0u;
+      __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations execute in order
+      asm volatile("" ::: "memory");
+      if (valid) {
+        BitSink<SINK_LDS> o;
+        o.dst = win + ((long long)(rel >> 5) - w0);
+        o.n = (int)(rel & 31);
+        code_block<SINK_LDS>(r, pred, t.dc[s ? 1 : 0], t.ac[s ? 1 : 0], o, bd);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      uint32_t* dst = raw + raw_base(e, f0, s0) + w0;
+      for (int i = lane; i < nw; i += 64) {
+        const uint32_t w = __builtin_bswap32(win[i]);
+        if (i == 0 || i == nw - 1) atomicOr(dst + i, w); else dst[i] = w;
+      }
+      __builtin_amdgcn_wave_barrier();  // the window is reused by the next iteration
+      asm volatile("" ::: "memory");
+    } else if (valid) {
+      BitSink<SINK_GLOBAL> o;
+      o.dst = raw + raw_base(e, frame, s) + (rel >> 5);
+      o.n = (int)(rel & 31);
+      code_block<SINK_GLOBAL>(r, pred, t.dc[s ? 1 : 0], t.ac[s ? 1 : 0], o, bd);
+    }
   }
 }
 
@@ -492,7 +579,8 @@ hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* cons
   ent_sizes(g, n, sz);
   const EntTab* tab = (const EntTab*)tab_dev;
   hipError_t err;
-  const unsigned gw = (unsigned)((nblk + 3) / 4);
+  const long long gw_need = (nblk + 255) / 256;
+  const unsigned gw = (unsigned)(gw_need < 2048 ? gw_need : 2048);  // 8 per CU, grid-stride beyond
   unsigned long long* bad = info + 6 * n;
   if ((err = hipMemsetAsync(bits + nblk, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
   if ((err = hipMemsetAsync(bad, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) return err;
@@ -502,7 +590,7 @@ hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* cons
   if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, bits, excl, (int)(nblk + 1), s)) != hipSuccess) return err;
   hipLaunchKernelGGL(k_ent_info, dim3((3 * n + 63) / 64), dim3(64), 0, s, e, n, excl, info, scan_bits);
   hipLaunchKernelGGL(k_ent_zero, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, e, nblk, bits, excl, info, raw);
-  hipLaunchKernelGGL(k_ent_pack, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, excl, info, raw);
+  hipLaunchKernelGGL(k_ent_pack, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, excl, info, raw);
   const dim3 cg(e.chunks < 64 ? e.chunks : 64, 3, n);
   if ((err = hipMemsetAsync(ffc, 0, sizeof(unsigned long long) * (nch + 1), s)) != hipSuccess) return err;
   hipLaunchKernelGGL(k_ent_ff, cg, dim3(256), 0, s, e, info, raw, ffc);
