@@ -115,6 +115,15 @@ void* jds_ctx_stream(jds_ctx* ctx);  /* the context's own hipStream_t */
  * stream: a hipStream_t (NULL = the HIP null stream).  Asynchronous. */
 int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n_frames, int64_t H, int64_t W,
                     jds_plan** out);
+/* Quality-sweep plan (BASELINE configs[3]; gui/worker.py:39-74 runs one
+ * compress_reconstruct per quality): n_frames frames x n_q tables, params has
+ * n_frames * n_q entries, item = frame * n_q + q.  jds_plan_run then takes rgb
+ * with n_frames frames and writes rgb_out / coeffs / stats for the n_frames *
+ * n_q items.  The quality-independent front end (colour, prefilter, subsample,
+ * DCT) runs once per frame and is quantised for every table.
+ * 8x8 blocks, n_q <= 8.  jds_plan_create(.., n, ..) = jds_plan_create_q(.., n, 1, ..). */
+int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int n_q, int64_t H, int64_t W,
+                      jds_plan** out);
 int jds_plan_run(jds_plan* plan, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs,
                  jds_frame_stats* stats, uint32_t flags, void* stream);
 int jds_plan_geometry(const jds_plan* plan, jds_geometry* out);

@@ -20,17 +20,19 @@ namespace jds {
 hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                         int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
                         double* part, bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel,
-                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases);
+                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div);
 hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, double c1, double c2,
                             double* scratch_planes, double* scratch_smap, double* scratch_chunks, double* out,
                             hipStream_t s);
 hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
 hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* chunk_sum, int max_chunks,
                           double* out, hipStream_t s);
-hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
+hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
-                           jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* fixcount, hipStream_t s,
-                           const Side* side);
+                           jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* fixcount, float* dct32,
+                           hipStream_t s, const Side* side);
+int quant_mq_tiles(const Geo& g);
+constexpr int MAXQ_SHARED = 8;  // jds_fast.hip MAXQ
 void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
 size_t fast_q_size();
 hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse, hipStream_t s);
@@ -126,6 +128,8 @@ static int run_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int H, int W
 struct jds_plan {
   jds_ctx* ctx = nullptr;
   int n = 0, mode = 0;
+  int nq = 1;      // tables per frame (sweep plan): items = frames * nq, item = frame * nq + q
+  DevBuf dct32;    // sweep plans: fp32 coefficients of every frame (shared front end)
   bool pf = false;
   Geo g{};
   DevBuf fq, gk, part;
@@ -312,7 +316,17 @@ void jds_ctx_destroy(jds_ctx* c) {
 }
 
 int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n, int64_t H, int64_t W, jds_plan** out) {
-  if (!ctx || !params || !out || n < 1) return fail(JDS_EINVAL, "bad argument");
+  return jds_plan_create_q(ctx, params, n, 1, H, W, out);
+}
+
+int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int n_q, int64_t H, int64_t W,
+                      jds_plan** out) {
+  if (!ctx || !params || !out || n_frames < 1 || n_q < 1 || (long long)n_frames * n_q > (1 << 24))
+    return fail(JDS_EINVAL, "bad argument");
+  if (n_q > 1 && params[0].block_size != 8)
+    return fail(JDS_ENOTSUP, "quality sweep plans (n_q > 1) need 8x8 blocks");
+  if (n_q > MAXQ_SHARED) return fail(JDS_ENOTSUP, "at most %d tables per frame in a sweep plan", MAXQ_SHARED);
+  const int n = n_frames * n_q;
   Geo g;
   int mode;
   bool pf;
@@ -340,6 +354,7 @@ int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n, int64_t H, in
   }
   p->ctx = ctx;
   p->n = n;
+  p->nq = n_q;
   p->qt = (double*)malloc(sizeof(double) * 64 * (size_t)n);
   if (!p->qt) {
     free(hq);
@@ -383,9 +398,11 @@ int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n, int64_t H, in
     }
     const float gk32[3] = {(float)params[0].gauss[0], (float)params[0].gauss[1], (float)params[0].gauss[2]};
     const size_t nblk = (size_t)n * (size_t)(g.cpf / 64);
+    const size_t ptiles = (size_t)(n_q > 1 ? quant_mq_tiles(g) : g.tiles_y * g.tiles_x);
     if ((e = p->fq32.ensure(fqs * n)) != hipSuccess || (e = p->gk32.ensure(sizeof gk32)) != hipSuccess ||
         (e = p->fixlist.ensure(8 * nblk)) != hipSuccess || (e = p->counters.ensure(64)) != hipSuccess ||
-        (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * g.tiles_y * g.tiles_x)) != hipSuccess ||
+        (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * ptiles)) != hipSuccess ||
+        (n_q > 1 && (e = p->dct32.ensure(sizeof(float) * (size_t)n_frames * g.cpf)) != hipSuccess) ||
         (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess) {
       free(h32);
@@ -439,16 +456,16 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
     if (exact)
       HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                            (const double*)p->gk.p, stats, (double*)p->part.p, false, nullptr, nullptr, nullptr, 0,
-                           s, nullptr, 1));
+                           s, nullptr, 1, p->nq));
     else
-      HIP_TRY(launch_fast_fwd(p->mode, p->pf, p->g, p->n, rgb, coeffs, (const FrameQ*)p->fq.p, p->fq32.p,
+      HIP_TRY(launch_fast_fwd(p->mode, p->pf, p->g, p->n, p->nq, rgb, coeffs, (const FrameQ*)p->fq.p, p->fq32.p,
                               (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint32_t*)p->part32.p,
-                              (uint2*)p->fixlist.p, (unsigned*)p->counters.p, s, &p->side));
+                              (uint2*)p->fixlist.p, (unsigned*)p->counters.p, (float*)p->dct32.p, s, &p->side));
   }
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
-                         nullptr, nullptr, 0, s, nullptr, exact ? 6 : 2));
+                         nullptr, nullptr, 0, s, nullptr, exact ? 6 : 2, p->nq));
   return JDS_OK;
 }
 
@@ -465,6 +482,7 @@ void jds_plan_destroy(jds_plan* p) {
   p->counters.release();
   p->part32.release();
   p->planes.release();
+  p->dct32.release();
   for (DevBuf& b : p->ent) b.release();
   p->ent_hdr.release();
   p->ent_tab.release();
@@ -534,7 +552,7 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
   HIP_TRY(launch_codec(mode, pf, g, 1, (const uint8_t*)c->rgb.p, (uint8_t*)c->out.p, (int16_t*)c->coeffs.p,
                        (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
                        (double*)c->part.p, true, maps ? (double*)c->erry.p : nullptr,
-                       maps ? (double*)c->errrgb.p : nullptr, dsel, sel_blk, s, c->ev, 3));
+                       maps ? (double*)c->errrgb.p : nullptr, dsel, sel_blk, s, c->ev, 3, 1));
   HIP_TRY(hipMemcpyAsync(rgb_out, c->out.p, nimg, hipMemcpyDeviceToHost, s));
   if (coeffs) HIP_TRY(hipMemcpyAsync(coeffs, c->coeffs.p, ncf * sizeof(int16_t), hipMemcpyDeviceToHost, s));
   if (maps) {

@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(Cfg<MODE>::TF)
 k_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
       const FrameQ* __restrict__ fq, const double* __restrict__ gk,
       jds_frame_stats* __restrict__ st, jds_selected_block* __restrict__ sel,
-      int sel_frame, int sel_blk) {
+      int sel_frame, int sel_blk, int in_div) {
   using C = Cfg<MODE>;
   constexpr int WR = C::TH + 2, WC = C::TW + 2, WN = WR * WC;  // RGB window with 1-px ring
   constexpr bool CPLANE = (MODE != M444) && PF;
@@ -61,7 +61,7 @@ k_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs
   const int ty = blockIdx.x / g.tiles_x, tx = blockIdx.x - ty * g.tiles_x;
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
   const int y0 = m0y * C::MH, x0 = m0x * C::MW;  // tile origin (may be < 0: phantom MCUs)
-  const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
+  const uint8_t* img = rgb + (size_t)(frame / in_div) * g.H * g.W * 3;  // sweep plans: item -> frame
 
   // 1. stage RGB (+ring, BORDER_REFLECT_101 outside the image) as packed u32
   for (int i = tid; i < WN; i += C::TF) {
@@ -315,7 +315,7 @@ k_inv(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __restrict_
       const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out,
       jds_frame_stats* __restrict__ st, double* __restrict__ sse_y_part,
       double* __restrict__ err_y, double* __restrict__ err_rgb,
-      jds_selected_block* __restrict__ sel, int sel_frame, int sel_blk) {
+      jds_selected_block* __restrict__ sel, int sel_frame, int sel_blk, int in_div) {
   using C = Cfg<MODE>;
   constexpr int NT = C::TI;
   constexpr int NCHB = 2 * C::NRB;  // chroma blocks incl. ring, both planes
@@ -391,7 +391,7 @@ k_inv(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __restrict_
   const bool want_in = rgb_in != nullptr;
   unsigned long long sse = 0ull;
   double ssy = 0.0;
-  const uint8_t* in_f = want_in ? rgb_in + (size_t)frame * g.H * g.W * 3 : nullptr;
+  const uint8_t* in_f = want_in ? rgb_in + (size_t)(frame / in_div) * g.H * g.W * 3 : nullptr;
   uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
   for (int t = tid; t < C::TH * (C::TW / 8); t += NT) {
     const int r = t / (C::TW / 8), sg = t - r * (C::TW / 8);
@@ -611,10 +611,10 @@ hipError_t launch_finalize(const Geo& g, int n, jds_frame_stats* st, const doubl
 template <int MODE, bool PF>
 static hipError_t launch_fwd_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
                                const double* gk, jds_frame_stats* st, jds_selected_block* sel, int sel_blk,
-                               hipStream_t s) {
+                               hipStream_t s, int in_div) {
   dim3 grid(g.tiles_y * g.tiles_x, n);
   hipLaunchKernelGGL((k_fwd<MODE, PF>), grid, dim3(Cfg<MODE>::TF), 0, s, g, rgb, coeffs, fq, gk, st, sel,
-                     sel ? 0 : -1, sel_blk);
+                     sel ? 0 : -1, sel_blk, in_div);
   return hipGetLastError();
 }
 
@@ -622,17 +622,17 @@ template <int MODE>
 static hipError_t launch_inv_t(const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
                                const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part,
                                double* err_y, double* err_rgb, jds_selected_block* sel, int sel_blk,
-                               hipStream_t s) {
+                               hipStream_t s, int in_div) {
   dim3 grid(g.tiles_y * g.tiles_x, n);
   hipLaunchKernelGGL((k_inv<MODE>), grid, dim3(Cfg<MODE>::TI), 0, s, g, coeffs, fq, rgb_in, rgb_out, st, part,
-                     err_y, err_rgb, sel, sel ? 0 : -1, sel_blk);
+                     err_y, err_rgb, sel, sel ? 0 : -1, sel_blk, in_div);
   return hipGetLastError();
 }
 
 int inv_tiles(int mode, int H, int W);
 hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
                        const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y,
-                       double* err_rgb, hipStream_t s);
+                       double* err_rgb, hipStream_t s, int in_div);
 hipError_t launch_sel_recon(const int16_t* coeffs, const FrameQ* fq, jds_selected_block* sel, int sel_blk,
                             hipStream_t s);
 
@@ -641,22 +641,22 @@ hipError_t launch_sel_recon(const int16_t* coeffs, const FrameQ* fq, jds_selecte
 hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                         int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
                         double* part, bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel,
-                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases) {
+                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div) {
   hipError_t e = hipSuccess;
   const uint8_t* rin = (want_sse || err_y) ? rgb : nullptr;
   if (phases & 1) {
     if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
     switch (mode) {
       case M420:
-        e = pf ? launch_fwd_t<M420, true>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s)
-               : launch_fwd_t<M420, false>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s);
+        e = pf ? launch_fwd_t<M420, true>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s, in_div)
+               : launch_fwd_t<M420, false>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s, in_div);
         break;
       case M422:
-        e = pf ? launch_fwd_t<M422, true>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s)
-               : launch_fwd_t<M422, false>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s);
+        e = pf ? launch_fwd_t<M422, true>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s, in_div)
+               : launch_fwd_t<M422, false>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s, in_div);
         break;
       default:
-        e = launch_fwd_t<M444, false>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s);
+        e = launch_fwd_t<M444, false>(g, n, rgb, coeffs, fq, gk, st, sel, sel_blk, s, in_div);
         break;
     }
     if (e == hipSuccess) e = launch_fwd_finish(g, n, st, nullptr, 0, s);
@@ -665,17 +665,17 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
   if (phases & 2) {
     int tiles = g.tiles_y * g.tiles_x;
     if (!(phases & 4)) {  // jds_inv.hip (default); bit 2 selects the original k_inv
-      e = launch_inv2(mode, g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, s);
+      e = launch_inv2(mode, g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, s, in_div);
       tiles = inv_tiles(mode, g.H, g.W);
     } else switch (mode) {
       case M420:
-        e = launch_inv_t<M420>(g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, sel, sel_blk, s);
+        e = launch_inv_t<M420>(g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, sel, sel_blk, s, in_div);
         break;
       case M422:
-        e = launch_inv_t<M422>(g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, sel, sel_blk, s);
+        e = launch_inv_t<M422>(g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, sel, sel_blk, s, in_div);
         break;
       default:
-        e = launch_inv_t<M444>(g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, sel, sel_blk, s);
+        e = launch_inv_t<M444>(g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, sel, sel_blk, s, in_div);
         break;
     }
     if (e != hipSuccess || (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess)) return e;

@@ -190,11 +190,12 @@ __device__ __forceinline__ void stats_flush(LaneStats ls, bool valid, unsigned* 
 // maps for padding blocks), runs the column (axis-0) DCT, exchanges through LDS
 // and runs the row DCT.  Used for the border ring of tiles (or all tiles when
 // the interior kernel does not apply).
-template <int MODE, bool PF>
+template <int MODE, bool PF, bool MQ = false>
 __global__ void __launch_bounds__(Cfg<MODE>::TF)
 k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
         const FastQ* __restrict__ fq, const float* __restrict__ gk32, uint32_t* __restrict__ part,
-        uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int border, const int4 rect) {
+        uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int border, const int4 rect,
+        float* __restrict__ dct32) {
   using C = Cfg<MODE>;
   constexpr int WR = C::TH + 2, WC = C::TW + 2, WN = WR * WC;
   constexpr bool CPLANE = (MODE != M444) && PF;
@@ -238,7 +239,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
   const int y0 = m0y * C::MH, x0 = m0x * C::MW;
   const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
-  if (tid < 64) {
+  if (!MQ && tid < 64) {
     s_rq[tid] = fq[frame].rq[tid];
     s_thr[0][tid] = fq[frame].thr[0][tid];
     s_thr[1][tid] = fq[frame].thr[1][tid];
@@ -369,6 +370,16 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
 #pragma unroll
   for (int k = 0; k < 8; ++k) v[k] = valid ? s_blk[u * 8 + k] : 0.0f;
   fdct8_f32(v);
+  if constexpr (MQ) {  // shared front end: fp32 coefficients for k_quant_mq
+    if (valid) {
+      float4* d = reinterpret_cast<float4*>(dct32 + (long long)frame * g.cpf +
+                                            (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
+                                            (long long)bidx * 64 + u * 8);
+      d[0] = make_float4(v[0], v[1], v[2], v[3]);
+      d[1] = make_float4(v[4], v[5], v[6], v[7]);
+    }
+    return;
+  }
   const float4* rq4 = reinterpret_cast<const float4*>(s_rq + u * 8);
   const float4* th4 = reinterpret_cast<const float4*>(s_thr[plane ? 1 : 0] + u * 8);
   const float4 ra = rq4[0], rb = rq4[1], ta = th4[0], tb = th4[1];
@@ -402,11 +413,12 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
 // block's own (already consumed) LDS region: the 8 lanes of a block belong to
 // one wave, whose LDS operations execute in order, so no barrier is needed.
 // The certified bounds cover both pass orders (fast_fwd_thresholds).
-template <int MODE, bool PF>
+template <int MODE, bool PF, bool MQ = false>
 __global__ void __launch_bounds__(Cfg<MODE>::TF)
 k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
          const FastQ* __restrict__ fq, const float* __restrict__ gk32, uint32_t* __restrict__ part,
-         uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int4 rect) {
+         uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int4 rect,
+         float* __restrict__ dct32) {
   using C = Cfg<MODE>;
   constexpr int TH = C::TH, TW = C::TW, WR = TH + 2, SEG = TW / 8;
   constexpr bool SUB = MODE != M444;
@@ -426,7 +438,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
   const int y0 = m0y * C::MH, x0 = m0x * C::MW;
   const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
-  if (tid < 64) {
+  if (!MQ && tid < 64) {
     const int t = (tid & 7) * 8 + (tid >> 3);  // [v][k] <- [k][v]
     s_rqT[tid] = fq[frame].rq[t];
     s_thT[0][tid] = fq[frame].thr[0][t];
@@ -556,11 +568,19 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   LaneStats ls;
   // column `line` of a row-transformed block at `src` (row stride `rs` floats):
   // axis-0 DCT, quantise, int16 transpose in place, 16-byte row store
+  float* dctb = MQ ? dct32 + (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
+                         (long long)bidx * 64
+                   : nullptr;
   auto column = [&](float* src, int rs, int pl) {
     float v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = src[i * rs + line];
     fdct8_f32(v);
+    if constexpr (MQ) {  // shared front end: coefficient (k, line) for k_quant_mq
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dctb[k * 8 + line] = v[k];
+      return;
+    }
     const float4* rq4 = reinterpret_cast<const float4*>(s_rqT + line * 8);
     const float4* th4 = reinterpret_cast<const float4*>(s_thT[pl ? 1 : 0] + line * 8);
     const float4 ra = rq4[0], rb = rq4[1], ta = th4[0], tb = th4[1];
@@ -633,8 +653,10 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     float* P = plane == 0 ? s_y : (plane == 1 ? s_cb : s_cr);
     column(P + by_t * 8 * TW + bx_t * 8, TW, plane);
   }
-  flag_block(ls, true, line, frame, plane, bidx, fixlist, fixcount);
-  stats_flush(ls, true, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
+  if constexpr (!MQ) {
+    flag_block(ls, true, line, frame, plane, bidx, fixlist, fixcount);
+    stats_flush(ls, true, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
+  }
 }
 
 // ---- exact fp64 recomputation of one block column from global memory ----
@@ -688,7 +710,7 @@ template <int MODE, bool PF>
 __global__ void __launch_bounds__(64)
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
-          const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount) {
+          const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq) {
   constexpr bool CPLANE = (MODE != M444) && PF;
   constexpr int SY = Cfg<MODE>::SY;
   constexpr int WRR = 8 * SY + 2, WCC = 18;  // prefilter source window of one chroma block
@@ -705,7 +727,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     const int bidx = (int)(ent.y & 0xffffffu);
     const int nbx = plane ? g.ncx : g.nbx;
     const int gy = bidx / nbx, gx = bidx - gy * nbx;
-    const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
+    const uint8_t* img = rgb + (size_t)(frame / nq) * g.H * g.W * 3;  // item -> its frame
     const int i = t >> 3, j = t & 7;
     // prefiltered chroma of a block away from every edge: stage the source
     // window once (colour, then the row pass, in LDS), same fp64 operations
@@ -797,16 +819,124 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
   }
 }
 
+
+// ---- shared front end: one quality sweep item per table ------------------------
+//
+// A sweep plan (jds_plan_create_q) holds nq tables per frame.  The front-end
+// kernels (MQ = true) write each frame's fp32 coefficients once; here one thread
+// per block row certifies-and-quantises them for every table of the frame
+// (item = frame * nq + q), stores the int16 rows, lists uncertain blocks for
+// k_fix_fwd and keeps per-item statistics.  The colour / prefilter /
+// subsample / DCT work is then done once per frame instead of once per item
+// ("the Q-independent front end ... is reused across Qs").
+constexpr int MAXQ = 8;
+
+int quant_mq_tiles(const Geo& g) {  // workgroups per frame (<= 31 rows per lane: byte-wide histogram counters)
+  const long long rows = g.cpf / 8;
+  long long t = (rows + 256LL * 31 - 1) / (256LL * 31);
+  return (int)(t < 256 ? 256 : t);
+}
+
+__global__ void __launch_bounds__(256)
+k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* __restrict__ coeffs,
+           const FastQ* __restrict__ fq, uint32_t* __restrict__ part, uint2* __restrict__ fixlist,
+           unsigned* __restrict__ fixcount) {
+  __shared__ __attribute__((aligned(16))) float s_rq[MAXQ][64];
+  __shared__ __attribute__((aligned(16))) float s_th[MAXQ][2][64];
+  __shared__ unsigned s_st[MAXQ][NSTAT];
+  const int tid = threadIdx.x, f = blockIdx.y, ptiles = gridDim.x;
+  for (int i = tid; i < nq * 64; i += 256) {
+    const int q = i >> 6, k = i & 63;
+    const FastQ& t = fq[f * nq + q];
+    s_rq[q][k] = t.rq[k];
+    s_th[q][0][k] = t.thr[0][k];
+    s_th[q][1][k] = t.thr[1][k];
+  }
+  for (int i = tid; i < MAXQ * NSTAT; i += 256) (&s_st[0][0])[i] = 0u;
+  __syncthreads();
+  const long long rows = g.cpf / 8, nyb = (long long)g.nby * g.nbx, ncb = (long long)g.ncy * g.ncx;
+  unsigned nz[MAXQ], mb[MAXQ], be[MAXQ], bo[MAXQ], nrows = 0u;
+#pragma unroll
+  for (int q = 0; q < MAXQ; ++q) nz[q] = mb[q] = be[q] = bo[q] = 0u;
+  const long long step = (long long)ptiles * 256;
+  // uniform trip count per wave (flag_block ballots over the 8 rows of a block)
+  for (long long r0 = (long long)blockIdx.x * 256; r0 < rows; r0 += step) {
+    const long long rw = r0 + tid;
+    const bool valid = rw < rows;
+    const long long b = valid ? rw >> 3 : 0;
+    const int u = (int)(rw & 7);
+    const int plane = b < nyb ? 0 : (b < nyb + ncb ? 1 : 2);
+    const int bidx = (int)(b - (plane == 0 ? 0 : (plane == 1 ? nyb : nyb + ncb)));
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (valid) {
+      const float4* s4 = reinterpret_cast<const float4*>(dct32 + (long long)f * g.cpf + rw * 8);
+      const float4 x = s4[0], y = s4[1];
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+      ++nrows;
+    }
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+      if (q < nq) {
+        const float4* rq4 = reinterpret_cast<const float4*>(&s_rq[q][u * 8]);
+        const float4* th4 = reinterpret_cast<const float4*>(&s_th[q][plane ? 1 : 0][u * 8]);
+        const float4 ra = rq4[0], rb = rq4[1], ta = th4[0], tb = th4[1];
+        const float rq[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+        const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+        int qv[8];
+        LaneStats ls;
+        quant8(v, rq, thr, valid, qv, ls, s_st[q]);
+        const int item = f * nq + q;
+        if (valid) *reinterpret_cast<uint4*>(coeffs + (long long)item * g.cpf + rw * 8) = pack_q(qv);
+        flag_block(ls, valid, u, item, plane, bidx, fixlist, fixcount);
+        if (valid) {
+          nz[q] += ls.nz;
+          mb[q] += ls.mb;
+          be[q] += ls.hn & 0x0f0f0f0fu;         // bins 22, 24, 26, 28 (bytes)
+          bo[q] += (ls.hn >> 4) & 0x0f0f0f0fu;  // bins 23, 25, 27, 29
+        }
+      }
+    }
+  }
+  // per item: wave sums (16-bit fields), workgroup sums in LDS, one partial slot
+  const unsigned wrows = __reduce_add_sync(~0ull, nrows);
+#pragma unroll
+  for (int q = 0; q < MAXQ; ++q) {
+    if (q < nq) {
+      const unsigned w0 = __reduce_add_sync(~0ull, be[q] & 0x00ff00ffu), w1 = __reduce_add_sync(~0ull, (be[q] >> 8) & 0x00ff00ffu);
+      const unsigned w2 = __reduce_add_sync(~0ull, bo[q] & 0x00ff00ffu), w3 = __reduce_add_sync(~0ull, (bo[q] >> 8) & 0x00ff00ffu);
+      const unsigned wmb = __reduce_add_sync(~0ull, mb[q]), wnz = __reduce_add_sync(~0ull, nz[q]);
+      if ((tid & 63) == 0) {
+        atomicAdd(&s_st[q][0], wnz);
+        atomicAdd(&s_st[q][1], wmb + wnz);
+        const unsigned zeros = 8u * wrows - wnz;
+        const unsigned c[8] = {w0 & 0xffffu, w2 & 0xffffu, w1 & 0xffffu, (w3 & 0xffffu) - zeros,
+                               w0 >> 16,     w2 >> 16,     w1 >> 16,     w3 >> 16};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (c[j]) atomicAdd(&s_st[q][2 + 22 + j], c[j]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < nq * NSTAT; i += 256) {
+    const int q = i / NSTAT, j = i - q * NSTAT;
+    part[((size_t)(f * nq + q) * ptiles + blockIdx.x) * NSTAT + j] = s_st[q][j];
+  }
+}
+
 // ------------------------------------------------------------ launchers --
 
 hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uint32_t* part, int ptiles,
                              hipStream_t s);
 
 template <int MODE, bool PF>
-static hipError_t fast_fwd_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
+static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
                              const FastQ* fq32, const double* gk, const float* gk32, jds_frame_stats* st,
-                             uint32_t* part, uint2* fixlist, unsigned* fixcount, hipStream_t s, const Side* side) {
+                             uint32_t* part, uint2* fixlist, unsigned* fixcount, float* dct32, hipStream_t s,
+                             const Side* side) {
   using C = Cfg<MODE>;
+  const bool mq = nq > 1;  // sweep plan: front end once per frame into dct32, then k_quant_mq
+  const int nf = n / nq;   // frames (n = items)
   // Tiles lying wholly inside the image (no padding blocks, no phantom MCUs;
   // only the 1-px ring may reflect) form a rectangle of tile indices and take
   // k_fwd32i; the rest run in k_fwd32 beside it on the side stream.
@@ -825,40 +955,59 @@ static hipError_t fast_fwd_t(const Geo& g, int n, const uint8_t* rgb, int16_t* c
                  (e = hipStreamWaitEvent(sb, side->fork, 0)) != hipSuccess))
       return e;
     if (nout > 0) {
-      hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(nout, n), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32, part,
-                         fixlist, fixcount, 1, rect);
+      if (mq)
+        hipLaunchKernelGGL((k_fwd32<MODE, PF, true>), dim3(nout, nf), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32,
+                           part, fixlist, fixcount, 1, rect, dct32);
+      else
+        hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(nout, n), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32, part,
+                           fixlist, fixcount, 1, rect, nullptr);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (fork && (e = hipEventRecord(side->join, sb)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_fwd32i<MODE, PF>), dim3(nin, n), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32, part,
-                       fixlist, fixcount, rect);
+    if (mq)
+      hipLaunchKernelGGL((k_fwd32i<MODE, PF, true>), dim3(nin, nf), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32,
+                         part, fixlist, fixcount, rect, dct32);
+    else
+      hipLaunchKernelGGL((k_fwd32i<MODE, PF>), dim3(nin, n), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32, part,
+                         fixlist, fixcount, rect, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (fork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
   } else {
-    hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(g.tiles_y * g.tiles_x, n), dim3(C::TF), 0, s, g, rgb, coeffs, fq32,
-                       gk32, part, fixlist, fixcount, 0, rect);
+    if (mq)
+      hipLaunchKernelGGL((k_fwd32<MODE, PF, true>), dim3(g.tiles_y * g.tiles_x, nf), dim3(C::TF), 0, s, g, rgb,
+                         coeffs, fq32, gk32, part, fixlist, fixcount, 0, rect, dct32);
+    else
+      hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(g.tiles_y * g.tiles_x, n), dim3(C::TF), 0, s, g, rgb, coeffs,
+                         fq32, gk32, part, fixlist, fixcount, 0, rect, nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  int ptiles = g.tiles_y * g.tiles_x;
+  if (mq) {
+    ptiles = quant_mq_tiles(g);
+    hipLaunchKernelGGL(k_quant_mq, dim3(ptiles, nf), dim3(256), 0, s, g, nq, dct32, coeffs, fq32, part, fixlist,
+                       fixcount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(4096), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
-                     fixcount);
+                     fixcount, nq);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_fwd_finish(g, n, st, part, g.tiles_y * g.tiles_x, s);
+  return launch_fwd_finish(g, n, st, part, ptiles, s);
 }
 
-hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
+hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
-                           jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* fixcount, hipStream_t s,
-                           const Side* side) {
+                           jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* fixcount, float* dct32,
+                           hipStream_t s, const Side* side) {
   const FastQ* f = (const FastQ*)fq32;
   switch (mode) {
     case M420:
-      return pf ? fast_fwd_t<M420, true>(g, n, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, s, side)
-                : fast_fwd_t<M420, false>(g, n, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, s, side);
+      return pf ? fast_fwd_t<M420, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side)
+                : fast_fwd_t<M420, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side);
     case M422:
-      return pf ? fast_fwd_t<M422, true>(g, n, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, s, side)
-                : fast_fwd_t<M422, false>(g, n, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, s, side);
+      return pf ? fast_fwd_t<M422, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side)
+                : fast_fwd_t<M422, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side);
     default:
-      return fast_fwd_t<M444, false>(g, n, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, s, side);
+      return fast_fwd_t<M444, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side);
   }
 }
 

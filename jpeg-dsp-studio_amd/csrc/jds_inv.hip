@@ -187,7 +187,7 @@ template <int MODE, int XTRA>
 __global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(Inv<MODE>::WPE)))
 k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
        const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
-       double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb) {
+       double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb, const int in_div) {
   using I = Inv<MODE>;
   __shared__ __attribute__((aligned(16))) double s_mid[I::MB * MS];
   __shared__ __attribute__((aligned(16))) double s_cw[2][I::CWR * I::CWC];
@@ -257,7 +257,7 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
   const bool want_in = XTRA > 0;
   unsigned long long sse = 0ull;
   double ssy = 0.0;
-  const uint8_t* in_f = want_in ? rgb_in + (size_t)frame * g.H * g.W * 3 : nullptr;
+  const uint8_t* in_f = want_in ? rgb_in + (size_t)(frame / in_div) * g.H * g.W * 3 : nullptr;  // sweep: item -> frame
   uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
 #pragma unroll 1
   for (int r = 0; r < I::NYB / I::RB; ++r) {
@@ -427,29 +427,29 @@ int inv_tiles(int mode, int H, int W) {
 template <int MODE>
 static hipError_t inv2_t(const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq, const uint8_t* rgb_in,
                          uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y, double* err_rgb,
-                         hipStream_t s) {
+                         hipStream_t s, int in_div) {
   int tx;
   const int tiles = inv_tiles_t<MODE>(g.H, g.W, &tx);
   const dim3 grid(tiles, n), blk(Inv<MODE>::NT);
   if (err_y)
     hipLaunchKernelGGL((k_inv2<MODE, 2>), grid, blk, 0, s, g, tx, coeffs, fq, rgb_in, rgb_out, st, part, err_y,
-                       err_rgb);
+                       err_rgb, in_div);
   else if (rgb_in)
     hipLaunchKernelGGL((k_inv2<MODE, 1>), grid, blk, 0, s, g, tx, coeffs, fq, rgb_in, rgb_out, st, part, nullptr,
-                       nullptr);
+                       nullptr, in_div);
   else
     hipLaunchKernelGGL((k_inv2<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, nullptr,
-                       nullptr);
+                       nullptr, in_div);
   return hipGetLastError();
 }
 
 hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
                        const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y,
-                       double* err_rgb, hipStream_t s) {
+                       double* err_rgb, hipStream_t s, int in_div) {
   switch (mode) {
-    case M420: return inv2_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s);
-    case M422: return inv2_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s);
-    default: return inv2_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s);
+    case M420: return inv2_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div);
+    case M422: return inv2_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div);
+    default: return inv2_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div);
   }
 }
 

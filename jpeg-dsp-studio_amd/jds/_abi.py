@@ -76,6 +76,7 @@ _SIGS = {
     'jds_ctx_destroy': (None, [_P]),
     'jds_ctx_stream': (_P, [_P]),
     'jds_plan_create': (C.c_int, [_P, C.POINTER(Params), C.c_int, C.c_int64, C.c_int64, C.POINTER(_P)]),
+    'jds_plan_create_q': (C.c_int, [_P, C.POINTER(Params), C.c_int, C.c_int, C.c_int64, C.c_int64, C.POINTER(_P)]),
     'jds_plan_run': (C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
     'jds_plan_geometry': (C.c_int, [_P, C.POINTER(Geometry)]),
     'jds_plan_fix_counts': (C.c_int, [_P, _P]),
@@ -221,11 +222,16 @@ def geometry(p: Params, H: int, W: int) -> Geometry:
 class Plan:
     """A jds_plan: fixed geometry + per-frame tables for the device-resident batch path."""
 
-    def __init__(self, ctx: Context, params, H: int, W: int):
+    def __init__(self, ctx: Context, params, H: int, W: int, nq: int = 1):
+        """params: one per item; nq > 1 makes a quality-sweep plan (jds_plan_create_q):
+        len(params) // nq frames, item = frame * nq + q, shared front end."""
+        if nq < 1 or len(params) % nq:
+            raise ValueError(f'{len(params)} tables do not split into frames of {nq}')
         arr = (Params * len(params))(*params)
         h = C.c_void_p()
-        check(lib().jds_plan_create(ctx.handle, arr, len(params), H, W, C.byref(h)))
+        check(lib().jds_plan_create_q(ctx.handle, arr, len(params) // nq, nq, H, W, C.byref(h)))
         self.handle, self.ctx, self.n, self.H, self.W = h, ctx, len(params), H, W
+        self.nq, self.frames = nq, len(params) // nq
         self.geometry = Geometry()
         check(lib().jds_plan_geometry(h, C.byref(self.geometry)))
 

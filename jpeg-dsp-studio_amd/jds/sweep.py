@@ -4,9 +4,10 @@ the frame-sharded multi-GPU sweep of BASELINE cfg4 (64 frames x Q in
 
 * ``quality_sweep`` mirrors BatchSweepWorker.run: one ``compress_reconstruct``
   per quality in ``range(start, end + 1, step)``, returning ``[(q, result)]``.
-* ``sweep_device`` runs (frame, Q) items as ONE device-resident plan on one
-  GPU (frames replicated per quality on the device) and returns per-item
-  statistics: nonzero count, exact magnitude bits, histogram, integer SSE.
+* ``sweep_device`` runs (frame, Q) items as device-resident quality-sweep
+  plans on one GPU (the quality-independent front end once per frame) and
+  returns per-item statistics: nonzero count, exact magnitude bits, histogram,
+  integer SSE.
 * ``distributed_sweep`` shards frames across the ranks of an initialised
   ``torch.distributed`` group (one process per GPU, no data-path collective)
   and gathers the per-item statistics to every rank with one
@@ -49,8 +50,10 @@ def shard(n: int, rank: int, world: int) -> range:
 def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilter: bool = True,
                  device: int = 0) -> List[dict]:
     """All (frame, quality) items of `frames` (uint8 [F, H, W, 3], NumPy or a torch
-    tensor on the device) through one device-resident plan.  Items are ordered
-    frame-major.  Returns one dict per item."""
+    tensor on the device) through quality-sweep plans (jds_plan_create_q: the
+    colour / prefilter / subsample / DCT front end runs once per frame and is
+    quantised for up to 8 tables at a time).  Items are ordered frame-major.
+    Returns one dict per item."""
     import torch
     from jds import _abi, codec
     from engines.quantizer import scale_quant_matrix
@@ -59,34 +62,37 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
 
     dev = torch.device('cuda', device)
     fr = frames if isinstance(frames, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frames))
-    fr = fr.to(dev)
+    fr = fr.to(dev).contiguous()
     F, H, W = int(fr.shape[0]), int(fr.shape[1]), int(fr.shape[2])
     qs = [int(q) for q in qualities]
     gk = codec.gaussian_kernel3()
-    params = [_abi.make_params(q, scale_quant_matrix(JPEG_LUMA_Q50, q), mode, prefilter, gk)
-              for _ in range(F) for q in qs]
-    plan = _abi.Plan(_abi.context(device), params, H, W)
-    try:
-        rgb = fr.repeat_interleave(len(qs), dim=0).contiguous()
-        out = torch.empty_like(rgb)
-        cf = torch.empty((len(params), plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
-        st = torch.zeros((len(params), _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-        torch.cuda.synchronize(dev)
-        plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), _abi.RUN_SSE, 0)
-        torch.cuda.synchronize(dev)
-        stats = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(-1)
-    finally:
-        plan.close()
+    stats = np.zeros((F, len(qs)), dtype=_abi.STATS_DTYPE)
+    for c0 in range(0, len(qs), 8):
+        qc = qs[c0:c0 + 8]
+        params = [_abi.make_params(q, scale_quant_matrix(JPEG_LUMA_Q50, q), mode, prefilter, gk)
+                  for _ in range(F) for q in qc]
+        plan = _abi.Plan(_abi.context(device), params, H, W, nq=len(qc))
+        try:
+            out = torch.empty((F * len(qc), H, W, 3), dtype=torch.uint8, device=dev)
+            cf = torch.empty((len(params), plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+            st = torch.zeros((len(params), _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize(dev)
+            plan.run(fr.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), _abi.RUN_SSE, 0)
+            torch.cuda.synchronize(dev)
+            stats[:, c0:c0 + len(qc)] = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(F, len(qc))
+        finally:
+            plan.close()
     items = []
-    for i, s in enumerate(stats):
-        f, q = divmod(i, len(qs))
-        br = bitrate_from_counts(int(s['nonzero']), float(s['magnitude_bits']), int(s['total_coeffs']), (H, W), 8)
-        mse = float(s['sse_rgb']) / (H * W * 3)
-        items.append({'frame': f, 'quality': qs[q], 'nonzero': int(s['nonzero']),
-                      'magnitude_bits': int(s['magnitude_bits']), 'total_coeffs': int(s['total_coeffs']),
-                      'hist': s['hist'].astype(np.int64), 'sse_rgb': int(s['sse_rgb']),
-                      'psnr_rgb': float('inf') if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse)),
-                      'bpp': br['bpp'], 'compression_ratio': br['compression_ratio']})
+    for f in range(F):
+        for qi, q in enumerate(qs):
+            s = stats[f, qi]
+            br = bitrate_from_counts(int(s['nonzero']), float(s['magnitude_bits']), int(s['total_coeffs']), (H, W), 8)
+            mse = float(s['sse_rgb']) / (H * W * 3)
+            items.append({'frame': f, 'quality': q, 'nonzero': int(s['nonzero']),
+                          'magnitude_bits': int(s['magnitude_bits']), 'total_coeffs': int(s['total_coeffs']),
+                          'hist': s['hist'].astype(np.int64), 'sse_rgb': int(s['sse_rgb']),
+                          'psnr_rgb': float('inf') if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse)),
+                          'bpp': br['bpp'], 'compression_ratio': br['compression_ratio']})
     return items
 
 

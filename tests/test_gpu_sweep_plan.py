@@ -1,0 +1,109 @@
+"""GPU parity of quality-sweep plans (jds_plan_create_q, BASELINE configs[3]):
+the quality-independent front end runs once per frame (k_fwd32i / k_fwd32 in
+MQ mode -> fp32 coefficients), k_quant_mq certifies and quantises them for
+every table, k_fix_fwd recomputes uncertain blocks per item.  Every item must
+equal an independent per-item run (plain plan, exact fp64 kernels) and the
+oracle, bit for bit, statistics included."""
+import numpy as np
+import pytest
+
+from golden_util import golden, sha
+from oracle import cpu_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module', autouse=True)
+def gpu():
+    from jds import build, _abi
+    build.build()
+    assert _abi.device_count() >= 1, 'no HIP device: the MI355X path has no CPU fallback'
+
+
+def run_plan(frames, qs, mode, pf, flags, nq):
+    """frames: [F, H, W, 3]; nq > 1: one sweep plan over F frames x qs; nq == 1: a plain
+    plan over the replicated items.  Returns (rgb_out, coeffs, stats, fix counts) per item."""
+    import torch
+    from jds import _abi, codec
+    F, H, W = frames.shape[:3]
+    params = [_abi.make_params(q, cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q), mode, pf,
+                               codec.gaussian_kernel3()) for _ in range(F) for q in qs]
+    plan = _abi.Plan(_abi.context(0), params, H, W, nq=nq)
+    dev = torch.device('cuda:0')
+    src = frames if nq > 1 else np.repeat(frames, len(qs), axis=0)
+    rgb = torch.from_numpy(np.ascontiguousarray(src)).to(dev)
+    out = torch.empty((len(params), H, W, 3), dtype=torch.uint8, device=dev)
+    cf = torch.empty((len(params), plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+    st = torch.zeros((len(params), _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), flags,
+             torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    fix = plan.fix_counts()
+    plan.close()
+    return out.cpu().numpy(), cf.cpu().numpy(), st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(-1), fix
+
+
+@pytest.mark.parametrize('h,w,mode,pf', [(360, 648, '4:2:0', True), (200, 328, '4:2:2', True),
+                                          (184, 260, '4:4:4', False), (130, 98, '4:2:0', False),
+                                          (98, 196, '4:2:2', False), (1080, 1920, '4:2:0', True)])
+def test_sweep_plan_equals_per_item_runs(h, w, mode, pf):
+    from jds import _abi
+    qs = [5, 10, 20, 50, 80, 95] if h < 1000 else [10, 50, 95]
+    frames = np.stack([cpu_ref.random_image(h, w, 700 + i) for i in range(2)])
+    o_s, c_s, s_s, fix = run_plan(frames, qs, mode, pf, _abi.RUN_SSE, len(qs))
+    o_p, c_p, s_p, _ = run_plan(frames, qs, mode, pf, _abi.RUN_SSE | _abi.RUN_EXACT, 1)
+    assert np.array_equal(c_s, c_p)
+    assert np.array_equal(o_s, o_p)
+    for fld in ('nonzero', 'magnitude_bits', 'hist', 'sse_rgb', 'total_coeffs', 'block_overhead_bits', 'pixels'):
+        assert np.array_equal(s_s[fld], s_p[fld]), fld
+    ref = cpu_ref.compress_reconstruct(frames[1], qs[1], 8, mode, pf, metrics=False)
+    assert np.array_equal(c_s[len(qs) + 1], ref['coeffs'])
+    assert np.array_equal(o_s[len(qs) + 1], ref['reconstructed'])
+
+
+def test_sweep_plan_exact_mode():
+    """RUN_EXACT on a sweep plan: the all-fp64 kernels read frame item // nq."""
+    from jds import _abi
+    qs = [20, 80, 100]
+    frames = np.stack([cpu_ref.random_image(72, 96, 40 + i) for i in range(3)])
+    o_e, c_e, s_e, _ = run_plan(frames, qs, '4:2:0', True, _abi.RUN_SSE | _abi.RUN_EXACT, len(qs))
+    o_f, c_f, s_f, _ = run_plan(frames, qs, '4:2:0', True, _abi.RUN_SSE, len(qs))
+    assert np.array_equal(c_e, c_f) and np.array_equal(o_e, o_f)
+    assert np.array_equal(s_e['sse_rgb'], s_f['sse_rgb'])
+
+
+def test_sweep_plan_resolves_exact_ties():
+    """Flat frames put DC/Q on k + 1/2: every tie goes through the per-item fix-up."""
+    from jds import _abi
+    vals = (127, 129, 131, 133)
+    frames = np.stack([np.full((32, 48, 3), v, np.uint8) for v in vals])
+    o, c, s, fix = run_plan(frames, [50, 50], '4:2:0', True, 0, 2)
+    assert fix[0] > 0
+    for i, v in enumerate(vals):
+        g = golden()[f'flat{v}_q50_420_pf']
+        for q in range(2):
+            assert sha(c[2 * i + q]) == g['sha_coeffs'] and sha(o[2 * i + q]) == g['sha_recon']
+
+
+def test_sweep_device_chunks_more_than_eight_qualities():
+    from jds.sweep import sweep_device
+    frames = np.stack([cpu_ref.random_image(64, 96, s) for s in (5, 6)])
+    qs = list(range(5, 100, 9))  # 11 qualities: plans of 8 + 3
+    items = sweep_device(frames, qs, '4:2:2', False)
+    assert [(it['frame'], it['quality']) for it in items] == [(f, q) for f in range(2) for q in qs]
+    for it in items[::4]:
+        ref = cpu_ref.compress_reconstruct(frames[it['frame']], it['quality'], 8, '4:2:2', False, metrics=False)
+        assert it['nonzero'] == ref['bitrate']['nonzero_count']
+        assert np.array_equal(it['hist'], ref['hist'])
+        f = frames[it['frame']]
+        assert it['sse_rgb'] == int(((f.astype(np.int64) - ref['reconstructed']) ** 2).sum())
+
+
+def test_sweep_plan_rejects_bad_shapes():
+    from jds import _abi, codec
+    q = cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, 50)
+    p = _abi.make_params(50, q, '4:2:0', True, codec.gaussian_kernel3())
+    with pytest.raises(ValueError):
+        _abi.Plan(_abi.context(0), [p] * 18, 64, 64, nq=9)  # more than 8 tables per frame
+    with pytest.raises(ValueError):
+        _abi.Plan(_abi.context(0), [p] * 5, 64, 64, nq=2)   # not a whole number of frames
