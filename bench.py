@@ -49,6 +49,11 @@ def parse():
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
+    ap.add_argument('--sweep', action='store_true',
+                    help='BASELINE configs[3]: --frames frames per GPU x Q in {5,10,20,50,80,95} per step '
+                         '(quality-sweep plan: shared front end), SSE on; value = Mpixels/s over all items')
+    ap.add_argument('--sweep-replicate', action='store_true',
+                    help='with --sweep: a plain plan over frames replicated per Q (no shared front end)')
     ap.add_argument('--no-entropy', action='store_true',
                     help='skip the JPEG entropy-coding measurement (8x8 only, outside the timed region)')
     ap.add_argument('--chunks', type=int, default=1,
@@ -74,8 +79,93 @@ def cpu_baseline(frames_host, quality, mode, pf, budget_s, block=8):
                       f'compress_reconstruct without SSIM, {dt:.1f} s, 1 thread'}
 
 
+SWEEP_QS = [5, 10, 20, 50, 80, 95]  # BASELINE configs[3]
+
+
+def sweep_main(args):
+    """configs[3]: every frame at every sweep quality, frames sharded across ranks."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    from jds import _abi, codec
+    from engines.quantizer import scale_quant_matrix
+    from utils.constants import JPEG_LUMA_Q50
+    F, H, W, nq = args.frames, args.height, args.width, len(SWEEP_QS)
+    params = [_abi.make_params(q, scale_quant_matrix(JPEG_LUMA_Q50, q), args.mode, bool(args.prefilter),
+                               codec.gaussian_kernel3()) for _ in range(F) for q in SWEEP_QS]
+    rep = args.sweep_replicate
+    plan = _abi.Plan(_abi.context(local), params, H, W, nq=1 if rep else nq)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2000 + rank)
+    rgb = torch.randint(0, 256, (F, H, W, 3), dtype=torch.uint8, device=dev, generator=gen)
+    if rep:
+        rgb = rgb.repeat_interleave(nq, dim=0).contiguous()
+    out = torch.empty((F * nq, H, W, 3), dtype=torch.uint8, device=dev)
+    cf = torch.empty((F * nq, plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+    st = torch.zeros((F * nq, _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), _abi.RUN_SSE, s.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    items = F * nq * world
+    value = items * H * W * args.steps / elapsed / 1e6
+    result = {'metric': 'Mpixels/s quality sweep (configs[3]); items = frames x Q', 'value': round(value, 2),
+              'unit': 'Mpixels/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+              'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True, 'scaling': 'weak',
+              'vs_baseline': None, 'dtype': 'f32+f64', 'data': 'synthetic (uniform random RGB generated on device)',
+              'config': {'workload': f'{F} x {W}x{H} frames per GPU x Q{SWEEP_QS}, {args.mode}, '
+                                     f'prefilter={"on" if args.prefilter else "off"} (BASELINE configs[3])',
+                         'items_per_step': items, 'items_per_s': round(items * args.steps / elapsed, 1),
+                         'front_end': 'replicated per item' if rep else 'shared per frame (jds_plan_create_q)',
+                         'parallelism': f'frame-shard x{world}'}}
+    if rank == 0 and not args.no_parity:
+        from oracle import cpu_ref
+        stats = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(-1)
+        f0 = rgb[0].cpu().numpy()
+        bad = 0
+        for qi, q in enumerate(SWEEP_QS):
+            ref = cpu_ref.compress_reconstruct(f0, q, 8, args.mode, bool(args.prefilter), metrics=False)
+            bad += int(np.sum(cf[qi].cpu().numpy() != ref['coeffs']))
+            bad += int(stats[qi]['sse_rgb'] != int(((f0.astype(np.int64) - ref['reconstructed']) ** 2).sum()))
+        result['parity'] = {'frame': 0, 'qualities': SWEEP_QS, 'mismatches': bad}
+    plan.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.sweep:
+        return sweep_main(args)
     import numpy as np
     import torch
     import torch.distributed as dist

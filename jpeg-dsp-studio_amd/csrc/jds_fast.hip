@@ -143,12 +143,21 @@ __device__ __forceinline__ uint4 pack_q(const int (&q)[8]) {
 }
 
 // Flagged blocks (any uncertain coefficient among the block's 8 lanes) go to
-// the fix list; lane 8b of a wave speaks for block b.
+// the fix list; lane 8b of a wave speaks for block b.  One atomic per wave
+// reserves the wave's slots (at high quality a few % of all blocks are listed:
+// one atomic per block serialises on the counter).
 __device__ __forceinline__ void flag_block(const LaneStats& ls, bool valid, int line, int frame, int plane, int bidx,
                                            uint2* fixlist, unsigned* fixcount) {
   const unsigned long long fm = __ballot(valid && ls.nflag != 0u);
-  if (valid && line == 0 && ((fm >> ((threadIdx.x & 63) & ~7)) & 0xffull)) {
-    const unsigned slot = atomicAdd(fixcount, 1u);
+  if (!fm) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const bool mine = valid && line == 0 && ((fm >> (lane & ~7)) & 0xffull);
+  const unsigned long long lm = __ballot(mine);
+  unsigned base = 0u;
+  if (lane == __ffsll((long long)lm) - 1) base = atomicAdd(fixcount, (unsigned)__popcll(lm));
+  base = __shfl(base, __ffsll((long long)lm) - 1, 64);
+  if (mine) {
+    const unsigned slot = base + (unsigned)__popcll(lm & ((1ull << lane) - 1ull));
     fixlist[slot] = make_uint2((unsigned)frame, ((unsigned)plane << 24) | (unsigned)bidx);
   }
 }

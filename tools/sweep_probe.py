@@ -1,0 +1,34 @@
+"""Timing probe for quality-sweep plans (not product code): ms per plan run for
+different quality sets, shared front end vs replicated items."""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, 'jpeg-dsp-studio_amd'), ROOT]
+import torch
+from jds import _abi, codec
+from engines.quantizer import scale_quant_matrix
+from utils.constants import JPEG_LUMA_Q50
+
+F, H, W = 32, 1080, 1920
+dev = torch.device('cuda:0')
+rgb = torch.randint(0, 256, (F, H, W, 3), dtype=torch.uint8, device=dev)
+for qs in ([5] * 6, [50] * 6, [95] * 6, [5, 10, 20, 50, 80, 95], [50]):
+    for nq in sorted({1, len(qs)}):
+        params = [_abi.make_params(q, scale_quant_matrix(JPEG_LUMA_Q50, q), '4:2:0', True, codec.gaussian_kernel3())
+                  for _ in range(F) for q in qs]
+        plan = _abi.Plan(_abi.context(0), params, H, W, nq=nq)
+        src = rgb if nq > 1 else rgb.repeat_interleave(len(qs), dim=0).contiguous()
+        out = torch.empty((len(params), H, W, 3), dtype=torch.uint8, device=dev)
+        cf = torch.empty((len(params), plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+        st = torch.zeros((len(params), _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        for flags, name in ((_abi.RUN_FWD, 'fwd'), (_abi.RUN_SSE, 'fwd+inv')):
+            for _ in range(2):
+                plan.run(src.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), flags, 0)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                plan.run(src.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), flags, 0)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / 5 * 1e3
+            print(f'qs={qs} nq={nq} {name:8s} {ms:8.3f} ms  {ms / len(params) * 1e3:7.1f} us/item', flush=True)
+        plan.close()
+        del src, out, cf, st
