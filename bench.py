@@ -7,7 +7,9 @@ k_fwd32 / k_fix_fwd, RGB -> int16 coefficients + statistics; inverse phase:
 k_inv2, coefficients -> RGB).  One step = one pass over a batch of
 `--frames` device-resident 1080p frames per GPU (default 64, the size of the
 reference's cfg4 batch sweep); inputs are generated on the device before the
-timed region.  Multi-GPU: one process per GPU (torchrun), frames shard across
+timed region.  A step is one jds_plan_run (forward then inverse) on one stream;
+`--pipeline 1` instead overlaps the forward of batch k+1 with the inverse of
+batch k on a second stream (two buffer sets).  Multi-GPU: one process per GPU (torchrun), frames shard across
 ranks with no data-path collective (weak scaling); RCCL is used only for the
 barrier and the max-over-ranks time.
 
@@ -15,7 +17,8 @@ Prints ONE JSON line (rank 0).  The roofline object describes the dominant
 kernel (longer average launch) with ALGORITHMIC bytes: k_fwd reads 3 B/px RGB and
 writes 2*S B/px int16 coefficients, k_inv the reverse (S = coefficients per
 pixel, 1.5037 at 1080p 4:2:0).  Launch durations come from torch.cuda.Events on
-the stream the kernels run on.  `traffic` (HBM bytes/launch from rocprofv3 PMC)
+the stream the kernels run on, in a serial (non-overlapped) calibration pass
+after the timed region.  `traffic` (HBM bytes/launch from rocprofv3 PMC)
 is read from profiles/pmc_traffic.json when it matches this configuration.
 """
 import argparse
@@ -56,9 +59,34 @@ def parse():
                     help='with --sweep: a plain plan over frames replicated per Q (no shared front end)')
     ap.add_argument('--no-entropy', action='store_true',
                     help='skip the JPEG entropy-coding measurement (8x8 only, outside the timed region)')
-    ap.add_argument('--chunks', type=int, default=1,
-                    help='split the batch into this many plans; the forward of chunk c+1 overlaps the inverse of c')
+    ap.add_argument('--pipeline', type=int, default=0, choices=(0, 1),
+                    help='1: image-stream pipelining, two buffer sets; the forward of batch k+1 runs beside the '
+                         'inverse of batch k on a second stream (measured no faster: the launches share CUs at '
+                         'workgroup granularity).  0 (default): one jds_plan_run (forward then inverse) per step')
     return ap.parse_args()
+
+
+PREWARM_S = 0.3
+
+
+def prewarm(run_step, warmup, dev):
+    """The W untimed warmup steps, continued until PREWARM_S seconds of sustained
+    load have passed.  The MI355X raises its clocks over the first ~40 ms of
+    load: in a rocprofv3 trace of 3 warmup + 20 steps, k_inv2 took 549 us at
+    the start of the timed region and 404 us after 40 launches (k_fwd32i 420 ->
+    321 us), so a 3-step warmup times the ramp, not the steady state of an
+    image stream.  Returns the number of warmup steps run."""
+    import torch
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    k = 0
+    while k < warmup or (time.perf_counter() - t0 < PREWARM_S and k < 2000):
+        run_step(k)
+        k += 1
+        if k % 4 == 0:
+            torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)
+    return k
 
 
 def cpu_baseline(frames_host, quality, mode, pf, budget_s, block=8):
@@ -117,8 +145,7 @@ def sweep_main(args):
     def step():
         plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), _abi.RUN_SSE, s.cuda_stream)
 
-    for _ in range(args.warmup):
-        step()
+    nwarm = prewarm(lambda k: step(), args.warmup, dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -137,7 +164,7 @@ def sweep_main(args):
     value = items * H * W * args.steps / elapsed / 1e6
     result = {'metric': 'Mpixels/s quality sweep (configs[3]); items = frames x Q', 'value': round(value, 2),
               'unit': 'Mpixels/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-              'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True, 'scaling': 'weak',
+              'warmup_steps_run': nwarm, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True, 'scaling': 'weak',
               'vs_baseline': None, 'dtype': 'f32+f64', 'data': 'synthetic (uniform random RGB generated on device)',
               'config': {'workload': f'{F} x {W}x{H} frames per GPU x Q{SWEEP_QS}, {args.mode}, '
                                      f'prefilter={"on" if args.prefilter else "off"} (BASELINE configs[3])',
@@ -184,72 +211,85 @@ def main():
     from utils.constants import JPEG_LUMA_Q50
 
     B, H, W = args.frames, args.height, args.width
-    K = max(1, min(args.chunks, B))
     qt = scale_quant_matrix(JPEG_LUMA_Q50, args.quality)
     prm = _abi.make_params(args.quality, qt, args.mode, bool(args.prefilter), codec.gaussian_kernel3(), args.block)
-    # the batch in K chunks (one plan each) so the forward of chunk c+1 runs
-    # beside the inverse of chunk c on a second stream
-    bounds = [(B * c // K, B * (c + 1) // K) for c in range(K)]
-    plans = [_abi.Plan(_abi.context(local), [prm] * (b1 - b0), H, W) for b0, b1 in bounds]
+    # image stream: NS buffer sets (plan + frames + outputs); with pipelining the
+    # forward of batch k+1 (set (k+1) % 2) runs beside the inverse of batch k on
+    # a second stream, and batch k+2 reuses set k % 2 once batch k's inverse is done
+    NS = 2 if args.pipeline else 1
+    plans = [_abi.Plan(_abi.context(local), [prm] * B, H, W) for _ in range(NS)]
     geo = plans[0].geometry
     cpf = geo.coeffs_per_frame
 
-    # device-resident synthetic frames (uniform random RGB), distinct per rank
+    # device-resident synthetic frames (uniform random RGB), distinct per rank and set
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
-    rgb = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=gen)
-    out = torch.empty_like(rgb)
-    coeffs = torch.empty((B, cpf), dtype=torch.int16, device=dev)
-    stats = torch.zeros((B, _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    rgbs = [torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=gen) for _ in range(NS)]
+    outs = [torch.empty_like(r) for r in rgbs]
+    coefs = [torch.empty((B, cpf), dtype=torch.int16, device=dev) for _ in range(NS)]
+    stats_l = [torch.zeros((B, _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev) for _ in range(NS)]
+    rgb, out, coeffs, stats = rgbs[0], outs[0], coefs[0], stats_l[0]
     s_f = torch.cuda.Stream(dev)  # forward launches (and their events)
-    s_i = torch.cuda.Stream(dev) if K > 1 else s_f  # inverse launches
+    s_i = torch.cuda.Stream(dev) if NS > 1 else s_f  # inverse launches
     torch.cuda.synchronize(dev)  # inputs were produced on the default stream
     torch.cuda.set_stream(s_f)
-    done_inv = [torch.cuda.Event() for _ in range(K)]  # chunk c's inverse finished (its buffers are free)
-    fwd_done = [torch.cuda.Event() for _ in range(K)]
-    first = [True]
+    done_inv = [torch.cuda.Event() for _ in range(NS)]  # set b's last inverse finished (its buffers are free)
+    fwd_done = [torch.cuda.Event() for _ in range(NS)]
+    used = [False] * NS
 
-    def ptrs(c):
-        b0 = bounds[c][0]
-        return (rgb[b0].data_ptr(), out[b0].data_ptr(), coeffs[b0].data_ptr(), stats[b0].data_ptr())
+    def ptrs(b):
+        return (rgbs[b].data_ptr(), outs[b].data_ptr(), coefs[b].data_ptr(), stats_l[b].data_ptr())
 
-    def step(ev=None):
-        for c in range(K):
-            if not first[0]:
-                s_f.wait_event(done_inv[c])
-            if ev is not None:
-                ev[c][0].record(s_f)
-            plans[c].run(*ptrs(c), _abi.RUN_FWD, s_f.cuda_stream)
-            if ev is not None:
-                ev[c][1].record(s_f)
-            fwd_done[c].record(s_f)
-            s_i.wait_event(fwd_done[c])
-            if ev is not None:
-                ev[c][2].record(s_i)
-            plans[c].run(*ptrs(c), _abi.RUN_INV, s_i.cuda_stream)
-            if ev is not None:
-                ev[c][3].record(s_i)
-            done_inv[c].record(s_i)
-        first[0] = False
+    def step(k, ev=None, si=None):
+        si = si or s_i
+        b = k % NS
+        if used[b]:
+            s_f.wait_event(done_inv[b])
+        used[b] = True
+        if ev is not None:
+            ev[0].record(s_f)
+        plans[b].run(*ptrs(b), _abi.RUN_FWD, s_f.cuda_stream)
+        if ev is not None:
+            ev[1].record(s_f)
+        fwd_done[b].record(s_f)
+        si.wait_event(fwd_done[b])
+        if ev is not None:
+            ev[2].record(si)
+        plans[b].run(*ptrs(b), _abi.RUN_INV, si.cuda_stream)
+        if ev is not None:
+            ev[3].record(si)
+        done_inv[b].record(si)
 
-    for _ in range(args.warmup):
-        step()
-    evs = [[[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)] for _ in range(args.steps)]
+    def run_step(k):
+        if NS > 1:
+            step(k)
+        else:  # both phases in one call on one stream: no events inside the timed region
+            plans[0].run(*ptrs(0), 0, s_f.cuda_stream)
+
+    nwarm = prewarm(run_step, args.warmup, dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        run_step(nwarm + k)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    # average launch durations per chunk (forward phase: k_fwd32i + k_fwd32 + k_fix_fwd + reductions)
-    t_fwd = sum(e[c][0].elapsed_time(e[c][1]) for e in evs for c in range(K)) / (args.steps * K)
-    t_inv = sum(e[c][2].elapsed_time(e[c][3]) for e in evs for c in range(K)) / (args.steps * K)
-    plan = plans[-1]
+    # Per-kernel launch durations from a serial calibration pass (outside the
+    # timed region): with pipelining the forward and inverse launches overlap,
+    # so their in-stream durations would not describe either kernel alone.
+    # Forward phase = k_fwd32i + k_fwd32 (border tiles) + k_fix_fwd + reductions.
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    torch.cuda.synchronize(dev)
+    for k in range(args.steps):
+        step(k * NS, evs[k], si=s_f)
+    torch.cuda.synchronize(dev)
+    t_fwd = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    t_inv = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
+    plan = plans[0]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -258,9 +298,8 @@ def main():
     px_per_step = B * H * W
     value = world * px_per_step * args.steps / elapsed / 1e6
     S = cpf / (H * W)
-    px_chunk = px_per_step / K  # one launch processes one chunk
-    bytes_fwd = int(px_chunk * 3 + px_chunk * S * 2)
-    bytes_inv = int(px_chunk * S * 2 + px_chunk * 3)
+    bytes_fwd = int(px_per_step * 3 + px_per_step * S * 2)  # one launch processes one batch
+    bytes_inv = int(px_per_step * S * 2 + px_per_step * 3)
     dom = 'k_fwd' if t_fwd >= t_inv else 'k_inv'
     t_dom = max(t_fwd, t_inv)
     achieved = (bytes_fwd if dom == 'k_fwd' else bytes_inv) / (t_dom * 1e-3) / 1e9
@@ -278,7 +317,7 @@ def main():
             rec = json.load(open(tf))
             base = (f'{W}x{H}_q{args.quality}_{args.mode}_pf{int(bool(args.prefilter))}'
                     + ('_B16' if args.block == 16 else '') + '_b')
-            nl = bounds[0][1] - bounds[0][0]  # frames per launch
+            nl = B  # frames per launch
             if base + str(nl) in rec:
                 traffic = rec[base + str(nl)].get(dom)
             else:  # bytes scale with frames per launch; recorded for other launch sizes
@@ -296,6 +335,7 @@ def main():
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
+        'warmup_steps_run': nwarm,
         'ms_per_step': round(elapsed / args.steps * 1e3, 4),
         'higher_is_better': True,
         'scaling': 'weak',
@@ -305,18 +345,21 @@ def main():
         'config': {'workload': f'{W}x{H} RGB, Q={args.quality}, {args.mode}, prefilter={"on" if args.prefilter else "off"}, '
                                f'{args.block}x{args.block} blocks '
                                + ('(BASELINE configs[1])' if args.block == 8 else '(BASELINE configs[4] stretch)'),
-                   'frames_per_gpu_per_step': B, 'global_batch_frames': B * world, 'chunks': K,
+                   'frames_per_gpu_per_step': B, 'global_batch_frames': B * world,
+                   'pipeline': ('image stream: forward of batch k+1 beside the inverse of batch k (two streams, '
+                                'two buffer sets)' if NS > 1 else 'serial forward then inverse per step'),
                    'parallelism': f'frame-shard x{world}'},
         'roofline': {'bound': 'hbm', 'kernel': kname, 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'algorithmic_bytes_per_launch': bytes_fwd if dom == 'k_fwd' else bytes_inv,
-                     'avg_launch_ms': round(t_dom, 4)},
+                     'avg_launch_ms': round(t_dom, 4),
+                     'timing': 'HIP events on the launch stream, serial calibration pass after the timed region'},
         'kernels_ms': {'k_fwd': round(t_fwd, 4), 'k_inv': round(t_inv, 4)},
-        'fixups_last_step': {'fwd_blocks': int(sum(int(p_.fix_counts()[0]) for p_ in plans))},
+        'fixups_last_step': {'fwd_blocks': int(plans[0].fix_counts()[0])},
         'pipeline_roofline_frac': round(value / world * 1e6 * (6 + 2 * S) / (HBM_PEAK_GBS * 1e9), 4),
     }
 
-    if not args.no_entropy and args.block == 8 and K == 1:
+    if not args.no_entropy and args.block == 8:
         # JPEG entropy coding of the step's coefficients (jds_entropy.hip), timed on
         # its own after the headline region: files per frame, real bits per pixel
         from jds import entropy

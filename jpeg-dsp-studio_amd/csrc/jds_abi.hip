@@ -411,9 +411,13 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
     }
     free(h32);
   }
-  if ((e = hipStreamCreateWithFlags(&p->side.stream, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&p->side.fork, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&p->side.join, hipEventDisableTiming)) != hipSuccess) {
+  // Border tiles run on the plan's own stream after the interior tiles unless
+  // JDS_SIDE_STREAM=1 asks for the fork/join onto a side stream (A/B: tools/ab_probe.py).
+  const char* side_env = getenv("JDS_SIDE_STREAM");
+  if (side_env && side_env[0] == '1' &&
+      ((e = hipStreamCreateWithFlags(&p->side.stream, hipStreamNonBlocking)) != hipSuccess ||
+       (e = hipEventCreateWithFlags(&p->side.fork, hipEventDisableTiming)) != hipSuccess ||
+       (e = hipEventCreateWithFlags(&p->side.join, hipEventDisableTiming)) != hipSuccess)) {
     jds_plan_destroy(p);
     return fail(JDS_EHIP, "plan stream: %s", hipGetErrorString(e));
   }

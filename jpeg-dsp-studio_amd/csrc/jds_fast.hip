@@ -123,6 +123,9 @@ __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8]
     ls.hn += 1u << (o & 28u);  // bins 22..29; a rare q lands in some nibble and is taken back below
     nrare += o >= 32u ? 1u : 0u;
   }
+#ifdef JDS_PROBE_NORARE  // tools/probe: drop the rare-bin atomics
+  nrare = 0u;
+#endif
   if (nrare != 0u) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
