@@ -82,10 +82,13 @@ __device__ __forceinline__ void idct_col(const int16_t* __restrict__ blk, const 
 struct Col16 {
   int16_t q[8];
 };
-__device__ __forceinline__ Col16 load_col(const int16_t* __restrict__ blk, int v, bool ok) {
+// Blocks outside the grid (`ok` false) read block 0 of the plane instead: the
+// caller never transforms them, and unmasked loads need no per-load branches.
+__device__ __forceinline__ Col16 load_col(const int16_t* __restrict__ plane, long long boff, int v, bool ok) {
+  const int16_t* blk = plane + (ok ? boff : 0ll);
   Col16 c;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) c.q[r] = ok ? blk[r * 8 + v] : (int16_t)0;
+  for (int r = 0; r < 8; ++r) c.q[r] = blk[r * 8 + v];
   return c;
 }
 __device__ __forceinline__ void idct_col(const Col16& in, const double* __restrict__ q, int v,
@@ -123,26 +126,27 @@ __device__ __forceinline__ void idct_row(const double* __restrict__ src, int u, 
 // rejects odd ones), so the scale is exactly 1/2: pixel 2m reads
 // (s[m-1], s[m]) with weights (1/4, 3/4) and pixel 2m+1 reads (s[m], s[m+1])
 // with (3/4, 1/4), so each product serves two pixels.
-// cv2's vertical blend r0*b0 + r1*b1 for an exact 2x upsample, where
-// {b0, b1} = {1/4, 3/4}: the quarter product is exact, so one fma reproduces
-// the two roundings of the reference.
-__device__ __forceinline__ double vblend(double r0, double r1, double b0) {
-  return b0 == 0.25 ? fma(r0, 0.25, r1 * 0.75) : fma(r1, 0.25, r0 * 0.75);
-}
+// cv2's vertical blend r0*b0 + r1*b1 for an exact 2x upsample has weights
+// {1/4, 3/4} in one order or the other: with wq the window row weighted 1/4 and
+// wt the row weighted 3/4 it is fl(fl(h[wq]/4) + fl(h[wt]*3/4)), and the
+// quarter product is exact, so one fma reproduces the reference's two
+// roundings.  Picking the rows per thread (not the weights per pixel) keeps
+// the blend free of selects.
+__device__ __forceinline__ double vblend(double hq, double ht) { return fma(hq, 0.25, ht * 0.75); }
 
 template <int MODE>
-__device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo& g, int x0, int cwx0, int wr0,
-                                        int wr1, double b0, double b1, double (&C)[8]) {
+__device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo& g, int x0, int cwx0, int wq,
+                                        int wt, double (&C)[8]) {
   using I = Inv<MODE>;
   if constexpr (I::SX == 1) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) C[k] = cw[wr0 * I::CWC + x0 + k - cwx0];
+    for (int k = 0; k < 8; ++k) C[k] = cw[wq * I::CWC + x0 + k - cwx0];
   } else {
     const int c0 = x0 / 2 - 1 - cwx0;
     double h0[8];
 #pragma unroll
     for (int rr = 0; rr < (I::SY == 2 ? 2 : 1); ++rr) {
-      const double* s = &cw[(rr ? wr1 : wr0) * I::CWC + c0];
+      const double* s = &cw[(rr ? wt : wq) * I::CWC + c0];
       // s*0.25 is exact, so fl(s0*0.25 + fl(s1*0.75)) == fma(s0, 0.25, fl(s1*0.75))
       double q75[6];
 #pragma unroll
@@ -154,8 +158,8 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
           h0[2 * i] = e;
           h0[2 * i + 1] = o;
         } else {
-          C[2 * i] = vblend(h0[2 * i], e, b0);
-          C[2 * i + 1] = vblend(h0[2 * i + 1], o, b0);
+          C[2 * i] = vblend(h0[2 * i], e);
+          C[2 * i + 1] = vblend(h0[2 * i + 1], o);
         }
       }
     }
@@ -171,9 +175,9 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
       const int kl = side == 0 ? (x0 == 0 ? 0 : -1) : (g.W - 1 - x0 < 8 ? g.W - 1 - x0 : -1);
       if (kl >= 0) {
         const int e = (side == 0 ? 0 : g.wc - 1) - cwx0;
-        const double v0 = cw[wr0 * I::CWC + e];
+        const double v0 = cw[wq * I::CWC + e];
         double v = v0;
-        if constexpr (I::SY == 2) v = vblend(v0, cw[wr1 * I::CWC + e], b0);
+        if constexpr (I::SY == 2) v = vblend(v0, cw[wt * I::CWC + e]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) C[k] = k == kl ? v : C[k];  // selects, not branches
       }
@@ -183,8 +187,10 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
 
 // XTRA: 0 = RGB only, 1 = + exact integer SSE and luma SSE partials,
 //       2 = + IntermediateData error maps (pipeline.py:117-122)
+// (XTRA = 2 is the single-frame host path: it trades occupancy for registers
+// rather than spill to scratch)
 template <int MODE, int XTRA>
-__global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(Inv<MODE>::WPE)))
+__global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(XTRA > 1 ? 2 : Inv<MODE>::WPE)))
 k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
        const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
        double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb, const int in_div) {
@@ -223,7 +229,7 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
   {
     int by, bx;
     const bool ok = luma_blk(0, by, bx);
-    lq = load_col(cf + ((long long)by * g.nbx + bx) * 64, lv, ok);
+    lq = load_col(cf, ((long long)by * g.nbx + bx) * 64, lv, ok);
   }
 #ifndef JDS_PROBE_NOCHROMA  // tools/probe: skip the chroma window
   if (tid < I::NCB * 8) {
@@ -232,11 +238,11 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
     const bool bvalid = by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx;
     const bool need = !I::RY || (i == 0 ? lv == 7 : (i == I::CBR - 1 ? lv == 0 : true));
     const long long boff = ((long long)by * g.ncx + bx) * 64;
-    Col16 cq = load_col(cf + g.off_cb + boff, lv, bvalid);
+    Col16 cq = load_col(cf + g.off_cb, boff, lv, bvalid);
 #pragma unroll 1
     for (int p = 0; p < 2; ++p) {
       const Col16 cur = cq;
-      if (p == 0) cq = load_col(cf + g.off_cr + boff, lv, bvalid);  // next plane in flight
+      if (p == 0) cq = load_col(cf + g.off_cr, boff, lv, bvalid);  // next plane in flight
       if (bvalid) {
         idct_col(cur, s_q, lv, s_mid + lb * MS);
         if (need) {
@@ -267,7 +273,7 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
     if (r + 1 < I::NYB / I::RB) {  // next round's coefficients in flight
       int by1, bx1;
       const bool ok1 = luma_blk(r + 1, by1, bx1);
-      lq = load_col(cf + ((long long)by1 * g.nbx + bx1) * 64, lv, ok1);
+      lq = load_col(cf, ((long long)by1 * g.nbx + bx1) * 64, lv, ok1);
     }
     if (bvalid) idct_col(cur, s_q, lv, s_mid + lb * MS);
     // (the block's row pass reads what its own wave wrote: no barrier)
@@ -275,32 +281,51 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
     if (bvalid && y < g.H && x0 < g.W) {
       double Yv[8];
       idct_row(s_mid + lb * MS, lv, Yv);
-      // chroma rows (cv2 INTER_LINEAR: rows clamped, weights kept)
-      int wr0, wr1 = 0;
-      double b0 = 1.0, b1 = 0.0;
+      // chroma rows (cv2 INTER_LINEAR: rows clamped, weights kept): wq carries
+      // weight 1/4, wt weight 3/4 (4:2:0); without vertical subsampling wq = y
+      int wq, wt = 0;
       if constexpr (I::SY == 2) {
         float fy = (float)((y + 0.5) * g.up_sy - 0.5);
         const int sy = (int)floorf(fy);
-        fy -= (float)sy;
-        b0 = (double)(1.f - fy);
-        b1 = (double)fy;
-        wr0 = clampi(clampi(sy, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
-        wr1 = clampi(clampi(sy + 1, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+        fy -= (float)sy;  // 0.75 (b0 = 1/4: row sy is the quarter row) or 0.25
+        const int r0 = clampi(clampi(sy, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+        const int r1 = clampi(clampi(sy + 1, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+        const bool q0 = fy == 0.75f;
+        wq = q0 ? r0 : r1;
+        wt = q0 ? r1 : r0;
       } else {
-        wr0 = y - cwy0;
+        wq = y - cwy0;
       }
+      const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
+      uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
+      const bool wide = nx == 8 && ((((uintptr_t)o) & 7u) == 0);
+      // XTRA: the 8 input pixels (24 bytes, packed like the output) for the SSE
+      // and the error maps, loaded before the colour math so that per-pixel
+      // error terms are formed as the channels are (bounded register pressure)
+      uint32_t in[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+      if constexpr (XTRA > 0) {
+        const uint8_t* src = in_f + ((size_t)y * g.W + x0) * 3;
+        if (wide) {
+          const uint2* s2 = reinterpret_cast<const uint2*>(src);
+          const uint2 a = s2[0], b = s2[1], c = s2[2];
+          in[0] = a.x; in[1] = a.y; in[2] = b.x; in[3] = b.y; in[4] = c.x; in[5] = c.y;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 24; ++k)
+            if (k < 3 * nx) in[k >> 2] |= (uint32_t)src[k] << (8 * (k & 3));
+        }
+      }
+      auto byte_of = [](const uint32_t (&w)[6], int b) { return (int)((w[b >> 2] >> (8 * (b & 3))) & 255u); };
       // color_space.py:17-24 in NumPy's order, one chroma plane at a time to
       // bound register pressure: B and G's Cb term first, then R and G.
       uint32_t pk[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-      double Rc[8], Gc[8], Bc[8];
+      double eB[8];  // XTRA > 1: |B0 - clip(B)| (pipeline.py:121's last term)
       {
-        // one chroma plane at a time to bound register pressure: B and G's Cb
-        // term first, then R and G (same expressions, same order)
         double C[8], Gt[8];
         // floor(clip(v, 0, 255)) == clamp(trunc(v), 0, 255) for |v| < 2^31:
         // one conversion and integer min/max instead of two fp64 ops
 #ifndef JDS_PROBE_NOUPS
-        chroma8<MODE>(s_cw[0], g, x0, cwx0, wr0, wr1, b0, b1, C);
+        chroma8<MODE>(s_cw[0], g, x0, cwx0, wq, wt, C);
 #else
         for (int k = 0; k < 8; ++k) C[k] = Yv[k] * 0.5;
 #endif
@@ -308,12 +333,12 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
         for (int k = 0; k < 8; ++k) {
           const double B = Yv[k] + 1.772 * (C[k] - 128.0);
           Gt[k] = Yv[k] - 0.344136 * (C[k] - 128.0);
-          if constexpr (XTRA > 1) Bc[k] = fmin(fmax(B, 0.0), 255.0);
+          if constexpr (XTRA > 1) eB[k] = fabs((double)byte_of(in, 3 * k + 2) - fmin(fmax(B, 0.0), 255.0));
           const int b = 3 * k + 2;
           pk[b >> 2] |= (uint32_t)clampi((int)B, 0, 255) << (8 * (b & 3));
         }
 #ifndef JDS_PROBE_NOUPS
-        chroma8<MODE>(s_cw[1], g, x0, cwx0, wr0, wr1, b0, b1, C);
+        chroma8<MODE>(s_cw[1], g, x0, cwx0, wq, wt, C);
 #else
         for (int k = 0; k < 8; ++k) C[k] = Yv[k] * 0.25;
 #endif
@@ -321,18 +346,21 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
         for (int k = 0; k < 8; ++k) {
           const double R = Yv[k] + 1.402 * (C[k] - 128.0);
           const double G = Gt[k] - 0.714136 * (C[k] - 128.0);
-          if constexpr (XTRA > 1) {
-            Rc[k] = fmin(fmax(R, 0.0), 255.0);
-            Gc[k] = fmin(fmax(G, 0.0), 255.0);
-          }
           const int b = 3 * k;
           pk[b >> 2] |= (uint32_t)clampi((int)R, 0, 255) << (8 * (b & 3));
           pk[(b + 1) >> 2] |= (uint32_t)clampi((int)G, 0, 255) << (8 * ((b + 1) & 3));
+          if constexpr (XTRA > 1) {
+            if (k < nx) {
+              const double R0 = byte_of(in, b), G0 = byte_of(in, b + 1), B0 = byte_of(in, b + 2);
+              const size_t pix = (size_t)y * g.W + x0 + k;
+              err_y[pix] = fabs(luma(R0, G0, B0) - Yv[k]);  // pipeline.py:120
+              err_rgb[pix] = ((fabs(R0 - fmin(fmax(R, 0.0), 255.0)) + fabs(G0 - fmin(fmax(G, 0.0), 255.0))) + eB[k]) /
+                             3.0;  // pipeline.py:121
+            }
+          }
         }
       }
-      const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
-      uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
-      if (nx == 8 && ((((uintptr_t)o) & 7u) == 0)) {
+      if (wide) {
         uint2* o2 = reinterpret_cast<uint2*>(o);
         o2[0] = make_uint2(pk[0], pk[1]);
         o2[1] = make_uint2(pk[2], pk[3]);
@@ -343,26 +371,18 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
           if (b < 3 * nx) o[b] = (uint8_t)(pk[b >> 2] >> (8 * (b & 3)));
       }
       if constexpr (XTRA > 0) {
-        const uint8_t* src = in_f + ((size_t)y * g.W + x0) * 3;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           if (k < nx) {
-            const int o0 = src[3 * k], o1 = src[3 * k + 1], o2 = src[3 * k + 2];
             const int b = 3 * k;
-            const int ur = (pk[b >> 2] >> (8 * (b & 3))) & 255, ug = (pk[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 255,
-                      ub = (pk[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 255;
+            const int o0 = byte_of(in, b), o1 = byte_of(in, b + 1), o2 = byte_of(in, b + 2);
+            const int ur = byte_of(pk, b), ug = byte_of(pk, b + 1), ub = byte_of(pk, b + 2);
             const int d0 = o0 - ur, d1 = o1 - ug, d2 = o2 - ub;
             sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
-            const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
-            const double yo = luma(R0, G0, B0);
+            const double yo = luma((double)o0, (double)o1, (double)o2);
             const double yr = luma((double)ur, (double)ug, (double)ub);
             const double dy = yo - yr;
             ssy = ssy + dy * dy;
-            if constexpr (XTRA > 1) {
-              const size_t pix = (size_t)y * g.W + x0 + k;
-              err_y[pix] = fabs(yo - Yv[k]);                                                    // pipeline.py:120
-              err_rgb[pix] = ((fabs(R0 - Rc[k]) + fabs(G0 - Gc[k])) + fabs(B0 - Bc[k])) / 3.0;  // pipeline.py:121
-            }
           }
         }
       }
