@@ -404,7 +404,8 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
         (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * ptiles)) != hipSuccess ||
         (n_q > 1 && (e = p->dct32.ensure(sizeof(float) * (size_t)n_frames * g.cpf)) != hipSuccess) ||
         (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess) {
+        (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemset(p->counters.p, 0, 64)) != hipSuccess) {  // armed once; k_fwd_reduce re-arms
       free(h32);
       jds_plan_destroy(p);
       return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
@@ -427,7 +428,10 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
 
 int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   if (!p || !counts) return fail(JDS_EINVAL, "null argument");
-  HIP_TRY(hipMemcpy(counts, p->counters.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  uint32_t c[4];  // [0] live append counter, [2] the last run's forward fix-up list length
+  HIP_TRY(hipMemcpy(c, p->counters.p, sizeof c, hipMemcpyDeviceToHost));
+  counts[0] = c[2];
+  counts[1] = c[1];
   return JDS_OK;
 }
 
@@ -455,8 +459,9 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
     return JDS_OK;
   }
   if (phases & 1) {
-    HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
-    HIP_TRY(hipMemsetAsync(p->counters.p, 0, 64, s));
+    // the fast forward resets the statistics in its front-end launch and
+    // re-arms the fix-up counter in k_fwd_reduce (no memsets on its path)
+    if (exact) HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
     if (exact)
       HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                            (const double*)p->gk.p, stats, (double*)p->part.p, false, nullptr, nullptr, nullptr, 0,

@@ -207,7 +207,8 @@ __global__ void __launch_bounds__(Cfg<MODE>::TF)
 k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
         const FastQ* __restrict__ fq, const float* __restrict__ gk32, uint32_t* __restrict__ part,
         uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int border, const int4 rect,
-        float* __restrict__ dct32) {
+        float* __restrict__ dct32,
+        jds_frame_stats* __restrict__ stz, const int nzq) {
   using C = Cfg<MODE>;
   constexpr int WR = C::TH + 2, WC = C::TW + 2, WN = WR * WC;
   constexpr bool CPLANE = (MODE != M444) && PF;
@@ -225,6 +226,12 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   const int tid = threadIdx.x;
   const int frame = blockIdx.y;
   int ty, tx;
+  // this launch owns the frame statistics' reset (replaces a memset): tile 0
+  // of every frame clears its items' records before k_fwd_reduce adds to them
+  if (stz != nullptr && blockIdx.x == 0) {
+    uint64_t* z = reinterpret_cast<uint64_t*>(stz + (size_t)frame * nzq);
+    for (int i = tid; i < nzq * (int)(sizeof(jds_frame_stats) / 8); i += blockDim.x) z[i] = 0ull;
+  }
   if (border) {  // tiles outside the interior rectangle rect = (ty_lo, ty_hi, tx_lo, tx_hi) only
     int e = blockIdx.x;
     const int top = rect.x * g.tiles_x, bottom = (g.tiles_y - 1 - rect.y) * g.tiles_x;
@@ -430,7 +437,8 @@ __global__ void __launch_bounds__(Cfg<MODE>::TF)
 k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
          const FastQ* __restrict__ fq, const float* __restrict__ gk32, uint32_t* __restrict__ part,
          uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const int4 rect,
-         float* __restrict__ dct32) {
+         float* __restrict__ dct32,
+         jds_frame_stats* __restrict__ stz, const int nzq) {
   using C = Cfg<MODE>;
   constexpr int TH = C::TH, TW = C::TW, WR = TH + 2, SEG = TW / 8;
   constexpr bool SUB = MODE != M444;
@@ -446,6 +454,12 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 
   const int tid = threadIdx.x, frame = blockIdx.y;
   const int ncol = rect.w - rect.z + 1;
+  // this launch owns the frame statistics' reset (replaces a memset): tile 0
+  // of every frame clears its items' records before k_fwd_reduce adds to them
+  if (stz != nullptr && blockIdx.x == 0) {
+    uint64_t* z = reinterpret_cast<uint64_t*>(stz + (size_t)frame * nzq);
+    for (int i = tid; i < nzq * (int)(sizeof(jds_frame_stats) / 8); i += blockDim.x) z[i] = 0ull;
+  }
   const int ty = rect.x + (int)blockIdx.x / ncol, tx = rect.z + (int)blockIdx.x % ncol;
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
   const int y0 = m0y * C::MH, x0 = m0x * C::MW;
@@ -940,6 +954,12 @@ k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* 
 
 hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uint32_t* part, int ptiles,
                              hipStream_t s);
+hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, unsigned* counters,
+                             hipStream_t s);
+// k_fix_fwd workgroups (grid-stride over the list): enough that typical lists
+// (0.4 % of 3M blocks at Q50) need one block per workgroup -- up to ~29
+// one-wave workgroups per CU keep their load latencies in flight together
+constexpr int FIX_GRID = 16384;
 
 template <int MODE, bool PF>
 static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
@@ -969,28 +989,28 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     if (nout > 0) {
       if (mq)
         hipLaunchKernelGGL((k_fwd32<MODE, PF, true>), dim3(nout, nf), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32,
-                           part, fixlist, fixcount, 1, rect, dct32);
+                           part, fixlist, fixcount, 1, rect, dct32, nullptr, nq);
       else
         hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(nout, n), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32, part,
-                           fixlist, fixcount, 1, rect, nullptr);
+                           fixlist, fixcount, 1, rect, nullptr, nullptr, 1);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (fork && (e = hipEventRecord(side->join, sb)) != hipSuccess) return e;
     if (mq)
       hipLaunchKernelGGL((k_fwd32i<MODE, PF, true>), dim3(nin, nf), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32,
-                         part, fixlist, fixcount, rect, dct32);
+                         part, fixlist, fixcount, rect, dct32, st, nq);
     else
       hipLaunchKernelGGL((k_fwd32i<MODE, PF>), dim3(nin, n), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32, part,
-                         fixlist, fixcount, rect, nullptr);
+                         fixlist, fixcount, rect, nullptr, st, 1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (fork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
   } else {
     if (mq)
       hipLaunchKernelGGL((k_fwd32<MODE, PF, true>), dim3(g.tiles_y * g.tiles_x, nf), dim3(C::TF), 0, s, g, rgb,
-                         coeffs, fq32, gk32, part, fixlist, fixcount, 0, rect, dct32);
+                         coeffs, fq32, gk32, part, fixlist, fixcount, 0, rect, dct32, st, nq);
     else
       hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(g.tiles_y * g.tiles_x, n), dim3(C::TF), 0, s, g, rgb, coeffs,
-                         fq32, gk32, part, fixlist, fixcount, 0, rect, nullptr);
+                         fq32, gk32, part, fixlist, fixcount, 0, rect, nullptr, st, 1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   int ptiles = g.tiles_y * g.tiles_x;
@@ -1000,10 +1020,13 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
                        fixcount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(4096), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
-                     fixcount, nq);
+  // partials -> frame statistics (reset by the front-end launch above); the
+  // fix-up list length moves to fixcount[2] and fixcount[0] is re-armed
+  if ((e = launch_fwd_reduce(n, st, part, ptiles, fixcount, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(FIX_GRID), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
+                     fixcount + 2, nq);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_fwd_finish(g, n, st, part, ptiles, s);
+  return launch_fwd_finish(g, n, st, nullptr, 0, s);
 }
 
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,

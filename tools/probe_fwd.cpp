@@ -63,9 +63,9 @@ int main(int argc, char** argv) {
   rect.z = (g.tx_off * C::MW > 0) ? 1 : 0; rect.w = (g.W / C::MW + g.tx_off) / C::MX - 1;
   const int nin = (rect.y - rect.x + 1) * (rect.w - rect.z + 1);
   const dim3 gi(nin, n), gb(g.tiles_y * g.tiles_x - nin, n), ga(g.tiles_y * g.tiles_x, n);
-  time_it("fwd32 interior", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, rect, (float*)nullptr); });
-  time_it("fwd32 border", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32<M420, true>), gb, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 1, rect, (float*)nullptr); });
-  time_it("fwd32 general, all tiles", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32<M420, true>), ga, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 0, rect, (float*)nullptr); });
+  time_it("fwd32 interior", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, rect, (float*)nullptr, st, 1); });
+  time_it("fwd32 border", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32<M420, true>), gb, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 1, rect, (float*)nullptr, (jds_frame_stats*)nullptr, 1); });
+  time_it("fwd32 general, all tiles", [&] { hipMemsetAsync(cnt, 0, 64, 0); hipLaunchKernelGGL((k_fwd32<M420, true>), ga, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 0, rect, (float*)nullptr, st, 1); });
   time_it("inv2", [&] { launch_inv2(M420, g, n, cf, fq, nullptr, out, st, nullptr, nullptr, nullptr, 0, 1); });
   {
     hipStream_t s1, s2;
@@ -73,7 +73,7 @@ int main(int argc, char** argv) {
     hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
     auto both = [&](bool conc) {
       hipStream_t sa = s1, sb = conc ? s2 : s1;
-      hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, sa, g, rgb, cf, fq32, gk32, part, fl, cnt, rect, (float*)nullptr);
+      hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, sa, g, rgb, cf, fq32, gk32, part, fl, cnt, rect, (float*)nullptr, st, 1);
       launch_inv2(M420, g, n, cf, fq, nullptr, out, st, nullptr, nullptr, nullptr, sb, 1);
     };
     for (int conc = 0; conc < 2; ++conc) {
@@ -89,8 +89,8 @@ int main(int argc, char** argv) {
   }
   {
     unsigned hc = 0; hipMemset(cnt, 0, 64);
-    hipLaunchKernelGGL((k_fwd32<M420, true>), gb, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 1, rect, (float*)nullptr);
-    hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, rect, (float*)nullptr);
+    hipLaunchKernelGGL((k_fwd32<M420, true>), gb, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, 1, rect, (float*)nullptr, (jds_frame_stats*)nullptr, 1);
+    hipLaunchKernelGGL((k_fwd32i<M420, true>), gi, dim3(C::TF), 0, 0, g, rgb, cf, fq32, gk32, part, fl, cnt, rect, (float*)nullptr, st, 1);
     hipMemcpy(&hc, cnt, 4, hipMemcpyDeviceToHost);
     printf("flagged blocks (64 frames): %u\n", hc);
     std::vector<uint2> hl(hc);

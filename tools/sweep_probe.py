@@ -11,8 +11,15 @@ from utils.constants import JPEG_LUMA_Q50
 F, H, W = 32, 1080, 1920
 dev = torch.device('cuda:0')
 rgb = torch.randint(0, 256, (F, H, W, 3), dtype=torch.uint8, device=dev)
-for qs in ([5] * 6, [50] * 6, [95] * 6, [5, 10, 20, 50, 80, 95], [50]):
-    for nq in sorted({1, len(qs)}):
+# prewarm: clocks ramp over the first ~40 ms of load (bench.py prewarm)
+_x = torch.randn(4096, 4096, device=dev)
+_t0 = time.perf_counter()
+while time.perf_counter() - _t0 < 0.5:
+    _x = (_x @ _x).clamp_(-1, 1)
+torch.cuda.synchronize()
+SETS = os.environ.get('SETS')
+for qs in ([[int(x) for x in t.split(':')] for t in SETS.split(',')] if SETS else ([5] * 6, [50] * 6, [95] * 6, [5, 10, 20, 50, 80, 95], [50])):
+    for nq in sorted({1, len(qs)}) if not os.environ.get('NQ') else [len(qs)]:
         params = [_abi.make_params(q, scale_quant_matrix(JPEG_LUMA_Q50, q), '4:2:0', True, codec.gaussian_kernel3())
                   for _ in range(F) for q in qs]
         plan = _abi.Plan(_abi.context(0), params, H, W, nq=nq)
