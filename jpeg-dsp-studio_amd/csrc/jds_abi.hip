@@ -30,7 +30,7 @@ hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* ch
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
                            jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* fixcount, float* dct32,
-                           hipStream_t s, const Side* side);
+                           hipStream_t s, const Side* side, bool finish);
 int quant_mq_tiles(const Geo& g);
 constexpr int MAXQ_SHARED = 8;  // jds_fast.hip MAXQ
 void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
@@ -469,12 +469,13 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
     else
       HIP_TRY(launch_fast_fwd(p->mode, p->pf, p->g, p->n, p->nq, rgb, coeffs, (const FrameQ*)p->fq.p, p->fq32.p,
                               (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint32_t*)p->part32.p,
-                              (uint2*)p->fixlist.p, (unsigned*)p->counters.p, (float*)p->dct32.p, s, &p->side));
+                              (uint2*)p->fixlist.p, (unsigned*)p->counters.p, (float*)p->dct32.p, s, &p->side,
+                              phases == 1));  // forward + inverse: k_finalize adds the zero bin
   }
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
-                         nullptr, nullptr, 0, s, nullptr, exact ? 6 : 2, p->nq));
+                         nullptr, nullptr, 0, s, nullptr, exact ? 6 : (phases == 3 ? 2 | 8 : 2), p->nq));
   return JDS_OK;
 }
 

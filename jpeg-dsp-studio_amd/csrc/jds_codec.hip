@@ -599,14 +599,17 @@ hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uin
 }
 
 // Per-frame constants and the deterministic luma-SSE sum (inverse phase).
+// zero_bin: the forward phase of the same run deferred k_fwd_finish's zero
+// bin to here (one launch fewer per forward+inverse run; constants are set here).
 __global__ void k_finalize(const Geo g, jds_frame_stats* st, const double* __restrict__ sse_y_part,
-                           int tiles, int with_sse) {
+                           int tiles, int with_sse, int zero_bin) {
   const int f = blockIdx.x;
   if (threadIdx.x != 0) return;
   jds_frame_stats* s = st + f;
   s->total_coeffs = (uint64_t)g.cpf;
   s->block_overhead_bits = 2ull * (uint64_t)g.nby * (uint64_t)g.nbx;
   s->pixels = (uint64_t)g.H * (uint64_t)g.W;
+  if (zero_bin) s->hist[25] += (uint64_t)g.cpf - s->nonzero;  // zeros fall in bin 25 ([0, 4))
   if (with_sse) {
     double a = 0.0;
     for (int t = 0; t < tiles; ++t) a = a + sse_y_part[(size_t)f * tiles + t];
@@ -616,7 +619,7 @@ __global__ void k_finalize(const Geo g, jds_frame_stats* st, const double* __res
 
 hipError_t launch_finalize(const Geo& g, int n, jds_frame_stats* st, const double* part, int tiles, bool with_sse,
                            hipStream_t s) {
-  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, tiles, (int)with_sse);
+  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, tiles, (int)with_sse, 0);
   return hipGetLastError();
 }
 
@@ -651,7 +654,8 @@ hipError_t launch_sel_recon(const int16_t* coeffs, const FrameQ* fq, jds_selecte
                             hipStream_t s);
 
 // phases: bit 0 = forward (k_fwd), bit 1 = inverse (k_inv2 + finalize),
-//         bit 2 = use the original one-block-ring k_inv for the inverse
+//         bit 2 = use the original one-block-ring k_inv for the inverse,
+//         bit 3 = finalize also adds the zero bin (the fast forward deferred it)
 hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                         int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
                         double* part, bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel,
@@ -699,7 +703,7 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
       if (!(phases & 4) && (e = launch_sel_recon(coeffs, fq, sel, sel_blk, s)) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, tiles,
-                       (int)(rin != nullptr));
+                       (int)(rin != nullptr), (phases & 8) ? 1 : 0);
     e = hipGetLastError();
   }
   return e;

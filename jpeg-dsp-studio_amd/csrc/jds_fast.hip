@@ -965,7 +965,7 @@ template <int MODE, bool PF>
 static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
                              const FastQ* fq32, const double* gk, const float* gk32, jds_frame_stats* st,
                              uint32_t* part, uint2* fixlist, unsigned* fixcount, float* dct32, hipStream_t s,
-                             const Side* side) {
+                             const Side* side, bool finish) {
   using C = Cfg<MODE>;
   const bool mq = nq > 1;  // sweep plan: front end once per frame into dct32, then k_quant_mq
   const int nf = n / nq;   // frames (n = items)
@@ -1026,23 +1026,23 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(FIX_GRID), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                      fixcount + 2, nq);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_fwd_finish(g, n, st, nullptr, 0, s);
+  return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
 }
 
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
                            jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* fixcount, float* dct32,
-                           hipStream_t s, const Side* side) {
+                           hipStream_t s, const Side* side, bool finish) {
   const FastQ* f = (const FastQ*)fq32;
   switch (mode) {
     case M420:
-      return pf ? fast_fwd_t<M420, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side)
-                : fast_fwd_t<M420, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side);
+      return pf ? fast_fwd_t<M420, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish)
+                : fast_fwd_t<M420, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish);
     case M422:
-      return pf ? fast_fwd_t<M422, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side)
-                : fast_fwd_t<M422, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side);
+      return pf ? fast_fwd_t<M422, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish)
+                : fast_fwd_t<M422, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish);
     default:
-      return fast_fwd_t<M444, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side);
+      return fast_fwd_t<M444, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish);
   }
 }
 
