@@ -4,6 +4,7 @@
 // management and launches.  All per-pixel / per-coefficient arithmetic runs
 // in the HIP kernels of jds_codec.hip; there is no CPU fallback.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -230,10 +231,15 @@ static void make_fq(const jds_params* p, FrameQ* q) {
   }
 }
 
+// scale_quant_matrix (engines/quantizer.py:7-19) yields integers in [1, 255]
+// (floor, then clip); the kernels rely on it (integer dequantisation).
 static int check_tables(const jds_params* p) {
-  for (int i = 0; i < 64; ++i)
+  for (int i = 0; i < 64; ++i) {
     if (!(p->qtable[i] >= 1.0 && p->qtable[i] <= 255.0))
       return fail(JDS_EINVAL, "qtable[%d] = %g outside [1, 255]", i, p->qtable[i]);
+    if (p->qtable[i] != floor(p->qtable[i]))
+      return fail(JDS_EINVAL, "qtable[%d] = %g is not an integer", i, p->qtable[i]);
+  }
   return JDS_OK;
 }
 

@@ -63,15 +63,17 @@ constexpr int MS = 72;  // doubles per block in the transpose buffer (64 + 8: co
 __device__ __forceinline__ int tslot(int r, int c) { return r * 8 + ((((c >> 1) ^ (r & 3)) << 1) | (c & 1)); }
 
 // Dequantize (quantizer.py:27-29) and IDCT column v of a block (axis 0 first,
-// dct_engine.py:12-14) into dst[r*8 + v].  `q` holds Q/16: q*Q is an exact
-// integer and scaling by 2^-4 commutes exactly with every rounding of the
-// transform (no subnormals arise), so IDCT(q*Q/16) == IDCT(q*Q)/16 bit for bit
-// and pocketfft's fct = 1/16 costs nothing later.
-__device__ __forceinline__ void idct_col(const int16_t* __restrict__ blk, const double* __restrict__ q, int v,
+// dct_engine.py:12-14) into dst[r*8 + v].  `qi` holds the integer table Q:
+// q*Q is formed exactly in 24-bit integer arithmetic and converted once.  The
+// transform then runs on 16x the reference's operands (pocketfft's first-axis
+// fct = 1/16 not applied): scaling by 2^4 commutes exactly with every rounding
+// (no subnormals or overflow arise), so the row pass's outputs are exactly
+// 16x the reference's and idct_row folds the 1/16 into its +128 (one fma).
+__device__ __forceinline__ void idct_col(const int16_t* __restrict__ blk, const int* __restrict__ qi, int v,
                                          double* __restrict__ dst) {
   double c[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) c[r] = (double)blk[r * 8 + v] * q[r * 8 + v];
+  for (int r = 0; r < 8; ++r) c[r] = (double)__mul24((int)blk[r * 8 + v], qi[r * 8 + v]);
   dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
 #pragma unroll
   for (int r = 0; r < 8; ++r) dst[tslot(r, v)] = c[r];
@@ -91,17 +93,18 @@ __device__ __forceinline__ Col16 load_col(const int16_t* __restrict__ plane, lon
   for (int r = 0; r < 8; ++r) c.q[r] = blk[r * 8 + v];
   return c;
 }
-__device__ __forceinline__ void idct_col(const Col16& in, const double* __restrict__ q, int v,
+__device__ __forceinline__ void idct_col(const Col16& in, const int* __restrict__ qi, int v,
                                          double* __restrict__ dst) {
   double c[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) c[r] = (double)in.q[r] * q[r * 8 + v];
+  for (int r = 0; r < 8; ++r) c[r] = (double)__mul24((int)in.q[r], qi[r * 8 + v]);
   dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
 #pragma unroll
   for (int r = 0; r < 8; ++r) dst[tslot(r, v)] = c[r];
 }
 
-// Row u of a column-transformed block: axis-1 IDCT, fct 1/16, +128, clip
+// Row u of a column-transformed block: axis-1 IDCT, fct 1/16 and +128 in one
+// fma (x/16 is exact, so fl(x/16 + 128) == fl(fl(x/16) + 128)), clip
 // (dct_engine.py:23-27).
 __device__ __forceinline__ void idct_row(const double* __restrict__ src, int u, double (&c)[8]) {
   const int sw = u & 3;
@@ -114,7 +117,7 @@ __device__ __forceinline__ void idct_row(const double* __restrict__ src, int u, 
   dct3_line(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const double s = c[k] + 128.0;  // the fct 1/16 rides on the prescaled quantiser (exact)
+    const double s = fma(c[k], 0.0625, 128.0);
     c[k] = fmin(fmax(s, 0.0), 255.0);
   }
 }
@@ -197,7 +200,7 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
   using I = Inv<MODE>;
   __shared__ __attribute__((aligned(16))) double s_mid[I::MB * MS];
   __shared__ __attribute__((aligned(16))) double s_cw[2][I::CWR * I::CWC];
-  __shared__ double s_q[64];
+  __shared__ int s_q[64];  // integer quantiser table Q
   __shared__ double s_red[I::NT / 64];
   __shared__ unsigned long long s_sse;
 
@@ -206,7 +209,7 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int Y0 = ty * I::TH, X0 = tx * I::TW;
   const int16_t* cf = coeffs + (size_t)frame * g.cpf;
-  if (tid < 64) s_q[tid] = fq[frame].q[tid] * 0.0625;  // Q/16, exact
+  if (tid < 64) s_q[tid] = (int)fq[frame].q[tid];  // Q is an integer in [1, 255]
   if (XTRA && tid == 0) s_sse = 0ull;
   __syncthreads();
 
@@ -415,9 +418,9 @@ __global__ void __launch_bounds__(64) k_sel_recon(const int16_t* __restrict__ co
   __shared__ __attribute__((aligned(16))) double s[MS];
   const int t = threadIdx.x;
   if (t < 8) {
-    double qs[64];
+    int qs[64];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) qs[r * 8 + t] = fq[0].q[r * 8 + t] * 0.0625;
+    for (int r = 0; r < 8; ++r) qs[r * 8 + t] = (int)fq[0].q[r * 8 + t];
     idct_col(coeffs + (long long)sel_blk * 64, qs, t, s);
   }
   __syncthreads();

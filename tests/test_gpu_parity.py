@@ -239,3 +239,14 @@ def test_quality_sweep_matches_per_call_reference():
         ref = cpu_ref.compress_reconstruct(img, q, 8, '4:2:2', True, metrics=True)
         assert np.array_equal(r.reconstructed_image, ref['reconstructed'])
         assert (r.psnr_rgb, r.ssim_y) == (ref['metrics']['psnr_rgb'], ref['metrics']['ssim_y'])
+
+
+@pytest.mark.gpu
+def test_plan_rejects_non_integer_quant_table():
+    """scale_quant_matrix always yields integers (engines/quantizer.py:16-18); the
+    C-ABI rejects anything else with EINVAL (the kernels dequantise in integers)."""
+    from jds import _abi, codec
+    q = np.full((8, 8), 16.0)
+    q[3, 4] = 16.5
+    with pytest.raises(ValueError, match='not an integer'):
+        _abi.Plan(_abi.context(0), [_abi.make_params(50, q, '4:2:0', True, codec.gaussian_kernel3())], 16, 16)
