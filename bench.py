@@ -124,11 +124,12 @@ def sweep_main(args):
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
     from jds import _abi, codec
-    from engines.quantizer import scale_quant_matrix
-    from utils.constants import JPEG_LUMA_Q50
+    from jds.sweep import broadcast_tables
     F, H, W, nq = args.frames, args.height, args.width, len(SWEEP_QS)
-    params = [_abi.make_params(q, scale_quant_matrix(JPEG_LUMA_Q50, q), args.mode, bool(args.prefilter),
-                               codec.gaussian_kernel3()) for _ in range(F) for q in SWEEP_QS]
+    # rank 0's quant tables reach every rank in one broadcast (RCCL over xGMI at N > 1)
+    tables = broadcast_tables(SWEEP_QS)
+    params = [_abi.make_params(q, tables[i], args.mode, bool(args.prefilter), codec.gaussian_kernel3())
+              for _ in range(F) for i, q in enumerate(SWEEP_QS)]
     rep = args.sweep_replicate
     plan = _abi.Plan(_abi.context(local), params, H, W, nq=1 if rep else nq)
     gen = torch.Generator(device=dev)

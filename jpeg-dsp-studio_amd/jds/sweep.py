@@ -9,9 +9,10 @@ the frame-sharded multi-GPU sweep of BASELINE cfg4 (64 frames x Q in
   returns per-item statistics: nonzero count, exact magnitude bits, histogram,
   integer SSE.
 * ``distributed_sweep`` shards frames across the ranks of an initialised
-  ``torch.distributed`` group (one process per GPU, no data-path collective)
-  and gathers the per-item statistics to every rank with one
-  ``all_gather_object`` -- the only exchange the path has.
+  ``torch.distributed`` group (one process per GPU, no data-path collective):
+  rank 0 builds the quant tables and one ``broadcast`` (RCCL over xGMI with
+  the nccl backend) hands every rank the same float64 tables; the per-item
+  statistics come back to every rank with one ``all_gather_object``.
 """
 from __future__ import annotations
 
@@ -48,7 +49,7 @@ def shard(n: int, rank: int, world: int) -> range:
 
 
 def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilter: bool = True,
-                 device: int = 0) -> List[dict]:
+                 device: int = 0, tables: Optional[np.ndarray] = None) -> List[dict]:
     """All (frame, quality) items of `frames` (uint8 [F, H, W, 3], NumPy or a torch
     tensor on the device) through quality-sweep plans (jds_plan_create_q: the
     colour / prefilter / subsample / DCT front end runs once per frame and is
@@ -69,8 +70,8 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
     stats = np.zeros((F, len(qs)), dtype=_abi.STATS_DTYPE)
     for c0 in range(0, len(qs), 8):
         qc = qs[c0:c0 + 8]
-        params = [_abi.make_params(q, scale_quant_matrix(JPEG_LUMA_Q50, q), mode, prefilter, gk)
-                  for _ in range(F) for q in qc]
+        qt = [scale_quant_matrix(JPEG_LUMA_Q50, q) if tables is None else tables[c0 + i] for i, q in enumerate(qc)]
+        params = [_abi.make_params(q, qt[i], mode, prefilter, gk) for _ in range(F) for i, q in enumerate(qc)]
         plan = _abi.Plan(_abi.context(device), params, H, W, nq=len(qc))
         try:
             out = torch.empty((F * len(qc), H, W, 3), dtype=torch.uint8, device=dev)
@@ -96,18 +97,47 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
     return items
 
 
+def quant_tables(qualities: Sequence[int]) -> np.ndarray:
+    """[nq, 8, 8] float64: scale_quant_matrix(JPEG_LUMA_Q50, q) per quality
+    (engines/quantizer.py:7-19 applied to utils/constants.py:6-15)."""
+    from engines.quantizer import scale_quant_matrix
+    from utils.constants import JPEG_LUMA_Q50
+    return np.stack([scale_quant_matrix(JPEG_LUMA_Q50, int(q)) for q in qualities]).astype(np.float64)
+
+
+def broadcast_tables(qualities: Sequence[int], group=None) -> np.ndarray:
+    """Rank 0's quant tables on every rank: one broadcast of nq x 64 float64
+    (3 KB for the six sweep qualities) -- through RCCL over xGMI when the group's
+    backend is nccl (device tensor), gloo otherwise.  Every rank then quantises
+    with bit-identical tables, whatever its own host computed."""
+    import torch
+    import torch.distributed as dist
+    tables = quant_tables(qualities)
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return tables
+    dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend(group) == 'nccl' else torch.device('cpu')
+    t = torch.from_numpy(tables.reshape(len(qualities), 64)).to(dev)
+    if dist.get_rank(group) != 0:
+        t.zero_()
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast(t, src=src, group=group)
+    return t.cpu().numpy().reshape(-1, 8, 8)
+
+
 def distributed_sweep(n_frames: int, qualities: Sequence[int],
-                      compute: Callable[[range, Sequence[int]], List[dict]],
+                      compute: Callable[[range, Sequence[int], np.ndarray], List[dict]],
                       group=None) -> List[dict]:
     """Frame-shard a sweep over the ranks of the initialised torch.distributed
-    group: rank r computes `compute(frames_of_r, qualities)` (its items in
-    frame-major order, each dict carrying a global 'frame'), then one
-    all_gather_object gives every rank the whole list in global item order."""
+    group: rank 0's quant tables are broadcast to all ranks, rank r computes
+    `compute(frames_of_r, qualities, tables)` (its items in frame-major order,
+    each dict carrying a global 'frame'), then one all_gather_object gives
+    every rank the whole list in global item order."""
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     mine = shard(n_frames, rank, world)
-    local = compute(mine, list(qualities))
+    tables = broadcast_tables(qualities, group)
+    local = compute(mine, list(qualities), tables)
     if world == 1:
         return local
     parts: List[Optional[List[dict]]] = [None] * world
