@@ -406,12 +406,12 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
     const size_t nblk = (size_t)n * (size_t)(g.cpf / 64);
     const size_t ptiles = (size_t)(n_q > 1 ? quant_mq_tiles(g) : g.tiles_y * g.tiles_x);
     if ((e = p->fq32.ensure(fqs * n)) != hipSuccess || (e = p->gk32.ensure(sizeof gk32)) != hipSuccess ||
-        (e = p->fixlist.ensure(8 * nblk)) != hipSuccess || (e = p->counters.ensure(64)) != hipSuccess ||
+        (e = p->fixlist.ensure(8 * nblk)) != hipSuccess || (e = p->counters.ensure(8 * (size_t)n + 64)) != hipSuccess ||
         (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * ptiles)) != hipSuccess ||
         (n_q > 1 && (e = p->dct32.ensure(sizeof(float) * (size_t)n_frames * g.cpf)) != hipSuccess) ||
         (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemset(p->counters.p, 0, 64)) != hipSuccess) {  // armed once; k_fwd_reduce re-arms
+        (e = hipMemset(p->counters.p, 0, 8 * (size_t)n + 64)) != hipSuccess) {  // armed once; k_fwd_reduce re-arms
       free(h32);
       jds_plan_destroy(p);
       return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
@@ -434,10 +434,19 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
 
 int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   if (!p || !counts) return fail(JDS_EINVAL, "null argument");
-  uint32_t c[4];  // [0] live append counter, [2] the last run's forward fix-up list length
-  HIP_TRY(hipMemcpy(c, p->counters.p, sizeof c, hipMemcpyDeviceToHost));
-  counts[0] = c[2];
-  counts[1] = c[1];
+  // counters: [0, n) live per-item append counters, [n, 2n) the last run's
+  // per-item forward fix-up list lengths
+  counts[0] = counts[1] = 0u;
+  if (p->g.bs == 16 || p->counters.n < 8 * (size_t)p->n) return JDS_OK;
+  uint32_t* c = (uint32_t*)malloc(8 * (size_t)p->n);
+  if (!c) return fail(JDS_ENOMEM, "fix_counts: host allocation");
+  hipError_t e = hipMemcpy(c, p->counters.p, 8 * (size_t)p->n, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) {
+    free(c);
+    return fail(JDS_EHIP, "fix_counts: %s", hipGetErrorString(e));
+  }
+  for (int i = 0; i < p->n; ++i) counts[0] += c[p->n + i];
+  free(c);
   return JDS_OK;
 }
 

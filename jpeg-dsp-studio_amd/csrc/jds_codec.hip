@@ -536,17 +536,18 @@ __global__ void k_sel_dequant(const int16_t* __restrict__ coeffs, const FrameQ* 
 // Sum of the forward kernels' per-tile statistics partials (nonzero, magnitude
 // bits, hist[50] as u32 per tile) into the frame stats: 8 groups x 64 lanes
 // per workgroup, 64 tiles per workgroup, one u64 atomic per statistic.
-// With `counters` (fast path), the first workgroup also moves the fix-up list
-// length to counters[2] (read by k_fix_fwd and jds_plan_fix_counts) and resets
-// counters[0] for the next run's appends: every appending kernel precedes this
-// one on the stream, so no memset is needed per run.
+// With `counters` (fast path: one fix-up list counter per item, then their
+// stashed copies), workgroup (0, item) also moves the item's list length to
+// counters[n + item] (read by k_fix_fwd and jds_plan_fix_counts) and resets
+// counters[item] for the next run's appends: every appending kernel precedes
+// this one on the stream, so no memset is needed per run.
 __global__ void __launch_bounds__(512) k_fwd_reduce(jds_frame_stats* st, const uint32_t* __restrict__ part, int ptiles,
                                                    unsigned* __restrict__ counters) {
   __shared__ unsigned long long s_sum[8][64];
   const int f = blockIdx.y, j = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  if (counters != nullptr && blockIdx.x == 0 && f == 0 && threadIdx.x == 0) {
-    counters[2] = counters[0];
-    counters[0] = 0u;
+  if (counters != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    counters[gridDim.y + f] = counters[f];
+    counters[f] = 0u;
   }
   const int t0 = blockIdx.x * 64 + grp * 8;
   unsigned long long a = 0ull;

@@ -146,22 +146,24 @@ __device__ __forceinline__ uint4 pack_q(const int (&q)[8]) {
 }
 
 // Flagged blocks (any uncertain coefficient among the block's 8 lanes) go to
-// the fix list; lane 8b of a wave speaks for block b.  One atomic per wave
-// reserves the wave's slots (at high quality a few % of all blocks are listed:
-// one atomic per block serialises on the counter).
-__device__ __forceinline__ void flag_block(const LaneStats& ls, bool valid, int line, int frame, int plane, int bidx,
-                                           uint2* fixlist, unsigned* fixcount) {
+// their item's fix list (`cap` entries per item) and counter; lane 8b of a wave
+// speaks for block b.  One atomic per wave reserves the wave's slots, and the
+// counters are per item: a device-scope atomic on one shared word serialises
+// across the chip (all XCDs), which at high quality (a third of the waves
+// flag something at Q95) cost the sweep's quantiser 10x its Q5 time.
+__device__ __forceinline__ void flag_block(const LaneStats& ls, bool valid, int line, int item, int plane, int bidx,
+                                           uint2* fixlist, unsigned* fixcount, long long cap) {
   const unsigned long long fm = __ballot(valid && ls.nflag != 0u);
   if (!fm) return;  // wave-uniform
   const int lane = threadIdx.x & 63;
   const bool mine = valid && line == 0 && ((fm >> (lane & ~7)) & 0xffull);
   const unsigned long long lm = __ballot(mine);
   unsigned base = 0u;
-  if (lane == __ffsll((long long)lm) - 1) base = atomicAdd(fixcount, (unsigned)__popcll(lm));
+  if (lane == __ffsll((long long)lm) - 1) base = atomicAdd(fixcount + item, (unsigned)__popcll(lm));
   base = __shfl(base, __ffsll((long long)lm) - 1, 64);
   if (mine) {
     const unsigned slot = base + (unsigned)__popcll(lm & ((1ull << lane) - 1ull));
-    fixlist[slot] = make_uint2((unsigned)frame, ((unsigned)plane << 24) | (unsigned)bidx);
+    fixlist[(size_t)item * cap + slot] = make_uint2((unsigned)item, ((unsigned)plane << 24) | (unsigned)bidx);
   }
 }
 
@@ -410,7 +412,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   if (valid)
     *reinterpret_cast<uint4*>(coeffs + (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
                               (long long)bidx * 64 + u * 8) = pack_q(q);
-  flag_block(ls, valid, line, frame, plane, bidx, fixlist, fixcount);
+  flag_block(ls, valid, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
   stats_flush(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
 }
 
@@ -680,7 +682,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     column(P + by_t * 8 * TW + bx_t * 8, TW, plane);
   }
   if constexpr (!MQ) {
-    flag_block(ls, true, line, frame, plane, bidx, fixlist, fixcount);
+    flag_block(ls, true, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
     stats_flush(ls, true, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
   }
 }
@@ -744,10 +746,13 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
   __shared__ double s_w[CPLANE ? WRR * WCC : 1];         // fp64 chroma of the window
   __shared__ double s_rf[CPLANE ? WRR * (WCC - 2) : 1];  // after the row pass
   const int t = threadIdx.x;
-  const unsigned count = *fixcount;
+  // grid (x, items): item blockIdx.y's list, strided over blockIdx.x; its
+  // length was stashed at fixcount[item] by k_fwd_reduce
+  const unsigned count = fixcount[blockIdx.y];
+  const uint2* __restrict__ list = fixlist + (size_t)blockIdx.y * (size_t)(g.cpf / 64);
   const double k[3] = {gk[0], gk[1], gk[2]};
   for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
-    const uint2 ent = fixlist[e];
+    const uint2 ent = list[e];
     const int frame = (int)ent.x;
     const int plane = (int)(ent.y >> 24);
     const int bidx = (int)(ent.y & 0xffffffu);
@@ -913,7 +918,7 @@ k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* 
         quant8(v, rq, thr, valid, qv, ls, s_st[q]);
         const int item = f * nq + q;
         if (valid) *reinterpret_cast<uint4*>(coeffs + (long long)item * g.cpf + rw * 8) = pack_q(qv);
-        flag_block(ls, valid, u, item, plane, bidx, fixlist, fixcount);
+        flag_block(ls, valid, u, item, plane, bidx, fixlist, fixcount, g.cpf / 64);
         if (valid) {
           nz[q] += ls.nz;
           mb[q] += ls.mb;
@@ -1020,11 +1025,12 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
                        fixcount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  // partials -> frame statistics (reset by the front-end launch above); the
-  // fix-up list length moves to fixcount[2] and fixcount[0] is re-armed
+  // partials -> frame statistics (reset by the front-end launch above); each
+  // item's fix-up list length moves to fixcount[n + item], fixcount[item] is re-armed
   if ((e = launch_fwd_reduce(n, st, part, ptiles, fixcount, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(FIX_GRID), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
-                     fixcount + 2, nq);
+  const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
+  hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
+                     fixcount + n, nq);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
 }
