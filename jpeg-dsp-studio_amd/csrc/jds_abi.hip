@@ -30,7 +30,8 @@ hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* ch
                           double* out, hipStream_t s);
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
-                           jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* fixcount, float* dct32,
+                           jds_frame_stats* st, uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount,
+                           float* dct32,
                            hipStream_t s, const Side* side, bool finish);
 int quant_mq_tiles(const Geo& g);
 constexpr int MAXQ_SHARED = 8;  // jds_fast.hip MAXQ
@@ -135,7 +136,7 @@ struct jds_plan {
   Geo g{};
   DevBuf fq, gk, part;
   // fast path: fp32 tables, fix-up lists and counters
-  DevBuf fq32, gk32, fixlist, counters, part32;  // part32: per-tile forward statistics
+  DevBuf fq32, gk32, fixbits, fixlist, counters, part32;  // per-item fix-up bitmaps and lists; per-tile statistics
   Side side;  // border tiles run beside interior tiles
   DevBuf planes;  // 16x16 path: reconstructed chroma planes (n x 2 x hc x wc f64)
   double* qt = nullptr;  // host copy of the per-frame 8x8 tables (entropy headers)
@@ -406,12 +407,16 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
     const size_t nblk = (size_t)n * (size_t)(g.cpf / 64);
     const size_t ptiles = (size_t)(n_q > 1 ? quant_mq_tiles(g) : g.tiles_y * g.tiles_x);
     if ((e = p->fq32.ensure(fqs * n)) != hipSuccess || (e = p->gk32.ensure(sizeof gk32)) != hipSuccess ||
-        (e = p->fixlist.ensure(8 * nblk)) != hipSuccess || (e = p->counters.ensure(8 * (size_t)n + 64)) != hipSuccess ||
+        (e = p->fixbits.ensure(4 * (size_t)n * (size_t)fix_wpi(g))) != hipSuccess ||
+        (e = p->fixlist.ensure(8 * nblk)) != hipSuccess ||
+        (e = p->counters.ensure(8 * (size_t)n + 64)) != hipSuccess ||
         (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * ptiles)) != hipSuccess ||
         (n_q > 1 && (e = p->dct32.ensure(sizeof(float) * (size_t)n_frames * g.cpf)) != hipSuccess) ||
         (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemset(p->counters.p, 0, 8 * (size_t)n + 64)) != hipSuccess) {  // armed once; k_fwd_reduce re-arms
+        (e = hipMemset(p->counters.p, 0, 8 * (size_t)n + 64)) != hipSuccess ||
+        (e = hipMemset(p->fixbits.p, 0, 4 * (size_t)n * (size_t)fix_wpi(g))) != hipSuccess) {
+      // the fix-up bitmaps start clean once; k_fix_compact clears the words it consumes
       free(h32);
       jds_plan_destroy(p);
       return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
@@ -434,18 +439,17 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
 
 int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   if (!p || !counts) return fail(JDS_EINVAL, "null argument");
-  // counters: [0, n) live per-item append counters, [n, 2n) the last run's
-  // per-item forward fix-up list lengths
+  // counters[n, 2n): blocks the last run's k_fix_fwd recomputed, per item
   counts[0] = counts[1] = 0u;
   if (p->g.bs == 16 || p->counters.n < 8 * (size_t)p->n) return JDS_OK;
-  uint32_t* c = (uint32_t*)malloc(8 * (size_t)p->n);
+  uint32_t* c = (uint32_t*)malloc(4 * (size_t)p->n);
   if (!c) return fail(JDS_ENOMEM, "fix_counts: host allocation");
-  hipError_t e = hipMemcpy(c, p->counters.p, 8 * (size_t)p->n, hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpy(c, (const uint32_t*)p->counters.p + p->n, 4 * (size_t)p->n, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
     free(c);
     return fail(JDS_EHIP, "fix_counts: %s", hipGetErrorString(e));
   }
-  for (int i = 0; i < p->n; ++i) counts[0] += c[p->n + i];
+  for (int i = 0; i < p->n; ++i) counts[0] += c[i];
   free(c);
   return JDS_OK;
 }
@@ -484,7 +488,8 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
     else
       HIP_TRY(launch_fast_fwd(p->mode, p->pf, p->g, p->n, p->nq, rgb, coeffs, (const FrameQ*)p->fq.p, p->fq32.p,
                               (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint32_t*)p->part32.p,
-                              (uint2*)p->fixlist.p, (unsigned*)p->counters.p, (float*)p->dct32.p, s, &p->side,
+                              (uint32_t*)p->fixbits.p, (uint2*)p->fixlist.p, (unsigned*)p->counters.p,
+                              (float*)p->dct32.p, s, &p->side,
                               phases == 1));  // forward + inverse: k_finalize adds the zero bin
   }
   if (phases & 2)
@@ -505,6 +510,7 @@ void jds_plan_destroy(jds_plan* p) {
   p->gk32.release();
   p->fixlist.release();
   p->counters.release();
+  p->fixbits.release();
   p->part32.release();
   p->planes.release();
   p->dct32.release();

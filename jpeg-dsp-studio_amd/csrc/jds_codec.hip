@@ -533,43 +533,10 @@ __global__ void k_sel_dequant(const int16_t* __restrict__ coeffs, const FrameQ* 
   if (i < 64) sel->dequantized[i] = (double)coeffs[(long long)sel_blk * 64 + i] * fq[0].q[i];
 }
 
-// Sum of the forward kernels' per-tile statistics partials (nonzero, magnitude
-// bits, hist[50] as u32 per tile) into the frame stats: 8 groups x 64 lanes
-// per workgroup, 64 tiles per workgroup, one u64 atomic per statistic.
-// With `counters` (fast path: one fix-up list counter per item, then their
-// stashed copies), workgroup (0, item) also moves the item's list length to
-// counters[n + item] (read by k_fix_fwd and jds_plan_fix_counts) and resets
-// counters[item] for the next run's appends: every appending kernel precedes
-// this one on the stream, so no memset is needed per run.
-__global__ void __launch_bounds__(512) k_fwd_reduce(jds_frame_stats* st, const uint32_t* __restrict__ part, int ptiles,
-                                                   unsigned* __restrict__ counters) {
-  __shared__ unsigned long long s_sum[8][64];
-  const int f = blockIdx.y, j = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  if (counters != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
-    counters[gridDim.y + f] = counters[f];
-    counters[f] = 0u;
-  }
-  const int t0 = blockIdx.x * 64 + grp * 8;
-  unsigned long long a = 0ull;
-  if (j < 52) {
-    unsigned v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = t0 + i < ptiles ? part[((size_t)f * ptiles + t0 + i) * 52 + j] : 0u;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a += v[i];
-  }
-  s_sum[grp][j] = a;
-  __syncthreads();
-  if (threadIdx.x < 52) {
-    unsigned long long b = 0ull;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) b += s_sum[i][threadIdx.x];
-    jds_frame_stats* s = st + f;
-    unsigned long long* dst = threadIdx.x == 0 ? (unsigned long long*)&s->nonzero
-                              : threadIdx.x == 1 ? (unsigned long long*)&s->magnitude_bits
-                                                 : (unsigned long long*)&s->hist[threadIdx.x - 2];
-    if (b) atomicAdd(dst, b);
-  }
+// Sum of the forward kernels' per-tile statistics partials into the frame
+// stats (reduce_partials, jds_internal.hpp).
+__global__ void __launch_bounds__(512) k_fwd_reduce(jds_frame_stats* st, const uint32_t* __restrict__ part, int ptiles) {
+  reduce_partials(st, part, ptiles);
 }
 
 // End of the forward phase: per-frame constants and the histogram's zero bin.
@@ -583,16 +550,15 @@ __global__ void k_fwd_finish(const Geo g, jds_frame_stats* st) {
   s->hist[25] += (uint64_t)g.cpf - s->nonzero;  // zeros fall in bin 25 ([0, 4))
 }
 
-hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, unsigned* counters,
-                             hipStream_t s) {
-  hipLaunchKernelGGL(k_fwd_reduce, dim3((ptiles + 63) / 64, n), dim3(512), 0, s, st, part, ptiles, counters);
+hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_fwd_reduce, dim3((ptiles + 63) / 64, n), dim3(512), 0, s, st, part, ptiles);
   return hipGetLastError();
 }
 
 hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uint32_t* part, int ptiles,
                              hipStream_t s) {
   if (part) {
-    hipError_t e = launch_fwd_reduce(n, st, part, ptiles, nullptr, s);
+    hipError_t e = launch_fwd_reduce(n, st, part, ptiles, s);
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_fwd_finish, dim3(n), dim3(64), 0, s, g, st);

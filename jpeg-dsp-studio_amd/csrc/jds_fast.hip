@@ -104,9 +104,27 @@ struct LaneStats {
   unsigned nz = 0u, mb = 0u, hn = 0u, nflag = 0u;
 };
 
+// Rare bins in the quality-sweep quantiser (k_quant_mq, REPL): RH_COPIES
+// replicated histograms per table (lane & 3 picks one), slot 50 = q 100 (folded
+// into bin 49), and lanes with nothing to count in a slot add to a private
+// dummy word, so the 8 atomics of a lane need no per-coefficient branches.
+constexpr int RH_COPIES = 4, RH_STRIDE = 53;
+constexpr int RH_WORDS = RH_COPIES * RH_STRIDE + 64;
+
+__device__ __forceinline__ unsigned rare_bin_total(const unsigned* s_rh, int b) {
+  unsigned t = 0u;
+#pragma unroll
+  for (int c = 0; c < RH_COPIES; ++c) t += s_rh[c * RH_STRIDE + b] + (b == 49 ? s_rh[c * RH_STRIDE + 50] : 0u);
+  return t;
+}
+
 // Round 8 coefficients c*(1/Q) to int16, certify each rounding (t farther than
 // thr + |t| 2^-22 from a half-integer decides like the fp64 reference) and
-// count statistics.  Rare histogram bins (|q| > 12) go to LDS atomics.
+// count statistics.  Rare histogram bins (|q| > 12) go to LDS atomics: into
+// s_st's histogram with per-coefficient branches (REPL false: rare values are
+// sparse at the headline qualities), or branch-free into replicated
+// histograms at s_rh (REPL true).
+template <bool REPL = false>
 __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8], const float (&thr)[8], bool valid,
                                        int (&q)[8], LaneStats& ls, unsigned* s_st) {
   unsigned nrare = 0u;
@@ -121,12 +139,29 @@ __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8]
     ls.mb += (unsigned)__builtin_amdgcn_frexp_expf(r);
     const unsigned o = (unsigned)(q[k] + 12);
     ls.hn += 1u << (o & 28u);  // bins 22..29; a rare q lands in some nibble and is taken back below
-    nrare += o >= 32u ? 1u : 0u;
+    if constexpr (REPL)
+      nrare |= o;  // any o >= 32 sets a bit >= 5
+    else
+      nrare += o >= 32u ? 1u : 0u;
   }
 #ifdef JDS_PROBE_NORARE  // tools/probe: drop the rare-bin atomics
   nrare = 0u;
 #endif
-  if (nrare != 0u) {
+  if constexpr (REPL) {
+    if (nrare >= 32u) {
+      const int lane = threadIdx.x & 63;
+      unsigned* copy = s_st + (lane & (RH_COPIES - 1)) * RH_STRIDE;
+      unsigned* dummy = s_st + RH_COPIES * RH_STRIDE + lane;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const unsigned o = (unsigned)(q[k] + 12);
+        const bool rare = o >= 32u;
+        ls.hn -= rare ? 1u << (o & 28u) : 0u;
+        const unsigned h = (unsigned)(q[k] + 100);
+        atomicAdd(rare && valid && h <= 200u ? copy + (h >> 2) : dummy, 1u);
+      }
+    }
+  } else if (nrare != 0u) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const unsigned o = (unsigned)(q[k] + 12);
@@ -145,14 +180,20 @@ __device__ __forceinline__ uint4 pack_q(const int (&q)[8]) {
                     (uint32_t)(uint16_t)q[6] | ((uint32_t)(uint16_t)q[7] << 16));
 }
 
-// Flagged blocks (any uncertain coefficient among the block's 8 lanes) go to
-// their item's fix list (`cap` entries per item) and counter; lane 8b of a wave
-// speaks for block b.  One atomic per wave reserves the wave's slots, and the
-// counters are per item: a device-scope atomic on one shared word serialises
-// across the chip (all XCDs), which at high quality (a third of the waves
-// flag something at Q95) cost the sweep's quantiser 10x its Q5 time.
-__device__ __forceinline__ void flag_block(const LaneStats& ls, bool valid, int line, int item, int plane, int bidx,
-                                           uint2* fixlist, unsigned* fixcount, long long cap) {
+// Flagged blocks (any uncertain coefficient among the block's 8 lanes) are
+// queued for the exact fp64 fix-up; lane 8b of a wave speaks for block b.
+// Two forms, both per item (one shared device-scope counter serialises
+// across the chip's XCDs):
+// * flag_block_list (single-quality front ends): one atomic per wave reserves
+//   the wave's slots in the item's list (`cap` entries).  The wave waits for
+//   the atomic's return, which the large interior launch hides.
+// * flag_block_bits (k_quant_mq, up to 8 tables per row): the block's bit in
+//   the item's bitmap (`wpi` words) by an atomic OR that returns nothing the
+//   wave waits for -- a third of the quantiser's waves flag something at Q95
+//   and it has little other work to hide a round trip behind;
+//   k_fwd_reduce_fix turns the bitmaps into lists.
+__device__ __forceinline__ void flag_block_list(const LaneStats& ls, bool valid, int line, int item, int plane,
+                                                int bidx, uint2* fixlist, unsigned* fixcount, long long cap) {
   const unsigned long long fm = __ballot(valid && ls.nflag != 0u);
   if (!fm) return;  // wave-uniform
   const int lane = threadIdx.x & 63;
@@ -165,6 +206,15 @@ __device__ __forceinline__ void flag_block(const LaneStats& ls, bool valid, int 
     const unsigned slot = base + (unsigned)__popcll(lm & ((1ull << lane) - 1ull));
     fixlist[(size_t)item * cap + slot] = make_uint2((unsigned)item, ((unsigned)plane << 24) | (unsigned)bidx);
   }
+}
+
+__device__ __forceinline__ void flag_block_bits(const LaneStats& ls, bool valid, int line, int item, long long gblk,
+                                                uint32_t* fixbits, int wpi) {
+  const unsigned long long fm = __ballot(valid && ls.nflag != 0u);
+  if (!fm) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  if (valid && line == 0 && ((fm >> (lane & ~7)) & 0xffull))
+    atomicOr(fixbits + (size_t)item * wpi + (gblk >> 5), 1u << (gblk & 31));
 }
 
 // Wave sums through DPP, then the workgroup's statistics go to this tile's slot
@@ -229,10 +279,11 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   const int frame = blockIdx.y;
   int ty, tx;
   // this launch owns the frame statistics' reset (replaces a memset): tile 0
-  // of every frame clears its items' records before k_fwd_reduce adds to them
+  // of every frame clears its items' records before k_fwd_reduce_fix adds to them
   if (stz != nullptr && blockIdx.x == 0) {
     uint64_t* z = reinterpret_cast<uint64_t*>(stz + (size_t)frame * nzq);
     for (int i = tid; i < nzq * (int)(sizeof(jds_frame_stats) / 8); i += blockDim.x) z[i] = 0ull;
+    if (tid < nzq) fixcount[gridDim.y * nzq + frame * nzq + tid] = 0u;  // and the items' final fix-up counts
   }
   if (border) {  // tiles outside the interior rectangle rect = (ty_lo, ty_hi, tx_lo, tx_hi) only
     int e = blockIdx.x;
@@ -412,7 +463,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   if (valid)
     *reinterpret_cast<uint4*>(coeffs + (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
                               (long long)bidx * 64 + u * 8) = pack_q(q);
-  flag_block(ls, valid, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
+  flag_block_list(ls, valid, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
   stats_flush(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
 }
 
@@ -457,10 +508,11 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   const int tid = threadIdx.x, frame = blockIdx.y;
   const int ncol = rect.w - rect.z + 1;
   // this launch owns the frame statistics' reset (replaces a memset): tile 0
-  // of every frame clears its items' records before k_fwd_reduce adds to them
+  // of every frame clears its items' records before k_fwd_reduce_fix adds to them
   if (stz != nullptr && blockIdx.x == 0) {
     uint64_t* z = reinterpret_cast<uint64_t*>(stz + (size_t)frame * nzq);
     for (int i = tid; i < nzq * (int)(sizeof(jds_frame_stats) / 8); i += blockDim.x) z[i] = 0ull;
+    if (tid < nzq) fixcount[gridDim.y * nzq + frame * nzq + tid] = 0u;  // and the items' final fix-up counts
   }
   const int ty = rect.x + (int)blockIdx.x / ncol, tx = rect.z + (int)blockIdx.x % ncol;
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
@@ -682,7 +734,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     column(P + by_t * 8 * TW + bx_t * 8, TW, plane);
   }
   if constexpr (!MQ) {
-    flag_block(ls, true, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
+    flag_block_list(ls, true, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
     stats_flush(ls, true, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
   }
 }
@@ -731,6 +783,60 @@ __device__ double sample64(const uint8_t* img, const Geo& g, int plane, int pr, 
     return (s[0][0] + s[0][1]) * 0.5;
 }
 
+// End of the certified forward's producer launches: the statistics partials
+// into the frame stats (reduce_partials), then (sweep plans) bitmap -> list:
+// each wave takes 64 bitmap words of the workgroup's share of item f's
+// bitmap, prefix-sums their set bits, reserves its slots with one atomic on
+// the item's counter (zeroed by the front-end launch), writes the block
+// indices in order and clears the words for the next run.  Only this small
+// launch waits for an atomic's return; the producers' atomic ORs do not.
+__global__ void __launch_bounds__(512)
+k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ part, int ptiles,
+                 uint32_t* __restrict__ fixbits, uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount) {
+  reduce_partials(st, part, ptiles);
+  // fixcount[0, n): live counters the single-quality front ends appended to;
+  // fixcount[n, 2n): this run's list lengths (k_fix_fwd, jds_plan_fix_counts)
+  unsigned* const fixlen = fixcount + gridDim.y;
+  if (fixbits == nullptr) {  // single-quality front ends appended to the lists themselves
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      fixlen[blockIdx.y] = fixcount[blockIdx.y];
+      fixcount[blockIdx.y] = 0u;  // re-armed for the next run
+    }
+    return;
+  }
+  const int item = blockIdx.y, wpi = fix_wpi(g), lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int per = (wpi + gridDim.x - 1) / gridDim.x, w_end = min(wpi, (blockIdx.x + 1) * per);
+  const long long nyb = (long long)g.nby * g.nbx, ncb = (long long)g.ncy * g.ncx, cap = g.cpf / 64;
+  uint32_t* bits = fixbits + (size_t)item * wpi;
+  uint2* list = fixlist + (size_t)item * cap;
+  for (int w0 = blockIdx.x * per + wave * 64; w0 < w_end; w0 += 8 * 64) {
+    const int w = w0 + lane;
+    uint32_t word = 0u;
+    if (w < w_end) {
+      word = bits[w];
+      if (word) bits[w] = 0u;
+    }
+    if (!__ballot(word != 0u)) continue;  // wave-uniform
+    const unsigned c = (unsigned)__popc(word);
+    unsigned incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    unsigned base = 0u;
+    if (lane == 63) base = atomicAdd(fixlen + item, incl);  // zeroed by the front-end launch
+    base = __shfl(base, 63, 64) + incl - c;
+    while (word) {
+      const long long b = (long long)w * 32 + (__ffs(word) - 1);
+      word &= word - 1u;
+      const int plane = b < nyb ? 0 : (b < nyb + ncb ? 1 : 2);
+      const int bidx = (int)(b - (plane == 0 ? 0 : (plane == 1 ? nyb : nyb + ncb)));
+      list[base++] = make_uint2((unsigned)item, ((unsigned)plane << 24) | (unsigned)bidx);
+    }
+  }
+}
+
 // One listed block per 64-thread workgroup iteration (grid-strides over the
 // fix list): every thread forms one sample exactly, then 8 threads run the
 // column and row transforms, requantize and correct the statistics.
@@ -747,7 +853,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
   __shared__ double s_rf[CPLANE ? WRR * (WCC - 2) : 1];  // after the row pass
   const int t = threadIdx.x;
   // grid (x, items): item blockIdx.y's list, strided over blockIdx.x; its
-  // length was stashed at fixcount[item] by k_fwd_reduce
+  // length is fixcount[item] (k_fwd_reduce_fix)
   const unsigned count = fixcount[blockIdx.y];
   const uint2* __restrict__ list = fixlist + (size_t)blockIdx.y * (size_t)(g.cpf / 64);
   const double k[3] = {gk[0], gk[1], gk[2]};
@@ -870,11 +976,11 @@ int quant_mq_tiles(const Geo& g) {  // workgroups per frame (<= 31 rows per lane
 
 __global__ void __launch_bounds__(256)
 k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* __restrict__ coeffs,
-           const FastQ* __restrict__ fq, uint32_t* __restrict__ part, uint2* __restrict__ fixlist,
-           unsigned* __restrict__ fixcount) {
+           const FastQ* __restrict__ fq, uint32_t* __restrict__ part, uint32_t* __restrict__ fixbits) {
   __shared__ __attribute__((aligned(16))) float s_rq[MAXQ][64];
   __shared__ __attribute__((aligned(16))) float s_th[MAXQ][2][64];
   __shared__ unsigned s_st[MAXQ][NSTAT];
+  __shared__ unsigned s_rh[MAXQ][RH_WORDS];  // replicated rare-bin histograms (quant8<true>)
   const int tid = threadIdx.x, f = blockIdx.y, ptiles = gridDim.x;
   for (int i = tid; i < nq * 64; i += 256) {
     const int q = i >> 6, k = i & 63;
@@ -884,6 +990,7 @@ k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* 
     s_th[q][1][k] = t.thr[1][k];
   }
   for (int i = tid; i < MAXQ * NSTAT; i += 256) (&s_st[0][0])[i] = 0u;
+  for (int i = tid; i < MAXQ * RH_WORDS; i += 256) (&s_rh[0][0])[i] = 0u;
   __syncthreads();
   const long long rows = g.cpf / 8, nyb = (long long)g.nby * g.nbx, ncb = (long long)g.ncy * g.ncx;
   unsigned nz[MAXQ], mb[MAXQ], be[MAXQ], bo[MAXQ], nrows = 0u;
@@ -915,10 +1022,10 @@ k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* 
         const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
         int qv[8];
         LaneStats ls;
-        quant8(v, rq, thr, valid, qv, ls, s_st[q]);
+        quant8<true>(v, rq, thr, valid, qv, ls, s_rh[q]);
         const int item = f * nq + q;
         if (valid) *reinterpret_cast<uint4*>(coeffs + (long long)item * g.cpf + rw * 8) = pack_q(qv);
-        flag_block(ls, valid, u, item, plane, bidx, fixlist, fixcount, g.cpf / 64);
+        flag_block_bits(ls, valid, u, item, b, fixbits, fix_wpi(g));
         if (valid) {
           nz[q] += ls.nz;
           mb[q] += ls.mb;
@@ -951,7 +1058,8 @@ k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* 
   __syncthreads();
   for (int i = tid; i < nq * NSTAT; i += 256) {
     const int q = i / NSTAT, j = i - q * NSTAT;
-    part[((size_t)(f * nq + q) * ptiles + blockIdx.x) * NSTAT + j] = s_st[q][j];
+    part[((size_t)(f * nq + q) * ptiles + blockIdx.x) * NSTAT + j] =
+        s_st[q][j] + (j >= 2 ? rare_bin_total(s_rh[q], j - 2) : 0u);
   }
 }
 
@@ -959,17 +1067,14 @@ k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* 
 
 hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uint32_t* part, int ptiles,
                              hipStream_t s);
-hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, unsigned* counters,
-                             hipStream_t s);
-// k_fix_fwd workgroups (grid-stride over the list): enough that typical lists
-// (0.4 % of 3M blocks at Q50) need one block per workgroup -- up to ~29
-// one-wave workgroups per CU keep their load latencies in flight together
+// k_fix_fwd workgroups in all (x items, grid-stride over each item's list):
+// typical lists (0.4 % of 3M blocks at Q50) need one block per workgroup
 constexpr int FIX_GRID = 16384;
 
 template <int MODE, bool PF>
 static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
                              const FastQ* fq32, const double* gk, const float* gk32, jds_frame_stats* st,
-                             uint32_t* part, uint2* fixlist, unsigned* fixcount, float* dct32, hipStream_t s,
+                             uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount, float* dct32, hipStream_t s,
                              const Side* side, bool finish) {
   using C = Cfg<MODE>;
   const bool mq = nq > 1;  // sweep plan: front end once per frame into dct32, then k_quant_mq
@@ -1021,13 +1126,14 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   int ptiles = g.tiles_y * g.tiles_x;
   if (mq) {
     ptiles = quant_mq_tiles(g);
-    hipLaunchKernelGGL(k_quant_mq, dim3(ptiles, nf), dim3(256), 0, s, g, nq, dct32, coeffs, fq32, part, fixlist,
-                       fixcount);
+    hipLaunchKernelGGL(k_quant_mq, dim3(ptiles, nf), dim3(256), 0, s, g, nq, dct32, coeffs, fq32, part, fixbits);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  // partials -> frame statistics (reset by the front-end launch above); each
-  // item's fix-up list length moves to fixcount[n + item], fixcount[item] is re-armed
-  if ((e = launch_fwd_reduce(n, st, part, ptiles, fixcount, s)) != hipSuccess) return e;
+  // partials -> frame statistics (reset by the front-end launch above), list
+  // lengths to fixcount[n + item] (sweep plans: bitmaps -> lists)
+  hipLaunchKernelGGL(k_fwd_reduce_fix, dim3((ptiles + 63) / 64, n), dim3(512), 0, s, g, st, part, ptiles,
+                     mq ? fixbits : nullptr, fixlist, fixcount);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
   hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                      fixcount + n, nq);
@@ -1037,18 +1143,18 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
 
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
-                           jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* fixcount, float* dct32,
+                           jds_frame_stats* st, uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount, float* dct32,
                            hipStream_t s, const Side* side, bool finish) {
   const FastQ* f = (const FastQ*)fq32;
   switch (mode) {
     case M420:
-      return pf ? fast_fwd_t<M420, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish)
-                : fast_fwd_t<M420, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish);
+      return pf ? fast_fwd_t<M420, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish)
+                : fast_fwd_t<M420, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish);
     case M422:
-      return pf ? fast_fwd_t<M422, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish)
-                : fast_fwd_t<M422, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish);
+      return pf ? fast_fwd_t<M422, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish)
+                : fast_fwd_t<M422, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish);
     default:
-      return fast_fwd_t<M444, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixlist, fixcount, dct32, s, side, finish);
+      return fast_fwd_t<M444, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish);
   }
 }
 

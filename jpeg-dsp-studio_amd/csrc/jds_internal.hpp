@@ -1,6 +1,6 @@
 // jds_internal.hpp — types shared by the HIP kernels and the host-side C-ABI.
 #pragma once
-#include <hip/hip_runtime_api.h>
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "jds.h"
@@ -26,6 +26,10 @@ struct Geo {
   double up_sy, up_sx;  // cv2.resize scale (src/dst) of the chroma upsample
   int bs;               // block size: 8, or 16 (jds_b16.hip)
 };
+
+// Fix-up bitmap words per item of the certified forward path (one bit per
+// 8x8 block of the item's coefficient array).
+__host__ __device__ inline int fix_wpi(const Geo& g) { return (int)((g.cpf / 64 + 31) / 32); }
 
 // A second stream with fork/join events: lets a plan run independent launches
 // (border tiles beside interior tiles) concurrently.  All null = serial.
@@ -62,5 +66,35 @@ struct Cfg {
   static constexpr int CWC = 8 * CBC + 2 * RX;
   static constexpr int TI = 384;                      // inverse threads
 };
+
+// Workgroup (x, f) of a (ceil(ptiles / 64), n) x 512 launch: sums tiles
+// [64x, 64x + 64) of frame f's per-tile statistics partials (nonzero,
+// magnitude bits, hist[50] as u32 per tile) into the frame stats, 8 groups x 64
+// lanes, one u64 atomic per statistic.
+__device__ inline void reduce_partials(jds_frame_stats* st, const uint32_t* __restrict__ part, int ptiles) {
+  __shared__ unsigned long long s_sum[8][64];
+  const int f = blockIdx.y, j = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int t0 = blockIdx.x * 64 + grp * 8;
+  unsigned long long a = 0ull;
+  if (j < 52) {
+    unsigned v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = t0 + i < ptiles ? part[((size_t)f * ptiles + t0 + i) * 52 + j] : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a += v[i];
+  }
+  s_sum[grp][j] = a;
+  __syncthreads();
+  if (threadIdx.x < 52) {
+    unsigned long long b = 0ull;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b += s_sum[i][threadIdx.x];
+    jds_frame_stats* s = st + f;
+    unsigned long long* dst = threadIdx.x == 0 ? (unsigned long long*)&s->nonzero
+                              : threadIdx.x == 1 ? (unsigned long long*)&s->magnitude_bits
+                                                 : (unsigned long long*)&s->hist[threadIdx.x - 2];
+    if (b) atomicAdd(dst, b);
+  }
+}
 
 }  // namespace jds

@@ -18,7 +18,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libjds.so')
+# JDS_LIB_PATH: load another build of the same ABI (A/B timing of kernel variants, tools/ab_lib.sh)
+LIB_PATH = os.environ.get('JDS_LIB_PATH') or os.path.join(_HERE, 'libjds.so')
 
 JDS_OK, JDS_EINVAL, JDS_ENOTSUP, JDS_EHIP, JDS_ENOMEM = 0, -1, -2, -3, -4
 SS_444, SS_422, SS_420 = 0, 1, 2
