@@ -250,3 +250,62 @@ def test_plan_rejects_non_integer_quant_table():
     q[3, 4] = 16.5
     with pytest.raises(ValueError, match='not an integer'):
         _abi.Plan(_abi.context(0), [_abi.make_params(50, q, '4:2:0', True, codec.gaussian_kernel3())], 16, 16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('nq', [1, 3])
+def test_repeated_runs_any_phase_order_give_identical_results(nq):
+    """The plan keeps no per-run state that leaks into the next run: the
+    statistics reset, the per-item fix-up counters and bitmaps are re-armed by
+    the kernels themselves (no memsets).  Any sequence of combined, forward-only,
+    inverse-only and exact runs reproduces the first run's coefficients, bytes,
+    statistics and fix-up count."""
+    import torch
+    from jds import _abi, codec
+    h, w = 200, 328
+    qs = [50, 95, 100][:nq]
+    frames = np.stack([cpu_ref.random_image(h, w, 900 + i) for i in range(2)])
+    params = [_abi.make_params(q, cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q), '4:2:0', True,
+                               codec.gaussian_kernel3()) for _ in range(2) for q in qs]
+    plan = _abi.Plan(_abi.context(0), params, h, w, nq=nq)
+    dev = torch.device('cuda:0')
+    rgb = torch.from_numpy(frames).to(dev)
+    n = len(params)
+    out = torch.empty((n, h, w, 3), dtype=torch.uint8, device=dev)
+    cf = torch.empty((n, plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+    st = torch.zeros((n, _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+
+    def snap():
+        torch.cuda.synchronize()
+        s = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(-1)
+        return (out.cpu().numpy().copy(), cf.cpu().numpy().copy(),
+                {f: s[f].copy() for f in ('nonzero', 'magnitude_bits', 'hist', 'sse_rgb', 'total_coeffs')},
+                int(plan.fix_counts()[0]))
+
+    def run(flags):
+        out.zero_()
+        cf.zero_()
+        plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), flags, 0)
+
+    try:
+        run(_abi.RUN_SSE)
+        ref = snap()
+        assert ref[3] > 0  # Q >= 50 on random frames always needs some fix-up
+        seqs = [[_abi.RUN_SSE], [_abi.RUN_FWD, _abi.RUN_INV | _abi.RUN_SSE], [_abi.RUN_FWD, _abi.RUN_FWD],
+                [_abi.RUN_SSE | _abi.RUN_EXACT], [_abi.RUN_SSE]]
+        for seq in seqs:
+            for fl in seq:
+                if fl == _abi.RUN_INV | _abi.RUN_SSE:
+                    plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), fl, 0)
+                else:
+                    run(fl)
+            if seq == [_abi.RUN_FWD, _abi.RUN_FWD]:
+                plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), _abi.RUN_INV | _abi.RUN_SSE, 0)
+            got = snap()
+            assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), seq
+            for f in ref[2]:
+                assert np.array_equal(got[2][f], ref[2][f]), (seq, f)
+            if not (seq[0] & _abi.RUN_EXACT):
+                assert got[3] == ref[3], seq
+    finally:
+        plan.close()
