@@ -69,6 +69,35 @@ def parse():
 PREWARM_S = 0.3
 
 
+def init_dist(world, local):
+    """One process per GPU over RCCL (backend nccl).  JDS_BENCH_BACKEND=gloo with
+    JDS_BENCH_SHARE_GPU=1 rehearses the N > 1 path with several ranks on one GPU
+    (a one-GPU box; RCCL refuses two ranks on one device): ranks map onto the
+    visible devices round-robin and the timing reductions go through host
+    tensors.  Returns (device index, backend)."""
+    import torch
+    import torch.distributed as dist
+    backend = os.environ.get('JDS_BENCH_BACKEND', 'nccl')
+    if os.environ.get('JDS_BENCH_SHARE_GPU') == '1':
+        local = local % max(1, torch.cuda.device_count())
+    if world > 1:
+        torch.cuda.set_device(local)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
+    return local, backend
+
+
+def max_over_ranks(x, dev, backend):
+    """The slowest rank's value (one all-reduce)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def prewarm(run_step, warmup, dev):
     """The W untimed warmup steps, continued until PREWARM_S seconds of sustained
     load have passed.  The MI355X raises its clocks over the first ~40 ms of
@@ -118,9 +147,7 @@ def sweep_main(args):
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    local, backend = init_dist(world, local)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
     from jds import _abi, codec
@@ -158,9 +185,7 @@ def sweep_main(args):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, dev, backend)
     items = F * nq * world
     value = items * H * W * args.steps / elapsed / 1e6
     result = {'metric': 'Mpixels/s quality sweep (configs[3]); items = frames x Q', 'value': round(value, 2),
@@ -201,9 +226,7 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    local, backend = init_dist(world, local)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
 
@@ -292,9 +315,7 @@ def main():
     t_inv = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
     plan = plans[0]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, dev, backend)
 
     px_per_step = B * H * W
     value = world * px_per_step * args.steps / elapsed / 1e6
