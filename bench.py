@@ -375,7 +375,9 @@ def main():
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'algorithmic_bytes_per_launch': bytes_fwd if dom == 'k_fwd' else bytes_inv,
                      'avg_launch_ms': round(t_dom, 4),
-                     'timing': 'HIP events on the launch stream, serial calibration pass after the timed region'},
+                     'timing': 'HIP events on the launch stream, serial calibration pass after the timed region',
+                     'limiter': 'VALU issue, not HBM: the forward computes in certified fp32, the bit-exact '
+                                'inverse in fp64 (DESIGN.md section 4, profiles/*_pmc_summary.json)'},
         'kernels_ms': {'k_fwd': round(t_fwd, 4), 'k_inv': round(t_inv, 4)},
         'fixups_last_step': {'fwd_blocks': int(plans[0].fix_counts()[0])},
         'pipeline_roofline_frac': round(value / world * 1e6 * (6 + 2 * S) / (HBM_PEAK_GBS * 1e9), 4),
