@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <new>
 
@@ -34,6 +35,7 @@ hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const
                            float* dct32,
                            hipStream_t s, const Side* side, bool finish);
 int quant_mq_tiles(const Geo& g);
+int inv16_tiles(int mode, int H, int W);
 constexpr int MAXQ_SHARED = 8;  // jds_fast.hip MAXQ
 void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
 size_t fast_q_size();
@@ -374,7 +376,9 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
   p->g = g;
   hipError_t e;
   if ((e = p->fq.ensure(sizeof(FrameQ) * n)) != hipSuccess || (e = p->gk.ensure(3 * sizeof(double))) != hipSuccess ||
-      (e = p->part.ensure(sizeof(double) * (size_t)n * g.tiles_y * g.tiles_x)) != hipSuccess ||
+      (e = p->part.ensure(sizeof(double) * (size_t)n *
+                          (size_t)std::max(g.tiles_y * g.tiles_x, g.bs == 16 ? inv16_tiles(mode, (int)H, (int)W) : 0))) !=
+          hipSuccess ||
       (e = hipMemcpy(p->fq.p, hq, sizeof(FrameQ) * n, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(p->gk.p, params[0].gauss, 3 * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess) {
     free(hq);
@@ -539,7 +543,7 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
   if ((rc = check_tables(prm))) return rc;
   HIP_TRY(hipSetDevice(c->device));
   const size_t npx = (size_t)H * (size_t)W, nimg = npx * 3, ncf = (size_t)g.cpf;
-  const int tiles = g.tiles_y * g.tiles_x;
+  const int tiles = std::max(g.tiles_y * g.tiles_x, g.bs == 16 ? inv16_tiles(mode, (int)H, (int)W) : 0);
   HIP_TRY(c->rgb.ensure(nimg));
   HIP_TRY(c->out.ensure(nimg));
   HIP_TRY(c->coeffs.ensure(ncf * sizeof(int16_t)));

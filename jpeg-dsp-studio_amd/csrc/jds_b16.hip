@@ -487,12 +487,237 @@ k_inv16(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __restric
   }
 }
 
+
+// ------------------------------------------------- fused inverse (4:2:x) --
+//
+// k_inv16f<MODE, XTRA>: the whole inverse of one TH x TW tile in one launch,
+// the 8x8 path's k_inv2 design for 16x16 blocks.  Chroma blocks covering the
+// tile's chroma window (+ the 1-sample ring the bilinear taps reach) are
+// dequantised and 16-point IDCT'd by 16-lane groups into an fp64 LDS window
+// (the row passes' crop is implicit: the taps clamp to hc-1 / wc-1); then each
+// lane IDCTs one row of a luma block, upsamples the chroma of its 16 pixels
+// from the window, converts, clips, truncates and stores 48 bytes.  It replaces
+// k_chroma16 + k_inv16, whose fp64 chroma planes went through HBM (16 B per
+// pixel written and read again at 4:2:2).  Same operations, same order: bytes
+// are identical (tests/test_gpu_block16.py).
+template <int MODE>
+struct Inv16 {
+  static constexpr int SY = Cfg16<MODE>::SY;
+  static_assert(Cfg16<MODE>::SX == 2, "chroma subsampled horizontally");
+  static constexpr int TH = (MODE == M420) ? 64 : 32, TW = (MODE == M420) ? 64 : 128;
+  static constexpr int NT = 256, NG = NT / 16;  // 16-lane groups = blocks in flight
+  static constexpr int RY = SY == 2 ? 1 : 0;
+  static constexpr int CWR = TH / SY + 2 * RY, CWC = TW / 2 + 2;  // chroma window (samples)
+  static constexpr int YBC = TW / 16, NYB = (TH / 16) * YBC;      // luma blocks per tile
+  static constexpr int CBR = (MODE == M420) ? TH / 32 + 2 : TH / 16, CBC = TW / 32 + 2;
+  static constexpr int NCB = CBR * CBC;                            // chroma blocks per plane
+  static_assert(NYB == NG, "one luma round");
+};
+
+template <int MODE, int XTRA>
+__global__ void __launch_bounds__(Inv16<MODE>::NT)
+k_inv16f(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+         const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
+         double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb) {
+  using I = Inv16<MODE>;
+  __shared__ __attribute__((aligned(16))) double s_b[I::NG * BS16];
+  __shared__ double s_cw[2][I::CWR * I::CWC];
+  __shared__ double s_q[64];
+  __shared__ double s_red[I::NT / 64];
+  __shared__ unsigned long long s_sse;
+
+  const int tid = threadIdx.x, grp = tid >> 4, line = tid & 15;
+  const int frame = blockIdx.y, tile = blockIdx.x;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int Y0 = ty * I::TH, X0 = tx * I::TW;
+  const int16_t* cf = coeffs + (size_t)frame * g.cpf;
+  if (tid < 64) s_q[tid] = fq[frame].q[tid];
+  if (XTRA && tid == 0) s_sse = 0ull;
+  __syncthreads();
+
+  // ---- 1. chroma window ----------------------------------------------------
+  const int cwy0 = Y0 / I::SY - I::RY, cwx0 = X0 / 2 - 1;
+  const int cby0 = (Y0 / I::SY) / 16 - I::RY, cbx0 = (X0 / 2) / 16 - 1;
+  double* const sb = s_b + grp * BS16;
+#pragma unroll 1
+  for (int b0 = 0; b0 < 2 * I::NCB; b0 += I::NG) {
+    const int blk = b0 + grp;
+    if (blk < 2 * I::NCB) {
+      const int p = blk >= I::NCB, bi = blk - p * I::NCB;
+      const int by = cby0 + bi / I::CBC, bx = cbx0 + bi % I::CBC;
+      if (by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx) {  // uniform per 16-lane group
+        double r[16];
+        idct16_block(cf + (p ? g.off_cr : g.off_cb) + ((long long)by * g.ncx + bx) * 256, s_q, sb, line, r);
+        const int wr = by * 16 + line - cwy0;
+        if ((unsigned)wr < (unsigned)I::CWR) {
+          double* w = &s_cw[p][wr * I::CWC];
+          const int wc0 = bx * 16 - cwx0;
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = r[k];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. luma row, upsample, colour, store ------------------------------------
+  unsigned long long sse = 0ull;
+  double ssy = 0.0;
+  const uint8_t* in_f = XTRA ? rgb_in + (size_t)frame * g.H * g.W * 3 : nullptr;
+  uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
+  const int by = Y0 / 16 + grp / I::YBC, bx = X0 / 16 + grp % I::YBC;
+  const int y = by * 16 + line;
+  if (by < g.nby && bx < g.nbx) {  // uniform per 16-lane group
+    double Yv[16];
+    idct16_block(cf + ((long long)by * g.nbx + bx) * 256, s_q, sb, line, Yv);
+    if (y < g.H) {
+      int wq, wt = 0;
+      if constexpr (I::SY == 2) {  // cv2 INTER_LINEAR rows: wq weight 1/4, wt weight 3/4 (k_inv2)
+        float fy = (float)((y + 0.5) * g.up_sy - 0.5);
+        const int sy = (int)floorf(fy);
+        fy -= (float)sy;
+        const int r0 = clampi(clampi(sy, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+        const int r1 = clampi(clampi(sy + 1, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+        const bool q0 = fy == 0.75f;
+        wq = q0 ? r0 : r1;
+        wt = q0 ? r1 : r0;
+      } else {
+        wq = y - cwy0;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int x0 = bx * 16 + 8 * h;
+        if (x0 >= g.W) break;
+        // horizontal taps (pixel 2m: (s[m-1], s[m]) x (1/4, 3/4); 2m+1: (s[m], s[m+1]) x (3/4, 1/4)),
+        // vertical blend, edge pixels copied (cv2's clamped taps) -- chroma8 in jds_inv.hip
+        double C[2][8];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const double* cw = s_cw[p];
+          const int c0 = x0 / 2 - 1 - cwx0;
+          double h0[8];
+#pragma unroll
+          for (int rr = 0; rr < I::SY; ++rr) {
+            const double* sp = &cw[(rr ? wt : wq) * I::CWC + c0];
+            double q75[5];
+#pragma unroll
+            for (int j = 1; j < 5; ++j) q75[j] = sp[j] * 0.75;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const double e = fma(sp[i], 0.25, q75[i + 1]), o = fma(sp[i + 2], 0.25, q75[i + 1]);
+              if (rr == 0) {
+                h0[2 * i] = e;
+                h0[2 * i + 1] = o;
+              } else {
+                C[p][2 * i] = fma(h0[2 * i], 0.25, e * 0.75);
+                C[p][2 * i + 1] = fma(h0[2 * i + 1], 0.25, o * 0.75);
+              }
+            }
+          }
+          if constexpr (I::SY == 1) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) C[p][k] = h0[k];
+          }
+#pragma unroll
+          for (int side = 0; side < 2; ++side) {
+            const int kl = side == 0 ? (x0 == 0 ? 0 : -1) : (g.W - 1 - x0 < 8 ? g.W - 1 - x0 : -1);
+            if (kl >= 0) {
+              const int e = (side == 0 ? 0 : g.wc - 1) - cwx0;
+              double v = cw[wq * I::CWC + e];
+              if constexpr (I::SY == 2) v = fma(v, 0.25, cw[wt * I::CWC + e] * 0.75);
+#pragma unroll
+              for (int k = 0; k < 8; ++k) C[p][k] = k == kl ? v : C[p][k];
+            }
+          }
+        }
+        const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
+        uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
+        uint32_t pk[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+        double R[8], G[8], B[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {  // color_space.py:17-24, pipeline.py:93-95
+          const double Yk = Yv[8 * h + k];
+          R[k] = Yk + 1.402 * (C[1][k] - 128.0);
+          G[k] = Yk - 0.344136 * (C[0][k] - 128.0) - 0.714136 * (C[1][k] - 128.0);
+          B[k] = Yk + 1.772 * (C[0][k] - 128.0);
+          const int b = 3 * k;
+          pk[b >> 2] |= (uint32_t)clampi((int)R[k], 0, 255) << (8 * (b & 3));
+          pk[(b + 1) >> 2] |= (uint32_t)clampi((int)G[k], 0, 255) << (8 * ((b + 1) & 3));
+          pk[(b + 2) >> 2] |= (uint32_t)clampi((int)B[k], 0, 255) << (8 * ((b + 2) & 3));
+        }
+        if (nx == 8 && ((((uintptr_t)o) & 7u) == 0)) {
+          uint2* o2 = reinterpret_cast<uint2*>(o);
+          o2[0] = make_uint2(pk[0], pk[1]);
+          o2[1] = make_uint2(pk[2], pk[3]);
+          o2[2] = make_uint2(pk[4], pk[5]);
+        } else {
+#pragma unroll
+          for (int b = 0; b < 24; ++b)
+            if (b < 3 * nx) o[b] = (uint8_t)(pk[b >> 2] >> (8 * (b & 3)));
+        }
+        if constexpr (XTRA > 0) {
+          const uint8_t* src = in_f + ((size_t)y * g.W + x0) * 3;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if (k < nx) {
+              const int o0 = src[3 * k], o1 = src[3 * k + 1], o2 = src[3 * k + 2];
+              const int b = 3 * k;
+              const int ur = (pk[b >> 2] >> (8 * (b & 3))) & 255, ug = (pk[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 255,
+                        ub = (pk[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 255;
+              const int d0 = o0 - ur, d1 = o1 - ug, d2 = o2 - ub;
+              sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
+              const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
+              const double yo = luma(R0, G0, B0);
+              const double yr = luma((double)ur, (double)ug, (double)ub);
+              const double dy = yo - yr;
+              ssy = ssy + dy * dy;
+              if constexpr (XTRA > 1) {
+                const size_t pix = (size_t)y * g.W + x0 + k;
+                err_y[pix] = fabs(yo - Yv[8 * h + k]);  // pipeline.py:120
+                err_rgb[pix] = ((fabs(R0 - fmin(fmax(R[k], 0.0), 255.0)) + fabs(G0 - fmin(fmax(G[k], 0.0), 255.0))) +
+                                fabs(B0 - fmin(fmax(B[k], 0.0), 255.0))) / 3.0;  // pipeline.py:121
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  if constexpr (XTRA > 0) {
+    unsigned long long sv = sse;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sv += __shfl_xor(sv, o, 64);
+    if ((tid & 63) == 0) atomicAdd(&s_sse, sv);
+    double d = ssy;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d = d + __shfl_xor(d, o, 64);
+    if ((tid & 63) == 0) s_red[tid >> 6] = d;
+    __syncthreads();
+    if (tid == 0) {
+      double a = 0.0;
+      for (int i = 0; i < I::NT / 64; ++i) a = a + s_red[i];
+      sse_y_part[(size_t)frame * gridDim.x + tile] = a;
+      atomicAdd((unsigned long long*)&st[frame].sse_rgb, s_sse);
+    }
+  }
+}
+
 // ------------------------------------------------------------ launchers --
 
 hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uint32_t* part, int ptiles,
                              hipStream_t s);
 hipError_t launch_finalize(const Geo& g, int n, jds_frame_stats* st, const double* part, int tiles, bool with_sse,
                            hipStream_t s);
+
+// tiles of the fused 16x16 inverse (sse_y partials per tile); 0 for 4:4:4
+int inv16_tiles(int mode, int H, int W) {
+  switch (mode) {
+    case M420: return ((H + Inv16<M420>::TH - 1) / Inv16<M420>::TH) * ((W + Inv16<M420>::TW - 1) / Inv16<M420>::TW);
+    case M422: return ((H + Inv16<M422>::TH - 1) / Inv16<M422>::TH) * ((W + Inv16<M422>::TW - 1) / Inv16<M422>::TW);
+    default: return 0;
+  }
+}
 
 int tile_dims16(int mode, int* MY, int* MX) {
   switch (mode) {
@@ -521,15 +746,33 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
   }
   if (phases & 2) {
-    const int cblocks = 2 * g.ncy * g.ncx;
-    hipLaunchKernelGGL((k_chroma16<MODE>), dim3((cblocks + 15) / 16, n), dim3(256), 0, s, g, coeffs, fq, planes);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint8_t* rin = (want_sse || err_y) ? rgb : nullptr;
-    hipLaunchKernelGGL((k_inv16<MODE>), grid, dim3(C::TI), 0, s, g, coeffs, fq, planes, rin, rgb_out, st, part,
-                       err_y, err_rgb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    int tiles = g.tiles_y * g.tiles_x;
+    if constexpr (MODE != M444) {  // fused: chroma window in LDS (k_inv16f)
+      using I = Inv16<MODE>;
+      const int tx = (g.W + I::TW - 1) / I::TW;
+      tiles = ((g.H + I::TH - 1) / I::TH) * tx;
+      const dim3 gi(tiles, n), bi(I::NT);
+      if (err_y)
+        hipLaunchKernelGGL((k_inv16f<MODE, 2>), gi, bi, 0, s, g, tx, coeffs, fq, rin, rgb_out, st, part, err_y,
+                           err_rgb);
+      else if (rin)
+        hipLaunchKernelGGL((k_inv16f<MODE, 1>), gi, bi, 0, s, g, tx, coeffs, fq, rin, rgb_out, st, part, nullptr,
+                           nullptr);
+      else
+        hipLaunchKernelGGL((k_inv16f<MODE, 0>), gi, bi, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, nullptr,
+                           nullptr);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else {
+      const int cblocks = 2 * g.ncy * g.ncx;
+      hipLaunchKernelGGL((k_chroma16<MODE>), dim3((cblocks + 15) / 16, n), dim3(256), 0, s, g, coeffs, fq, planes);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      hipLaunchKernelGGL((k_inv16<MODE>), grid, dim3(C::TI), 0, s, g, coeffs, fq, planes, rin, rgb_out, st, part,
+                         err_y, err_rgb);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
-    e = launch_finalize(g, n, st, part, g.tiles_y * g.tiles_x, rin != nullptr, s);
+    e = launch_finalize(g, n, st, part, tiles, rin != nullptr, s);
   }
   return e;
 }
