@@ -168,7 +168,7 @@ k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
       const double k0 = gk[0], k1 = gk[1];
       const int sc = reflect_pad(gx * 16 + line, g.wc);
       const int wc0 = C::SX * sc - x0 + 1;
-#pragma unroll
+#pragma unroll 2  // full unrolling kept every sample's operands live: 195 VGPRs, 2 waves/SIMD
       for (int i = 0; i < 16; ++i) {
         const int sr = reflect_pad(gy * 16 + i, g.hc);
         const int wr0 = C::SY * sr - y0 + 1;
