@@ -71,6 +71,7 @@ k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   __shared__ uint32_t s_rgb[WN];
   __shared__ __attribute__((aligned(16))) double s_u[U_D];
   __shared__ double s_q32[64];
+  __shared__ double s_rq32[64];  // fl(1 / (32 Q))
   __shared__ unsigned s_hist[50];
   __shared__ int s_acc[2];
 
@@ -87,7 +88,10 @@ k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
     const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
     s_rgb[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
   }
-  if (tid < 64) s_q32[tid] = 32.0 * fq[frame].q[tid];  // exact
+  if (tid < 64) {
+    s_q32[tid] = 32.0 * fq[frame].q[tid];  // exact
+    s_rq32[tid] = 1.0 / s_q32[tid];
+  }
   if (tid < 50) s_hist[tid] = 0u;
   if (tid < 2) s_acc[tid] = 0;
   __syncthreads();
@@ -212,10 +216,27 @@ k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = s_blk[u * 16 + k];
     dct2_line16(v);
+    // quantizer.py:22-24: rint of the true IEEE quotient.  t = fl(v * fl(1/Q))
+    // lies within 3 * 2^-53 |v/Q| of fl(v/Q), so unless t is within |t| 2^-50
+    // of a half-integer both round to the same integer; the rare others (and
+    // exact ties) take the division.  |t - rint(t)| is exact (Sterbenz).
+    double qd[16];
+    unsigned need = 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const double t = v[k] * q16_of(s_rq32, u, k);
+      qd[k] = __builtin_rint(t);
+      need |= (fabs(fabs(t - qd[k]) - 0.5) <= fabs(t) * 0x1p-50 ? 1u : 0u) << k;
+    }
+    if (__ballot(need != 0u)) {  // wave-uniform: almost never taken
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if ((need >> k) & 1u) qd[k] = __builtin_rint(v[k] / q16_of(s_q32, u, k));
+    }
     int q[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      q[k] = (int)__builtin_rint(v[k] / q16_of(s_q32, u, k));  // quantizer.py:22-24
+      q[k] = (int)qd[k];
       const int m = q[k] < 0 ? -q[k] : q[k];
       if (m) {
         ++nz;
