@@ -765,7 +765,9 @@ __device__ double sample64(const uint8_t* img, const Geo& g, int plane, int pr, 
   constexpr int SY = Cfg<MODE>::SY;
   const int sr = reflect_pad(pr, g.hc), sc = reflect_pad(pc, g.wc);
   double s[SY][2];
+#pragma unroll 1
   for (int a = 0; a < SY; ++a) {
+#pragma unroll 1
     for (int b = 0; b < 2; ++b) {
       const int y = SY * sr + a, x = 2 * sc + b;
       if constexpr (PF) {
@@ -841,7 +843,7 @@ k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ 
 // fix list): every thread forms one sample exactly, then 8 threads run the
 // column and row transforms, requantize and correct the statistics.
 template <int MODE, bool PF>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
           const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq) {
@@ -855,10 +857,15 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
   // grid (x, items): item blockIdx.y's list, strided over blockIdx.x; its
   // length is fixcount[item] (k_fwd_reduce_fix)
   const unsigned count = fixcount[blockIdx.y];
-  const uint2* __restrict__ list = fixlist + (size_t)blockIdx.y * (size_t)(g.cpf / 64);
+  const unsigned cap = (unsigned)(g.cpf / 64);  // list capacity per item
+  const uint2* __restrict__ list = fixlist + (size_t)blockIdx.y * cap;
+  // the first entry is read beside the count (in bounds, maybe stale when
+  // blockIdx.x >= count, then unused): one memory latency instead of two
+  uint2 next = blockIdx.x < cap ? list[blockIdx.x] : make_uint2(0u, 0u);
   const double k[3] = {gk[0], gk[1], gk[2]};
   for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
-    const uint2 ent = list[e];
+    const uint2 ent = next;
+    if (e + gridDim.x < count) next = list[e + gridDim.x];
     const int frame = (int)ent.x;
     const int plane = (int)(ent.y >> 24);
     const int bidx = (int)(ent.y & 0xffffffu);
@@ -866,15 +873,40 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     const int gy = bidx / nbx, gx = bidx - gy * nbx;
     const uint8_t* img = rgb + (size_t)(frame / nq) * g.H * g.W * 3;  // item -> its frame
     const int i = t >> 3, j = t & 7;
+    // lanes 0-7 (row u = t of the block): the stored row, fetched now so its
+    // latency hides under the sampling below
+    const long long off = (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
+                          (long long)bidx * 64 + (t & 7) * 8;
+    uint4* dst = reinterpret_cast<uint4*>(coeffs + off);
+    uint4 old = make_uint4(0u, 0u, 0u, 0u);
+    if (t < 8) old = *dst;
     // prefiltered chroma of a block away from every edge: stage the source
     // window once (colour, then the row pass, in LDS), same fp64 operations
     const int wy0 = SY * 8 * gy - 1, wx0 = 16 * gx - 1;
     const bool staged = CPLANE && plane != 0 && gy * 8 + 8 <= g.hc && gx * 8 + 8 <= g.wc && wy0 >= 0 &&
                         wx0 >= 0 && wy0 + WRR <= g.H && wx0 + WCC <= g.W;
     if (staged) {  // uniform per workgroup
-      for (int q = t; q < WRR * WCC; q += 64) {
-        const int r = q / WCC, c = q - r * WCC;
-        s_w[q] = px_chroma64(img, g, wy0 + r, wx0 + c, plane);
+      // every window load in flight before the first use (one memory latency)
+      constexpr int NWL = (WRR * WCC + 63) / 64;
+      uint32_t px[NWL];
+#pragma unroll
+      for (int l = 0; l < NWL; ++l) {
+        const int q = t + 64 * l;
+        px[l] = 0u;
+        if (q < WRR * WCC) {
+          const int r = q / WCC, c = q - r * WCC;
+          const uint8_t* p = img + ((size_t)(wy0 + r) * g.W + wx0 + c) * 3;
+          px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < NWL; ++l) {
+        const int q = t + 64 * l;
+        if (q < WRR * WCC) {
+          double R, G, B;
+          unpack(px[l], R, G, B);
+          s_w[q] = plane == 1 ? chroma_b(R, G, B) : chroma_r(R, G, B);
+        }
       }
       __syncthreads();
       for (int q = t; q < WRR * (WCC - 2); q += 64) {
@@ -919,10 +951,6 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
 #pragma unroll
       for (int c = 0; c < 8; ++c) v[c] = s_b[u * 8 + c];
       dct2_line(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
-      const long long off = (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
-                            (long long)bidx * 64 + u * 8;
-      uint4* dst = reinterpret_cast<uint4*>(coeffs + off);
-      const uint4 old = *dst;
       const uint32_t ow[4] = {old.x, old.y, old.z, old.w};
       uint32_t nw[4] = {0u, 0u, 0u, 0u};
       long long dnz = 0, dmb = 0;
