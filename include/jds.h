@@ -111,7 +111,8 @@ void* jds_ctx_stream(jds_ctx* ctx);  /* the context's own hipStream_t */
  * HxW share one subsampling/prefilter setting; params[i] gives frame i's table.
  * Buffers are device pointers: rgb (n*H*W*3 u8), rgb_out (same), coeffs
  * (n * coeffs_per_frame int16, reference layout: Y blocks, Cb blocks, Cr blocks,
- * raster order, each block row-major), stats (n entries, overwritten).
+ * raster order, each block row-major), stats (n entries, overwritten), each
+ * 16-byte aligned (JDS_EINVAL otherwise; hipMalloc / torch allocations are).
  * stream: a hipStream_t (NULL = the HIP null stream).  Asynchronous. */
 int jds_plan_create(jds_ctx* ctx, const jds_params* params, int n_frames, int64_t H, int64_t W,
                     jds_plan** out);

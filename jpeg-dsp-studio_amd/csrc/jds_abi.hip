@@ -467,6 +467,8 @@ int jds_plan_geometry(const jds_plan* p, jds_geometry* out) {
 int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs, jds_frame_stats* stats,
                  uint32_t flags, void* stream) {
   if (!p || !rgb || !rgb_out || !coeffs || !stats) return fail(JDS_EINVAL, "null argument");
+  if (((uintptr_t)rgb | (uintptr_t)rgb_out | (uintptr_t)coeffs | (uintptr_t)stats) & 15u)
+    return fail(JDS_EINVAL, "rgb, rgb_out, coeffs and stats must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (torch's default stream)
   int phases = (flags & JDS_RUN_FWD ? 1 : 0) | (flags & JDS_RUN_INV ? 2 : 0);
   if (!phases) phases = 3;

@@ -253,6 +253,27 @@ def test_plan_rejects_non_integer_quant_table():
 
 
 @pytest.mark.gpu
+def test_plan_rejects_misaligned_buffers():
+    """Batch buffers must be 16-byte aligned (the kernels' wide loads and stores)."""
+    import torch
+    from jds import _abi, codec
+    params = [_abi.make_params(50, cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, 50), '4:2:0', True,
+                               codec.gaussian_kernel3())]
+    plan = _abi.Plan(_abi.context(0), params, 32, 32)
+    dev = torch.device('cuda:0')
+    raw = torch.zeros(32 * 32 * 3 + 16, dtype=torch.uint8, device=dev)
+    out = torch.empty(32 * 32 * 3, dtype=torch.uint8, device=dev)
+    cf = torch.empty(plan.geometry.coeffs_per_frame, dtype=torch.int16, device=dev)
+    st = torch.zeros(_abi.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    try:
+        with pytest.raises(ValueError, match='16-byte aligned'):
+            plan.run(raw.data_ptr() + 1, out.data_ptr(), cf.data_ptr(), st.data_ptr(), 0, 0)
+        plan.run(raw.data_ptr() + 16, out.data_ptr(), cf.data_ptr(), st.data_ptr(), 0, 0)
+        torch.cuda.synchronize()
+    finally:
+        plan.close()
+
+
 @pytest.mark.parametrize('nq', [1, 3])
 def test_repeated_runs_any_phase_order_give_identical_results(nq):
     """The plan keeps no per-run state that leaks into the next run: the
