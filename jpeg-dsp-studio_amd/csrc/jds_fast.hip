@@ -1002,7 +1002,7 @@ int quant_mq_tiles(const Geo& g) {  // workgroups per frame (<= 31 rows per lane
   return (int)(t < 256 ? 256 : t);
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* __restrict__ coeffs,
            const FastQ* __restrict__ fq, uint32_t* __restrict__ part, uint32_t* __restrict__ fixbits) {
   __shared__ __attribute__((aligned(16))) float s_rq[MAXQ][64];
@@ -1025,6 +1025,13 @@ k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* 
 #pragma unroll
   for (int q = 0; q < MAXQ; ++q) nz[q] = mb[q] = be[q] = bo[q] = 0u;
   const long long step = (long long)ptiles * 256;
+  // the next row's coefficients are requested before this row is quantised
+  const float4* __restrict__ src = reinterpret_cast<const float4*>(dct32 + (long long)f * g.cpf);
+  float4 nx = make_float4(0.f, 0.f, 0.f, 0.f), ny = nx;
+  {
+    const long long rw = (long long)blockIdx.x * 256 + tid;
+    if (rw < rows) { nx = src[rw * 2]; ny = src[rw * 2 + 1]; }
+  }
   // uniform trip count per wave (flag_block ballots over the 8 rows of a block)
   for (long long r0 = (long long)blockIdx.x * 256; r0 < rows; r0 += step) {
     const long long rw = r0 + tid;
@@ -1033,13 +1040,9 @@ k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* 
     const int u = (int)(rw & 7);
     const int plane = b < nyb ? 0 : (b < nyb + ncb ? 1 : 2);
     const int bidx = (int)(b - (plane == 0 ? 0 : (plane == 1 ? nyb : nyb + ncb)));
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (valid) {
-      const float4* s4 = reinterpret_cast<const float4*>(dct32 + (long long)f * g.cpf + rw * 8);
-      const float4 x = s4[0], y = s4[1];
-      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
-      ++nrows;
-    }
+    const float v[8] = {nx.x, nx.y, nx.z, nx.w, ny.x, ny.y, ny.z, ny.w};  // stale past the end (every use is masked by valid)
+    nrows += valid ? 1u : 0u;
+    if (rw + step < rows) { nx = src[(rw + step) * 2]; ny = src[(rw + step) * 2 + 1]; }
 #pragma unroll
     for (int q = 0; q < MAXQ; ++q) {
       if (q < nq) {
