@@ -842,30 +842,75 @@ k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ 
 // One listed block per 64-thread workgroup iteration (grid-strides over the
 // fix list): every thread forms one sample exactly, then 8 threads run the
 // column and row transforms, requantize and correct the statistics.
+// Two grid shapes (a block's exact chain is latency-bound, so the lever is how
+// many chains run at once):
+// * per item (n_flat = 0; single-quality plans, similar list lengths): grid
+//   (x, items), item blockIdx.y's list strided over blockIdx.x;
+// * flat (n_flat = items; sweep plans, where the Q95 item's list is ~10x the
+//   Q5 item's): one grid over the concatenated lists, so a long list gets as
+//   many workgroups as it has entries.  Each workgroup prefix-sums the n list
+//   lengths in LDS (dynamic, 4 (n + 1) bytes) and maps its entry index to
+//   (item, slot) by binary search.
 template <int MODE, bool PF>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
-          const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq) {
+          const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq, const int n_flat) {
   constexpr bool CPLANE = (MODE != M444) && PF;
   constexpr int SY = Cfg<MODE>::SY;
   constexpr int WRR = 8 * SY + 2, WCC = 18;  // prefilter source window of one chroma block
   __shared__ double s_b[64];
   __shared__ double s_w[CPLANE ? WRR * WCC : 1];         // fp64 chroma of the window
   __shared__ double s_rf[CPLANE ? WRR * (WCC - 2) : 1];  // after the row pass
+  extern __shared__ unsigned s_off[];                    // flat grids: list starts, [n_flat + 1]
   const int t = threadIdx.x;
-  // grid (x, items): item blockIdx.y's list, strided over blockIdx.x; its
-  // length is fixcount[item] (k_fwd_reduce_fix)
-  const unsigned count = fixcount[blockIdx.y];
   const unsigned cap = (unsigned)(g.cpf / 64);  // list capacity per item
-  const uint2* __restrict__ list = fixlist + (size_t)blockIdx.y * cap;
-  // the first entry is read beside the count (in bounds, maybe stale when
-  // blockIdx.x >= count, then unused): one memory latency instead of two
-  uint2 next = blockIdx.x < cap ? list[blockIdx.x] : make_uint2(0u, 0u);
+  unsigned count;
+  const uint2* __restrict__ list;
+  uint2 next;
+  if (n_flat) {
+#pragma unroll 8
+    for (int i = t; i < n_flat; i += 64) s_off[i + 1] = fixcount[i];
+    if (t == 0) s_off[0] = 0u;
+    __syncthreads();
+    unsigned run = 0u;
+    for (int c0 = 0; c0 < n_flat; c0 += 64) {  // inclusive scan, 64 lengths at a time
+      const int i = c0 + t;
+      unsigned x = i < n_flat ? s_off[i + 1] : 0u;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(x, o, 64);
+        if (t >= o) x += y;
+      }
+      if (i < n_flat) s_off[i + 1] = run + x;
+      run += __shfl(x, 63, 64);
+    }
+    __syncthreads();
+    count = s_off[n_flat];
+    list = fixlist;
+    next = make_uint2(0u, 0u);
+  } else {
+    // length fixcount[item] (k_fwd_reduce_fix); the first entry is read beside
+    // it (in bounds, maybe stale when blockIdx.x >= count, then unused): one
+    // memory latency instead of two
+    count = fixcount[blockIdx.y];
+    list = fixlist + (size_t)blockIdx.y * cap;
+    next = blockIdx.x < cap ? list[blockIdx.x] : make_uint2(0u, 0u);
+  }
   const double k[3] = {gk[0], gk[1], gk[2]};
   for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
-    const uint2 ent = next;
-    if (e + gridDim.x < count) next = list[e + gridDim.x];
+    uint2 ent;
+    if (n_flat) {  // entry e of the concatenated lists: item = last start <= e
+      int lo = 0, hi = n_flat - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= e) lo = mid; else hi = mid - 1;
+      }
+      ent = list[(size_t)lo * cap + (e - s_off[lo])];
+    } else {
+      ent = next;
+      if (e + gridDim.x < count) next = list[e + gridDim.x];
+    }
     const int frame = (int)ent.x;
     const int plane = (int)(ent.y >> 24);
     const int bidx = (int)(ent.y & 0xffffffu);
@@ -1165,9 +1210,14 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   hipLaunchKernelGGL(k_fwd_reduce_fix, dim3((ptiles + 63) / 64, n), dim3(512), 0, s, g, st, part, ptiles,
                      mq ? fixbits : nullptr, fixlist, fixcount);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
-  hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
-                     fixcount + n, nq);
+  if (mq && n < 8192) {  // sweep: one flat grid over every item's list (list starts in <= 32 KB of LDS)
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(FIX_GRID), dim3(64), sizeof(unsigned) * (n + 1), s, g, rgb,
+                       coeffs, fq, gk, st, fixlist, fixcount + n, nq, n);
+  } else {
+    const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
+                       fixcount + n, nq, 0);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
 }
