@@ -82,11 +82,25 @@ k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   const int y0 = m0y * C::MH, x0 = m0x * C::MW;
   const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
 
-  for (int i = tid; i < WN; i += C::TF) {
-    const int r = i / WC, c = i - r * WC;
-    const int yy = reflect101(y0 - 1 + r, g.H), xx = reflect101(x0 - 1 + c, g.W);
-    const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
-    s_rgb[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+  {  // every window load in flight before the first LDS store (one memory latency)
+    constexpr int NL = (WN + C::TF - 1) / C::TF;
+    uint32_t px[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      px[l] = 0u;
+      if (i < WN) {
+        const int r = i / WC, c = i - r * WC;
+        const int yy = reflect101(y0 - 1 + r, g.H), xx = reflect101(x0 - 1 + c, g.W);
+        const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
+        px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      if (i < WN) s_rgb[i] = px[l];
+    }
   }
   if (tid < 64) {
     s_q32[tid] = 32.0 * fq[frame].q[tid];  // exact

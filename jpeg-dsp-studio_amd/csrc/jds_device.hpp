@@ -20,6 +20,7 @@ __device__ __forceinline__ int reflect_pad(int i, int n) {
 
 // cv2 BORDER_REFLECT_101 for any i (GaussianBlur default border)
 __device__ __forceinline__ int reflect101(int i, int n) {
+  if ((unsigned)i < (unsigned)n) return i;  // inside: no modulo
   if (n == 1) return 0;
   const int p = 2 * (n - 1);
   i = i < 0 ? -i : i;
