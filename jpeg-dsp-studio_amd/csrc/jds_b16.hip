@@ -113,11 +113,15 @@ k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   if constexpr (CPLANE) {  // full-resolution chroma + Gaussian row pass (cv2 RowFilter<double>)
     double* s_cb = s_u;
     double* s_cr = s_u + WN;
-    for (int i = tid; i < WN; i += C::TF) {
-      double R, G, B;
-      unpack(s_rgb[i], R, G, B);
-      s_cb[i] = chroma_b(R, G, B);
-      s_cr[i] = chroma_r(R, G, B);
+#pragma unroll
+    for (int l = 0; l < (WN + C::TF - 1) / C::TF; ++l) {
+      const int i = tid + l * C::TF;
+      if (i < WN) {
+        double R, G, B;
+        unpack(s_rgb[i], R, G, B);
+        s_cb[i] = chroma_b(R, G, B);
+        s_cr[i] = chroma_r(R, G, B);
+      }
     }
     __syncthreads();
     constexpr int NRP = WR * (WC - 2);
