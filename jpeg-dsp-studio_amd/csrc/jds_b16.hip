@@ -298,11 +298,19 @@ k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
 // 16 lanes (line = 0..15) that own it; the same lanes do both passes, so the
 // exchange is wave-local (a block's 16 lanes are in one wave).  Returns the
 // clipped spatial row `line` in r[16] (dct_engine.py:23-27).
-__device__ __forceinline__ void idct16_block(const int16_t* __restrict__ src, const double* __restrict__ q8,
-                                             double* __restrict__ s_b, int line, double* r) {
+// A lane's coefficient row of a 16x16 block (16 int16, two 16-byte loads).
+struct Row16 {
+  uint4 a, b;
+};
+__device__ __forceinline__ Row16 load_row16(const int16_t* __restrict__ src, int line) {
+  const uint4* p = reinterpret_cast<const uint4*>(src + line * 16);
+  return Row16{p[0], p[1]};
+}
+
+__device__ __forceinline__ void idct16_rows(const Row16& rw, const double* __restrict__ q8,
+                                            double* __restrict__ s_b, int line, double* r) {
   {
-    const uint4* p = reinterpret_cast<const uint4*>(src + line * 16);
-    const uint4 a = p[0], b = p[1];
+    const uint4 a = rw.a, b = rw.b;
     const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -326,6 +334,11 @@ __device__ __forceinline__ void idct16_block(const int16_t* __restrict__ src, co
     const double s = c[k] * 0.03125 + 128.0;  // fct 1/32 (exact), then +128
     r[k] = fmin(fmax(s, 0.0), 255.0);
   }
+}
+
+__device__ __forceinline__ void idct16_block(const int16_t* __restrict__ src, const double* __restrict__ q8,
+                                             double* __restrict__ s_b, int line, double* r) {
+  idct16_rows(load_row16(src, line), q8, s_b, line, r);
 }
 
 // Every chroma block -> cropped fp64 planes cb/cr (hc x wc each, per frame).
@@ -578,15 +591,30 @@ k_inv16f(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, con
   const int cwy0 = Y0 / I::SY - I::RY, cwx0 = X0 / 2 - 1;
   const int cby0 = (Y0 / I::SY) / 16 - I::RY, cbx0 = (X0 / 2) / 16 - 1;
   double* const sb = s_b + grp * BS16;
-#pragma unroll 1
-  for (int b0 = 0; b0 < 2 * I::NCB; b0 += I::NG) {
-    const int blk = b0 + grp;
+  // every coefficient row this lane will transform (its chroma blocks and its
+  // luma block) is requested before the first transform: one memory latency
+  constexpr int NCR = (2 * I::NCB + I::NG - 1) / I::NG;  // chroma rounds
+  Row16 crow[NCR];
+#pragma unroll
+  for (int k = 0; k < NCR; ++k) {
+    const int blk = k * I::NG + grp;
+    const int p = blk >= I::NCB, bi = blk - p * I::NCB;
+    const int by = cby0 + bi / I::CBC, bx = cbx0 + bi % I::CBC;
+    if (blk < 2 * I::NCB && by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx)
+      crow[k] = load_row16(cf + (p ? g.off_cr : g.off_cb) + ((long long)by * g.ncx + bx) * 256, line);
+  }
+  const int lby = Y0 / 16 + grp / I::YBC, lbx = X0 / 16 + grp % I::YBC;
+  Row16 lrow;
+  if (lby < g.nby && lbx < g.nbx) lrow = load_row16(cf + ((long long)lby * g.nbx + lbx) * 256, line);
+#pragma unroll
+  for (int k = 0; k < NCR; ++k) {
+    const int blk = k * I::NG + grp;
     if (blk < 2 * I::NCB) {
       const int p = blk >= I::NCB, bi = blk - p * I::NCB;
       const int by = cby0 + bi / I::CBC, bx = cbx0 + bi % I::CBC;
       if (by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx) {  // uniform per 16-lane group
         double r[16];
-        idct16_block(cf + (p ? g.off_cr : g.off_cb) + ((long long)by * g.ncx + bx) * 256, s_q, sb, line, r);
+        idct16_rows(crow[k], s_q, sb, line, r);
         const int wr = by * 16 + line - cwy0;
         if ((unsigned)wr < (unsigned)I::CWR) {
           double* w = &s_cw[p][wr * I::CWC];
@@ -605,11 +633,11 @@ k_inv16f(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, con
   double ssy = 0.0;
   const uint8_t* in_f = XTRA ? rgb_in + (size_t)frame * g.H * g.W * 3 : nullptr;
   uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
-  const int by = Y0 / 16 + grp / I::YBC, bx = X0 / 16 + grp % I::YBC;
+  const int by = lby, bx = lbx;
   const int y = by * 16 + line;
   if (by < g.nby && bx < g.nbx) {  // uniform per 16-lane group
     double Yv[16];
-    idct16_block(cf + ((long long)by * g.nbx + bx) * 256, s_q, sb, line, Yv);
+    idct16_rows(lrow, s_q, sb, line, Yv);
     if (y < g.H) {
       int wq, wt = 0;
       if constexpr (I::SY == 2) {  // cv2 INTER_LINEAR rows: wq weight 1/4, wt weight 3/4 (k_inv2)
