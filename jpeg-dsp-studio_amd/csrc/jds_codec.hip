@@ -64,11 +64,26 @@ k_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs
   const uint8_t* img = rgb + (size_t)(frame / in_div) * g.H * g.W * 3;  // sweep plans: item -> frame
 
   // 1. stage RGB (+ring, BORDER_REFLECT_101 outside the image) as packed u32
-  for (int i = tid; i < WN; i += C::TF) {
-    const int r = i / WC, c = i - r * WC;
-    const int yy = reflect101(y0 - 1 + r, g.H), xx = reflect101(x0 - 1 + c, g.W);
-    const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
-    s_rgb[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+  // (every load in flight before the first LDS store: one memory latency)
+  constexpr int NL = (WN + C::TF - 1) / C::TF;
+  {
+    uint32_t px[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      px[l] = 0u;
+      if (i < WN) {
+        const int r = i / WC, c = i - r * WC;
+        const int yy = reflect101(y0 - 1 + r, g.H), xx = reflect101(x0 - 1 + c, g.W);
+        const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
+        px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      if (i < WN) s_rgb[i] = px[l];
+    }
   }
   if (tid < 64) s_q16[tid] = fq[frame].q16[tid];
   if (tid < 50) s_hist[tid] = 0u;
@@ -79,11 +94,15 @@ k_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs
   if constexpr (CPLANE) {
     double* s_cb = s_u;
     double* s_cr = s_u + WN;
-    for (int i = tid; i < WN; i += C::TF) {
-      double R, G, B;
-      unpack(s_rgb[i], R, G, B);
-      s_cb[i] = chroma_b(R, G, B);
-      s_cr[i] = chroma_r(R, G, B);
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      if (i < WN) {
+        double R, G, B;
+        unpack(s_rgb[i], R, G, B);
+        s_cb[i] = chroma_b(R, G, B);
+        s_cr[i] = chroma_r(R, G, B);
+      }
     }
     __syncthreads();
     constexpr int NRP = WR * (WC - 2);

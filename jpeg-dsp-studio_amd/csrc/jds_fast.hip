@@ -339,13 +339,28 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   float v[8];
 
   // 1. stage the RGB window
+  // (every load in flight before the first LDS store: one memory latency)
   const bool inside = y0 - 1 >= 0 && x0 - 1 >= 0 && y0 + C::TH + 1 <= g.H && x0 + C::TW + 1 <= g.W;
-  for (int i = tid; i < WN; i += C::TF) {
-    const int r = i / WC, c = i - r * WC;
-    const int yy = inside ? y0 - 1 + r : reflect101(y0 - 1 + r, g.H);
-    const int xx = inside ? x0 - 1 + c : reflect101(x0 - 1 + c, g.W);
-    const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
-    s_rgb[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+  constexpr int NL = (WN + C::TF - 1) / C::TF;
+  {
+    uint32_t px[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      px[l] = 0u;
+      if (i < WN) {
+        const int r = i / WC, c = i - r * WC;
+        const int yy = inside ? y0 - 1 + r : reflect101(y0 - 1 + r, g.H);
+        const int xx = inside ? x0 - 1 + c : reflect101(x0 - 1 + c, g.W);
+        const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
+        px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      if (i < WN) s_rgb[i] = px[l];
+    }
   }
   __syncthreads();
 
@@ -353,11 +368,15 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   if constexpr (CPLANE) {
     float* s_cb = s_u;
     float* s_cr = s_u + WN;
-    for (int i = tid; i < WN; i += C::TF) {
-      float R, G, B;
-      unpack32(s_rgb[i], R, G, B);
-      s_cb[i] = cb32(R, G, B);
-      s_cr[i] = cr32(R, G, B);
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      if (i < WN) {
+        float R, G, B;
+        unpack32(s_rgb[i], R, G, B);
+        s_cb[i] = cb32(R, G, B);
+        s_cr[i] = cr32(R, G, B);
+      }
     }
     __syncthreads();
     constexpr int NRP = WR * (WC - 2);
