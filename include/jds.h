@@ -25,7 +25,7 @@ extern "C" {
 
 #define JDS_OK       0
 #define JDS_EINVAL  (-1)  /* bad argument                    -> ValueError   */
-#define JDS_ENOTSUP (-2)  /* e.g. block_size not 8/16, odd size -> ValueError */
+#define JDS_ENOTSUP (-2)  /* e.g. block_size not 8/16          -> ValueError   */
 #define JDS_EHIP    (-3)  /* HIP runtime / device failure     -> RuntimeError */
 #define JDS_ENOMEM  (-4)  /* device allocation failed         -> RuntimeError */
 
@@ -207,6 +207,12 @@ int jds_encode_jfif(jds_ctx* ctx, const jds_params* p, int64_t H, int64_t W, con
 int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t inverse);
 /* The same for 16x16 blocks (jds_dct16.hpp). */
 int jds_selftest_dct16x16(const double* in, double* out, int64_t n, int32_t inverse);
+
+/* Test-only: the host-built cv2 INTER_AREA table of one axis (OpenCV
+ * computeResizeAreaTab, used by the odd-size path) for src -> dst samples:
+ * per destination index its tap count n[d] (<= 4) and taps si[4d..], a[4d..].
+ * Pinned on the CPU against oracle/cpu_ref.py:area_tab. */
+int jds_selftest_area_tab(int32_t src, int32_t dst, int32_t* n, int32_t* si, double* a);
 
 #ifdef __cplusplus
 }

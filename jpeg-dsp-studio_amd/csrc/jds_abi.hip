@@ -22,7 +22,13 @@ namespace jds {
 hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                         int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
                         double* part, bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel,
-                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div);
+                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div, const GenBufs* gb);
+int area_tab_build(int src, int dst, AreaTap* tab);
+size_t gen_sub_doubles(const Geo& g);
+size_t gen_rec_doubles(const Geo& g);
+int gen_px_tiles(const Geo& g);
+hipError_t stage_area_gen(const double* in, int H, int W, const AreaTap* ytab, const AreaTap* xtab, double* out,
+                          int oh, int ow, hipStream_t s);
 hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, double c1, double c2,
                             double* scratch_planes, double* scratch_smap, double* scratch_chunks, double* out,
                             hipStream_t s);
@@ -116,6 +122,7 @@ struct jds_ctx {
   DevBuf chunks;
   DevBuf planes;  // 16x16 path: reconstructed chroma planes
   DevBuf ent[8], ent_hdr, ent_tab, ent_cf, ent_out, ent_meta;  // entropy coder (jds_encode_jfif)
+  DevBuf gen_tab, gen_sub, gen_rec;  // general-geometry path (jds_gen.hip)
 };
 
 // SSIM scratch in the context; returns the device pointer of 5 result doubles
@@ -143,6 +150,8 @@ struct jds_plan {
   DevBuf planes;  // 16x16 path: reconstructed chroma planes (n x 2 x hc x wc f64)
   double* qt = nullptr;  // host copy of the per-frame 8x8 tables (entropy headers)
   DevBuf ent[8], ent_hdr, ent_tab;  // entropy coder scratch, allocated by the first jds_plan_entropy
+  DevBuf gen_tab, gen_sub, gen_rec;  // general-geometry path (jds_gen.hip)
+  GenBufs gen() const { return {(const AreaTap*)gen_tab.p, (double*)gen_sub.p, (double*)gen_rec.p}; }
 };
 
 // ------------------------------------------------------------- geometry --
@@ -162,11 +171,19 @@ static int make_geo(const jds_params* p, int64_t H, int64_t W, Geo* g, int* mode
     return fail(JDS_EINVAL, "unsupported image size %lldx%lld", (long long)H, (long long)W);
   const int mode = p->subsampling;
   const int sy = mode == JDS_SS_420 ? 2 : 1, sx = mode == JDS_SS_444 ? 1 : 2;
-  if ((sy == 2 && (H % 2)) || (sx == 2 && (W % 2)))
-    return fail(JDS_ENOTSUP,
-                "odd image size %lldx%lld with chroma subsampling needs cv2's fractional INTER_AREA "
-                "path, which is not implemented",
-                (long long)H, (long long)W);
+  // cv2.resize(c, (W // 2, H // sy), INTER_AREA) (engines/color_space.py:42-49)
+  // asserts a non-empty destination
+  if (H / sy < 1 || W / sx < 1)
+    return fail(JDS_EINVAL,
+                "OpenCV(4.8.0) resize.cpp: error: (-215:Assertion failed) !dsize.empty() in function 'resize' "
+                "(image %lldx%lld, %s)",
+                (long long)H, (long long)W, mode == JDS_SS_420 ? "4:2:0" : "4:2:2");
+  // odd H (4:2:0) or odd W (4:2:x): cv2's fractional INTER_AREA and non-2x
+  // INTER_LINEAR -> the general-geometry kernels (jds_gen.hip)
+  const bool gen = (sy == 2 && (H % 2)) || (sx == 2 && (W % 2));
+  if (gen && B == 16)
+    return fail(JDS_ENOTSUP, "16x16 blocks with an odd %s image size (%lldx%lld) are not supported",
+                mode == JDS_SS_420 ? "4:2:0" : "4:2:2", (long long)H, (long long)W);
   Geo& G = *g;
   memset(&G, 0, sizeof G);
   G.H = (int)H;
@@ -174,6 +191,8 @@ static int make_geo(const jds_params* p, int64_t H, int64_t W, Geo* g, int* mode
   G.hc = (int)(H / sy);
   G.wc = (int)(W / sx);
   G.bs = B;
+  G.gen = gen ? 1 : 0;
+  if (gen) area_fast_scales((int)H, (int)(H / sy), (int)W, (int)(W / sx), &G.afy, &G.afx);
   G.nby = (int)((H + B - 1) / B);
   G.nbx = (int)((W + B - 1) / B);
   G.ncy = (G.hc + B - 1) / B;
@@ -243,6 +262,26 @@ static int check_tables(const jds_params* p) {
     if (p->qtable[i] != floor(p->qtable[i]))
       return fail(JDS_EINVAL, "qtable[%d] = %g is not an integer", i, p->qtable[i]);
   }
+  return JDS_OK;
+}
+
+// Area tables (y then x) and plane scratch of the general-geometry path for
+// n items of n_frames frames.
+static int gen_prepare(const Geo& g, int n_frames, int n, DevBuf& tab, DevBuf& sub, DevBuf& rec, hipStream_t s) {
+  const size_t nt = (size_t)g.hc + g.wc;
+  AreaTap* h = (AreaTap*)malloc(sizeof(AreaTap) * nt);
+  if (!h) return fail(JDS_ENOMEM, "host allocation failed");
+  if (area_tab_build(g.H, g.hc, h) < 0 || area_tab_build(g.W, g.wc, h + g.hc) < 0) {
+    free(h);
+    return fail(JDS_EINVAL, "INTER_AREA table with more than 4 taps per sample (%dx%d)", g.H, g.W);
+  }
+  hipError_t e = tab.ensure(sizeof(AreaTap) * nt);
+  if (e == hipSuccess) e = hipMemcpyAsync(tab.p, h, sizeof(AreaTap) * nt, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);  // h is freed below
+  free(h);
+  HIP_TRY(e);
+  HIP_TRY(sub.ensure(sizeof(double) * gen_sub_doubles(g) * (size_t)n_frames));
+  HIP_TRY(rec.ensure(sizeof(double) * gen_rec_doubles(g) * (size_t)n));
   return JDS_OK;
 }
 
@@ -318,6 +357,9 @@ void jds_ctx_destroy(jds_ctx* c) {
   c->ent_cf.release();
   c->ent_out.release();
   c->ent_meta.release();
+  c->gen_tab.release();
+  c->gen_sub.release();
+  c->gen_rec.release();
   for (hipEvent_t e : c->ev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -345,9 +387,10 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
   if (!hq) return fail(JDS_ENOMEM, "host allocation failed");
   for (int i = 0; i < n; ++i) {
     if (params[i].subsampling != params[0].subsampling || params[i].block_size != params[0].block_size ||
-        (params[i].prefilter != 0) != (params[0].prefilter != 0)) {
+        (params[i].prefilter != 0) != (params[0].prefilter != 0) ||
+        (pf && memcmp(params[i].gauss, params[0].gauss, sizeof params[0].gauss) != 0)) {
       free(hq);
-      return fail(JDS_EINVAL, "all frames of a plan must share subsampling / prefilter / block size");
+      return fail(JDS_EINVAL, "all frames of a plan must share subsampling / prefilter (taps) / block size");
     }
     if ((rc = check_tables(params + i))) {
       free(hq);
@@ -377,7 +420,8 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
   hipError_t e;
   if ((e = p->fq.ensure(sizeof(FrameQ) * n)) != hipSuccess || (e = p->gk.ensure(3 * sizeof(double))) != hipSuccess ||
       (e = p->part.ensure(sizeof(double) * (size_t)n *
-                          (size_t)std::max(g.tiles_y * g.tiles_x, g.bs == 16 ? inv16_tiles(mode, (int)H, (int)W) : 0))) !=
+                          (size_t)std::max(std::max(g.tiles_y * g.tiles_x, g.gen ? gen_px_tiles(g) : 0),
+                                           g.bs == 16 ? inv16_tiles(mode, (int)H, (int)W) : 0))) !=
           hipSuccess ||
       (e = hipMemcpy(p->fq.p, hq, sizeof(FrameQ) * n, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(p->gk.p, params[0].gauss, 3 * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess) {
@@ -389,7 +433,13 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
     return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
   }
   free(hq);
-  if (g.bs == 16) {
+  if (g.gen) {
+    // general geometry: exact fp64 kernels over HBM planes (jds_gen.hip)
+    if ((rc = gen_prepare(g, n_frames, n, p->gen_tab, p->gen_sub, p->gen_rec, ctx->stream))) {
+      jds_plan_destroy(p);
+      return rc;
+    }
+  } else if (g.bs == 16) {
     // 16x16 stretch path: exact fp64 kernels only (jds_b16.hip); chroma planes scratch
     if ((e = p->planes.ensure(sizeof(double) * 2 * (size_t)n * g.hc * g.wc)) != hipSuccess ||
         (e = p->counters.ensure(64)) != hipSuccess) {
@@ -445,10 +495,13 @@ int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   if (!p || !counts) return fail(JDS_EINVAL, "null argument");
   // counters[n, 2n): blocks the last run's k_fix_fwd recomputed, per item
   counts[0] = counts[1] = 0u;
-  if (p->g.bs == 16 || p->counters.n < 8 * (size_t)p->n) return JDS_OK;
+  if (p->g.bs == 16 || p->g.gen || p->counters.n < 8 * (size_t)p->n) return JDS_OK;
   uint32_t* c = (uint32_t*)malloc(4 * (size_t)p->n);
   if (!c) return fail(JDS_ENOMEM, "fix_counts: host allocation");
-  hipError_t e = hipMemcpy(c, (const uint32_t*)p->counters.p + p->n, 4 * (size_t)p->n, hipMemcpyDeviceToHost);
+  // the last run may be in flight on any stream: wait for the device first
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess)
+    e = hipMemcpy(c, (const uint32_t*)p->counters.p + p->n, 4 * (size_t)p->n, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
     free(c);
     return fail(JDS_EHIP, "fix_counts: %s", hipGetErrorString(e));
@@ -473,6 +526,14 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   int phases = (flags & JDS_RUN_FWD ? 1 : 0) | (flags & JDS_RUN_INV ? 2 : 0);
   if (!phases) phases = 3;
   const bool exact = (flags & JDS_RUN_EXACT) != 0;
+  if (p->g.gen) {  // general geometry: exact kernels only (jds_gen.hip)
+    if (phases & 1) HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
+    const GenBufs gb = p->gen();
+    HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
+                         (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
+                         nullptr, nullptr, 0, s, nullptr, phases, p->nq, &gb));
+    return JDS_OK;
+  }
   if (p->g.bs == 16) {
     if (phases & 1) {
       HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
@@ -490,7 +551,7 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
     if (exact)
       HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                            (const double*)p->gk.p, stats, (double*)p->part.p, false, nullptr, nullptr, nullptr, 0,
-                           s, nullptr, 1, p->nq));
+                           s, nullptr, 1, p->nq, nullptr));
     else
       HIP_TRY(launch_fast_fwd(p->mode, p->pf, p->g, p->n, p->nq, rgb, coeffs, (const FrameQ*)p->fq.p, p->fq32.p,
                               (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint32_t*)p->part32.p,
@@ -501,7 +562,7 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
-                         nullptr, nullptr, 0, s, nullptr, exact ? 6 : (phases == 3 ? 2 | 8 : 2), p->nq));
+                         nullptr, nullptr, 0, s, nullptr, exact ? 6 : (phases == 3 ? 2 | 8 : 2), p->nq, nullptr));
   return JDS_OK;
 }
 
@@ -520,6 +581,9 @@ void jds_plan_destroy(jds_plan* p) {
   p->part32.release();
   p->planes.release();
   p->dct32.release();
+  p->gen_tab.release();
+  p->gen_sub.release();
+  p->gen_rec.release();
   for (DevBuf& b : p->ent) b.release();
   p->ent_hdr.release();
   p->ent_tab.release();
@@ -545,7 +609,8 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
   if ((rc = check_tables(prm))) return rc;
   HIP_TRY(hipSetDevice(c->device));
   const size_t npx = (size_t)H * (size_t)W, nimg = npx * 3, ncf = (size_t)g.cpf;
-  const int tiles = std::max(g.tiles_y * g.tiles_x, g.bs == 16 ? inv16_tiles(mode, (int)H, (int)W) : 0);
+  const int tiles = std::max(std::max(g.tiles_y * g.tiles_x, g.gen ? gen_px_tiles(g) : 0),
+                             g.bs == 16 ? inv16_tiles(mode, (int)H, (int)W) : 0);
   HIP_TRY(c->rgb.ensure(nimg));
   HIP_TRY(c->out.ensure(nimg));
   HIP_TRY(c->coeffs.ensure(ncf * sizeof(int16_t)));
@@ -574,6 +639,11 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
   FrameQ hq;
   make_fq(prm, &hq);
   hipStream_t s = c->stream;
+  GenBufs gb{};
+  if (g.gen) {
+    if ((rc = gen_prepare(g, 1, 1, c->gen_tab, c->gen_sub, c->gen_rec, s))) return rc;
+    gb = {(const AreaTap*)c->gen_tab.p, (double*)c->gen_sub.p, (double*)c->gen_rec.p};
+  }
   HIP_TRY(hipMemcpyAsync(c->fq.p, &hq, sizeof hq, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(c->gk.p, prm->gauss, 3 * sizeof(double), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(c->rgb.p, rgb, nimg, hipMemcpyHostToDevice, s));
@@ -589,7 +659,7 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
   HIP_TRY(launch_codec(mode, pf, g, 1, (const uint8_t*)c->rgb.p, (uint8_t*)c->out.p, (int16_t*)c->coeffs.p,
                        (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
                        (double*)c->part.p, true, maps ? (double*)c->erry.p : nullptr,
-                       maps ? (double*)c->errrgb.p : nullptr, dsel, sel_blk, s, c->ev, 3, 1));
+                       maps ? (double*)c->errrgb.p : nullptr, dsel, sel_blk, s, c->ev, 3, 1, &gb));
   HIP_TRY(hipMemcpyAsync(rgb_out, c->out.p, nimg, hipMemcpyDeviceToHost, s));
   if (coeffs) HIP_TRY(hipMemcpyAsync(coeffs, c->coeffs.p, ncf * sizeof(int16_t), hipMemcpyDeviceToHost, s));
   if (maps) {
@@ -697,21 +767,45 @@ int jds_stage_subsample(jds_ctx* c, const double* cb, const double* cr, int64_t 
   if (!c || !cb || !cr || !cb_out || !cr_out || !gauss || H < 1 || W < 1) return fail(JDS_EINVAL, "bad argument");
   if (mode != JDS_SS_422 && mode != JDS_SS_420) return fail(JDS_EINVAL, "Unknown subsampling mode: %d", mode);
   const int sy = mode == JDS_SS_420 ? 2 : 1;
-  if ((W % 2) || (sy == 2 && (H % 2)))
-    return fail(JDS_ENOTSUP, "odd plane size needs cv2's fractional INTER_AREA path (not implemented)");
+  const int oh = (int)(H / sy), ow = (int)(W / 2);
+  if (oh < 1 || ow < 1)
+    return fail(JDS_EINVAL,
+                "OpenCV(4.8.0) resize.cpp: error: (-215:Assertion failed) !dsize.empty() in function 'resize'");
+  // odd sizes take cv2's fractional INTER_AREA path (tables as in jds_gen.hip)
+  const bool gen = (W % 2) || (sy == 2 && (H % 2));
   HIP_TRY(hipSetDevice(c->device));
-  const size_t n = (size_t)H * W, bi = n * sizeof(double), bo = (n / (2 * sy)) * sizeof(double);
+  const size_t n = (size_t)H * W, bi = n * sizeof(double), bo = (size_t)oh * ow * sizeof(double);
   void *din, *t1, *t2, *dout;
   int rc;
   if ((rc = stage_io(c, 1, nullptr, bi, &t1)) || (rc = stage_io(c, 2, nullptr, bi, &t2)) ||
       (rc = stage_io(c, 3, nullptr, bo, &dout)))
     return rc;
+  if (gen) {
+    Geo g{};
+    g.H = (int)H;
+    g.W = (int)W;
+    g.hc = oh;
+    g.wc = ow;
+    if ((rc = gen_prepare(g, 0, 0, c->gen_tab, c->gen_sub, c->gen_rec, c->stream))) return rc;
+  }
   const double* planes[2] = {cb, cr};
   double* outs[2] = {cb_out, cr_out};
   for (int p = 0; p < 2; ++p) {
     if ((rc = stage_io(c, 0, planes[p], bi, &din))) return rc;
-    HIP_TRY(stage_subsample((const double*)din, (double*)t1, (double*)t2, (double*)dout, (int)H, (int)W, sy,
-                            prefilter, gauss, c->stream));
+    if (gen) {
+      // blur (if any) as the fast path does, then the fractional area resize
+      const double* src = (const double*)din;
+      if (prefilter) {
+        HIP_TRY(stage_subsample((const double*)din, (double*)t1, (double*)t2, nullptr, (int)H, (int)W, sy, 1, gauss,
+                                c->stream));
+        src = (const double*)t2;
+      }
+      const AreaTap* tabs = (const AreaTap*)c->gen_tab.p;
+      HIP_TRY(stage_area_gen(src, (int)H, (int)W, tabs, tabs + oh, (double*)dout, oh, ow, c->stream));
+    } else {
+      HIP_TRY(stage_subsample((const double*)din, (double*)t1, (double*)t2, (double*)dout, (int)H, (int)W, sy,
+                              prefilter, gauss, c->stream));
+    }
     if ((rc = stage_out(c, outs[p], dout, bo))) return rc;
   }
   return JDS_OK;
@@ -778,6 +872,16 @@ static int ent_prepare(const Geo& g, int mode, int n, const double* qt, DevBuf* 
                        hipStream_t s) {
   if (g.bs != 8) return fail(JDS_ENOTSUP, "JPEG entropy coding needs 8x8 blocks (block_size %d)", g.bs);
   if (g.H > 65535 || g.W > 65535) return fail(JDS_ENOTSUP, "baseline JPEG is limited to 65535 x 65535");
+  if (g.gen) {
+    // T.81 sizes a subsampled component ceil(W/2) x ceil(H/sy); the reference's
+    // planes are floor-sized (cv2.resize).  The scans are valid only when both
+    // give the same block grid.
+    const int sy = mode == JDS_SS_420 ? 2 : 1;
+    const int jw = (g.W + 1) / 2, jh = (g.H + sy - 1) / sy;
+    if ((jw + 7) / 8 != g.ncx || (jh + 7) / 8 != g.ncy)
+      return fail(JDS_ENOTSUP, "%dx%d: the chroma block grid (%dx%d) differs from baseline JPEG's (%dx%d)", g.H,
+                  g.W, g.ncy, g.ncx, (jh + 7) / 8, (jw + 7) / 8);
+  }
   size_t sz[8];
   ent_sizes(g, n, sz);
   for (int i = 0; i < 8; ++i)
@@ -886,6 +990,25 @@ int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t invers
     }
     for (int i = 0; i < 64; ++i) out[64 * b + i] = t[i] * 0.0625;  // pocketfft fct = 1/16
   }
+  return JDS_OK;
+}
+
+int jds_selftest_area_tab(int32_t src, int32_t dst, int32_t* n, int32_t* si, double* a) {
+  if (src < 1 || dst < 1 || dst > src || !n || !si || !a) return fail(JDS_EINVAL, "bad argument");
+  AreaTap* t = (AreaTap*)malloc(sizeof(AreaTap) * (size_t)dst);
+  if (!t) return fail(JDS_ENOMEM, "host allocation failed");
+  if (area_tab_build(src, dst, t) < 0) {
+    free(t);
+    return fail(JDS_EINVAL, "more than 4 taps per sample");
+  }
+  for (int d = 0; d < dst; ++d) {
+    n[d] = t[d].n;
+    for (int k = 0; k < 4; ++k) {
+      si[4 * d + k] = k < t[d].n ? t[d].si[k] : -1;
+      a[4 * d + k] = k < t[d].n ? t[d].a[k] : 0.0;
+    }
+  }
+  free(t);
   return JDS_OK;
 }
 

@@ -642,12 +642,33 @@ hipError_t launch_sel_recon(const int16_t* coeffs, const FrameQ* fq, jds_selecte
 // phases: bit 0 = forward (k_fwd), bit 1 = inverse (k_inv2 + finalize),
 //         bit 2 = use the original one-block-ring k_inv for the inverse,
 //         bit 3 = finalize also adds the zero bin (the fast forward deferred it)
+hipError_t launch_gen(bool pf, const Geo& g, int n, int in_div, const uint8_t* rgb, uint8_t* rgb_out,
+                      int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st, double* part,
+                      bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel, int sel_blk,
+                      const AreaTap* tabs, double* sub, double* rec, hipStream_t s, hipEvent_t* ev, int phases);
+int gen_px_tiles(const Geo& g);
+
+// g.gen (fractional chroma resampling): the general-geometry kernels of
+// jds_gen.hip with the same tail (selected block, finalize); `gb` holds their
+// area tables and plane scratch.
 hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                         int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
                         double* part, bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel,
-                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div) {
+                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div, const GenBufs* gb) {
   hipError_t e = hipSuccess;
   const uint8_t* rin = (want_sse || err_y) ? rgb : nullptr;
+  if (g.gen) {
+    if (!gb) return hipErrorInvalidValue;
+    e = launch_gen(pf, g, n, in_div, rgb, rgb_out, coeffs, fq, gk, st, part, rin != nullptr, err_y, err_rgb, sel,
+                   sel_blk, gb->tabs, gb->sub, gb->rec, s, ev, phases & 3);
+    if (e != hipSuccess || !(phases & 2)) return e;
+    if (sel) {
+      hipLaunchKernelGGL(k_sel_dequant, dim3(1), dim3(64), 0, s, coeffs, fq, sel, sel_blk);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, gen_px_tiles(g), (int)(rin != nullptr), 0);
+    return hipGetLastError();
+  }
   if (phases & 1) {
     if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
     switch (mode) {

@@ -204,7 +204,10 @@ __device__ __forceinline__ void flag_block_list(const LaneStats& ls, bool valid,
   base = __shfl(base, __ffsll((long long)lm) - 1, 64);
   if (mine) {
     const unsigned slot = base + (unsigned)__popcll(lm & ((1ull << lane) - 1ull));
-    fixlist[(size_t)item * cap + slot] = make_uint2((unsigned)item, ((unsigned)plane << 24) | (unsigned)bidx);
+    // a list holds at most every block of its item; the bound keeps a counter
+    // left stale by an aborted run from writing past the item's list
+    if (slot < (unsigned long long)cap)
+      fixlist[(size_t)item * cap + slot] = make_uint2((unsigned)item, ((unsigned)plane << 24) | (unsigned)bidx);
   }
 }
 
@@ -820,7 +823,8 @@ k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ 
   unsigned* const fixlen = fixcount + gridDim.y;
   if (fixbits == nullptr) {  // single-quality front ends appended to the lists themselves
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-      fixlen[blockIdx.y] = fixcount[blockIdx.y];
+      const unsigned cap = (unsigned)(g.cpf / 64);
+      fixlen[blockIdx.y] = min(fixcount[blockIdx.y], cap);
       fixcount[blockIdx.y] = 0u;  // re-armed for the next run
     }
     return;

@@ -25,6 +25,40 @@ struct Geo {
   long long off_cb, off_cr;
   double up_sy, up_sx;  // cv2.resize scale (src/dst) of the chroma upsample
   int bs;               // block size: 8, or 16 (jds_b16.hip)
+  int gen;              // 1: cv2's fractional INTER_AREA applies (odd H in 4:2:0, odd W in 4:2:x):
+                        // the general-geometry kernels of jds_gen.hip run instead of the tiled ones
+  int afx, afy;         // gen: cv2's integer-scale INTER_AREA window (e.g. 3 x 2 for a 3-row 4:2:0
+                        // frame), 0 when the fractional tables apply (area_fast_scales)
+};
+
+// One destination index of cv2's fractional INTER_AREA table on one axis
+// (OpenCV computeResizeAreaTab): up to 4 source indices and their float
+// weights (as doubles), in table order.  Built on the host (area_tab_build).
+// cv::hal::resize's INTER_AREA dispatch for src -> dst on both axes: scale =
+// 1 / (dst / src); both scales integral (|scale - cvRound(scale)| < DBL_EPSILON)
+// selects resizeAreaFast.  Sets the window (fx, fy), or 0, 0 for the tables.
+inline void area_fast_scales(int src_h, int dst_h, int src_w, int dst_w, int* fy, int* fx) {
+  const double sy = 1.0 / ((double)dst_h / (double)src_h), sx = 1.0 / ((double)dst_w / (double)src_w);
+  const double ry = __builtin_rint(sy), rx = __builtin_rint(sx);
+  const double eps = 2.220446049250313e-16;
+  const bool fast = __builtin_fabs(sy - ry) < eps && __builtin_fabs(sx - rx) < eps;
+  *fy = fast ? (int)ry : 0;
+  *fx = fast ? (int)rx : 0;
+}
+
+struct AreaTap {
+  int n;
+  int si[4];
+  int pad;
+  double a[4];
+};
+
+// Device buffers of the general-geometry path: the y then x area tables
+// (hc + wc entries), fp64 subsampled chroma planes and reconstructed planes.
+struct GenBufs {
+  const AreaTap* tabs;
+  double* sub;
+  double* rec;
 };
 
 // Fix-up bitmap words per item of the certified forward path (one bit per

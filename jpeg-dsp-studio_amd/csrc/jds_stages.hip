@@ -234,6 +234,7 @@ hipError_t stage_subsample(const double* in, double* tmp, double* tmp2, double* 
     hipLaunchKernelGGL(k_stage_blur_cols, dim3(nblk(n, 256)), dim3(256), 0, s, tmp, tmp2, H, W, k[0], k[1]);
     src = tmp2;
   }
+  if (!out) return hipGetLastError();  // blur only (the fractional-area caller resizes tmp2)
   hipLaunchKernelGGL(k_stage_area, dim3(nblk((long long)(H / sy) * (W / 2), 256)), dim3(256), 0, s, src, out, H, W,
                      sy);
   return hipGetLastError();

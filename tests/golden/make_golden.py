@@ -48,8 +48,8 @@ def _install_cv2_standin():
 
     def resize(src, dsize, interpolation=1):
         w, h = dsize
-        if interpolation == 3:
-            return cpu_ref.resize_area_fast(src, src.shape[1] // w, src.shape[0] // h)
+        if interpolation == 3:  # fast integer path or fractional area path, as cv::hal::resize picks
+            return cpu_ref.resize_area(src, h, w)
         if interpolation == 1:
             return cpu_ref.resize_linear(src, h, w)
         raise NotImplementedError(interpolation)
@@ -151,6 +151,24 @@ def cases(ti):
         img = np.full((32, 48, 3), v, np.uint8)
         out.append((f'flat{v}_q50_444', img, 50, '4:4:4', False, (0, 0), True))
         out.append((f'flat{v}_q50_420_pf', img, 50, '4:2:0', True, (0, 0), True))
+    # odd sizes with chroma subsampling: cv2's fractional INTER_AREA and non-2x INTER_LINEAR
+    out += [
+        ('odd37x53_s14_q50_420_pf', rnd(37, 53, 14), 50, '4:2:0', True, (4, 6), True),
+        ('odd37x53_s14_q50_420_nopf', rnd(37, 53, 14), 50, '4:2:0', False, (1, 1), True),
+        ('odd40x37_s15_q50_422_pf', rnd(40, 37, 15), 50, '4:2:2', True, (2, 3), True),
+        ('odd40x37_s15_q50_422_nopf', rnd(40, 37, 15), 50, '4:2:2', False, (0, 0), True),
+        ('odd33x64_s16_q75_420_pf', rnd(33, 64, 16), 75, '4:2:0', True, (4, 7), True),
+        ('odd64x33_s17_q30_420_nopf', rnd(64, 33, 17), 30, '4:2:0', False, (7, 4), True),
+        ('odd64x33_s17_q30_422_pf', rnd(64, 33, 17), 30, '4:2:2', True, (3, 2), True),
+        ('odd7x9_s18_q50_420_pf', rnd(7, 9, 18), 50, '4:2:0', True, (0, 1), True),
+        ('odd9x7_s19_q95_422_pf', rnd(9, 7, 19), 95, '4:2:2', True, (1, 0), True),
+        ('odd17x17_s20_q90_420_pf', rnd(17, 17, 20), 90, '4:2:0', True, (2, 2), True),
+        ('odd17x17_s20_q5_420_nopf', rnd(17, 17, 20), 5, '4:2:0', False, (0, 0), True),
+        ('odd255x257_s21_q10_420_pf', rnd(255, 257, 21), 10, '4:2:0', True, (31, 32), True),
+        ('checker257_q50_420_pf', ti.generate_colored_checkerboard(257), 50, '4:2:0', True, (5, 5), True),
+        ('gradient131_q60_422_pf', ti.generate_gradient(131), 60, '4:2:2', True, (3, 9), True),
+        ('odd1081x1919_s13_q50_420_pf', rnd(1081, 1919, 13), 50, '4:2:0', True, (67, 119), False),
+    ]
     out += [
         ('cfg2_rand1080p_s0_q50_420_pf', rnd(1080, 1920, 0), 50, '4:2:0', True, (67, 119), False),
         ('cfg3_rand4k_s0_q10_420_nopf', rnd(2160, 3840, 0), 10, '4:2:0', False, (0, 0), False),
@@ -199,7 +217,7 @@ def main():
             for k in ('original', 'shifted', 'dct', 'quantized', 'dequantized', 'reconstructed'):
                 arrays[f'{name}/sel_{k}'] = getattr(inter, f'selected_block_{k}')
         if full:
-            if not name.startswith('rand'):
+            if not name.startswith(('rand', 'odd')):
                 arrays[f'{name}/input'] = img
             arrays[f'{name}/recon'] = rec
             arrays[f'{name}/coeffs'] = coeffs

@@ -93,8 +93,17 @@ def test_errors_map_to_reference_exceptions(L):
     g16 = _abi.geometry(_abi.make_params(50, q, '4:2:0', False, codec.gaussian_kernel3(), block_size=16), 1080, 1920)
     assert (g16.y_blocks_y, g16.y_blocks_x, g16.c_blocks_y, g16.c_blocks_x) == (68, 120, 34, 60)
     assert g16.coeffs_per_frame == 256 * (68 * 120 + 2 * 34 * 60)
-    with pytest.raises(ValueError, match='odd image size'):
-        _abi.geometry(_abi.make_params(50, q, '4:2:0', False, codec.gaussian_kernel3()), 63, 64)
+    # odd sizes with subsampling: cv2's floor-sized chroma planes (engines/color_space.py:42-49)
+    g = _abi.geometry(_abi.make_params(50, q, '4:2:0', False, codec.gaussian_kernel3()), 63, 65)
+    assert (g.chroma_h, g.chroma_w, g.y_blocks_y, g.y_blocks_x, g.c_blocks_y, g.c_blocks_x) == (31, 32, 8, 9, 4, 4)
+    g = _abi.geometry(_abi.make_params(50, q, '4:2:2', False, codec.gaussian_kernel3()), 17, 17)
+    assert (g.chroma_h, g.chroma_w, g.c_blocks_y, g.c_blocks_x) == (17, 8, 3, 1)
+    # an empty chroma plane is cv2.resize's !dsize.empty() assertion in the reference
+    for h, w, mode in ((1, 64, '4:2:0'), (64, 1, '4:2:2')):
+        with pytest.raises(ValueError, match='dsize.empty'):
+            _abi.geometry(_abi.make_params(50, q, mode, False, codec.gaussian_kernel3()), h, w)
+    with pytest.raises(ValueError, match='16x16 blocks with an odd'):
+        _abi.geometry(_abi.make_params(50, q, '4:2:0', False, codec.gaussian_kernel3(), block_size=16), 63, 64)
     # 4:4:4 takes any size
     assert _abi.geometry(_abi.make_params(50, q, '4:4:4', False, codec.gaussian_kernel3()), 63, 65).tiles > 0
 
@@ -149,3 +158,24 @@ def test_struct_layouts_match_the_c_header(tmp_path):
         for fname, _ in py._fields_:
             assert int(got[f'{cname}.{fname}']) == getattr(py, fname).offset, (cname, fname)
     assert _abi.STATS_DTYPE.itemsize == C.sizeof(_abi.FrameStats)
+
+
+@pytest.mark.parametrize('src', [3, 5, 7, 9, 17, 37, 53, 255, 257, 1081, 1919, 2161, 4095, 40, 1080])
+def test_area_table_matches_oracle(L, src):
+    """The host-built cv2 INTER_AREA table (jds_gen.hip area_tab_build, OpenCV
+    computeResizeAreaTab) equals the oracle's restatement tap for tap."""
+    for dst in sorted({src // 2, src}):
+        n = np.zeros(dst, np.int32)
+        si = np.zeros(4 * dst, np.int32)
+        a = np.zeros(4 * dst, np.float64)
+        assert L.jds_selftest_area_tab(src, dst, n.ctypes.data, si.ctypes.data, a.ctypes.data) == 0
+        di_r, si_r, a_r = cpu_ref.area_tab(src, dst)
+        k = 0
+        for d in range(dst):
+            for t in range(n[d]):
+                assert di_r[k] == d and si_r[k] == si[4 * d + t] and a_r[k] == a[4 * d + t], (src, dst, d, t)
+                k += 1
+        assert k == len(di_r)
+        # weights sum to 1 up to the partial cells OpenCV drops (< 1e-3 of a source sample)
+        sums = np.bincount(di_r, weights=a_r, minlength=dst)
+        assert np.allclose(sums, 1.0, atol=1e-3)

@@ -92,7 +92,11 @@ def check_geometry(H, W, mode):
 def sizes():
     out = set()
     for v in golden().values():
-        out.add((v['shape'][0], v['shape'][1], v['mode']))
+        h, w, mode = v['shape'][0], v['shape'][1], v['mode']
+        # odd sizes with subsampling run the untiled general-geometry kernels (jds_gen.hip)
+        if (mode != '4:4:4' and w % 2) or (mode == '4:2:0' and h % 2):
+            continue
+        out.add((h, w, mode))
     rng = np.random.default_rng(0)
     for _ in range(60):
         mode = ('4:4:4', '4:2:2', '4:2:0')[rng.integers(3)]
