@@ -8,7 +8,8 @@
 // real forward FFT (radf4 then radf2).  Its twiddles come from its own
 // sincos_2pibyn tables and are NOT all correctly rounded; the constants below
 // are the exact doubles pocketfft uses (found by bit-exact search against
-// SciPy 1.15.3 / 1.7.1, pinned by tests/test_device_math.py).
+// SciPy 1.15.3 / 1.7.1, pinned by tests/test_abi_cpu.py::
+// test_device_dct_expressions_bit_exact_vs_scipy).
 //
 // Every expression below is one IEEE operation, evaluated in pocketfft's
 // order; the translation unit is compiled with FP contraction OFF so no FMA is

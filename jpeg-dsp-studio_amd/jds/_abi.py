@@ -188,7 +188,8 @@ _tls = threading.local()
 
 
 def context(device: int = 0) -> Context:
-    """Per-thread, per-device context (the ABI is re-entrant per ctx)."""
+    """Per-thread, per-device context for long-lived owners (plans, benches):
+    the ABI is re-entrant per ctx."""
     ctxs = getattr(_tls, 'ctxs', None)
     if ctxs is None:
         ctxs = _tls.ctxs = {}
@@ -196,6 +197,51 @@ def context(device: int = 0) -> Context:
     if c is None:
         c = ctxs[device] = Context(device)
     return c
+
+
+# Contexts for single calls (engines.compress_reconstruct and the per-stage
+# API).  The reference's callers run the pipeline from short-lived worker
+# threads -- one QThread per run (gui/worker.py:10-36), concurrently from
+# dialogs (gui/dialogs/aliasing_demo_dialog.py:158, report_exporter.py:107) --
+# so a context per thread would create a HIP stream and grow device scratch on
+# every run.  A call leases an idle context of its device for its duration
+# instead: concurrent calls get distinct contexts (streams, scratch), and the
+# next thread reuses the warm one.
+_POOL_MAX = 8
+_pool: dict = {}
+_pool_lock = threading.Lock()
+
+
+class lease:
+    """`with lease(device) as ctx:` -- exclusive use of a pooled Context."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self.ctx = None
+
+    def __enter__(self) -> Context:
+        with _pool_lock:
+            free = _pool.setdefault(self.device, [])
+            self.ctx = free.pop() if free else None
+        if self.ctx is None:
+            self.ctx = Context(self.device)
+        return self.ctx
+
+    def __exit__(self, *exc):
+        c, self.ctx = self.ctx, None
+        with _pool_lock:
+            free = _pool.setdefault(self.device, [])
+            if len(free) < _POOL_MAX:
+                free.append(c)
+                c = None
+        if c is not None:
+            c.close()
+        return False
+
+
+def pool_size(device: int = 0) -> int:
+    with _pool_lock:
+        return len(_pool.get(device, []))
 
 
 def make_params(quality: int, qtable: np.ndarray, mode: str, prefilter: bool, gauss: np.ndarray,

@@ -14,7 +14,7 @@ from typing import Dict, Tuple
 import numpy as np
 
 from . import _abi
-from ._abi import check, context, lib, make_params
+from ._abi import check, lease, lib, make_params
 
 
 def gaussian_kernel3(sigma: float = 0.75) -> np.ndarray:
@@ -48,7 +48,6 @@ def compress_reconstruct_raw(image: np.ndarray, quality: int, qtable: np.ndarray
     H, W = img.shape[:2]
     p = make_params(quality, qtable, mode, prefilter, gaussian_kernel3(0.75), block_size)
     geo = _abi.geometry(p, H, W)
-    ctx = context(device)
     out = np.empty_like(img)
     coeffs = np.empty(geo.coeffs_per_frame, dtype=np.int16)
     st = _abi.FrameStats()
@@ -56,10 +55,11 @@ def compress_reconstruct_raw(image: np.ndarray, quality: int, qtable: np.ndarray
     er = np.empty((H, W), np.float64) if maps else None
     sel = _abi.SelectedBlock()
     sel_ok = C.c_int32(0)
-    check(lib().jds_compress_reconstruct(
-        ctx.handle, C.byref(p), img.ctypes.data, H, W, out.ctypes.data, coeffs.ctypes.data, C.byref(st),
-        ey.ctypes.data if maps else None, er.ctypes.data if maps else None,
-        int(selected_block_idx[0]), int(selected_block_idx[1]), C.byref(sel), C.byref(sel_ok)))
+    with lease(device) as ctx:
+        check(lib().jds_compress_reconstruct(
+            ctx.handle, C.byref(p), img.ctypes.data, H, W, out.ctypes.data, coeffs.ctypes.data, C.byref(st),
+            ey.ctypes.data if maps else None, er.ctypes.data if maps else None,
+            int(selected_block_idx[0]), int(selected_block_idx[1]), C.byref(sel), C.byref(sel_ok)))
     res: Dict[str, object] = {'reconstructed': out, 'coeffs': coeffs, 'stats': st, 'geometry': geo,
                               'error_map_y': ey, 'error_map_rgb': er, 'selected': None}
     if sel_ok.value:
@@ -78,8 +78,8 @@ def psnr_ssim_raw(a: np.ndarray, b: np.ndarray, device: int = 0) -> np.ndarray:
     if a.shape != b.shape:
         raise ValueError('Input images must have the same dimensions.')
     out = np.empty(6, np.float64)
-    check(lib().jds_psnr_ssim(context(device).handle, a.ctypes.data, b.ctypes.data, a.shape[0], a.shape[1],
-                              out.ctypes.data))
+    with lease(device) as ctx:
+        check(lib().jds_psnr_ssim(ctx.handle, a.ctypes.data, b.ctypes.data, a.shape[0], a.shape[1], out.ctypes.data))
     return out
 
 
@@ -95,7 +95,8 @@ def stage_rgb_ycbcr(x: np.ndarray, inverse: bool) -> np.ndarray:
         raise IndexError('index 2 is out of bounds for axis 2')
     out = np.empty_like(x)
     fn = lib().jds_stage_ycbcr_to_rgb if inverse else lib().jds_stage_rgb_to_ycbcr
-    check(fn(context().handle, x.ctypes.data, out.ctypes.data, x.size // 3))
+    with lease() as ctx:
+        check(fn(ctx.handle, x.ctypes.data, out.ctypes.data, x.size // 3))
     return out
 
 
@@ -106,17 +107,19 @@ def stage_subsample(cb: np.ndarray, cr: np.ndarray, mode: str, prefilter: bool):
     ocb = np.empty((oh, W // 2), np.float64)
     ocr = np.empty((oh, W // 2), np.float64)
     g = gaussian_kernel3(0.75)
-    check(lib().jds_stage_subsample(context().handle, cb.ctypes.data, cr.ctypes.data, H, W,
-                                    _abi.MODE_CODES[mode], 1 if prefilter else 0, g.ctypes.data,
-                                    ocb.ctypes.data, ocr.ctypes.data))
+    with lease() as ctx:
+        check(lib().jds_stage_subsample(ctx.handle, cb.ctypes.data, cr.ctypes.data, H, W,
+                                        _abi.MODE_CODES[mode], 1 if prefilter else 0, g.ctypes.data,
+                                        ocb.ctypes.data, ocr.ctypes.data))
     return ocb, ocr
 
 
 def stage_resize(x: np.ndarray, H: int, W: int, nearest: bool) -> np.ndarray:
     x = _f64(x)
     out = np.empty((H, W), np.float64)
-    check(lib().jds_stage_upsample(context().handle, x.ctypes.data, x.shape[0], x.shape[1], H, W,
-                                   1 if nearest else 0, out.ctypes.data))
+    with lease() as ctx:
+        check(lib().jds_stage_upsample(ctx.handle, x.ctypes.data, x.shape[0], x.shape[1], H, W,
+                                       1 if nearest else 0, out.ctypes.data))
     return out
 
 
@@ -127,7 +130,8 @@ def stage_block(x: np.ndarray, op: int) -> np.ndarray:
         raise ValueError(f'the MI355X block transforms are 8x8 and 16x16 (got {x.shape})')
     b = x.shape[-1]
     out = np.empty_like(x)
-    check(lib().jds_stage_block_dct_n(context().handle, x.ctypes.data, out.ctypes.data, x.size // (b * b), b, op))
+    with lease() as ctx:
+        check(lib().jds_stage_block_dct_n(ctx.handle, x.ctypes.data, out.ctypes.data, x.size // (b * b), b, op))
     return out
 
 
@@ -143,6 +147,7 @@ def stage_quant(x: np.ndarray, q: np.ndarray, dequant: bool) -> np.ndarray:
     else:
         x = _f64(x)
         out = np.empty(x.shape, np.int16)
-    check(lib().jds_stage_quantize_n(context().handle, x.ctypes.data, q.ctypes.data, q.size, out.ctypes.data,
-                                     x.size, 1 if dequant else 0))
+    with lease() as ctx:
+        check(lib().jds_stage_quantize_n(ctx.handle, x.ctypes.data, q.ctypes.data, q.size, out.ctypes.data,
+                                         x.size, 1 if dequant else 0))
     return out

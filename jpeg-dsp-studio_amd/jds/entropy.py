@@ -10,7 +10,7 @@ from typing import List, Tuple
 import numpy as np
 
 from . import _abi
-from ._abi import check, context, lib, make_params
+from ._abi import check, lib, make_params
 
 
 def encode_jfif(coeffs: np.ndarray, H: int, W: int, mode: str, qtable: np.ndarray,
@@ -28,8 +28,9 @@ def encode_jfif(coeffs: np.ndarray, H: int, W: int, mode: str, qtable: np.ndarra
     cap = max(1 << 16, 8 * cf.size)
     while True:
         out = np.empty(cap, np.uint8)
-        rc = lib().jds_encode_jfif(context(device).handle, C.byref(p), H, W, cf.ctypes.data, out.ctypes.data,
-                                   cap, C.byref(n), bits)
+        with _abi.lease(device) as ctx:
+            rc = lib().jds_encode_jfif(ctx.handle, C.byref(p), H, W, cf.ctypes.data, out.ctypes.data,
+                                       cap, C.byref(n), bits)
         if rc == _abi.JDS_EINVAL and n.value > cap:
             cap = n.value
             continue

@@ -50,15 +50,10 @@ class Timer:
         return result
 
 
-def bitrate_from_counts(nonzero: int, magnitude_bits, total_coeffs: int, original_shape: tuple,
-                        block_size: int = 8) -> Dict:
-    """The tail of estimate_bitrate_no_entropy (utils/metrics.py:62-92) from counts.
-
-    The reference sums ceil(log2(|q|+1)) + 1 as float32 (np.log2 of int16):
-    `magnitude_bits` is that float32 sum (the GPU reproduces NumPy's buffered
-    float32 reduction; below 2**24 it equals the exact integer).  Evaluating
-    the reference's expression with that np.float32 scalar reproduces its
-    NumPy-version-dependent promotion (float32 under NumPy >= 2, float64 under 1.x)."""
+def _bitrate_tail(coeff_bits, nonzero: int, total_coeffs: int, original_shape: tuple, block_size: int) -> Dict:
+    """utils/metrics.py:62-70 and :83-92: block overhead, totals and the dict,
+    with `coeff_bits` kept in whatever NumPy type the caller's sum produced
+    (the reference's promotion decides the float32 / float64 result)."""
     h, w = original_shape
     num_pixels = h * w
     original_bits = num_pixels * 3 * 8
@@ -66,11 +61,6 @@ def bitrate_from_counts(nonzero: int, magnitude_bits, total_coeffs: int, origina
     padded_w = ((w + block_size - 1) // block_size) * block_size
     num_blocks = (padded_h // block_size) * (padded_w // block_size)
     block_overhead_bits = num_blocks * 2
-    if nonzero > 0:
-        position_bits = 6 * int(nonzero)
-        coeff_bits = position_bits + np.float32(magnitude_bits)
-    else:
-        coeff_bits = 0
     estimated_bits = block_overhead_bits + coeff_bits
     return {
         'estimated_bits': int(estimated_bits),
@@ -82,14 +72,37 @@ def bitrate_from_counts(nonzero: int, magnitude_bits, total_coeffs: int, origina
     }
 
 
+def bitrate_from_counts(nonzero: int, magnitude_bits, total_coeffs: int, original_shape: tuple,
+                        block_size: int = 8) -> Dict:
+    """The tail of estimate_bitrate_no_entropy (utils/metrics.py:62-92) from the
+    pipeline's GPU counts.
+
+    The pipeline's coefficients are int16, for which the reference sums
+    ceil(log2(|q|+1)) + 1 as float32 (np.log2 of int16 is float32):
+    `magnitude_bits` is that float32 sum (k_mag_f32 reproduces NumPy's buffered
+    pairwise float32 reduction; below 2**24 it equals the exact integer).
+    Evaluating the reference's expression with that np.float32 scalar reproduces
+    its NumPy-version-dependent promotion (float32 under NumPy >= 2, float64
+    under 1.x)."""
+    coeff_bits = 6 * int(nonzero) + np.float32(magnitude_bits) if nonzero > 0 else 0
+    return _bitrate_tail(coeff_bits, nonzero, total_coeffs, original_shape, block_size)
+
+
 def estimate_bitrate_no_entropy(quantized_coeffs: np.ndarray, original_shape: tuple, block_size: int = 8) -> Dict:
     """Estimate compressed size WITHOUT entropy coding (utils/metrics.py:51-92).
 
     Per nonzero coefficient: 6 position bits + ceil(log2(|c|+1)) + 1 magnitude
-    bits; plus 2 bits per luma block."""
+    bits; plus 2 bits per luma block.  A standalone host utility on a NumPy
+    array (the pipeline itself uses the GPU counts, bitrate_from_counts): the
+    magnitude sum is the reference's own NumPy expression on the caller's
+    array, so its dtype rules hold -- float32 accumulation (pairwise order) for
+    int8/int16 input, float64 for int32/int64, wrap-around of |int16 min|."""
     q = np.asarray(quantized_coeffs)
-    nz = q[q != 0].astype(np.int64)
-    mags = np.abs(nz)
-    # ceil(log2(m + 1)) == bit_length(m) for integers m >= 1
-    magnitude_bits = int(np.sum(np.frexp(mags.astype(np.float64))[1] + 1)) if nz.size else 0
-    return bitrate_from_counts(int(nz.size), magnitude_bits, int(q.size), original_shape, block_size)
+    mask = q != 0
+    nz = q[mask]
+    if len(nz) > 0:
+        mags = np.abs(nz)
+        coeff_bits = 6 * len(nz) + np.sum(np.ceil(np.log2(mags + 1)) + 1)
+    else:
+        coeff_bits = 0
+    return _bitrate_tail(coeff_bits, int(np.sum(mask)), int(q.size), original_shape, block_size)

@@ -1,7 +1,7 @@
 """Synthetic test-image generators (utils/test_images.py:6-178 of the reference).
 
 Vectorised restatements producing byte-identical images (pinned against the
-reference's own outputs in tests/test_dropin_cpu.py).
+reference's own outputs in tests/test_host_utils_cpu.py).
 """
 
 from typing import Optional

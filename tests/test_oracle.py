@@ -78,3 +78,14 @@ def test_quant_tables_at_sweep_qualities():
         t = cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q)
         assert (t.min(), t.max(), int((t == 255).sum()), int((t == 1).sum())) == (lo, hi, n255, n1)
     assert np.all(cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, 100) == 1)
+
+
+@pytest.mark.parametrize('mode,pf', [('4:2:0', True), ('4:2:2', False), ('4:4:4', False)])
+def test_faithful_per_block_loop_equals_vectorised(mode, pf):
+    """bench.py's 'faithful' CPU baseline (per-block scipy calls, the
+    reference's loop structure) computes the same outputs as the batched oracle."""
+    img = cpu_ref.random_image(72, 104, 11)
+    a = cpu_ref.compress_reconstruct_faithful(img, 40, mode, pf)
+    b = cpu_ref.compress_reconstruct(img, 40, 8, mode, pf, metrics=False)
+    assert np.array_equal(a['coeffs'], b['coeffs'])
+    assert np.array_equal(a['reconstructed'], b['reconstructed'])
