@@ -39,6 +39,10 @@ extern "C" {
 #define JDS_RUN_FWD 2u  /* forward phase only (stats reset + k_fwd); with neither FWD nor INV: both */
 #define JDS_RUN_INV 4u  /* inverse phase only (k_inv + finalize); needs the forward's coeffs/stats */
 #define JDS_RUN_EXACT 8u /* all-fp64 kernels (default: certified fp32 + exact fp64 fix-up, same results) */
+#define JDS_RUN_EXACT_INV 16u /* inverse only: the replayed-order fp64 kernel instead of the certified fast
+                                 inverse + tile fix-up (same bytes; A/B and tests) */
+#define JDS_RUN_INV_FIXALL 32u /* test: the certified fast inverse lists every tile, so the exact
+                                  list kernel recomputes the whole frame (exercises the fix-up path) */
 
 typedef struct jds_ctx jds_ctx;    /* one per (thread, device): owns a HIP stream + scratch */
 typedef struct jds_plan jds_plan;  /* fixed geometry + per-frame quant tables, device-resident */
@@ -128,7 +132,8 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
 int jds_plan_run(jds_plan* plan, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs,
                  jds_frame_stats* stats, uint32_t flags, void* stream);
 int jds_plan_geometry(const jds_plan* plan, jds_geometry* out);
-/* Entries the last run's fix-up lists received: [0] forward blocks, [1] inverse pixels. */
+/* Entries the last run's fix-up lists received: [0] forward blocks recomputed exactly (k_fix_fwd),
+   [1] inverse tiles the certified fast inverse handed to the exact kernel (k_inv2_list). */
 int jds_plan_fix_counts(const jds_plan* plan, uint32_t* counts);
 void jds_plan_destroy(jds_plan* plan);
 

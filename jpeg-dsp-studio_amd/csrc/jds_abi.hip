@@ -22,7 +22,9 @@ namespace jds {
 hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                         int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
                         double* part, bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel,
-                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div, const GenBufs* gb);
+                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div, const GenBufs* gb,
+                        const InvFix* fx = nullptr);
+int inv_tiles(int mode, int H, int W);
 int area_tab_build(int src, int dst, AreaTap* tab);
 size_t gen_sub_doubles(const Geo& g);
 size_t gen_rec_doubles(const Geo& g);
@@ -146,6 +148,10 @@ struct jds_plan {
   DevBuf fq, gk, part;
   // fast path: fp32 tables, fix-up lists and counters
   DevBuf fq32, gk32, fixbits, fixlist, counters, part32;  // per-item fix-up bitmaps and lists; per-tile statistics
+  DevBuf invfix;  // certified fast inverse: [count | (frame, tile) list] (jds_inv_fast.hip)
+  InvFix inv_fix() const {
+    return {(uint2*)((char*)invfix.p + 64), (unsigned*)invfix.p, 0};
+  }
   Side side;  // border tiles run beside interior tiles
   DevBuf planes;  // 16x16 path: reconstructed chroma planes (n x 2 x hc x wc f64)
   double* qt = nullptr;  // host copy of the per-frame 8x8 tables (entropy headers)
@@ -465,6 +471,8 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
         (e = p->fixlist.ensure(8 * nblk)) != hipSuccess ||
         (e = p->counters.ensure(8 * (size_t)n + 64)) != hipSuccess ||
         (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * ptiles)) != hipSuccess ||
+        (e = p->invfix.ensure(64 + 8 * (size_t)n * (size_t)inv_tiles(mode, (int)H, (int)W))) != hipSuccess ||
+        (e = hipMemset(p->invfix.p, 0, 64)) != hipSuccess ||
         (n_q > 1 && (e = p->dct32.ensure(sizeof(float) * (size_t)n_frames * g.cpf)) != hipSuccess) ||
         (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess ||
@@ -493,20 +501,23 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
 
 int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   if (!p || !counts) return fail(JDS_EINVAL, "null argument");
-  // counters[n, 2n): blocks the last run's k_fix_fwd recomputed, per item
+  // counters[n, 2n): blocks the last run's k_fix_fwd recomputed, per item;
+  // invfix[0]: tiles the last run's certified inverse handed to the exact kernel
   counts[0] = counts[1] = 0u;
   if (p->g.bs == 16 || p->g.gen || p->counters.n < 8 * (size_t)p->n) return JDS_OK;
-  uint32_t* c = (uint32_t*)malloc(4 * (size_t)p->n);
+  uint32_t* c = (uint32_t*)malloc(4 * (size_t)p->n + 4);
   if (!c) return fail(JDS_ENOMEM, "fix_counts: host allocation");
   // the last run may be in flight on any stream: wait for the device first
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess)
     e = hipMemcpy(c, (const uint32_t*)p->counters.p + p->n, 4 * (size_t)p->n, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && p->invfix.p) e = hipMemcpy(c + p->n, p->invfix.p, 4, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
     free(c);
     return fail(JDS_EHIP, "fix_counts: %s", hipGetErrorString(e));
   }
   for (int i = 0; i < p->n; ++i) counts[0] += c[i];
+  counts[1] = p->invfix.p ? c[p->n] : 0u;
   free(c);
   return JDS_OK;
 }
@@ -559,10 +570,14 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
                               (float*)p->dct32.p, s, &p->side,
                               phases == 1));  // forward + inverse: k_finalize adds the zero bin
   }
+  InvFix fx = p->inv_fix();
+  fx.fix_all = (flags & JDS_RUN_INV_FIXALL) ? 1 : 0;
+  const bool exact_inv = exact || (flags & JDS_RUN_EXACT_INV) != 0;
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
-                         nullptr, nullptr, 0, s, nullptr, exact ? 6 : (phases == 3 ? 2 | 8 : 2), p->nq, nullptr));
+                         nullptr, nullptr, 0, s, nullptr, exact ? 6 : (phases == 3 ? 2 | 8 : 2), p->nq, nullptr,
+                         exact_inv || !p->invfix.p ? nullptr : &fx));
   return JDS_OK;
 }
 
@@ -579,6 +594,7 @@ void jds_plan_destroy(jds_plan* p) {
   p->counters.release();
   p->fixbits.release();
   p->part32.release();
+  p->invfix.release();
   p->planes.release();
   p->dct32.release();
   p->gen_tab.release();

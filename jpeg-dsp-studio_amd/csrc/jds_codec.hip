@@ -633,6 +633,9 @@ static hipError_t launch_inv_t(const Geo& g, int n, const int16_t* coeffs, const
 }
 
 int inv_tiles(int mode, int H, int W);
+hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
+                           const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part,
+                           const InvFix& fx, hipStream_t s, int in_div);
 hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
                        const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y,
                        double* err_rgb, hipStream_t s, int in_div);
@@ -654,7 +657,8 @@ int gen_px_tiles(const Geo& g);
 hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                         int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
                         double* part, bool want_sse, double* err_y, double* err_rgb, jds_selected_block* sel,
-                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div, const GenBufs* gb) {
+                        int sel_blk, hipStream_t s, hipEvent_t* ev, int phases, int in_div, const GenBufs* gb,
+                        const InvFix* fx) {
   hipError_t e = hipSuccess;
   const uint8_t* rin = (want_sse || err_y) ? rgb : nullptr;
   if (g.gen) {
@@ -690,7 +694,12 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
   if (phases & 2) {
     int tiles = g.tiles_y * g.tiles_x;
     if (!(phases & 4)) {  // jds_inv.hip (default); bit 2 selects the original k_inv
-      e = launch_inv2(mode, g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, s, in_div);
+      // certified fast inverse + exact fix-up of listed tiles (jds_inv_fast.hip)
+      // unless the caller wants the exact kernels or the IntermediateData maps
+      if (fx && !err_y)
+        e = launch_inv_fast(mode, g, n, coeffs, fq, rin, rgb_out, st, part, *fx, s, in_div);
+      else
+        e = launch_inv2(mode, g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, s, in_div);
       tiles = inv_tiles(mode, g.H, g.W);
     } else switch (mode) {
       case M420:

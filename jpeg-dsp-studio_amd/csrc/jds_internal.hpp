@@ -72,6 +72,14 @@ struct Side {
   hipEvent_t fork = nullptr, join = nullptr;
 };
 
+// Tile fix-up list of the certified fast inverse (jds_inv_fast.hip): (frame,
+// tile) pairs the exact inverse recomputes; `count` is reset by each run.
+struct InvFix {
+  uint2* list;
+  unsigned* count;
+  int fix_all;  // test: list every tile
+};
+
 // Per-frame quantiser: q16 = 16*Q (pocketfft's first-axis fct = 1/16 folded in), q = Q.
 struct FrameQ {
   double q16[64];

@@ -28,39 +28,11 @@
 #include "jds_dct8.hpp"
 #include "jds_device.hpp"
 #include "jds_internal.hpp"
+#include "jds_inv_common.hpp"
 
 #pragma clang fp contract(off)
 
 namespace jds {
-
-template <int MODE>
-struct Inv {
-  static constexpr int SY = Cfg<MODE>::SY, SX = Cfg<MODE>::SX;
-  static constexpr int TH = (MODE == M420) ? 64 : 32;
-  static constexpr int TW = (MODE == M444) ? 64 : 128;
-  static constexpr int NT = (MODE == M444) ? 256 : 512;
-  static constexpr int RY = (SY == 2) ? 1 : 0, RX = (SX == 2) ? 1 : 0;
-  static constexpr int YBC = TW / 8, NYB = (TH / 8) * YBC;
-  static constexpr int RB = NT / 8;                                        // luma blocks per round
-  static constexpr int CBR = TH / (8 * SY) + 2 * RY, CBC = TW / (8 * SX) + 2 * RX;  // chroma blocks incl. ring
-  static constexpr int NCB = CBR * CBC;                                    // per plane
-  static constexpr int CWR = TH / SY + 2 * RY, CWC = TW / SX + 2 * RX;     // chroma sample window
-  static constexpr int NROW = (CBR - 2 * RY) * CBC * 8 + 2 * RY * CBC;     // chroma row tasks per plane
-  static constexpr int MB = NCB > RB ? NCB : RB;                           // transpose-buffer blocks
-  static constexpr int WPE = (MODE == M444) ? 3 : 4;                       // 2 or 3 workgroups per CU
-  static_assert(NCB * 8 <= NT && NROW <= NT && NYB % RB == 0, "one round per chroma plane");
-};
-
-constexpr int MS = 72;  // doubles per block in the transpose buffer (64 + 8: conflict-free column writes)
-
-// Transpose-buffer slot of element (r, c) of a block: the 16-B pair c/2 of row r
-// is stored at pair (c/2) ^ (r & 3).  Column passes (lane c writes row r) still
-// fill each row's 64 B with two blocks per 16-lane ds_write_b64 group on
-// disjoint banks; row passes (lane r reads row r as 4 x ds_read_b128) then put
-// the 4 lanes of every 16-lane group that share a 64-B window (MS*8 = 576 B
-// shifts blocks by 16 banks) on 4 different 16-B slots: conflict-free instead
-// of 4-way (MI355X_MICROARCH.md §LDS bank rules).
-__device__ __forceinline__ int tslot(int r, int c) { return r * 8 + ((((c >> 1) ^ (r & 3)) << 1) | (c & 1)); }
 
 // Dequantize (quantizer.py:27-29) and IDCT column v of a block (axis 0 first,
 // dct_engine.py:12-14) into dst[r*8 + v].  `qi` holds the integer table Q:
@@ -79,20 +51,6 @@ __device__ __forceinline__ void idct_col(const int16_t* __restrict__ blk, const 
   for (int r = 0; r < 8; ++r) dst[tslot(r, v)] = c[r];
 }
 
-// The same with the column's coefficients already loaded (software
-// prefetch: the loads of the next block are issued before this one's math).
-struct Col16 {
-  int16_t q[8];
-};
-// Blocks outside the grid (`ok` false) read block 0 of the plane instead: the
-// caller never transforms them, and unmasked loads need no per-load branches.
-__device__ __forceinline__ Col16 load_col(const int16_t* __restrict__ plane, long long boff, int v, bool ok) {
-  const int16_t* blk = plane + (ok ? boff : 0ll);
-  Col16 c;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) c.q[r] = blk[r * 8 + v];
-  return c;
-}
 __device__ __forceinline__ void idct_col(const Col16& in, const int* __restrict__ qi, int v,
                                          double* __restrict__ dst) {
   double c[8];
@@ -192,20 +150,33 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
 //       2 = + IntermediateData error maps (pipeline.py:117-122)
 // (XTRA = 2 is the single-frame host path: it trades occupancy for registers
 // rather than spill to scratch)
+// One tile (frame, tile) of the exact inverse; `ntiles` = tiles per frame (the
+// luma-SSE partials are per tile).  The caller's shared arrays are reused
+// tile after tile by the list form.
 template <int MODE, int XTRA>
-__global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(XTRA > 1 ? 2 : Inv<MODE>::WPE)))
-k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
-       const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
-       double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb, const int in_div) {
+struct InvShared {
+  double mid[Inv<MODE>::MB * MS];
+  double cw[2][Inv<MODE>::CWR * Inv<MODE>::CWC];
+  int q[64];  // integer quantiser table Q
+  double red[Inv<MODE>::NT / 64];
+  unsigned long long sse;
+};
+
+template <int MODE, int XTRA>
+__device__ __forceinline__ void inv2_tile(InvShared<MODE, XTRA>& sh, const Geo& g, const int tiles_x, const int ntiles,
+                                          const int frame, const int tile, const int16_t* __restrict__ coeffs,
+                                          const FrameQ* __restrict__ fq, const uint8_t* __restrict__ rgb_in,
+                                          uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
+                                          double* __restrict__ sse_y_part, double* __restrict__ err_y,
+                                          double* __restrict__ err_rgb, const int in_div) {
   using I = Inv<MODE>;
-  __shared__ __attribute__((aligned(16))) double s_mid[I::MB * MS];
-  __shared__ __attribute__((aligned(16))) double s_cw[2][I::CWR * I::CWC];
-  __shared__ int s_q[64];  // integer quantiser table Q
-  __shared__ double s_red[I::NT / 64];
-  __shared__ unsigned long long s_sse;
+  double* s_mid = sh.mid;
+  double (*s_cw)[I::CWR * I::CWC] = sh.cw;
+  int* s_q = sh.q;
+  double* s_red = sh.red;
+  unsigned long long& s_sse = sh.sse;
 
   const int tid = threadIdx.x, lv = tid & 7, lb = tid >> 3;
-  const int frame = blockIdx.y, tile = blockIdx.x;
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int Y0 = ty * I::TH, X0 = tx * I::TW;
   const int16_t* cf = coeffs + (size_t)frame * g.cpf;
@@ -405,9 +376,38 @@ k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const
     if (tid == 0) {
       double a = 0.0;
       for (int i = 0; i < I::NT / 64; ++i) a = a + s_red[i];
-      sse_y_part[(size_t)frame * gridDim.x + tile] = a;
+      sse_y_part[(size_t)frame * ntiles + tile] = a;
       atomicAdd((unsigned long long*)&st[frame].sse_rgb, s_sse);
     }
+  }
+}
+
+template <int MODE, int XTRA>
+__global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(XTRA > 1 ? 2 : Inv<MODE>::WPE)))
+k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+       const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
+       double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb, const int in_div) {
+  __shared__ __attribute__((aligned(16))) InvShared<MODE, XTRA> sh;
+  inv2_tile<MODE, XTRA>(sh, g, tiles_x, gridDim.x, blockIdx.y, blockIdx.x, coeffs, fq, rgb_in, rgb_out, st,
+                        sse_y_part, err_y, err_rgb, in_div);
+}
+
+// The exact inverse over the tiles the certified fast inverse listed
+// (jds_inv_fast.hip): a fixed grid walks the list; every workgroup re-reads the
+// count, which the fast launch completed before this one started.
+template <int MODE, int XTRA>
+__global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(Inv<MODE>::WPE)))
+k_inv2_list(const Geo g, const int tiles_x, const int ntiles, const int16_t* __restrict__ coeffs,
+            const FrameQ* __restrict__ fq, const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out,
+            jds_frame_stats* __restrict__ st, double* __restrict__ sse_y_part, const uint2* __restrict__ list,
+            const unsigned* __restrict__ count, const int in_div) {
+  __shared__ __attribute__((aligned(16))) InvShared<MODE, XTRA> sh;
+  const unsigned n = *count;
+  for (unsigned e = blockIdx.x; e < n; e += gridDim.x) {
+    const uint2 ft = list[e];
+    inv2_tile<MODE, XTRA>(sh, g, tiles_x, ntiles, (int)ft.x, (int)ft.y, coeffs, fq, rgb_in, rgb_out, st, sse_y_part,
+                          nullptr, nullptr, in_div);
+    __syncthreads();  // the next tile reloads the table and rewrites the window
   }
 }
 
@@ -473,6 +473,34 @@ hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, con
     case M420: return inv2_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div);
     case M422: return inv2_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div);
     default: return inv2_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div);
+  }
+}
+
+template <int MODE>
+static hipError_t inv2_list_t(const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq, const uint8_t* rgb_in,
+                              uint8_t* rgb_out, jds_frame_stats* st, double* part, const uint2* list,
+                              const unsigned* count, hipStream_t s, int in_div) {
+  int tx;
+  const int tiles = inv_tiles_t<MODE>(g.H, g.W, &tx);
+  // a fixed grid (2 workgroups per CU) walks however many tiles were listed
+  const long long total = (long long)tiles * n;
+  const dim3 grid((unsigned)(total < 512 ? total : 512)), blk(Inv<MODE>::NT);
+  if (rgb_in)
+    hipLaunchKernelGGL((k_inv2_list<MODE, 1>), grid, blk, 0, s, g, tx, tiles, coeffs, fq, rgb_in, rgb_out, st, part,
+                       list, count, in_div);
+  else
+    hipLaunchKernelGGL((k_inv2_list<MODE, 0>), grid, blk, 0, s, g, tx, tiles, coeffs, fq, nullptr, rgb_out, st,
+                       part, list, count, in_div);
+  return hipGetLastError();
+}
+
+hipError_t launch_inv2_list(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
+                            const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part,
+                            const uint2* list, const unsigned* count, hipStream_t s, int in_div) {
+  switch (mode) {
+    case M420: return inv2_list_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, list, count, s, in_div);
+    case M422: return inv2_list_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, list, count, s, in_div);
+    default: return inv2_list_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, list, count, s, in_div);
   }
 }
 
