@@ -148,9 +148,12 @@ struct jds_plan {
   DevBuf fq, gk, part;
   // fast path: fp32 tables, fix-up lists and counters
   DevBuf fq32, gk32, fixbits, fixlist, counters, part32;  // per-item fix-up bitmaps and lists; per-tile statistics
-  DevBuf invfix;  // certified fast inverse: [count | (frame, tile) list] (jds_inv_fast.hip)
+  DevBuf invfix;  // certified fast inverse: run and per-item counters (InvFix, jds_inv_fast.hip)
+  unsigned inv_runs = 0;  // fast-inverse runs so far: picks the list counter (InvFix::parity)
+  bool last_inv_fast = false;  // the last run's inverse was the certified fast one
   InvFix inv_fix() const {
-    return {(uint2*)((char*)invfix.p + 64), (unsigned*)invfix.p, 0};
+    return {(unsigned*)invfix.p, (unsigned*)invfix.p + 16, 0, (int)(inv_runs & 1u), (int)(inv_runs % 3u),
+            (int)(inv_runs % 16u == 15u)};
   }
   Side side;  // border tiles run beside interior tiles
   DevBuf planes;  // 16x16 path: reconstructed chroma planes (n x 2 x hc x wc f64)
@@ -471,8 +474,8 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
         (e = p->fixlist.ensure(8 * nblk)) != hipSuccess ||
         (e = p->counters.ensure(8 * (size_t)n + 64)) != hipSuccess ||
         (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * ptiles)) != hipSuccess ||
-        (e = p->invfix.ensure(64 + 8 * (size_t)n * (size_t)inv_tiles(mode, (int)H, (int)W))) != hipSuccess ||
-        (e = hipMemset(p->invfix.p, 0, 64)) != hipSuccess ||
+        (e = p->invfix.ensure(64 + 12 * (size_t)n)) != hipSuccess ||
+        (e = hipMemset(p->invfix.p, 0, 64 + 12 * (size_t)n)) != hipSuccess ||
         (n_q > 1 && (e = p->dct32.ensure(sizeof(float) * (size_t)n_frames * g.cpf)) != hipSuccess) ||
         (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess ||
@@ -511,13 +514,15 @@ int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess)
     e = hipMemcpy(c, (const uint32_t*)p->counters.p + p->n, 4 * (size_t)p->n, hipMemcpyDeviceToHost);
-  if (e == hipSuccess && p->invfix.p) e = hipMemcpy(c + p->n, p->invfix.p, 4, hipMemcpyDeviceToHost);
+  // the last fast-inverse run appended to counter (inv_runs - 1) & 1
+  if (e == hipSuccess && p->last_inv_fast)
+    e = hipMemcpy(c + p->n, (const uint32_t*)p->invfix.p + ((p->inv_runs + 1u) & 1u), 4, hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
     free(c);
     return fail(JDS_EHIP, "fix_counts: %s", hipGetErrorString(e));
   }
   for (int i = 0; i < p->n; ++i) counts[0] += c[i];
-  counts[1] = p->invfix.p ? c[p->n] : 0u;
+  counts[1] = p->last_inv_fast ? c[p->n] : 0u;
   free(c);
   return JDS_OK;
 }
@@ -578,6 +583,10 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
                          nullptr, nullptr, 0, s, nullptr, exact ? 6 : (phases == 3 ? 2 | 8 : 2), p->nq, nullptr,
                          exact_inv || !p->invfix.p ? nullptr : &fx));
+  if (phases & 2) {
+    p->last_inv_fast = !exact_inv && p->invfix.p;
+    if (p->last_inv_fast) p->inv_runs++;
+  }
   return JDS_OK;
 }
 

@@ -694,9 +694,11 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
   if (phases & 2) {
     int tiles = g.tiles_y * g.tiles_x;
     if (!(phases & 4)) {  // jds_inv.hip (default); bit 2 selects the original k_inv
-      // certified fast inverse + exact fix-up of listed tiles (jds_inv_fast.hip)
-      // unless the caller wants the exact kernels or the IntermediateData maps
-      if (fx && !err_y)
+      // certified fast inverse (jds_inv_fast.hip) unless the caller wants the
+      // exact kernels, the IntermediateData maps or the SSE: with the SSE terms
+      // (sweeps) the fast kernel measured slower than k_inv2<MODE, 1> (register
+      // pressure of both paths in one kernel), so those runs stay exact
+      if (fx && !err_y && !rin)
         e = launch_inv_fast(mode, g, n, coeffs, fq, rin, rgb_out, st, part, *fx, s, in_div);
       else
         e = launch_inv2(mode, g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, s, in_div);

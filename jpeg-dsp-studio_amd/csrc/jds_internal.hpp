@@ -72,12 +72,25 @@ struct Side {
   hipEvent_t fork = nullptr, join = nullptr;
 };
 
-// Tile fix-up list of the certified fast inverse (jds_inv_fast.hip): (frame,
-// tile) pairs the exact inverse recomputes; `count` is reset by each run.
+// Counters of the certified fast inverse (jds_inv_fast.hip).
+// * count[0..1]: tiles recomputed exactly in a run.  They alternate between
+//   runs (`parity`): a run counts into count[parity] and zeroes
+//   count[parity ^ 1] for the next; count[parity] stays readable for
+//   jds_plan_fix_counts until then.
+// * item[3][n]: the same per item, rotating over three runs (`rot`): a run
+//   reads the previous run's counts, writes its own and zeroes the next run's.
+//   An item whose previous run recomputed more than 1/8 of its tiles (e.g. very
+//   low qualities: saturated, flat gray reconstructions are exact integers)
+//   runs the exact tile code directly; every 16th run (`probe`) tries the fast
+//   path again.
+// All zeroed at plan creation.
 struct InvFix {
-  uint2* list;
   unsigned* count;
-  int fix_all;  // test: list every tile
+  unsigned* item;
+  int fix_all;  // test: recompute every tile
+  int parity;
+  int rot;
+  int probe;
 };
 
 // Per-frame quantiser: q16 = 16*Q (pocketfft's first-axis fct = 1/16 folded in), q = Q.

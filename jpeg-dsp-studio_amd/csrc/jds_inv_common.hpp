@@ -41,8 +41,9 @@ __device__ __forceinline__ int tslot(int r, int c) { return r * 8 + ((((c >> 1) 
 
 // The same with the column's coefficients already loaded (software
 // prefetch: the loads of the next block are issued before this one's math).
+// (held sign-extended: signed 16-bit loads, no per-use extension)
 struct Col16 {
-  int16_t q[8];
+  int q[8];
 };
 // Blocks outside the grid (`ok` false) read block 0 of the plane instead: the
 // caller never transforms them, and unmasked loads need no per-load branches.

@@ -21,12 +21,15 @@
 // operation orders, with every fused multiply-add counted as two roundings).
 // If no integer lies within E of v_fast, trunc(clip(v_fast)) ==
 // trunc(clip(v_ref)): the byte is certified.  Each lane tracks the smallest
-// distance |v - rint(v)| over its samples and the largest |q|; a workgroup
-// whose tile has any uncertain sample lists (frame, tile) and the exact kernel
-// recomputes that whole tile afterwards (k_inv2_list).  On the bench's random
-// frames E ~ 1e-8 and a tile is listed with probability ~1e-3; exact ties
-// (flat or saturated regions whose reference value is an integer up to
-// pocketfft noise) are always listed, so those tiles cost fast + exact.
+// distance to an integer over its samples and the largest |q|; a workgroup
+// whose tile has any uncertain sample recomputes the whole tile at once with
+// the exact replayed-order code (jds_inv_exact.hpp, the body of k_inv2), in the
+// same LDS.  On the bench's random frames E ~ 1e-8 and a tile needs that with
+// probability ~1e-3; exact ties (flat gray or saturated regions whose
+// reference value is an integer up to pocketfft noise) always do, so those
+// tiles cost fast + exact.  (Recomputing only the affected blocks was
+// measured slower: the per-round bookkeeping cost the common path more than
+// it saved.)
 //
 // Work decomposition and LDS layout are k_inv2's (jds_inv_common.hpp): one
 // workgroup per tile, chroma window (with the ring the upsample reaches into)
@@ -37,6 +40,7 @@
 #include "jds_device.hpp"
 #include "jds_internal.hpp"
 #include "jds_inv_common.hpp"
+#include "jds_inv_exact.hpp"
 
 // every fusion the compiler forms is covered by the bound (two roundings per
 // fused pair); reassociation stays off
@@ -45,8 +49,8 @@
 namespace jds {
 
 // tools/inv_bound.py: e_fast + e_ref <= K_LIN * Dmax + K_CONST (x2 safety included)
-constexpr double K_LIN = 1.126219e-12 * 1.01;
-constexpr double K_CONST = 2.810569e-12 * 1.01;
+constexpr double K_LIN = 1.422823e-12 * 1.01;
+constexpr double K_CONST = 3.188096e-12 * 1.01;
 
 // AAN scale factors a_k = sqrt(2) cos(k pi / 16), a_0 = 1 (correctly rounded)
 __constant__ double c_aan[8] = {1.0,
@@ -122,10 +126,13 @@ __device__ __forceinline__ void fast_row(const double* __restrict__ src, int u, 
 // One plane's upsampled (chroma - 128) at the lane's 8 pixels (cv2
 // INTER_LINEAR at an exact 2x scale: pixel 2m weights (1/4, 3/4) on chroma
 // columns (m-1, m), pixel 2m+1 (3/4, 1/4) on (m, m+1); rows likewise with
-// clamped indices; the two image-edge pixels copy the edge column).
+// clamped indices).  cv2 copies the edge column at the two image-edge pixels;
+// here the window holds that column replicated into the ring (see the window
+// writes), so the same blend gives the same real value: no per-pixel selects.
+// Horizontal blend in difference form: C = s_near + (s_far - s_near) / 4.
 template <int MODE>
-__device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, const Geo& g, int x0, int cwx0, int wq,
-                                             int wt, double (&C)[8]) {
+__device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int x0, int cwx0, int wq, int wt,
+                                             double (&C)[8]) {
   using I = Inv<MODE>;
   if constexpr (I::SX == 1) {
 #pragma unroll
@@ -140,53 +147,62 @@ __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, cons
       else
         vb[j] = cw[wq * I::CWC + c0 + j];
     }
-    double t[6];
+    double d[5];
 #pragma unroll
-    for (int j = 1; j < 5; ++j) t[j] = vb[j] * 0.75;
+    for (int j = 0; j < 5; ++j) d[j] = vb[j] - vb[j + 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      C[2 * i] = vb[i] * 0.25 + t[i + 1];
-      C[2 * i + 1] = vb[i + 2] * 0.25 + t[i + 1];
-    }
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-      const int kl = side == 0 ? (x0 == 0 ? 0 : -1) : (g.W - 1 - x0 < 8 ? g.W - 1 - x0 : -1);
-      if (kl >= 0) {
-        const int e = (side == 0 ? 0 : g.wc - 1) - cwx0;
-        double v = cw[wq * I::CWC + e];
-        if constexpr (I::SY == 2) v = v * 0.25 + cw[wt * I::CWC + e] * 0.75;
-        // (pixels past the image's right edge take 0: their window columns may
-        // be outside the written ring, and they are certified like the rest)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) C[k] = k == kl ? v : (side == 1 && k > kl ? 0.0 : C[k]);
-      }
+      C[2 * i] = d[i] * 0.25 + vb[i + 1];           // (1/4, 3/4) on (m-1, m)
+      C[2 * i + 1] = d[i + 1] * -0.25 + vb[i + 1];  // (3/4, 1/4) on (m, m+1)
     }
   }
 }
 
-__device__ __forceinline__ uint32_t byte_cert(double v, double& dmin) {
-  dmin = fmin(dmin, fabs(v - rint(v)));
-  return (uint32_t)clampi((int)v, 0, 255);
+// Byte and certificate of one output value v in one fp64 add: y = v + 1.5 * 2^20
+// has a fixed exponent for |v| < 2^19, so its high word is 0x41380000 +
+// floor(v') and its low word is frac(v') * 2^32, where v' = y - 1.5 * 2^20 is v
+// rounded to a multiple of 2^-32 (|v' - v| <= 2^-33, added to the bound).
+// med3 of the high word against [0x41380000, 0x413800FF] leaves
+// clamp(floor(v'), 0, 255) in its low byte (the reference's clip +
+// astype(uint8), pipeline.py:95); the smallest and largest low words seen
+// tell how close any value came to an integer.
+constexpr double MAGIC = 0x1.8p+20;
+constexpr uint32_t MAGIC_HI = 0x41380000u;
+
+__device__ __forceinline__ uint32_t byte_cert(double v, uint32_t& lo_min, uint32_t& lo_max) {
+  const double y = v + MAGIC;
+  const uint32_t lo = (uint32_t)__double2loint(y), hi = (uint32_t)__double2hiint(y);
+  lo_min = lo_min < lo ? lo_min : lo;
+  lo_max = lo_max > lo ? lo_max : lo;
+  const uint32_t c = hi < MAGIC_HI ? MAGIC_HI : hi;
+  return c > MAGIC_HI + 255u ? MAGIC_HI + 255u : c;  // v_med3_u32; the byte is bits 0-7
 }
 
-// XTRA: 0 = RGB only; 1 = + exact integer SSE and luma SSE partials (sweeps),
-// committed only for certified tiles (listed tiles are redone by k_inv2_list).
+// Four bytes (bits 0-7 of a, b, c, d) into one word: two byte permutes and an or.
+__device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t ab = __builtin_amdgcn_perm(b, a, 0x0c0c0400u);  // a.b0 | b.b0 << 8
+  const uint32_t cd = __builtin_amdgcn_perm(d, c, 0x04000c0cu);  // c.b0 << 16 | d.b0 << 24
+  return ab | cd;
+}
+
+// The fast pass over one tile (sets sh.redo when the tile must be recomputed).
 template <int MODE, int XTRA>
-__global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(Inv<MODE>::WPE)))
-k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
-           const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
-           double* __restrict__ sse_y_part, uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount,
-           const int in_div, const int fix_all) {
+__device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const Geo& g, const int tiles_x,
+                                              const int frame, const int tile, const int16_t* __restrict__ coeffs,
+                                              const FrameQ* __restrict__ fq, const uint8_t* __restrict__ rgb_in,
+                                              uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
+                                              double* __restrict__ sse_y_part, unsigned* __restrict__ fixcount,
+                                              unsigned* __restrict__ next_count, unsigned* __restrict__ cnt_now,
+                                              const int in_div, const int fix_all) {
   using I = Inv<MODE>;
-  __shared__ __attribute__((aligned(16))) double s_mid[I::MB * MS];
-  __shared__ __attribute__((aligned(16))) double s_cw[2][I::CWR * I::CWC];
+  double* s_mid = sh.mid;
+  double (*s_cw)[I::CWR * I::CWC] = sh.cw;
   __shared__ double s_qs[64];  // Q[u][v] * a_u * a_v / 8
   __shared__ double s_qmax;
-  __shared__ double s_red[I::NT / 64], s_dmin[I::NT / 64], s_dq[I::NT / 64];
+  __shared__ double s_red[I::NT / 64], s_dq[I::NT / 64];
+  __shared__ uint32_t s_lmin[I::NT / 64], s_lmax[I::NT / 64];
   __shared__ unsigned long long s_sse;
-
   const int tid = threadIdx.x, lv = tid & 7, lb = tid >> 3;
-  const int frame = blockIdx.y, tile = blockIdx.x;
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int Y0 = ty * I::TH, X0 = tx * I::TW;
   const int16_t* cf = coeffs + (size_t)frame * g.cpf;
@@ -201,8 +217,7 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
   if (XTRA && tid == 0) s_sse = 0ull;
   __syncthreads();
 
-  double dq = 0.0;     // max |q| this lane read
-  double dmin = 1.0;   // min distance of an output value to an integer
+  double dq = 0.0;  // max |q| this lane read
   const double dc_add = lv == 0 ? 128.0 : 0.0;
 
   // ---- 1. chroma window: (clip(IDCT) - 128) of the blocks the tile reaches --
@@ -242,6 +257,18 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
 #pragma unroll
           for (int k = 0; k < 8; ++k)
             if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k] - 128.0;
+          if constexpr (I::SX == 2) {
+            // cv2's clamped taps at the image's left / right edge pixels read the
+            // edge column alone: replicate it into the ring (and past the
+            // plane's right end, where pixels beyond the image read too)
+            if (bx == 0 && wc0 >= 1) w[wc0 - 1] = c[0] - 128.0;
+            const int ke = g.wc - 1 - bx * 8;
+            if ((unsigned)ke < 8u) {
+              const double e = (ke == 0 ? c[0] : ke == 1 ? c[1] : ke == 2 ? c[2] : ke == 3 ? c[3]
+                                : ke == 4 ? c[4] : ke == 5 ? c[5] : ke == 6 ? c[6] : c[7]) - 128.0;
+              for (int col = wc0 + ke + 1; col < I::CWC; ++col) w[col] = e;
+            }
+          }
         }
       }
     }
@@ -249,6 +276,8 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
   __syncthreads();
 
   // ---- 2. luma rounds: IDCT, upsample, colour, certify, store ----------------
+  // the certificate: smallest / largest fraction word of the lane's outputs
+  uint32_t lo_min = 0xffffffffu, lo_max = 0u;
   unsigned long long sse = 0ull;
   double ssy = 0.0;
   const uint8_t* in_f = XTRA ? rgb_in + (size_t)(frame / in_div) * g.H * g.W * 3 : nullptr;
@@ -257,6 +286,9 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
   for (int r = 0; r < I::NYB / I::RB; ++r) {
     int by, bx;
     const bool bvalid = luma_blk(r, by, bx);
+    // the luma SSE in the exact kernel's order: per-round sums, added per round
+    unsigned long long r_sse = 0ull;
+    double r_ssy = 0.0;
     const Col16 cur = lq;
     if (r + 1 < I::NYB / I::RB) {
       int by1, bx1;
@@ -281,28 +313,28 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
       const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
       uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
       const bool wide = nx == 8 && ((((uintptr_t)o) & 7u) == 0);
-      uint32_t pk[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+      uint32_t pk[6];
       {
+        // channel words (byte in bits 0-7) in output order R0 G0 B0 R1 ...
+        uint32_t cb[24];
         double C[8], Gt[8];
-        chroma8_fast<MODE>(s_cw[0], g, x0, cwx0, wq, wt, C);
+        chroma8_fast<MODE>(s_cw[0], x0, cwx0, wq, wt, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const double B = Yv[k] + C[k] * 1.772;
           Gt[k] = Yv[k] + C[k] * -0.344136;
-          const int b = 3 * k + 2;
-          const uint32_t ub = byte_cert(B, dmin);
-          pk[b >> 2] |= ub << (8 * (b & 3));
+          cb[3 * k + 2] = byte_cert(B, lo_min, lo_max);
         }
-        chroma8_fast<MODE>(s_cw[1], g, x0, cwx0, wq, wt, C);
+        chroma8_fast<MODE>(s_cw[1], x0, cwx0, wq, wt, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const double R = Yv[k] + C[k] * 1.402;
           const double G = Gt[k] + C[k] * -0.714136;
-          const int b = 3 * k;
-          const uint32_t ur = byte_cert(R, dmin), ug = byte_cert(G, dmin);
-          pk[b >> 2] |= ur << (8 * (b & 3));
-          pk[(b + 1) >> 2] |= ug << (8 * ((b + 1) & 3));
+          cb[3 * k] = byte_cert(R, lo_min, lo_max);
+          cb[3 * k + 1] = byte_cert(G, lo_min, lo_max);
         }
+#pragma unroll
+        for (int w = 0; w < 6; ++w) pk[w] = pack4(cb[4 * w], cb[4 * w + 1], cb[4 * w + 2], cb[4 * w + 3]);
       }
       if (wide) {
         uint2* o2 = reinterpret_cast<uint2*>(o);
@@ -336,24 +368,30 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
             const int o0 = byte_of(in, b), o1 = byte_of(in, b + 1), o2 = byte_of(in, b + 2);
             const int ur = byte_of(pk, b), ug = byte_of(pk, b + 1), ub = byte_of(pk, b + 2);
             const int d0 = o0 - ur, d1 = o1 - ug, d2 = o2 - ub;
-            sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
+            r_sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
             {
 #pragma clang fp contract(off)
               const double yo = luma((double)o0, (double)o1, (double)o2);
               const double yr = luma((double)ur, (double)ug, (double)ub);
               const double dy = yo - yr;
-              ssy = ssy + dy * dy;
+              r_ssy = r_ssy + dy * dy;
             }
           }
         }
       }
     }
+    if constexpr (XTRA > 0) {
+      sse += r_sse;
+      ssy = ssy + r_ssy;
+    }
   }
 
-  // ---- 3. certification: the tile's smallest distance vs its bound -----------
+  // ---- 3. certification: the tile's closest approach to an integer vs its bound
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    dmin = fmin(dmin, __shfl_xor(dmin, o, 64));
+    const uint32_t a = __shfl_xor(lo_min, o, 64), b = __shfl_xor(lo_max, o, 64);
+    lo_min = lo_min < a ? lo_min : a;
+    lo_max = lo_max > b ? lo_max : b;
     dq = fmax(dq, __shfl_xor(dq, o, 64));
   }
   if constexpr (XTRA > 0) {
@@ -367,34 +405,77 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
     if ((tid & 63) == 0) s_red[tid >> 6] = d;
   }
   if ((tid & 63) == 0) {
-    s_dmin[tid >> 6] = dmin;
+    s_lmin[tid >> 6] = lo_min;
+    s_lmax[tid >> 6] = lo_max;
     s_dq[tid >> 6] = dq;
   }
   __syncthreads();
   if (tid == 0) {
-    double m = 1.0, q = 0.0;
+    uint32_t mn = 0xffffffffu, mx = 0u;
+    double q = 0.0;
     for (int i = 0; i < I::NT / 64; ++i) {
-      m = fmin(m, s_dmin[i]);
+      mn = mn < s_lmin[i] ? mn : s_lmin[i];
+      mx = mx > s_lmax[i] ? mx : s_lmax[i];
       q = fmax(q, s_dq[i]);
     }
-    const double E = K_LIN * (q * s_qmax) + K_CONST;
-    if (m <= E || fix_all) {
-      const unsigned slot = atomicAdd(fixcount, 1u);
-      fixlist[slot] = make_uint2((unsigned)frame, (unsigned)tile);
+    // |v_fast - v_ref| <= E, plus the magic add's rounding (2^-33); T in units of 2^-32
+    const double E = K_LIN * (q * s_qmax) + K_CONST + 0x1p-33;
+    const double T = ceil(E * 0x1p+32) + 1.0;
+    const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
+    sh.redo = uncertain || fix_all;
+    if (sh.redo) {
+      atomicAdd(fixcount, 1u);  // tiles recomputed (jds_plan_fix_counts)
+      atomicAdd(cnt_now + frame, 1u);
     } else if constexpr (XTRA > 0) {
       double a = 0.0;
       for (int i = 0; i < I::NT / 64; ++i) a = a + s_red[i];
       sse_y_part[(size_t)frame * gridDim.x + tile] = a;
       atomicAdd((unsigned long long*)&st[frame].sse_rgb, s_sse);
     }
+    if (frame == 0 && tile == 0) *next_count = 0u;  // the next run counts from zero
   }
+  __syncthreads();  // sh.redo is visible to the caller's uniform branch
+}
+
+// XTRA: 0 = RGB only; 1 = + exact integer SSE and luma SSE partials (sweeps),
+// committed by the fast pass only for certified tiles (the exact tile code
+// commits the others).
+template <int MODE, int XTRA>
+__global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(Inv<MODE>::WPE)))
+k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+           const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
+           double* __restrict__ sse_y_part, unsigned* __restrict__ fixcount, unsigned* __restrict__ next_count,
+           unsigned* __restrict__ item_cnt, const int rot, const int probe, const int in_div, const int fix_all) {
+  // the transpose buffer and chroma window are the exact fallback's own
+  __shared__ __attribute__((aligned(16))) InvShared<MODE, XTRA> sh;
+  const int tid = threadIdx.x;
+  const int frame = blockIdx.y, tile = blockIdx.x;
+  // per-item adaptivity (InvFix): the previous run's recomputed tiles of this item
+  const unsigned n_items = gridDim.y, ntile = gridDim.x;
+  unsigned* cnt_prev = item_cnt + ((rot + 2) % 3) * n_items;
+  unsigned* cnt_now = item_cnt + rot * n_items;
+  const unsigned prev = cnt_prev[frame];
+  if (tile == 0 && tid == 0) item_cnt[((rot + 1) % 3) * n_items + frame] = 0u;  // the next run's
+  const bool item_exact = !probe && !fix_all && prev * 8u > ntile;
+  if (item_exact) {
+    // (uniform) this item runs the exact tile code directly and keeps its count
+    if (tile == 0 && tid == 0) {
+      cnt_now[frame] = prev;
+      atomicAdd(fixcount, ntile);
+      if (frame == 0) *next_count = 0u;
+    }
+  } else {
+    sh.redo = 0;
+    inv_fast_tile<MODE, XTRA>(sh, g, tiles_x, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part, fixcount,
+                              next_count, cnt_now, in_div, fix_all);
+  }
+  // one call site of the exact tile code: items in exact mode, uncertain tiles
+  if (item_exact || sh.redo)  // (uniform)
+    inv2_tile<MODE, XTRA>(sh, g, tiles_x, ntile, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part, nullptr,
+                          nullptr, in_div);
 }
 
 // ------------------------------------------------------------ launchers --
-
-hipError_t launch_inv2_list(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
-                            const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part,
-                            const uint2* list, const unsigned* count, hipStream_t s, int in_div);
 
 template <int MODE>
 static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq, const uint8_t* rgb_in,
@@ -402,16 +483,13 @@ static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const F
                              int in_div) {
   const int ty = (g.H + Inv<MODE>::TH - 1) / Inv<MODE>::TH, tx = (g.W + Inv<MODE>::TW - 1) / Inv<MODE>::TW;
   const dim3 grid(ty * tx, n), blk(Inv<MODE>::NT);
-  hipError_t e = hipMemsetAsync(fx.count, 0, sizeof(unsigned), s);
-  if (e != hipSuccess) return e;
-  if (rgb_in)
-    hipLaunchKernelGGL((k_inv_fast<MODE, 1>), grid, blk, 0, s, g, tx, coeffs, fq, rgb_in, rgb_out, st, part,
-                       fx.list, fx.count, in_div, fx.fix_all);
-  else
-    hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part,
-                       fx.list, fx.count, in_div, fx.fix_all);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_inv2_list(MODE, g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx.list, fx.count, s, in_div);
+  // count[parity] was zeroed by the previous run; this run zeroes the other
+  unsigned* cnt = fx.count + fx.parity;
+  unsigned* nxt = fx.count + (fx.parity ^ 1);
+  (void)rgb_in;  // SSE runs take the exact kernel (launch_codec)
+  hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, cnt, nxt,
+                     fx.item, fx.rot, fx.probe, in_div, fx.fix_all);
+  return hipGetLastError();
 }
 
 hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,

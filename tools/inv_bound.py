@@ -171,7 +171,17 @@ def colour_bound(ey, ec_, chain, mode):
     def ups(x):
         if mode == '4:4:4':
             return x
-        # horizontal: fma(s0, w0, s1 * w1); vertical (4:2:0) the same again
+        if chain == 'fast':
+            # vertical (4:2:0): a * 0.25 + b * 0.75; horizontal in difference
+            # form: near + (far - near) * (+-0.25)  (jds_inv_fast.hip chroma8_fast)
+            v = x
+            if mode == '4:2:0':
+                v = add(mul(x, 0.25), mul(x, 0.75)); v.cap = x.cap
+            w = fresh(v.cap, v.el, v.ec)
+            d = add(v, w, -1)
+            h = add(mul(d, 0.25), w); h.cap = x.cap
+            return h
+        # reference (cv2): horizontal fma pair, then vertical likewise
         h = add(mul(x, 0.25), mul(x, 0.75)); h.cap = x.cap
         if mode == '4:2:0':
             h = add(mul(h, 0.25), mul(h, 0.75)); h.cap = x.cap
