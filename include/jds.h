@@ -213,6 +213,16 @@ int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t invers
 /* The same for 16x16 blocks (jds_dct16.hpp). */
 int jds_selftest_dct16x16(const double* in, double* out, int64_t n, int32_t inverse);
 
+/* Test-only: the certified forward's fp32 chain (jds_fast.hip: colour, prefilter,
+ * area average, fdct8_f32 along both axes) evaluated on the host for every 8x8
+ * block of one plane (0 Y, 1 Cb, 2 Cr) of an H x W RGB image whose plane size is
+ * a multiple of 8, in either pass order (rows_first 1 = k_fwd32i, 0 = k_fwd32),
+ * coefficients before quantisation (n_blocks x 64 f32, raster block order);
+ * bound[64] = the rigorous bound on |c_fp32 - c_exact| the kernels certify
+ * with (fast_fwd_bounds).  Lets the CPU suite test the bound adversarially. */
+int jds_selftest_fwd32(int32_t subsampling, int32_t prefilter, const double* gauss, const uint8_t* rgb, int64_t H,
+                       int64_t W, int32_t plane, int32_t rows_first, float* coeffs, double* bound);
+
 /* Test-only: the host-built cv2 INTER_AREA table of one axis (OpenCV
  * computeResizeAreaTab, used by the odd-size path) for src -> dst samples:
  * per destination index its tap count n[d] (<= 4) and taps si[4d..], a[4d..].

@@ -45,6 +45,9 @@ hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const
 int quant_mq_tiles(const Geo& g);
 int inv16_tiles(int mode, int H, int W);
 constexpr int MAXQ_SHARED = 8;  // jds_fast.hip MAXQ
+void fast_fwd_bounds(int mode, bool pf, const double* gk, double* E);
+int fwd32_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
+                     bool rows_first, float* out);
 void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
 size_t fast_q_size();
 hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse, hipStream_t s);
@@ -1015,6 +1018,20 @@ int jds_selftest_dct8x8(const double* in, double* out, int64_t n, int32_t invers
     }
     for (int i = 0; i < 64; ++i) out[64 * b + i] = t[i] * 0.0625;  // pocketfft fct = 1/16
   }
+  return JDS_OK;
+}
+
+int jds_selftest_fwd32(int32_t subsampling, int32_t prefilter, const double* gauss, const uint8_t* rgb, int64_t H,
+                       int64_t W, int32_t plane, int32_t rows_first, float* coeffs, double* bound) {
+  if (!gauss || !rgb || !coeffs || !bound || H < 1 || W < 1 || H > 4096 || W > 4096 || plane < 0 || plane > 2 ||
+      subsampling < JDS_SS_444 || subsampling > JDS_SS_420)
+    return fail(JDS_EINVAL, "bad argument");
+  const bool pf = prefilter != 0 && subsampling != JDS_SS_444;
+  double E[128];
+  fast_fwd_bounds(subsampling, pf, gauss, E);
+  memcpy(bound, E + (plane ? 64 : 0), 64 * sizeof(double));
+  if (fwd32_host_plane(subsampling, pf, gauss, rgb, (int)H, (int)W, plane, rows_first != 0, coeffs))
+    return fail(JDS_EINVAL, "plane size must be a multiple of 8");
   return JDS_OK;
 }
 

@@ -44,7 +44,7 @@ static constexpr float FW[8][4] = {
 
 // fp32 forward DCT-II of one line: 8 add/sub + 8 four-term FMA chains.  The
 // host-side bound (fast_fwd_thresholds) follows exactly this sequence.
-__device__ __forceinline__ void fdct8_f32(float (&x)[8]) {
+__host__ __device__ __forceinline__ void fdct8_f32(float (&x)[8]) {
   const float s0 = x[0] + x[7], s1 = x[1] + x[6], s2 = x[2] + x[5], s3 = x[3] + x[4];
   const float d0 = x[0] - x[7], d1 = x[1] - x[6], d2 = x[2] - x[5], d3 = x[3] - x[4];
 #pragma unroll
@@ -55,18 +55,18 @@ __device__ __forceinline__ void fdct8_f32(float (&x)[8]) {
 }
 
 // fp32 colour conversions (any rounding order is fine: bounded on the host)
-__device__ __forceinline__ float luma32(float R, float G, float B) {
+__host__ __device__ __forceinline__ float luma32(float R, float G, float B) {
   return fmaf(0.114f, B, fmaf(0.587f, G, 0.299f * R));
 }
 // luma - 128 with the level shift folded into the chain: three roundings of
 // magnitude <= 128 instead of luma32's, inside fwd_input_error's luma bound
-__device__ __forceinline__ float luma32m(float R, float G, float B) {
+__host__ __device__ __forceinline__ float luma32m(float R, float G, float B) {
   return fmaf(0.114f, B, fmaf(0.587f, G, fmaf(0.299f, R, -128.0f)));
 }
-__device__ __forceinline__ float cb32(float R, float G, float B) {
+__host__ __device__ __forceinline__ float cb32(float R, float G, float B) {
   return fmaf(-0.168736f, R, fmaf(-0.331264f, G, fmaf(0.5f, B, 128.0f)));
 }
-__device__ __forceinline__ float cr32(float R, float G, float B) {
+__host__ __device__ __forceinline__ float cr32(float R, float G, float B) {
   return fmaf(-0.081312f, B, fmaf(-0.418688f, G, fmaf(0.5f, R, 128.0f)));
 }
 
@@ -1314,14 +1314,15 @@ static double fwd_input_error(int plane, int mode, bool pf, const double* gk) {
   return e + u * 128;                                     // -128
 }
 
-void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr) {
+// E[p][k][l] (p: 0 luma, 1 chroma): the rigorous bound on |c_fp32 - c_exact|
+// of coefficient (k, l) for either pass order, before the quotient.
+void fast_fwd_bounds(int mode, bool pf, const double* gk, double* E) {
   static const double W[8][4] = {
       {FW[0][0], FW[0][1], FW[0][2], FW[0][3]}, {FW[1][0], FW[1][1], FW[1][2], FW[1][3]},
       {FW[2][0], FW[2][1], FW[2][2], FW[2][3]}, {FW[3][0], FW[3][1], FW[3][2], FW[3][3]},
       {FW[4][0], FW[4][1], FW[4][2], FW[4][3]}, {FW[5][0], FW[5][1], FW[5][2], FW[5][3]},
       {FW[6][0], FW[6][1], FW[6][2], FW[6][3]}, {FW[7][0], FW[7][1], FW[7][2], FW[7][3]},
   };
-  for (int i = 0; i < 64; ++i) rq[i] = (float)(1.0 / Q[i]);
   for (int p = 0; p < 2; ++p) {
     const double e_in = fwd_input_error(p, mode, pf, gk);
     double X1[8], e1[8];
@@ -1335,19 +1336,93 @@ void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, f
     for (int k = 0; k < 8; ++k) {
       for (int l = 0; l < 8; ++l) {
         // coefficient (k, l): axis 0 first (k_fwd32) or axis 1 first (k_fwd32i);
-        // second-order slack, the fp64 reference's own error, quotient scaling
+        // second-order slack and the fp64 reference's own error
         const double e2l = E2[k][l] > E2[l][k] ? E2[k][l] : E2[l][k];
-        const double E = e2l * (1 + 1e-5) + 1e-9;
-        const double t = E / Q[k * 8 + l] * (1 + 1e-5) + 1e-7;
-        // stored as the certification limit on |t - rint(t)|: 0.5 - t - 2^-23
-        // (covers the fp32 rounding of the in-kernel fma), rounded down
-        const double lim = 0.5 - t * (1 + 0x1p-20) - 0x1p-23;
-        float f = (float)lim;
-        if ((double)f > lim) f = nextafterf(f, 0.0f);
-        thr[p * 64 + k * 8 + l] = f;
+        E[p * 64 + k * 8 + l] = e2l * (1 + 1e-5) + 1e-9;
       }
     }
   }
+}
+
+void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr) {
+  double Eb[128];
+  fast_fwd_bounds(mode, pf, gk, Eb);
+  for (int i = 0; i < 64; ++i) rq[i] = (float)(1.0 / Q[i]);
+  for (int p = 0; p < 2; ++p) {
+    for (int i = 0; i < 64; ++i) {
+      // quotient scaling, stored as the certification limit on |t - rint(t)|:
+      // 0.5 - t - 2^-23 (covers the fp32 rounding of the in-kernel fma), rounded down
+      const double t = Eb[p * 64 + i] / Q[i] * (1 + 1e-5) + 1e-7;
+      const double lim = 0.5 - t * (1 + 0x1p-20) - 0x1p-23;
+      float f = (float)lim;
+      if ((double)f > lim) f = nextafterf(f, 0.0f);
+      thr[p * 64 + i] = f;
+    }
+  }
+}
+
+// ---------------------------------------------- host: the fp32 chain (tests) --
+//
+// The forward kernels' fp32 arithmetic restated on the host, expression for
+// expression (k_fwd32i / k_fwd32: luma32m, cb32 / cr32, the prefilter's row
+// then column FMA chains with BORDER_REFLECT_101, the area average, fdct8_f32
+// along both axes in either order), so the CPU test suite can check the bound
+// above against the exact reference on adversarial inputs.  Test-only.
+static int refl101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+  return i;
+}
+
+int fwd32_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
+                     bool rows_first, float* out) {
+  const int sy = mode == M420 ? 2 : 1, sx = mode == M444 ? 1 : 2;
+  const int ph = plane == 0 ? H : H / sy, pw = plane == 0 ? W : W / sx;
+  if (ph % 8 || pw % 8) return -1;
+  const float k0 = (float)gk[0], k1 = (float)gk[1], k2 = (float)gk[2];
+  auto px = [&](int y, int x, int c) { return (float)rgb[((size_t)y * W + x) * 3 + c]; };
+  auto chroma = [&](int y, int x) {  // full-resolution chroma sample (not shifted)
+    const float R = px(y, x, 0), G = px(y, x, 1), B = px(y, x, 2);
+    return plane == 1 ? cb32(R, G, B) : cr32(R, G, B);
+  };
+  auto rowf = [&](int y, int x) {  // prefilter row pass at (y, x)
+    const float bl = chroma(y, refl101(x - 1, W)), c = chroma(y, x), br = chroma(y, refl101(x + 1, W));
+    return fmaf(k2, br, fmaf(k1, c, k0 * bl));
+  };
+  auto sample = [&](int y, int x) -> float {  // plane sample (y, x), level-shifted
+    if (plane == 0) return luma32m(px(y, x, 0), px(y, x, 1), px(y, x, 2));
+    if (mode == M444) return chroma(y, x) - 128.0f;
+    float s[2][2];
+    for (int a = 0; a < sy; ++a)
+      for (int b = 0; b < 2; ++b) {
+        const int yy = sy * y + a, xx = 2 * x + b;
+        if (pf)
+          s[a][b] = fmaf(k0, rowf(refl101(yy + 1, H), xx) + rowf(refl101(yy - 1, H), xx), k1 * rowf(yy, xx));
+        else
+          s[a][b] = chroma(yy, xx);
+      }
+    if (sy == 2) return (((s[0][0] + s[0][1]) + s[1][0]) + s[1][1]) * 0.25f - 128.0f;
+    return (s[0][0] + s[0][1]) * 0.5f - 128.0f;
+  };
+  const int nbx = pw / 8;
+  for (int by = 0; by < ph / 8; ++by)
+    for (int bx = 0; bx < nbx; ++bx) {
+      float b[8][8];
+      for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j) b[i][j] = sample(by * 8 + i, bx * 8 + j);
+      for (int pass = 0; pass < 2; ++pass) {
+        const bool rows = (pass == 0) == rows_first;  // axis 1 (along a row) or axis 0
+        for (int i = 0; i < 8; ++i) {
+          float v[8];
+          for (int j = 0; j < 8; ++j) v[j] = rows ? b[i][j] : b[j][i];
+          fdct8_f32(v);
+          for (int j = 0; j < 8; ++j) (rows ? b[i][j] : b[j][i]) = v[j];
+        }
+      }
+      float* o = out + ((size_t)by * nbx + bx) * 64;
+      for (int i = 0; i < 64; ++i) o[i] = b[i / 8][i % 8];
+    }
+  return 0;
 }
 
 size_t fast_q_size() { return sizeof(FastQ); }
