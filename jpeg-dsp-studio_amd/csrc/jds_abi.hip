@@ -35,6 +35,7 @@ hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, do
                             double* scratch_planes, double* scratch_smap, double* scratch_chunks, double* out,
                             hipStream_t s);
 hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
+size_t mag_scratch_bytes(long long nblocks, int max_chunks);
 hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* chunk_sum, int max_chunks,
                           double* out, hipStream_t s);
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
@@ -133,9 +134,9 @@ struct jds_ctx {
 // SSIM scratch in the context; returns the device pointer of 5 result doubles
 static int run_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int H, int W, double* dres) {
   const size_t n = (size_t)H * W;
-  HIP_TRY(c->ss_planes.ensure(5 * n * sizeof(double)));
-  HIP_TRY(c->ss_map.ensure((size_t)(H - 6) * (W - 6) * sizeof(double)));
-  HIP_TRY(c->ss_chunks.ensure(((n + 8191) / 8192 + 1) * sizeof(double)));
+  HIP_TRY(c->ss_planes.ensure(4 * 5 * n * sizeof(double)));  // the four channels at once
+  HIP_TRY(c->ss_map.ensure(4 * (size_t)(H - 6) * (W - 6) * sizeof(double)));
+  HIP_TRY(c->ss_chunks.ensure(4 * ((n + 8191) / 8192 + 1) * sizeof(double)));
   HIP_TRY(launch_psnr_ssim(a, b, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_planes.p, (double*)c->ss_map.p,
                            (double*)c->ss_chunks.p, dres, c->stream));
   return JDS_OK;
@@ -698,7 +699,7 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
     // NumPy float32 magnitude_bits (utils/metrics.py:77-78)
     const long long nblk = g.cpf / 64;
     const int max_chunks = (int)((g.cpf + 8191) / 8192) + 1;
-    HIP_TRY(c->chunks.ensure(sizeof(unsigned) * (size_t)max_chunks));
+    HIP_TRY(c->chunks.ensure(mag_scratch_bytes(nblk, max_chunks)));
     HIP_TRY(launch_mag_f32((const int16_t*)c->coeffs.p, nblk, (unsigned*)c->chunks.p, max_chunks,
                            &((jds_frame_stats*)c->stats.p)->magnitude_bits_f32, s));
   }

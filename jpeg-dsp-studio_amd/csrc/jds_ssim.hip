@@ -40,58 +40,70 @@ __device__ __forceinline__ double chan_val(const uint8_t* img, size_t px, int c)
   return 0.299 * R + 0.587 * G + 0.114 * B;  // utils/metrics.py:17-18
 }
 
-// pass along axis 0 (columns): 5 running sums per column, one channel.
-// out: 5 planes [q][H][W], q = x, y, xx, yy, xy
-__global__ void k_uf_axis0(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int H, int W, int c,
-                           double* __restrict__ out) {
+// pass along axis 0 (columns): one running sum per thread -- column j,
+// quantity q (x, y, xx, yy, xy) and channel c from the grid -- so the four
+// channels' 5 quantities run in parallel (scipy NI_UniformFilter1D per line).
+// out: [c][q][H][W].  The loads of the next rows are issued ahead of the
+// recurrence (they do not depend on it).
+__device__ __forceinline__ double uf_term(const uint8_t* a, const uint8_t* b, size_t px, int c, int q) {
+  const double x = (q == 1 || q == 3) ? 0.0 : chan_val(a, px, c);
+  const double y = (q == 0 || q == 2) ? 0.0 : chan_val(b, px, c);
+  return q == 0 ? x : q == 1 ? y : q == 2 ? x * x : q == 3 ? y * y : x * y;
+}
+
+__global__ void __launch_bounds__(64) k_uf_axis0(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int H,
+                                                 int W, double* __restrict__ out) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = blockIdx.y, c = blockIdx.z;
   if (j >= W) return;
   const size_t plane = (size_t)H * W;
-  double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int k = -3; k <= 3; ++k) {
-    const size_t px = (size_t)refl_sym(k, H) * W + j;
-    const double x = chan_val(a, px, c), y = chan_val(b, px, c);
-    s[0] = s[0] + x;
-    s[1] = s[1] + y;
-    s[2] = s[2] + x * x;
-    s[3] = s[3] + y * y;
-    s[4] = s[4] + x * y;
+  double* o = out + ((size_t)c * 5 + q) * plane;
+  double s = 0.0;
+  for (int k = -3; k <= 3; ++k) s = s + uf_term(a, b, (size_t)refl_sym(k, H) * W + j, c, q);
+  o[j] = s / 7.0;
+  constexpr int U = 8;
+  int i = 1;
+  for (; i + U <= H; i += U) {
+    double d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ii = i + u;
+      // (xn - xo) etc.: scipy adds the difference of the new and old terms
+      const size_t pn = (size_t)refl_sym(ii + 3, H) * W + j, po = (size_t)refl_sym(ii - 4, H) * W + j;
+      d[u] = uf_term(a, b, pn, c, q) - uf_term(a, b, po, c, q);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s = s + d[u];
+      o[(size_t)(i + u) * W + j] = s / 7.0;
+    }
   }
-  for (int q = 0; q < 5; ++q) out[q * plane + j] = s[q] / 7.0;
-  for (int i = 1; i < H; ++i) {
+  for (; i < H; ++i) {
     const size_t pn = (size_t)refl_sym(i + 3, H) * W + j, po = (size_t)refl_sym(i - 4, H) * W + j;
-    const double xn = chan_val(a, pn, c), yn = chan_val(b, pn, c);
-    const double xo = chan_val(a, po, c), yo = chan_val(b, po, c);
-    s[0] = s[0] + (xn - xo);
-    s[1] = s[1] + (yn - yo);
-    s[2] = s[2] + (xn * xn - xo * xo);
-    s[3] = s[3] + (yn * yn - yo * yo);
-    s[4] = s[4] + (xn * yn - xo * yo);
-    const size_t o = (size_t)i * W + j;
-    for (int q = 0; q < 5; ++q) out[q * plane + o] = s[q] / 7.0;
+    s = s + (uf_term(a, b, pn, c, q) - uf_term(a, b, po, c, q));
+    o[(size_t)i * W + j] = s / 7.0;
   }
 }
 
-// pass along axis 1 (rows) over the 5 planes, then the SSIM map on the cropped region
-__global__ void k_uf_axis1_ssim(const double* __restrict__ in, int H, int W, SsimConsts k,
-                                double* __restrict__ smap) {
+// pass along axis 1 (rows) over the 5 planes of channel blockIdx.y, then the
+// SSIM map on the cropped region (smap: [c][H-6][W-6])
+__global__ void __launch_bounds__(64) k_uf_axis1_ssim(const double* __restrict__ in, int H, int W, SsimConsts k,
+                                                      double* __restrict__ smap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
   if (i >= H) return;
   const size_t plane = (size_t)H * W;
+  const int cw = W - 6;
+  smap += (size_t)c * (H - 6) * cw;
   const double* r[5];
-  for (int q = 0; q < 5; ++q) r[q] = in + q * plane + (size_t)i * W;
+  for (int q = 0; q < 5; ++q) r[q] = in + ((size_t)c * 5 + q) * plane + (size_t)i * W;
   double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   for (int t = -3; t <= 3; ++t) {
     const int jj = refl_sym(t, W);
     for (int q = 0; q < 5; ++q) s[q] = s[q] + r[q][jj];
   }
   const bool row_in = i >= 3 && i < H - 3;
-  const int cw = W - 6;
-  for (int j = 0; j < W; ++j) {
-    if (j > 0) {
-      const int jn = refl_sym(j + 3, W), jo = refl_sym(j - 4, W);
-      for (int q = 0; q < 5; ++q) s[q] = s[q] + (r[q][jn] - r[q][jo]);
-    }
+  auto emit = [&](int j) {
     if (row_in && j >= 3 && j < W - 3) {
       const double ux = s[0] / 7.0, uy = s[1] / 7.0, uxx = s[2] / 7.0, uyy = s[3] / 7.0, uxy = s[4] / 7.0;
       // skimage structural_similarity (sample covariance)
@@ -103,6 +115,29 @@ __global__ void k_uf_axis1_ssim(const double* __restrict__ in, int H, int W, Ssi
       const double d = b1 * b2;
       smap[(size_t)(i - 3) * cw + (j - 3)] = (a1 * a2) / d;
     }
+  };
+  emit(0);
+  constexpr int U = 4;
+  int j = 1;
+  for (; j + U <= W; j += U) {
+    double dn[U][5];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int jn = refl_sym(j + u + 3, W), jo = refl_sym(j + u - 4, W);
+#pragma unroll
+      for (int q = 0; q < 5; ++q) dn[u][q] = r[q][jn] - r[q][jo];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) s[q] = s[q] + dn[u][q];
+      emit(j + u);
+    }
+  }
+  for (; j < W; ++j) {
+    const int jn = refl_sym(j + 3, W), jo = refl_sym(j - 4, W);
+    for (int q = 0; q < 5; ++q) s[q] = s[q] + (r[q][jn] - r[q][jo]);
+    emit(j);
   }
 }
 
@@ -207,8 +242,10 @@ __device__ void np_chunk_sum(Get get, long long n, double* chunk_out) {
   if (threadIdx.x == 0) chunk_out[blockIdx.x] = pw_combine(m, s_ls);
 }
 
-__global__ void k_chunks_smap(const double* __restrict__ smap, long long n, double* __restrict__ chunk_out) {
-  np_chunk_sum([&](long long i) { return smap[i]; }, n, chunk_out);
+__global__ void k_chunks_smap(const double* __restrict__ smap, long long n, double* __restrict__ chunk_out,
+                              int nch) {
+  const double* m = smap + (size_t)blockIdx.y * n;  // channel blockIdx.y
+  np_chunk_sum([&](long long i) { return m[i]; }, n, chunk_out + (size_t)blockIdx.y * nch);
 }
 
 __global__ void k_chunks_ydiff(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, long long n,
@@ -248,76 +285,144 @@ hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsign
 // utils/metrics.py:77-78 — magnitude_bits = np.sum(np.ceil(np.log2(|nz| + 1)) + 1)
 // over the nonzero coefficients in all_quantized_coeffs order, a float32
 // reduction: NumPy sums 8192-element buffers (exact here: terms are integers
-// <= 12, so a buffer sum < 2^24) and accumulates the buffer sums in float32.
-// One workgroup walks the blocks in order, ranking nonzeros with a block scan.
-__global__ void __launch_bounds__(1024)
-k_mag_f32(const int16_t* __restrict__ coeffs, long long nblocks, unsigned* __restrict__ chunk_sum,
-          int max_chunks, double* __restrict__ out) {
-  __shared__ unsigned s_scan[1024];
-  __shared__ unsigned long long s_base;
-  const int t = threadIdx.x;
-  if (t == 0) s_base = 0;
+// <= 17, so a buffer sum < 2^24) and accumulates the buffer sums in float32.
+// Three parallel passes: per-block nonzero counts with a workgroup scan, the
+// scan of the workgroup totals, then each block adds its terms to the (at most
+// two) buffers its nonzeros fall in; one lane accumulates the buffer sums.
+constexpr int MAG_WG = 256;
+
+__device__ __forceinline__ unsigned block_nz(const int16_t* blk) {
+  const uint4* v = reinterpret_cast<const uint4*>(blk);
+  unsigned n = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 w = v[i];
+    const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) n += ((x[k] & 0xffffu) != 0u) + ((x[k] >> 16) != 0u);
+  }
+  return n;
+}
+
+__global__ void __launch_bounds__(MAG_WG) k_mag_count(const int16_t* __restrict__ coeffs, long long nblocks,
+                                                      unsigned* __restrict__ local_rank, unsigned* __restrict__ wg_tot) {
+  __shared__ unsigned s[MAG_WG];
+  const long long b = (long long)blockIdx.x * MAG_WG + threadIdx.x;
+  const unsigned n = b < nblocks ? block_nz(coeffs + b * 64) : 0u;
+  s[threadIdx.x] = n;
   __syncthreads();
-  for (long long b0 = 0; b0 < nblocks; b0 += 1024) {
-    const long long b = b0 + t;
-    unsigned cnt = 0;
-    if (b < nblocks)
-      for (int i = 0; i < 64; ++i) cnt += coeffs[b * 64 + i] != 0;
-    s_scan[t] = cnt;
+  for (int o = 1; o < MAG_WG; o <<= 1) {  // inclusive Hillis-Steele scan
+    const unsigned v = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0u;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
-      const unsigned v = t >= o ? s_scan[t - o] : 0u;
-      __syncthreads();
-      s_scan[t] += v;
-      __syncthreads();
-    }
-    unsigned long long rank = s_base + s_scan[t] - cnt;
-    if (b < nblocks) {
-      for (int i = 0; i < 64; ++i) {
-        const int q = coeffs[b * 64 + i];
-        if (q) {
-          const int m = q < 0 ? -q : q;
-          const long long ch = (long long)(rank >> 13);
-          if (ch < max_chunks) atomicAdd(&chunk_sum[ch], (unsigned)(33 - __clz(m)));
-          ++rank;
-        }
-      }
-    }
-    __syncthreads();
-    if (t == 1023) s_base += s_scan[1023];
+    s[threadIdx.x] += v;
     __syncthreads();
   }
-  if (t == 0) {
-    const long long nch = (long long)((s_base + 8191) >> 13);
-    float acc = 0.0f;
-    for (long long k = 0; k < nch && k < max_chunks; ++k) acc = acc + (float)chunk_sum[k];
-    *out = (double)acc;
+  if (b < nblocks) local_rank[b] = s[threadIdx.x] - n;
+  if (threadIdx.x == MAG_WG - 1) wg_tot[blockIdx.x] = s[MAG_WG - 1];
+}
+
+// exclusive scan of the workgroup totals in place (one workgroup, 1024-wide steps)
+__global__ void __launch_bounds__(1024) k_mag_scan(unsigned* __restrict__ wg_tot, int nwg) {
+  __shared__ unsigned s[1024];
+  __shared__ unsigned long long s_base;
+  if (threadIdx.x == 0) s_base = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < nwg; b0 += 1024) {
+    const int i = b0 + threadIdx.x;
+    const unsigned n = i < nwg ? wg_tot[i] : 0u;
+    s[threadIdx.x] = n;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const unsigned v = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0u;
+      __syncthreads();
+      s[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (i < nwg) wg_tot[i] = (unsigned)(s_base + s[threadIdx.x] - n);
+    __syncthreads();
+    if (threadIdx.x == 1023) s_base += s[1023];
+    __syncthreads();
   }
 }
 
-hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* chunk_sum, int max_chunks,
-                          double* out, hipStream_t s) {
+__global__ void __launch_bounds__(MAG_WG) k_mag_chunks(const int16_t* __restrict__ coeffs, long long nblocks,
+                                                       const unsigned* __restrict__ local_rank,
+                                                       const unsigned* __restrict__ wg_off,
+                                                       unsigned* __restrict__ chunk_sum, int max_chunks) {
+  const long long b = (long long)blockIdx.x * MAG_WG + threadIdx.x;
+  if (b >= nblocks) return;
+  unsigned long long rank = (unsigned long long)wg_off[blockIdx.x] + local_rank[b];
+  const long long c0 = (long long)(rank >> 13);
+  unsigned acc[2] = {0u, 0u};
+  const uint4* v = reinterpret_cast<const uint4*>(coeffs + b * 64);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 w = v[i];
+    const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = (int)(int16_t)(x[k >> 1] >> (16 * (k & 1)));
+      if (q) {
+        const int m = q < 0 ? -q : q;
+        acc[(long long)(rank >> 13) - c0] += (unsigned)(33 - __clz(m));  // bit length + 1
+        ++rank;
+      }
+    }
+  }
+  if (acc[0] && c0 < max_chunks) atomicAdd(&chunk_sum[c0], acc[0]);
+  if (acc[1] && c0 + 1 < max_chunks) atomicAdd(&chunk_sum[c0 + 1], acc[1]);
+}
+
+__global__ void k_mag_final(const unsigned* __restrict__ chunk_sum, const unsigned* __restrict__ wg_off, int nwg,
+                            const unsigned* __restrict__ wg_last, int max_chunks, double* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long total = (unsigned long long)wg_off[nwg - 1] + *wg_last;  // nonzeros
+  const long long nch = (long long)((total + 8191) >> 13);
+  float acc = 0.0f;
+  for (long long k = 0; k < nch && k < max_chunks; ++k) acc = acc + (float)chunk_sum[k];
+  *out = (double)acc;
+}
+
+// scratch: chunk_sum[max_chunks] | local_rank[nblocks] | wg_tot[nwg] | last wg total
+size_t mag_scratch_bytes(long long nblocks, int max_chunks) {
+  const long long nwg = (nblocks + MAG_WG - 1) / MAG_WG;
+  return sizeof(unsigned) * ((size_t)max_chunks + (size_t)nblocks + (size_t)nwg + 1);
+}
+
+hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* scratch, int max_chunks, double* out,
+                          hipStream_t s) {
+  const int nwg = (int)((nblocks + MAG_WG - 1) / MAG_WG);
+  unsigned* chunk_sum = scratch;
+  unsigned* local_rank = chunk_sum + max_chunks;
+  unsigned* wg_tot = local_rank + nblocks;
+  unsigned* wg_last = wg_tot + nwg;
   hipError_t e = hipMemsetAsync(chunk_sum, 0, sizeof(unsigned) * (size_t)max_chunks, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_mag_f32, dim3(1), dim3(1024), 0, s, coeffs, nblocks, chunk_sum, max_chunks, out);
+  hipLaunchKernelGGL(k_mag_count, dim3(nwg), dim3(MAG_WG), 0, s, coeffs, nblocks, local_rank, wg_tot);
+  if ((e = hipMemcpyAsync(wg_last, wg_tot + nwg - 1, sizeof(unsigned), hipMemcpyDeviceToDevice, s)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(k_mag_scan, dim3(1), dim3(1024), 0, s, wg_tot, nwg);
+  hipLaunchKernelGGL(k_mag_chunks, dim3(nwg), dim3(MAG_WG), 0, s, coeffs, nblocks, local_rank, wg_tot, chunk_sum,
+                     max_chunks);
+  hipLaunchKernelGGL(k_mag_final, dim3(1), dim3(64), 0, s, chunk_sum, wg_tot, nwg, wg_last, max_chunks, out);
   return hipGetLastError();
 }
 
 // ssim_out[0..3] = SSIM of R, G, B, Y; ssim_out[4] = MSE of Y (for PSNR-Y)
 hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, double c1, double c2,
-                            double* scratch_planes /*5*H*W*/, double* scratch_smap /*(H-6)*(W-6)*/,
-                            double* scratch_chunks /*>= ceil(H*W/8192)*/, double* out /*5 doubles*/,
+                            double* scratch_planes /*4*5*H*W*/, double* scratch_smap /*4*(H-6)*(W-6)*/,
+                            double* scratch_chunks /*>= 4*ceil(H*W/8192)*/, double* out /*5 doubles*/,
                             hipStream_t s) {
   SsimConsts k{c1, c2, 49.0 / 48.0};
   const long long ns = (long long)(H - 6) * (W - 6);
   const int nch_s = (int)((ns + NP_BUF - 1) / NP_BUF);
-  for (int c = 0; c < 4; ++c) {
-    hipLaunchKernelGGL(k_uf_axis0, dim3((W + 63) / 64), dim3(64), 0, s, a, b, H, W, c, scratch_planes);
-    hipLaunchKernelGGL(k_uf_axis1_ssim, dim3((H + 63) / 64), dim3(64), 0, s, scratch_planes, H, W, k,
-                       scratch_smap);
-    hipLaunchKernelGGL(k_chunks_smap, dim3(nch_s), dim3(128), 0, s, scratch_smap, ns, scratch_chunks);
-    hipLaunchKernelGGL(k_chunks_final, dim3(1), dim3(64), 0, s, scratch_chunks, nch_s, ns, out + c);
-  }
+  // all four channels at once: planes [c][q][H][W], maps [c][H-6][W-6]
+  hipLaunchKernelGGL(k_uf_axis0, dim3((W + 63) / 64, 5, 4), dim3(64), 0, s, a, b, H, W, scratch_planes);
+  hipLaunchKernelGGL(k_uf_axis1_ssim, dim3((H + 63) / 64, 4), dim3(64), 0, s, scratch_planes, H, W, k, scratch_smap);
+  hipLaunchKernelGGL(k_chunks_smap, dim3(nch_s, 4), dim3(128), 0, s, scratch_smap, ns, scratch_chunks, nch_s);
+  for (int c = 0; c < 4; ++c)
+    hipLaunchKernelGGL(k_chunks_final, dim3(1), dim3(64), 0, s, scratch_chunks + (size_t)c * nch_s, nch_s, ns,
+                       out + c);
   const long long np_ = (long long)H * W;
   const int nch_y = (int)((np_ + NP_BUF - 1) / NP_BUF);
   hipLaunchKernelGGL(k_chunks_ydiff, dim3(nch_y), dim3(128), 0, s, a, b, np_, scratch_chunks);
