@@ -220,32 +220,92 @@ __device__ __forceinline__ void flag_block_bits(const LaneStats& ls, bool valid,
     atomicOr(fixbits + (size_t)item * wpi + (gblk >> 5), 1u << (gblk & 31));
 }
 
-// Wave sums through DPP, then the workgroup's statistics go to this tile's slot
-// of the per-tile partials (plain stores; k_fwd_finish reduces them per frame).
+// Sums of four words over each 16-lane row of a wave: inclusive sums by four
+// DPP row shifts, the four words interleaved so that no DPP read waits on the
+// write before it.
+template <int SH>
+__device__ __forceinline__ void row_shr_add4(unsigned (&v)[4]) {
+  unsigned t[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v[k], 0x110 + SH, 0xf, 0xf, true);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] += t[k];
+}
+__device__ __forceinline__ void row_sums4(unsigned (&v)[4]) {
+  row_shr_add4<1>(v);
+  row_shr_add4<2>(v);
+  row_shr_add4<4>(v);
+  row_shr_add4<8>(v);  // lane 15 of each 16-lane row now holds the row's sums
+}
+
+// The workgroup's statistics into this tile's slot of the per-tile partials
+// (plain stores; k_fwd_reduce_fix reduces them per frame).  Each lane's eight
+// common-bin nibbles (<= 8 each) and nonzero count go into three words of
+// 10-bit fields (a wave sums to <= 512 per field), the magnitude bits into a
+// fourth; four-word row sums, one LDS record per row, and the last wave
+// decodes and adds the waves' rows to the rare bins the quantiser counted.
+// s_st holds NSTAT + 1 words: the last is the waves' ticket counter.
+constexpr int NW_MAX = 8;  // waves per forward workgroup (TF <= 512)
+
 __device__ __forceinline__ void stats_flush(LaneStats ls, bool valid, unsigned* s_st, uint32_t* __restrict__ slot) {
+  __shared__ __attribute__((aligned(16))) unsigned s_wave[NW_MAX][4][4];  // [wave][row][word]
+  __shared__ unsigned s_nvalid[NW_MAX];
   if (!valid) ls = LaneStats();
 #ifdef JDS_PROBE_NOSTATS  // tools/probe: stop before the statistics
   if (ls.hn == 0x12345u && ls.mb == 7u && ls.nz == 3u) slot[0] = 1u;
   return;
 #endif
-  // widen the nibbles to 16-bit fields: (22|26), (24|28), (23|27), (25|29)
-  const unsigned e = ls.hn & 0x0f0f0f0fu, o = (ls.hn >> 4) & 0x0f0f0f0fu;
-  const unsigned w0 = __reduce_add_sync(~0ull, e & 0x00ff00ffu), w1 = __reduce_add_sync(~0ull, (e >> 8) & 0x00ff00ffu);
-  const unsigned w2 = __reduce_add_sync(~0ull, o & 0x00ff00ffu), w3 = __reduce_add_sync(~0ull, (o >> 8) & 0x00ff00ffu);
-  const unsigned wmb = __reduce_add_sync(~0ull, ls.mb), wnz = __reduce_add_sync(~0ull, ls.nz);
+  const unsigned h = ls.hn;
+  unsigned v[4] = {(h & 15u) | ((h >> 4) & 15u) << 10 | ((h >> 8) & 15u) << 20,
+                   ((h >> 12) & 15u) | ((h >> 16) & 15u) << 10 | ((h >> 20) & 15u) << 20,
+                   ((h >> 24) & 15u) | (h >> 28) << 10 | ls.nz << 20, ls.mb};
+  row_sums4(v);
   const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&s_st[0], wnz);
-    atomicAdd(&s_st[1], wmb + wnz);  // magnitude bits = bit length + 1 per nonzero
-    const unsigned zeros = 8u * nvalid - wnz;
-    const unsigned c[8] = {w0 & 0xffffu, w2 & 0xffffu, w1 & 0xffffu, (w3 & 0xffffu) - zeros,
-                           w0 >> 16,     w2 >> 16,     w1 >> 16,     w3 >> 16};
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (c[j]) atomicAdd(&s_st[2 + 22 + j], c[j]);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nw = (int)(blockDim.x >> 6);
+  // no workgroup barrier: the four row-total lanes leave the wave's rows, lane 0
+  // takes a ticket, and the last wave of the workgroup (the LDS performs one
+  // wave's operations in order, so everyone's rows and rare-bin atomics
+  // precede the last ticket) decodes and stores the tile's slot
+  if ((lane & 15) == 15) {
+    *reinterpret_cast<uint4*>(&s_wave[w][lane >> 4][0]) = make_uint4(v[0], v[1], v[2], v[3]);
+    if (lane == 63) s_nvalid[w] = nvalid;
   }
-  __syncthreads();
-  if (threadIdx.x < NSTAT) slot[threadIdx.x] = s_st[threadIdx.x];
+  // (a compiler barrier only: a memory fence would also wait for the wave's
+  // global coefficient stores)
+  __asm__ volatile("" ::: "memory");
+  unsigned ticket = 0u;
+  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
+  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
+  if (ticket != (unsigned)(nw - 1)) return;
+  __asm__ volatile("" ::: "memory");
+  const int t = lane;
+  if (t < NSTAT) {
+    unsigned tot = s_st[t];  // rare bins (quant8's LDS atomics)
+    for (int i = 0; i < nw; ++i) {
+      unsigned wv[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint4 x = *reinterpret_cast<const uint4*>(&s_wave[i][r][0]);
+        wv[0] += x.x;
+        wv[1] += x.y;
+        wv[2] += x.z;
+        wv[3] += x.w;
+      }
+      const unsigned nz = (wv[2] >> 20) & 1023u;
+      if (t == 0) {
+        tot += nz;
+      } else if (t == 1) {
+        tot += wv[3] + nz;  // magnitude bits = bit length + 1 per nonzero
+      } else if (t >= 2 + 22 && t < 2 + 30) {
+        const int b = t - 2 - 22;  // common bin 22 + b: word b / 3, field b % 3
+        unsigned c = (wv[b / 3] >> (10 * (b % 3))) & 1023u;
+        if (b == 3) c -= 8u * s_nvalid[i] - nz;  // zeros fall in bin 25: k_finalize adds them
+        tot += c;
+      }
+    }
+    slot[t] = tot;
+  }
 }
 
 // ---- general tiles ------------------------------------------------------------
@@ -276,7 +336,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   __shared__ __attribute__((aligned(16))) float s_u[U_F];
   __shared__ __attribute__((aligned(16))) float s_rq[64];
   __shared__ __attribute__((aligned(16))) float s_thr[2][64];
-  __shared__ unsigned s_st[NSTAT];
+  __shared__ unsigned s_st[NSTAT + 1];  // + stats_flush's ticket
 
   const int tid = threadIdx.x;
   const int frame = blockIdx.y;
@@ -319,7 +379,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
     s_thr[0][tid] = fq[frame].thr[0][tid];
     s_thr[1][tid] = fq[frame].thr[1][tid];
   }
-  if (tid < NSTAT) s_st[tid] = 0u;
+  if (tid <= NSTAT) s_st[tid] = 0u;
 
   const int blk = tid >> 3, line = tid & 7;
   int plane, by_t, bx_t;
@@ -525,7 +585,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   __shared__ __attribute__((aligned(16))) float s_cd[NCD * BS32];   // chroma blocks after the row DCT
   __shared__ __attribute__((aligned(16))) float s_rqT[64];          // 1/Q transposed: [v][k]
   __shared__ __attribute__((aligned(16))) float s_thT[2][64];
-  __shared__ unsigned s_st[NSTAT];
+  __shared__ unsigned s_st[NSTAT + 1];  // + stats_flush's ticket
 
   const int tid = threadIdx.x, frame = blockIdx.y;
   const int ncol = rect.w - rect.z + 1;
@@ -546,7 +606,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     s_thT[0][tid] = fq[frame].thr[0][t];
     s_thT[1][tid] = fq[frame].thr[1][t];
   }
-  if (tid < NSTAT) s_st[tid] = 0u;
+  if (tid <= NSTAT) s_st[tid] = 0u;
   const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
   float* s_cb = s_c;
   float* s_cr = s_c + CR * TW;
