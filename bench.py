@@ -49,7 +49,10 @@ def parse():
     ap.add_argument('--mode', default='4:2:0')
     ap.add_argument('--prefilter', type=int, default=1)
     ap.add_argument('--block', type=int, default=8, choices=(8, 16),
-                    help='16 = the configs[4] 16x16 stretch path (jds_b16.hip, exact fp64 kernels)')
+                    help='16 = the configs[4] 16x16 stretch path (jds_fast16.hip certified fp32 forward, '
+                         'jds_b16.hip fp64 inverse)')
+    ap.add_argument('--exact', action='store_true',
+                    help='all-fp64 kernels (JDS_RUN_EXACT) instead of the certified fast ones (A/B)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=20.0,
                     help='CPU budget over the 4 legs (faithful / vectorised x 1 core / pool)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -381,6 +384,8 @@ def main():
     fwd_done = [torch.cuda.Event() for _ in range(NS)]
     used = [False] * NS
 
+    xflags = _abi.RUN_EXACT if args.exact else 0
+
     def ptrs(b):
         return (rgbs[b].data_ptr(), outs[b].data_ptr(), coefs[b].data_ptr(), stats_l[b].data_ptr())
 
@@ -392,14 +397,14 @@ def main():
         used[b] = True
         if ev is not None:
             ev[0].record(s_f)
-        plans[b].run(*ptrs(b), _abi.RUN_FWD, s_f.cuda_stream)
+        plans[b].run(*ptrs(b), _abi.RUN_FWD | xflags, s_f.cuda_stream)
         if ev is not None:
             ev[1].record(s_f)
         fwd_done[b].record(s_f)
         si.wait_event(fwd_done[b])
         if ev is not None:
             ev[2].record(si)
-        plans[b].run(*ptrs(b), _abi.RUN_INV, si.cuda_stream)
+        plans[b].run(*ptrs(b), _abi.RUN_INV | xflags, si.cuda_stream)
         if ev is not None:
             ev[3].record(si)
         done_inv[b].record(si)
@@ -408,7 +413,7 @@ def main():
         if NS > 1:
             step(k)
         else:  # both phases in one call on one stream: no events inside the timed region
-            plans[0].run(*ptrs(0), 0, s_f.cuda_stream)
+            plans[0].run(*ptrs(0), xflags, s_f.cuda_stream)
 
     nwarm = prewarm(run_step, args.warmup, dev)
     if world > 1:
@@ -448,7 +453,10 @@ def main():
     mcode = {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[args.mode]
     pfs = 'true' if (args.prefilter and mcode != 0) else 'false'
     if args.block == 16:
-        kname = f'k_fwd16<{mcode},{pfs}>' if dom == 'k_fwd' else f'k_chroma16<{mcode}> + k_inv16<{mcode}>'
+        if dom == 'k_fwd':
+            kname = f'k_fwd16<{mcode},{pfs}>' if args.exact else f'k_fwd16f<{mcode},{pfs}> + k_fix_fwd16<{mcode},{pfs}>'
+        else:
+            kname = f'k_inv16f<{mcode},0>' if mcode else f'k_chroma16<{mcode}> + k_inv16<{mcode}>'
     else:
         kname = (f'k_fwd32i<{mcode},{pfs}> + k_fwd32<{mcode},{pfs}> (border tiles) + k_fix_fwd'
                  if dom == 'k_fwd' else f'k_inv2<{mcode},0>')

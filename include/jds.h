@@ -41,8 +41,10 @@ extern "C" {
 #define JDS_RUN_EXACT 8u /* all-fp64 kernels (default: certified fp32 + exact fp64 fix-up, same results) */
 #define JDS_RUN_EXACT_INV 16u /* inverse only: the replayed-order fp64 kernel instead of the certified fast
                                  inverse + tile fix-up (same bytes; A/B and tests) */
-#define JDS_RUN_INV_FIXALL 32u /* test: the certified fast inverse lists every tile, so the exact
-                                  list kernel recomputes the whole frame (exercises the fix-up path) */
+#define JDS_RUN_INV_FIXALL 32u /* test: the certified fast inverse flags every tile, so the exact
+                                  tile code recomputes the whole frame (exercises the fix-up path) */
+#define JDS_RUN_FWD_FIXALL 64u /* test, 16x16 plans: the certified fp32 forward lists every block, so
+                                  k_fix_fwd16 recomputes the whole frame (exercises the fix-up path) */
 
 typedef struct jds_ctx jds_ctx;    /* one per (thread, device): owns a HIP stream + scratch */
 typedef struct jds_plan jds_plan;  /* fixed geometry + per-frame quant tables, device-resident */
@@ -221,6 +223,11 @@ int jds_selftest_dct16x16(const double* in, double* out, int64_t n, int32_t inve
  * bound[64] = the rigorous bound on |c_fp32 - c_exact| the kernels certify
  * with (fast_fwd_bounds).  Lets the CPU suite test the bound adversarially. */
 int jds_selftest_fwd32(int32_t subsampling, int32_t prefilter, const double* gauss, const uint8_t* rgb, int64_t H,
+                       int64_t W, int32_t plane, int32_t rows_first, float* coeffs, double* bound);
+/* The same for the certified 16x16 forward (jds_fast16.hip: fdct16_f32, plane
+ * size a multiple of 16; rows_first 0 = k_fwd16f's order): n_blocks x 256 f32
+ * coefficients and bound[256] (fast_fwd16_bounds). */
+int jds_selftest_fwd16(int32_t subsampling, int32_t prefilter, const double* gauss, const uint8_t* rgb, int64_t H,
                        int64_t W, int32_t plane, int32_t rows_first, float* coeffs, double* bound);
 
 /* Test-only: the host-built cv2 INTER_AREA table of one axis (OpenCV

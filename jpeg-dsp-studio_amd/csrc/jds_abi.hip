@@ -71,7 +71,12 @@ hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* cons
 hipError_t launch_codec16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                           int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st, double* part,
                           double* planes, bool want_sse, double* err_y, double* err_rgb, hipStream_t s,
-                          hipEvent_t* ev, int phases);
+                          hipEvent_t* ev, int phases, const Fwd16Fast* ff);
+void fast_fwd16_bounds(int mode, bool pf, const double* gk, double* E);
+void fast_fwd16_thresholds(const double* Q8, int mode, bool pf, const double* gk, void* out);
+size_t fast_q16_size();
+int fwd16_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
+                     bool rows_first, float* out);
 }
 
 // skimage: C1 = (K1 * R) ** 2, C2 = (K2 * R) ** 2 with R = data_range = 255
@@ -155,6 +160,7 @@ struct jds_plan {
   DevBuf invfix;  // certified fast inverse: run and per-item counters (InvFix, jds_inv_fast.hip)
   unsigned inv_runs = 0;  // fast-inverse runs so far: picks the list counter (InvFix::parity)
   bool last_inv_fast = false;  // the last run's inverse was the certified fast one
+  bool last_fwd16_fast = false;  // 16x16: the last forward was the certified fp32 one
   InvFix inv_fix() const {
     return {(unsigned*)invfix.p, (unsigned*)invfix.p + 16, 0, (int)(inv_runs & 1u), (int)(inv_runs % 3u),
             (int)(inv_runs % 16u == 15u)};
@@ -453,12 +459,30 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
       return rc;
     }
   } else if (g.bs == 16) {
-    // 16x16 stretch path: exact fp64 kernels only (jds_b16.hip); chroma planes scratch
-    if ((e = p->planes.ensure(sizeof(double) * 2 * (size_t)n * g.hc * g.wc)) != hipSuccess ||
-        (e = p->counters.ensure(64)) != hipSuccess) {
+    // 16x16 stretch path (jds_b16.hip, jds_fast16.hip): chroma planes scratch
+    // (4:4:4 inverse), the certified forward's fp32 tables, fix-up list, counters
+    const size_t fqs = fast_q16_size();
+    char* h16 = (char*)malloc(fqs * (size_t)n);
+    if (!h16) {
+      jds_plan_destroy(p);
+      return fail(JDS_ENOMEM, "host allocation failed");
+    }
+    for (int i = 0; i < n; ++i) fast_fwd16_thresholds(params[i].qtable, mode, pf, params[i].gauss, h16 + fqs * i);
+    const float gk32[3] = {(float)params[0].gauss[0], (float)params[0].gauss[1], (float)params[0].gauss[2]};
+    const size_t nblk = (size_t)n * (size_t)(g.cpf / 256);
+    if ((e = p->planes.ensure(mode == JDS_SS_444 ? sizeof(double) * 2 * (size_t)n * g.hc * g.wc : 8)) !=
+            hipSuccess ||
+        (e = p->fq32.ensure(fqs * n)) != hipSuccess || (e = p->gk32.ensure(sizeof gk32)) != hipSuccess ||
+        (e = p->fixlist.ensure(8 * nblk)) != hipSuccess || (e = p->counters.ensure(64)) != hipSuccess ||
+        (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * g.tiles_y * g.tiles_x)) != hipSuccess ||
+        (e = hipMemcpy(p->fq32.p, h16, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemset(p->counters.p, 0, 64)) != hipSuccess) {
+      free(h16);
       jds_plan_destroy(p);
       return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
     }
+    free(h16);
   } else {
     const size_t fqs = fast_q_size();
     char* h32 = (char*)malloc(fqs * (size_t)n);
@@ -511,7 +535,14 @@ int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   // counters[n, 2n): blocks the last run's k_fix_fwd recomputed, per item;
   // invfix[0]: tiles the last run's certified inverse handed to the exact kernel
   counts[0] = counts[1] = 0u;
-  if (p->g.bs == 16 || p->g.gen || p->counters.n < 8 * (size_t)p->n) return JDS_OK;
+  if (p->g.bs == 16) {  // counters[2]: blocks the last certified 16x16 forward recomputed
+    if (!p->last_fwd16_fast) return JDS_OK;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(counts, (const uint32_t*)p->counters.p + 2, 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail(JDS_EHIP, "fix_counts: %s", hipGetErrorString(e));
+    return JDS_OK;
+  }
+  if (p->g.gen || p->counters.n < 8 * (size_t)p->n) return JDS_OK;
   uint32_t* c = (uint32_t*)malloc(4 * (size_t)p->n + 4);
   if (!c) return fail(JDS_ENOMEM, "fix_counts: host allocation");
   // the last run may be in flight on any stream: wait for the device first
@@ -555,13 +586,15 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
     return JDS_OK;
   }
   if (p->g.bs == 16) {
-    if (phases & 1) {
-      HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
-      HIP_TRY(hipMemsetAsync(p->counters.p, 0, 64, s));
-    }
+    // the certified fp32 forward unless JDS_RUN_EXACT (k_fix_fwd16 re-arms its counters)
+    const Fwd16Fast ff{p->fq32.p, (const float*)p->gk32.p, (uint32_t*)p->part32.p, (uint2*)p->fixlist.p,
+                       (unsigned*)p->counters.p,
+                       (flags & JDS_RUN_FWD_FIXALL) ? 1 : 0};
+    if (phases & 1) HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
     HIP_TRY(launch_codec16(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                            (const double*)p->gk.p, stats, (double*)p->part.p, (double*)p->planes.p,
-                           (flags & JDS_RUN_SSE) != 0, nullptr, nullptr, s, nullptr, phases));
+                           (flags & JDS_RUN_SSE) != 0, nullptr, nullptr, s, nullptr, phases, exact ? nullptr : &ff));
+    if (phases & 1) p->last_fwd16_fast = !exact;
     return JDS_OK;
   }
   if (phases & 1) {
@@ -683,7 +716,7 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
     HIP_TRY(launch_codec16(mode, pf, g, 1, (const uint8_t*)c->rgb.p, (uint8_t*)c->out.p, (int16_t*)c->coeffs.p,
                            (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
                            (double*)c->part.p, (double*)c->planes.p, true, maps ? (double*)c->erry.p : nullptr,
-                           maps ? (double*)c->errrgb.p : nullptr, s, c->ev, 3));
+                           maps ? (double*)c->errrgb.p : nullptr, s, c->ev, 3, nullptr));
   } else
   HIP_TRY(launch_codec(mode, pf, g, 1, (const uint8_t*)c->rgb.p, (uint8_t*)c->out.p, (int16_t*)c->coeffs.p,
                        (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
@@ -1033,6 +1066,20 @@ int jds_selftest_fwd32(int32_t subsampling, int32_t prefilter, const double* gau
   memcpy(bound, E + (plane ? 64 : 0), 64 * sizeof(double));
   if (fwd32_host_plane(subsampling, pf, gauss, rgb, (int)H, (int)W, plane, rows_first != 0, coeffs))
     return fail(JDS_EINVAL, "plane size must be a multiple of 8");
+  return JDS_OK;
+}
+
+int jds_selftest_fwd16(int32_t subsampling, int32_t prefilter, const double* gauss, const uint8_t* rgb, int64_t H,
+                       int64_t W, int32_t plane, int32_t rows_first, float* coeffs, double* bound) {
+  if (!gauss || !rgb || !coeffs || !bound || H < 1 || W < 1 || H > 4096 || W > 4096 || plane < 0 || plane > 2 ||
+      subsampling < JDS_SS_444 || subsampling > JDS_SS_420)
+    return fail(JDS_EINVAL, "bad argument");
+  const bool pf = prefilter != 0 && subsampling != JDS_SS_444;
+  double E[512];
+  fast_fwd16_bounds(subsampling, pf, gauss, E);
+  memcpy(bound, E + (plane ? 256 : 0), 256 * sizeof(double));
+  if (fwd16_host_plane(subsampling, pf, gauss, rgb, (int)H, (int)W, plane, rows_first != 0, coeffs))
+    return fail(JDS_EINVAL, "plane size must be a multiple of 16");
   return JDS_OK;
 }
 

@@ -776,6 +776,10 @@ hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uin
                              hipStream_t s);
 hipError_t launch_finalize(const Geo& g, int n, jds_frame_stats* st, const double* part, int tiles, bool with_sse,
                            hipStream_t s);
+hipError_t launch_fast_fwd16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
+                             const FrameQ* fq, const void* fq16, const double* gk, const float* gk32,
+                             jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* counters, int fix_all,
+                             hipStream_t s);
 
 // tiles of the fused 16x16 inverse (sse_y partials per tile); 0 for 4:4:4
 int inv16_tiles(int mode, int H, int W) {
@@ -798,17 +802,20 @@ template <int MODE>
 static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs,
                              const FrameQ* fq, const double* gk, jds_frame_stats* st, double* part, double* planes,
                              bool want_sse, double* err_y, double* err_rgb, hipStream_t s, hipEvent_t* ev,
-                             int phases) {
+                             int phases, const Fwd16Fast* ff) {
   using C = Cfg16<MODE>;
   const dim3 grid(g.tiles_y * g.tiles_x, n);
   hipError_t e = hipSuccess;
   if (phases & 1) {
     if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
-    if (MODE != M444 && pf)
+    if (ff)  // certified fp32 forward + exact fix-up of the listed blocks (jds_fast16.hip)
+      e = launch_fast_fwd16(MODE, pf, g, n, rgb, coeffs, fq, ff->fq16, gk, ff->gk32, st, ff->part, ff->fixlist, ff->counters,
+                            ff->fix_all, s);
+    else if (MODE != M444 && pf)
       hipLaunchKernelGGL((k_fwd16<MODE, (MODE != M444)>), grid, dim3(C::TF), 0, s, g, rgb, coeffs, fq, gk, st);
     else
       hipLaunchKernelGGL((k_fwd16<MODE, false>), grid, dim3(C::TF), 0, s, g, rgb, coeffs, fq, gk, st);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_fwd_finish(g, n, st, nullptr, 0, s)) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
   }
@@ -844,21 +851,22 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
   return e;
 }
 
-// phases: bit 0 forward, bit 1 inverse (chroma planes + tiles + finalize)
+// phases: bit 0 forward, bit 1 inverse (chroma planes + tiles + finalize);
+// ff: the certified fp32 forward's buffers, nullptr = the exact fp64 forward
 hipError_t launch_codec16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                           int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st, double* part,
                           double* planes, bool want_sse, double* err_y, double* err_rgb, hipStream_t s,
-                          hipEvent_t* ev, int phases) {
+                          hipEvent_t* ev, int phases, const Fwd16Fast* ff) {
   switch (mode) {
     case M420:
       return launch16_t<M420>(pf, g, n, rgb, rgb_out, coeffs, fq, gk, st, part, planes, want_sse, err_y, err_rgb,
-                              s, ev, phases);
+                              s, ev, phases, ff);
     case M422:
       return launch16_t<M422>(pf, g, n, rgb, rgb_out, coeffs, fq, gk, st, part, planes, want_sse, err_y, err_rgb,
-                              s, ev, phases);
+                              s, ev, phases, ff);
     default:
       return launch16_t<M444>(false, g, n, rgb, rgb_out, coeffs, fq, gk, st, part, planes, want_sse, err_y,
-                              err_rgb, s, ev, phases);
+                              err_rgb, s, ev, phases, ff);
   }
 }
 

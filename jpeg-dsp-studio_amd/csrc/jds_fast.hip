@@ -20,6 +20,7 @@
 #include "jds_dct8.hpp"
 #include "jds_device.hpp"
 #include "jds_internal.hpp"
+#include "jds_fwd_common.hpp"
 
 #pragma clang fp contract(off)
 
@@ -54,22 +55,6 @@ __host__ __device__ __forceinline__ void fdct8_f32(float (&x)[8]) {
   }
 }
 
-// fp32 colour conversions (any rounding order is fine: bounded on the host)
-__host__ __device__ __forceinline__ float luma32(float R, float G, float B) {
-  return fmaf(0.114f, B, fmaf(0.587f, G, 0.299f * R));
-}
-// luma - 128 with the level shift folded into the chain: three roundings of
-// magnitude <= 128 instead of luma32's, inside fwd_input_error's luma bound
-__host__ __device__ __forceinline__ float luma32m(float R, float G, float B) {
-  return fmaf(0.114f, B, fmaf(0.587f, G, fmaf(0.299f, R, -128.0f)));
-}
-__host__ __device__ __forceinline__ float cb32(float R, float G, float B) {
-  return fmaf(-0.168736f, R, fmaf(-0.331264f, G, fmaf(0.5f, B, 128.0f)));
-}
-__host__ __device__ __forceinline__ float cr32(float R, float G, float B) {
-  return fmaf(-0.081312f, B, fmaf(-0.418688f, G, fmaf(0.5f, R, 128.0f)));
-}
-
 __device__ __forceinline__ void unpack32(uint32_t v, float& R, float& G, float& B) {
   R = (float)(v & 255u);
   G = (float)((v >> 8) & 255u);
@@ -90,7 +75,6 @@ constexpr int BS32 = 72;  // floats per 8x8 block in LDS (column writes conflict
 // sample index mod 4 puts them on 4 different slots (MI355X_MICROARCH.md §LDS).
 template <int SY>
 __device__ __forceinline__ int csw(int row) { return (row / SY) & 3; }
-constexpr int NSTAT = 52; // per-tile statistics: nonzero, magnitude bits, hist[50]
 
 __device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[6], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255u; }
 
@@ -218,24 +202,6 @@ __device__ __forceinline__ void flag_block_bits(const LaneStats& ls, bool valid,
   const int lane = threadIdx.x & 63;
   if (valid && line == 0 && ((fm >> (lane & ~7)) & 0xffull))
     atomicOr(fixbits + (size_t)item * wpi + (gblk >> 5), 1u << (gblk & 31));
-}
-
-// Sums of four words over each 16-lane row of a wave: inclusive sums by four
-// DPP row shifts, the four words interleaved so that no DPP read waits on the
-// write before it.
-template <int SH>
-__device__ __forceinline__ void row_shr_add4(unsigned (&v)[4]) {
-  unsigned t[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) t[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v[k], 0x110 + SH, 0xf, 0xf, true);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) v[k] += t[k];
-}
-__device__ __forceinline__ void row_sums4(unsigned (&v)[4]) {
-  row_shr_add4<1>(v);
-  row_shr_add4<2>(v);
-  row_shr_add4<4>(v);
-  row_shr_add4<8>(v);  // lane 15 of each 16-lane row now holds the row's sums
 }
 
 // The workgroup's statistics into this tile's slot of the per-tile partials
@@ -821,52 +787,6 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   }
 }
 
-// ---- exact fp64 recomputation of one block column from global memory ----
-
-__device__ __forceinline__ double px_chroma64(const uint8_t* img, const Geo& g, int y, int x, int plane) {
-  const uint8_t* p = img + ((size_t)y * g.W + x) * 3;
-  const double R = p[0], G = p[1], B = p[2];
-  return plane == 1 ? chroma_b(R, G, B) : chroma_r(R, G, B);
-}
-
-// cv2 RowFilter<double> at (y, x), BORDER_REFLECT_101
-__device__ double row_pass64(const uint8_t* img, const Geo& g, int y, int x, int plane, const double* k) {
-  double t = k[0] * px_chroma64(img, g, y, reflect101(x - 1, g.W), plane);
-  t = t + k[1] * px_chroma64(img, g, y, x, plane);
-  return t + k[2] * px_chroma64(img, g, y, reflect101(x + 1, g.W), plane);
-}
-
-template <int MODE, bool PF>
-__device__ double sample64(const uint8_t* img, const Geo& g, int plane, int pr, int pc, const double* k) {
-  if (plane == 0 || MODE == M444) {
-    const int y = reflect_pad(pr, g.H), x = reflect_pad(pc, g.W);
-    const uint8_t* p = img + ((size_t)y * g.W + x) * 3;
-    const double R = p[0], G = p[1], B = p[2];
-    return plane == 0 ? luma(R, G, B) : (plane == 1 ? chroma_b(R, G, B) : chroma_r(R, G, B));
-  }
-  constexpr int SY = Cfg<MODE>::SY;
-  const int sr = reflect_pad(pr, g.hc), sc = reflect_pad(pc, g.wc);
-  double s[SY][2];
-#pragma unroll 1
-  for (int a = 0; a < SY; ++a) {
-#pragma unroll 1
-    for (int b = 0; b < 2; ++b) {
-      const int y = SY * sr + a, x = 2 * sc + b;
-      if constexpr (PF) {
-        const double d = k[1] * row_pass64(img, g, y, x, plane, k) + 0.0;
-        s[a][b] = d + k[0] * (row_pass64(img, g, reflect101(y + 1, g.H), x, plane, k) +
-                              row_pass64(img, g, reflect101(y - 1, g.H), x, plane, k));
-      } else {
-        s[a][b] = px_chroma64(img, g, y, x, plane);
-      }
-    }
-  }
-  if constexpr (SY == 2)
-    return (((s[0][0] + s[0][1]) + s[1][0]) + s[1][1]) * 0.25;
-  else
-    return (s[0][0] + s[0][1]) * 0.5;
-}
-
 // End of the certified forward's producer launches: the statistics partials
 // into the frame stats (reduce_partials), then (sweep plans) bitmap -> list:
 // each wave takes 64 bitmap words of the workgroup's share of item f's
@@ -1334,7 +1254,7 @@ hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const
 // |W_k0..3| (the magnitudes the FMA chain can reach), the b_k term covering the
 // fp32 representation error of W (<= u|W|).  Axis 0 then axis 1.
 
-static void pass_bound(double X, double e, const double* Xin, const double* ein, double* Xout, double* eout,
+void pass_bound(double X, double e, const double* Xin, const double* ein, double* Xout, double* eout,
                        const double W[8][4]) {
   const double u = 0x1p-24;
   for (int k = 0; k < 8; ++k) {
@@ -1350,7 +1270,7 @@ static void pass_bound(double X, double e, const double* Xin, const double* ein,
   }
 }
 
-static double fwd_input_error(int plane, int mode, bool pf, const double* gk) {
+double fwd_input_error(int plane, int mode, bool pf, const double* gk) {
   const double u = 0x1p-24;
   // luma32: fmaf(kb, B, fmaf(kg, G, kr*R)); constants in fp32; then -128
   const double dkl = fabs((double)0.299f - 0.299) + fabs((double)0.587f - 0.587) + fabs((double)0.114f - 0.114);

@@ -1,0 +1,702 @@
+// jds_fast16.hip — the certified fp32 forward for 16x16 blocks (BASELINE
+// configs[4] stretch): the 8x8 path's scheme (jds_fast.hip) with 16-point
+// transforms.  Colour, prefilter, area average and the 16x16 DCT run in fp32;
+// a host-derived rigorous bound E_uv on |c_fp32 - c_exact| per coefficient
+// (fast_fwd16_thresholds: fwd_input_error for the samples, then two passes of
+// 8-term FMA chains) decides whether round-half-even(c / Q16) is certain.
+// Blocks with an uncertain coefficient are listed; k_fix_fwd16 recomputes them
+// with the exact fp64 chain of k_fwd16 (jds_b16.hip: every sample exactly from
+// global memory, pocketfft's 16-point DCT-II) and corrects the statistics by
+// delta.  Results are bit-identical to k_fwd16 and to the oracle with the
+// kron(Q8, ones(2,2)) table (engines/pipeline.py:47-63 with block_size 16).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "jds_dct16.hpp"
+#include "jds_device.hpp"
+#include "jds_fwd_common.hpp"
+#include "jds_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace jds {
+
+// orthonormal 16-point DCT-II rows restricted to i = 0..7, rounded to fp32:
+// W16[k][i] = s(k) cos((2i+1) k pi / 32), s(0) = 1/4, s(k) = sqrt(2/16); even
+// rows act on s_i = x_i + x_{15-i}, odd rows on d_i = x_i - x_{15-i}
+static constexpr float W16[16][8] = {
+    {0x1.0000000000000p-2f, 0x1.0000000000000p-2f, 0x1.0000000000000p-2f, 0x1.0000000000000p-2f, 0x1.0000000000000p-2f, 0x1.0000000000000p-2f, 0x1.0000000000000p-2f, 0x1.0000000000000p-2f},
+    {0x1.684b9c0000000p-2f, 0x1.5a730c0000000p-2f, 0x1.3f4a240000000p-2f, 0x1.17dc140000000p-2f, 0x1.cb598c0000000p-3f, 0x1.5553e40000000p-3f, 0x1.a4608a0000000p-4f, 0x1.1be3520000000p-5f},
+    {0x1.63150c0000000p-2f, 0x1.2d062e0000000p-2f, 0x1.92469c0000000p-3f, 0x1.1a855e0000000p-4f, -0x1.1a855e0000000p-4f, -0x1.92469c0000000p-3f, -0x1.2d062e0000000p-2f, -0x1.63150c0000000p-2f},
+    {0x1.5a730c0000000p-2f, 0x1.cb598c0000000p-3f, 0x1.1be3520000000p-5f, -0x1.5553e40000000p-3f, -0x1.3f4a240000000p-2f, -0x1.684b9c0000000p-2f, -0x1.17dc140000000p-2f, -0x1.a4608a0000000p-4f},
+    {0x1.4e7aea0000000p-2f, 0x1.1517a80000000p-3f, -0x1.1517a80000000p-3f, -0x1.4e7aea0000000p-2f, -0x1.4e7aea0000000p-2f, -0x1.1517a80000000p-3f, 0x1.1517a80000000p-3f, 0x1.4e7aea0000000p-2f},
+    {0x1.3f4a240000000p-2f, 0x1.1be3520000000p-5f, -0x1.17dc140000000p-2f, -0x1.5a730c0000000p-2f, -0x1.a4608a0000000p-4f, 0x1.cb598c0000000p-3f, 0x1.684b9c0000000p-2f, 0x1.5553e40000000p-3f},
+    {0x1.2d062e0000000p-2f, -0x1.1a855e0000000p-4f, -0x1.63150c0000000p-2f, -0x1.92469c0000000p-3f, 0x1.92469c0000000p-3f, 0x1.63150c0000000p-2f, 0x1.1a855e0000000p-4f, -0x1.2d062e0000000p-2f},
+    {0x1.17dc140000000p-2f, -0x1.5553e40000000p-3f, -0x1.5a730c0000000p-2f, 0x1.1be3520000000p-5f, 0x1.684b9c0000000p-2f, 0x1.a4608a0000000p-4f, -0x1.3f4a240000000p-2f, -0x1.cb598c0000000p-3f},
+    {0x1.0000000000000p-2f, -0x1.0000000000000p-2f, -0x1.0000000000000p-2f, 0x1.0000000000000p-2f, 0x1.0000000000000p-2f, -0x1.0000000000000p-2f, -0x1.0000000000000p-2f, 0x1.0000000000000p-2f},
+    {0x1.cb598c0000000p-3f, -0x1.3f4a240000000p-2f, -0x1.a4608a0000000p-4f, 0x1.684b9c0000000p-2f, -0x1.1be3520000000p-5f, -0x1.5a730c0000000p-2f, 0x1.5553e40000000p-3f, 0x1.17dc140000000p-2f},
+    {0x1.92469c0000000p-3f, -0x1.63150c0000000p-2f, 0x1.1a855e0000000p-4f, 0x1.2d062e0000000p-2f, -0x1.2d062e0000000p-2f, -0x1.1a855e0000000p-4f, 0x1.63150c0000000p-2f, -0x1.92469c0000000p-3f},
+    {0x1.5553e40000000p-3f, -0x1.684b9c0000000p-2f, 0x1.cb598c0000000p-3f, 0x1.a4608a0000000p-4f, -0x1.5a730c0000000p-2f, 0x1.17dc140000000p-2f, 0x1.1be3520000000p-5f, -0x1.3f4a240000000p-2f},
+    {0x1.1517a80000000p-3f, -0x1.4e7aea0000000p-2f, 0x1.4e7aea0000000p-2f, -0x1.1517a80000000p-3f, -0x1.1517a80000000p-3f, 0x1.4e7aea0000000p-2f, -0x1.4e7aea0000000p-2f, 0x1.1517a80000000p-3f},
+    {0x1.a4608a0000000p-4f, -0x1.17dc140000000p-2f, 0x1.684b9c0000000p-2f, -0x1.3f4a240000000p-2f, 0x1.5553e40000000p-3f, 0x1.1be3520000000p-5f, -0x1.cb598c0000000p-3f, 0x1.5a730c0000000p-2f},
+    {0x1.1a855e0000000p-4f, -0x1.92469c0000000p-3f, 0x1.2d062e0000000p-2f, -0x1.63150c0000000p-2f, 0x1.63150c0000000p-2f, -0x1.2d062e0000000p-2f, 0x1.92469c0000000p-3f, -0x1.1a855e0000000p-4f},
+    {0x1.1be3520000000p-5f, -0x1.a4608a0000000p-4f, 0x1.5553e40000000p-3f, -0x1.cb598c0000000p-3f, 0x1.17dc140000000p-2f, -0x1.3f4a240000000p-2f, 0x1.5a730c0000000p-2f, -0x1.684b9c0000000p-2f},
+};
+
+// 8 add/sub + 16 eight-term FMA chains (the host bound follows this sequence)
+__host__ __device__ __forceinline__ void fdct16_f32(float (&x)[16]) {
+  float sd[2][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sd[0][i] = x[i] + x[15 - i];
+    sd[1][i] = x[i] - x[15 - i];
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float* v = sd[k & 1];
+    float a = W16[k][0] * v[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) a = fmaf(W16[k][i], v[i], a);
+    x[k] = a;
+  }
+}
+
+struct FastQ16 {
+  float rq[256];      // fp32(1 / Q16)
+  float thr[2][256];  // certification limits on |t - rint(t)|: [0] luma, [1] chroma
+};
+
+template <int MODE>
+struct Cfg16F {
+  static constexpr int SY = (MODE == M420) ? 2 : 1;
+  static constexpr int SX = (MODE == M444) ? 1 : 2;
+  static constexpr int MH = 16 * SY, MW = 16 * SX;
+  static constexpr int TH = 2 * MH, TW = 64;  // jds_b16.hip's Cfg16 tiles (Geo tiles_y / tiles_x)
+  static constexpr int MY = TH / MH, MX = TW / MW;
+  static constexpr int YBR = TH / 16, YBC = TW / 16;
+  static constexpr int CBR = MY, CBC = MX;
+  static constexpr int NYB = YBR * YBC, NCB = CBR * CBC;
+  static constexpr int NB = NYB + 2 * NCB;
+  static constexpr int TF = NB * 16;  // one thread per block column
+};
+
+constexpr int BS16F = 272;  // floats per 16x16 block in LDS (256 + 16 pad: column writes spread over banks)
+
+// The workgroup's statistics into its tile's slot of the per-tile partials
+// (k_fwd_reduce sums them per frame): each lane's 8 common-bin counts (two
+// nibble words, <= 16 per bin together) and nonzero count into three words of
+// 10-bit fields, the magnitude bits into a fourth; DPP row sums (<= 256 per
+// field over a 16-lane row, decoded per row), one LDS record per row, and the
+// workgroup's last wave (ticket in s_st[NSTAT]; the LDS performs a wave's
+// operations in order, so every row record and rare-bin atomic precedes the
+// last ticket) decodes them and adds the rare bins.  Zeros are not binned here:
+// k_fwd_finish / k_finalize add bin 25's zeros from the nonzero count.
+constexpr int NW16 = 6;  // waves per k_fwd16f workgroup (TF <= 384)
+
+__device__ __forceinline__ void stats_flush16(unsigned h0, unsigned h1, unsigned nz, unsigned mb, bool valid,
+                                              unsigned* s_st, uint32_t* __restrict__ slot) {
+  __shared__ __attribute__((aligned(16))) unsigned s_row[NW16][4][4];  // [wave][row][word]
+  __shared__ unsigned s_nvalid[NW16];
+  const unsigned e = (h0 & 0x0f0f0f0fu) + (h1 & 0x0f0f0f0fu);                 // bins 0, 2, 4, 6 (bytes)
+  const unsigned o = ((h0 >> 4) & 0x0f0f0f0fu) + ((h1 >> 4) & 0x0f0f0f0fu);   // bins 1, 3, 5, 7
+  unsigned v[4] = {(e & 255u) | (o & 255u) << 10 | ((e >> 8) & 255u) << 20,
+                   ((o >> 8) & 255u) | ((e >> 16) & 255u) << 10 | ((o >> 16) & 255u) << 20,
+                   (e >> 24) | (o >> 24) << 10 | nz << 20, mb};
+  row_sums4(v);
+  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nw = (int)(blockDim.x >> 6);
+  if ((lane & 15) == 15) {
+    *reinterpret_cast<uint4*>(&s_row[w][lane >> 4][0]) = make_uint4(v[0], v[1], v[2], v[3]);
+    if (lane == 63) s_nvalid[w] = nvalid;
+  }
+  __asm__ volatile("" ::: "memory");  // a compiler barrier (a fence would wait on the coefficient stores)
+  unsigned ticket = 0u;
+  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
+  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
+  if (ticket != (unsigned)(nw - 1)) return;
+  __asm__ volatile("" ::: "memory");
+  const int t = lane;
+  if (t < NSTAT) {
+    unsigned tot = s_st[t];  // rare bins
+    unsigned nzt = 0u, nvt = 0u;
+    for (int i = 0; i < nw; ++i) {
+      nvt += s_nvalid[i];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint4 x = *reinterpret_cast<const uint4*>(&s_row[i][r][0]);
+        const unsigned wv[3] = {x.x, x.y, x.z};
+        const unsigned nzr = (x.z >> 20) & 1023u;
+        nzt += nzr;
+        if (t == 0) {
+          tot += nzr;
+        } else if (t == 1) {
+          tot += x.w + nzr;  // magnitude bits = bit length + 1 per nonzero
+        } else if (t >= 2 + 22 && t < 2 + 30) {
+          const int b = t - 2 - 22;  // common bin 22 + b: word b / 3, field b % 3
+          tot += (wv[b / 3] >> (10 * (b % 3))) & 1023u;
+        }
+      }
+    }
+    if (t == 2 + 25) tot -= 16u * nvt - nzt;  // the zeros counted in bin 25
+    slot[t] = tot;
+  }
+}
+
+// ---------------------------------------------------------------- forward --
+//
+// k_fwd16's decomposition in fp32: RGB window (+1 px ring) staged as packed
+// u32, the chroma planes converted and row-filtered in LDS, one thread per
+// block column: samples, column DCT (axis 0), LDS exchange, row DCT,
+// certified quantisation, 2 x 16-B stores, statistics.
+template <int MODE, bool PF>
+__global__ void __launch_bounds__(Cfg16F<MODE>::TF)
+k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
+         const FastQ16* __restrict__ fq16, const float* __restrict__ gk32, uint32_t* __restrict__ part,
+         uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const unsigned cap, const int fix_all) {
+  using C = Cfg16F<MODE>;
+  constexpr int WR = C::TH + 2, WC = C::TW + 2, WN = WR * WC;
+  constexpr bool CPLANE = (MODE != M444) && PF;
+  constexpr int PLANE_D = CPLANE ? 2 * WN : 0;
+  constexpr int BLK_D = C::NB * BS16F;
+  constexpr int U_D = PLANE_D > BLK_D ? PLANE_D : BLK_D;
+
+  __shared__ uint32_t s_rgb[WN];
+  __shared__ __attribute__((aligned(16))) float s_u[U_D];
+  __shared__ unsigned s_st[NSTAT + 1];  // rare histogram bins (+ stats_flush16's ticket)
+
+  const int tid = threadIdx.x;
+  const int frame = blockIdx.y;
+  const int ty = blockIdx.x / g.tiles_x, tx = blockIdx.x - ty * g.tiles_x;
+  const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
+  const int y0 = m0y * C::MH, x0 = m0x * C::MW;
+  const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
+  const FastQ16& fq = fq16[frame];
+
+  {  // every window load in flight before the first LDS store
+    constexpr int NL = (WN + C::TF - 1) / C::TF;
+    uint32_t px[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      px[l] = 0u;
+      if (i < WN) {
+        const int r = i / WC, c = i - r * WC;
+        const int yy = reflect101(y0 - 1 + r, g.H), xx = reflect101(x0 - 1 + c, g.W);
+        const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
+        px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int i = tid + l * C::TF;
+      if (i < WN) s_rgb[i] = px[l];
+    }
+  }
+  if (tid <= NSTAT) s_st[tid] = 0u;
+  const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
+  __syncthreads();
+
+  auto rgbf = [](uint32_t v, float& R, float& G, float& B) {
+    R = (float)(v & 255u);
+    G = (float)((v >> 8) & 255u);
+    B = (float)((v >> 16) & 255u);
+  };
+  if constexpr (CPLANE) {  // full-resolution chroma, then the prefilter's row pass in place
+    float* s_cb = s_u;
+    float* s_cr = s_u + WN;
+#pragma unroll
+    for (int l = 0; l < (WN + C::TF - 1) / C::TF; ++l) {
+      const int i = tid + l * C::TF;
+      if (i < WN) {
+        float R, G, B;
+        rgbf(s_rgb[i], R, G, B);
+        s_cb[i] = cb32(R, G, B);
+        s_cr[i] = cr32(R, G, B);
+      }
+    }
+    __syncthreads();
+    constexpr int NRP = WR * (WC - 2);
+    constexpr int PER = (NRP + C::TF - 1) / C::TF;
+    float tb[PER], tr[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * C::TF;
+      if (i < NRP) {
+        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
+        const float* b = s_cb + r * WC + c;
+        const float* q = s_cr + r * WC + c;
+        tb[j] = fmaf(k2, b[1], fmaf(k1, b[0], k0 * b[-1]));  // the 8x8 kernels' row chain
+        tr[j] = fmaf(k2, q[1], fmaf(k1, q[0], k0 * q[-1]));
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * C::TF;
+      if (i < NRP) {
+        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
+        s_cb[r * WC + c] = tb[j];
+        s_cr[r * WC + c] = tr[j];
+      }
+    }
+    __syncthreads();
+  }
+
+  const int blk = tid >> 4, line = tid & 15;
+  int plane, gy, gx;
+  if (blk < C::NYB) {
+    plane = 0;
+    gy = m0y * C::SY + blk / C::YBC;
+    gx = m0x * C::SX + blk % C::YBC;
+  } else {
+    const int bi = (blk - C::NYB) % C::NCB;
+    plane = 1 + (blk - C::NYB) / C::NCB;
+    gy = m0y + bi / C::CBC;
+    gx = m0x + bi % C::CBC;
+  }
+  const int nby = plane ? g.ncy : g.nby, nbx = plane ? g.ncx : g.nbx;
+  const bool valid = gy >= 0 && gx >= 0 && gy < nby && gx < nbx;
+  const int bidx = gy * nbx + gx;
+
+  float v[16];
+  if (valid) {
+    if (plane == 0 || MODE == M444) {
+      const int sx = reflect_pad(gx * 16 + line, g.W) - x0 + 1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int sy = reflect_pad(gy * 16 + i, g.H) - y0 + 1;
+        float R, G, B;
+        rgbf(s_rgb[sy * WC + sx], R, G, B);
+        v[i] = plane == 0 ? luma32m(R, G, B) : (plane == 1 ? cb32(R, G, B) : cr32(R, G, B)) - 128.0f;
+      }
+    } else {
+      // INTER_AREA mean of the (prefiltered) full-resolution chroma
+      const float* s_pl = s_u + (plane == 1 ? 0 : WN);
+      const int sc = reflect_pad(gx * 16 + line, g.wc);
+      const int wc0 = C::SX * sc - x0 + 1;
+#pragma unroll 4
+      for (int i = 0; i < 16; ++i) {
+        const int sr = reflect_pad(gy * 16 + i, g.hc);
+        const int wr0 = C::SY * sr - y0 + 1;
+        float s[C::SY][2];
+#pragma unroll
+        for (int a = 0; a < C::SY; ++a) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int w = (wr0 + a) * WC + wc0 + b;
+            if constexpr (CPLANE) {
+              s[a][b] = fmaf(k0, s_pl[w + WC] + s_pl[w - WC], k1 * s_pl[w]);  // the 8x8 kernels' column chain
+            } else {
+              float R, G, B;
+              rgbf(s_rgb[w], R, G, B);
+              s[a][b] = plane == 1 ? cb32(R, G, B) : cr32(R, G, B);
+            }
+          }
+        }
+        if constexpr (C::SY == 2)
+          v[i] = (((s[0][0] + s[0][1]) + s[1][0]) + s[1][1]) * 0.25f - 128.0f;
+        else
+          v[i] = (s[0][0] + s[0][1]) * 0.5f - 128.0f;
+      }
+    }
+    fdct16_f32(v);  // axis 0 (columns) first
+  }
+  if constexpr (CPLANE) __syncthreads();  // the block buffer aliases the chroma planes
+  float* s_blk = s_u + blk * BS16F;
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s_blk[i * 17 + line] = v[i];
+  }
+  __syncthreads();
+
+  // statistics per lane (one block row of 16 coefficients): nibble counters of
+  // the common bins 22..29 (|q| small), two words so no nibble exceeds 8
+  unsigned h[2] = {0u, 0u}, nz = 0u, mb = 0u, flag = (unsigned)fix_all;
+  if (valid) {
+    const int u = line;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = s_blk[u * 17 + k];
+    fdct16_f32(v);
+    const float* thr = fq.thr[plane ? 1 : 0];
+    int q[16];
+    unsigned nrare = 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float t = v[k] * fq.rq[u * 16 + k];
+      const float r = rintf(t);
+      // |t - r| is exact (Sterbenz); thr holds 0.5 - E/Q - slack, rounded down
+      flag |= fabsf(t - r) >= fmaf(fabsf(t), -0x1p-22f, thr[u * 16 + k]) ? 1u : 0u;
+      q[k] = (int)r;
+      nz += r != 0.0f ? 1u : 0u;
+      mb += (unsigned)__builtin_amdgcn_frexp_expf(r);  // bit length of |q|
+      const unsigned o = (unsigned)(q[k] + 12);     // bin 22 + o / 4 for q in [-12, 19]
+      h[k >> 3] += 1u << (o & 28u);
+      nrare += o >= 32u ? 1u : 0u;
+    }
+    if (nrare) {  // rare values: taken back out of the nibbles, LDS atomics on the bin
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const unsigned o = (unsigned)(q[k] + 12);
+        if (o >= 32u) {
+          h[k >> 3] -= 1u << (o & 28u);
+          if ((unsigned)(q[k] + 100) <= 200u) atomicAdd(&s_st[2 + (q[k] == 100 ? 49 : (q[k] + 100) >> 2)], 1u);
+        }
+      }
+    }
+    const long long off = (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
+                          (long long)bidx * 256 + u * 16;
+    uint4 pk[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int* qq = q + 8 * hh;
+      pk[hh].x = (uint32_t)(uint16_t)qq[0] | ((uint32_t)(uint16_t)qq[1] << 16);
+      pk[hh].y = (uint32_t)(uint16_t)qq[2] | ((uint32_t)(uint16_t)qq[3] << 16);
+      pk[hh].z = (uint32_t)(uint16_t)qq[4] | ((uint32_t)(uint16_t)qq[5] << 16);
+      pk[hh].w = (uint32_t)(uint16_t)qq[6] | ((uint32_t)(uint16_t)qq[7] << 16);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(coeffs + off);
+    dst[0] = pk[0];
+    dst[1] = pk[1];
+  }
+  // a block with any uncertain coefficient goes to the exact fix-up: its 16
+  // lanes are one quarter of a wave; the block's lane 0 appends it
+  const unsigned long long fm = __ballot(valid && flag);
+  if (fm) {  // wave-uniform
+    const int lane = tid & 63;
+    const bool mine = valid && line == 0 && ((fm >> (lane & ~15)) & 0xffffull);
+    const unsigned long long lm = __ballot(mine);
+    unsigned base = 0u;
+    if (lane == __ffsll((long long)lm) - 1) base = atomicAdd(fixcount, (unsigned)__popcll(lm));
+    base = __shfl(base, __ffsll((long long)lm) - 1, 64);
+    if (mine) {
+      const unsigned slot = base + (unsigned)__popcll(lm & ((1ull << lane) - 1ull));
+      if (slot < cap) fixlist[slot] = make_uint2((unsigned)frame, ((unsigned)plane << 24) | (unsigned)bidx);
+    }
+  }
+  stats_flush16(h[0], h[1], nz, mb, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + blockIdx.x) * NSTAT);
+}
+
+// ---------------------------------------------------------------- fix-up --
+//
+// One listed block per 64-thread workgroup iteration (a fixed grid strides
+// over the list; the forward launch completed before): every thread forms 4
+// samples of the padded plane exactly, 16 lanes run pocketfft's 16-point
+// DCT-II along axis 0 then axis 1 (jds_dct16.hpp: 32x the reference's values),
+// the quotient by 32 Q16 rounds half-even (k_fwd16's quantiser), and the
+// statistics change by the difference to the stored row.  Prefiltered chroma
+// blocks away from the image edges stage their source window once (fp64
+// colour, then the row pass, in LDS) -- the same fp64 operations as sample64,
+// which the other blocks call per sample.
+template <int MODE, bool PF>
+__global__ void __launch_bounds__(64)
+k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
+            const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
+            const uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, unsigned* __restrict__ fixlen,
+            const unsigned cap) {
+  constexpr bool CPLANE = (MODE != M444) && PF;
+  constexpr int SY = Cfg16F<MODE>::SY;
+  constexpr int WRR = 16 * SY + 2, WCC = 34;  // prefilter source window of one chroma block
+  __shared__ double s_b[16 * 17];
+  __shared__ double s_w[CPLANE ? WRR * WCC : 1];         // fp64 chroma of the window
+  __shared__ double s_rf[CPLANE ? WRR * (WCC - 2) : 1];  // after the row pass
+  const int t = threadIdx.x;
+  const unsigned c = *fixcount;
+  const unsigned count = c < cap ? c : cap;
+  const double k[3] = {gk[0], gk[1], gk[2]};
+  for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
+    const uint2 ent = fixlist[e];
+    const int frame = (int)ent.x;
+    const int plane = (int)(ent.y >> 24);
+    const int bidx = (int)(ent.y & 0xffffffu);
+    const int nbx = plane ? g.ncx : g.nbx;
+    const int gy = bidx / nbx, gx = bidx - gy * nbx;
+    const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
+    // lanes 0-15 (row u = t): the stored row, fetched now (its latency hides under the sampling)
+    const long long off = (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
+                          (long long)bidx * 256 + (t & 15) * 16;
+    uint4* dst = reinterpret_cast<uint4*>(coeffs + off);
+    uint4 o0 = make_uint4(0u, 0u, 0u, 0u), o1 = o0;
+    if (t < 16) {
+      o0 = dst[0];
+      o1 = dst[1];
+    }
+    const int wy0 = SY * 16 * gy - 1, wx0 = 32 * gx - 1;
+    const bool staged = CPLANE && plane != 0 && gy * 16 + 16 <= g.hc && gx * 16 + 16 <= g.wc && wy0 >= 0 &&
+                        wx0 >= 0 && wy0 + WRR <= g.H && wx0 + WCC <= g.W;
+    if (staged) {  // uniform per workgroup
+      constexpr int NWL = (WRR * WCC + 63) / 64;
+      uint32_t px[NWL];
+#pragma unroll
+      for (int l = 0; l < NWL; ++l) {
+        const int q = t + 64 * l;
+        px[l] = 0u;
+        if (q < WRR * WCC) {
+          const int r = q / WCC, cc = q - r * WCC;
+          const uint8_t* p = img + ((size_t)(wy0 + r) * g.W + wx0 + cc) * 3;
+          px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < NWL; ++l) {
+        const int q = t + 64 * l;
+        if (q < WRR * WCC) {
+          double R, G, B;
+          unpack(px[l], R, G, B);
+          s_w[q] = plane == 1 ? chroma_b(R, G, B) : chroma_r(R, G, B);
+        }
+      }
+      __syncthreads();
+      for (int q = t; q < WRR * (WCC - 2); q += 64) {  // cv2 RowFilter<double>
+        const int r = q / (WCC - 2), cc = q - r * (WCC - 2) + 1;
+        const double* w = s_w + r * WCC + cc;
+        double a = k[0] * w[-1];
+        a = a + k[1] * w[0];
+        s_rf[q] = a + k[2] * w[1];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        const int i = (t >> 4) + 4 * l, j = t & 15;
+        double sm[SY][2];
+#pragma unroll
+        for (int a = 0; a < SY; ++a) {
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) {
+            const double* f = s_rf + (SY * i + a + 1) * (WCC - 2) + 2 * j + bb;
+            const double d = k[1] * f[0] + 0.0;  // SymmColumnFilter<double>
+            sm[a][bb] = d + k[0] * (f[WCC - 2] + f[-(WCC - 2)]);
+          }
+        }
+        double v;
+        if constexpr (SY == 2)
+          v = (((sm[0][0] + sm[0][1]) + sm[1][0]) + sm[1][1]) * 0.25;
+        else
+          v = (sm[0][0] + sm[0][1]) * 0.5;
+        s_b[i * 17 + j] = v - 128.0;
+      }
+    } else {
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        const int i = (t >> 4) + 4 * l, j = t & 15;
+        s_b[i * 17 + j] = sample64<MODE, PF>(img, g, plane, gy * 16 + i, gx * 16 + j, k) - 128.0;
+      }
+    }
+    __syncthreads();
+    double v[16];
+    if (t < 16) {  // axis 0, column t
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = s_b[r * 17 + t];
+      dct2_line16(v);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s_b[r * 17 + t] = v[r];
+    }
+    __syncthreads();
+    if (t < 16) {  // axis 1, row u = t; requantize and correct the statistics
+      const int u = t;
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) v[cc] = s_b[u * 17 + cc];
+      dct2_line16(v);
+      const uint32_t ow[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+      uint32_t nw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+      long long dnz = 0, dmb = 0;
+      jds_frame_stats* fs = st + frame;
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) {
+        // quantizer.py:22-24: the true quotient of the reference's coefficient
+        // (v / 32, exact) by Q16 = Q8[u/2][cc/2]
+        const int qn = (int)__builtin_rint(v[cc] / (32.0 * fq[frame].q[(u >> 1) * 8 + (cc >> 1)]));
+        const int qo = (int16_t)((ow[cc >> 1] >> ((cc & 1) * 16)) & 0xffffu);
+        nw[cc >> 1] |= (uint32_t)(uint16_t)qn << ((cc & 1) * 16);
+        if (qn != qo) {
+          const int mo = qo < 0 ? -qo : qo, mn = qn < 0 ? -qn : qn;
+          if (mo) {
+            --dnz;
+            dmb -= 33 - __clz(mo);
+            if (qo >= -100 && qo <= 100)
+              atomicAdd((unsigned long long*)&fs->hist[qo == 100 ? 49 : (qo + 100) >> 2], ~0ull);
+          }
+          if (mn) {
+            ++dnz;
+            dmb += 33 - __clz(mn);
+            if (qn >= -100 && qn <= 100)
+              atomicAdd((unsigned long long*)&fs->hist[qn == 100 ? 49 : (qn + 100) >> 2], 1ull);
+          }
+        }
+      }
+      dst[0] = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+      dst[1] = make_uint4(nw[4], nw[5], nw[6], nw[7]);
+      if (dnz) atomicAdd((unsigned long long*)&fs->nonzero, (unsigned long long)dnz);
+      if (dmb) atomicAdd((unsigned long long*)&fs->magnitude_bits, (unsigned long long)dmb);
+    }
+    __syncthreads();
+  }
+  // the last workgroup re-arms the counter (its count kept in fixlen for
+  // jds_plan_fix_counts): every workgroup read it before taking a ticket
+  __syncthreads();
+  if (t == 0) {
+    const unsigned tk = atomicAdd(fixcount + 1, 1u);
+    if (tk == gridDim.x - 1) {
+      *fixlen = c;
+      fixcount[0] = 0u;
+      fixcount[1] = 0u;
+    }
+  }
+}
+
+// ------------------------------------------------------------ launchers --
+
+hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s);
+constexpr int FIX16_GRID = 2048;  // k_fix_fwd16 workgroups (8 per CU by LDS at 4:2:0)
+
+template <int MODE, bool PF>
+static hipError_t fast16_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
+                           const void* fq16, const double* gk, const float* gk32, jds_frame_stats* st,
+                           uint32_t* part, uint2* fixlist, unsigned* counters, int fix_all, hipStream_t s) {
+  using C = Cfg16F<MODE>;
+  const unsigned cap = (unsigned)((g.cpf / 256) * n);
+  const int tiles = g.tiles_y * g.tiles_x;
+  hipLaunchKernelGGL((k_fwd16f<MODE, PF>), dim3(tiles, n), dim3(C::TF), 0, s, g, rgb, coeffs, (const FastQ16*)fq16,
+                     gk32, part, fixlist, counters, cap, fix_all);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_fix_fwd16<MODE, PF>), dim3(FIX16_GRID), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
+                     counters, counters + 2, cap);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return launch_fwd_reduce(n, st, part, tiles, s);  // the per-tile partials (order-free: u64 atomics)
+}
+
+// counters: [0] list length (live), [1] fix-up tickets, [2] the last run's length
+hipError_t launch_fast_fwd16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
+                             const FrameQ* fq, const void* fq16, const double* gk, const float* gk32,
+                             jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* counters, int fix_all,
+                             hipStream_t s) {
+  switch (mode) {
+    case M420:
+      return pf ? fast16_t<M420, true>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s)
+                : fast16_t<M420, false>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s);
+    case M422:
+      return pf ? fast16_t<M422, true>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s)
+                : fast16_t<M422, false>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s);
+    default:
+      return fast16_t<M444, false>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s);
+  }
+}
+
+// ---------------------------------------------------- host: the bounds --
+//
+// fast_fwd_bounds with 16-point passes: each output is an 8-term FMA chain
+// over s_i / d_i (|.| <= 2X, error 2e + 2uX); its error is
+// b_k (2e + 2uX) + 2uX (b_k + P_k) with b_k = sum_i |W16_ki| and P_k the sum
+// of the chain's partial sums of |W16_k0..7| (covering the fp32
+// representation error of W16 and every rounding of the chain).
+static void pass_bound16(double X, double e, double* Xout, double* eout) {
+  const double u = 0x1p-24;
+  for (int k = 0; k < 16; ++k) {
+    double b = 0, P = 0, pre = 0;
+    for (int i = 0; i < 8; ++i) {
+      b += fabs((double)W16[k][i]);
+      pre += fabs((double)W16[k][i]);
+      P += pre;
+    }
+    Xout[k] = 2 * X * b;
+    eout[k] = b * (2 * e + 2 * u * X) + 2 * u * X * (b + P);
+  }
+}
+
+void fast_fwd16_bounds(int mode, bool pf, const double* gk, double* E /*2 x 256*/) {
+  for (int p = 0; p < 2; ++p) {
+    const double e_in = fwd_input_error(p, mode, pf, gk);
+    double X1[16], e1[16];
+    pass_bound16(128.0, e_in, X1, e1);
+    double E2[16][16];
+    for (int k = 0; k < 16; ++k) {
+      double X2[16], e2[16];
+      pass_bound16(X1[k], e1[k], X2, e2);
+      for (int l = 0; l < 16; ++l) E2[k][l] = e2[l];
+    }
+    for (int k = 0; k < 16; ++k)
+      for (int l = 0; l < 16; ++l) {
+        const double e2l = E2[k][l] > E2[l][k] ? E2[k][l] : E2[l][k];  // either pass order
+        E[p * 256 + k * 16 + l] = e2l * (1 + 1e-5) + 1e-9;            // + the fp64 reference's own error
+      }
+  }
+}
+
+// Q8: the frame's 8x8 table; the 16x16 table is Q16[u][v] = Q8[u/2][v/2].
+void fast_fwd16_thresholds(const double* Q8, int mode, bool pf, const double* gk, void* out) {
+  FastQ16* f = (FastQ16*)out;
+  double E[512];
+  fast_fwd16_bounds(mode, pf, gk, E);
+  for (int i = 0; i < 256; ++i) f->rq[i] = (float)(1.0 / Q8[((i >> 4) >> 1) * 8 + ((i & 15) >> 1)]);
+  for (int p = 0; p < 2; ++p)
+    for (int i = 0; i < 256; ++i) {
+      const double Q = Q8[((i >> 4) >> 1) * 8 + ((i & 15) >> 1)];
+      const double tq = E[p * 256 + i] / Q * (1 + 1e-5) + 1e-7;
+      const double lim = 0.5 - tq * (1 + 0x1p-20) - 0x1p-23;
+      float v = (float)lim;
+      if ((double)v > lim) v = nextafterf(v, 0.0f);
+      f->thr[p][i] = v;
+    }
+}
+
+size_t fast_q16_size() { return sizeof(FastQ16); }
+
+// Test-only: the fp32 chain of k_fwd16f for every 16x16 block of one plane of
+// an H x W RGB image (plane size a multiple of 16), in either pass order
+// (rows_first 0 = the kernel's columns first), before quantisation.
+int fwd16_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
+                     bool rows_first, float* out) {
+  const int sy = mode == M420 ? 2 : 1, sx = mode == M444 ? 1 : 2;
+  const int ph = plane == 0 ? H : H / sy, pw = plane == 0 ? W : W / sx;
+  if (ph % 16 || pw % 16) return -1;
+  const float k0 = (float)gk[0], k1 = (float)gk[1], k2 = (float)gk[2];
+  auto refl = [](int i, int n) {
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+    return i;
+  };
+  auto px = [&](int y, int x, int c) { return (float)rgb[((size_t)y * W + x) * 3 + c]; };
+  auto chroma = [&](int y, int x) {
+    const float R = px(y, x, 0), G = px(y, x, 1), B = px(y, x, 2);
+    return plane == 1 ? cb32(R, G, B) : cr32(R, G, B);
+  };
+  auto rowf = [&](int y, int x) {
+    return fmaf(k2, chroma(y, refl(x + 1, W)), fmaf(k1, chroma(y, x), k0 * chroma(y, refl(x - 1, W))));
+  };
+  auto sample = [&](int y, int x) -> float {
+    if (plane == 0) return luma32m(px(y, x, 0), px(y, x, 1), px(y, x, 2));
+    if (mode == M444) return chroma(y, x) - 128.0f;
+    float s[2][2];
+    for (int a = 0; a < sy; ++a)
+      for (int b = 0; b < 2; ++b) {
+        const int yy = sy * y + a, xx = 2 * x + b;
+        s[a][b] = pf ? fmaf(k0, rowf(refl(yy + 1, H), xx) + rowf(refl(yy - 1, H), xx), k1 * rowf(yy, xx))
+                     : chroma(yy, xx);
+      }
+    if (sy == 2) return (((s[0][0] + s[0][1]) + s[1][0]) + s[1][1]) * 0.25f - 128.0f;
+    return (s[0][0] + s[0][1]) * 0.5f - 128.0f;
+  };
+  const int nbx = pw / 16;
+  for (int by = 0; by < ph / 16; ++by)
+    for (int bx = 0; bx < nbx; ++bx) {
+      float b[16][16];
+      for (int i = 0; i < 16; ++i)
+        for (int j = 0; j < 16; ++j) b[i][j] = sample(by * 16 + i, bx * 16 + j);
+      for (int pass = 0; pass < 2; ++pass) {
+        const bool rows = (pass == 0) == rows_first;
+        for (int i = 0; i < 16; ++i) {
+          float v[16];
+          for (int j = 0; j < 16; ++j) v[j] = rows ? b[i][j] : b[j][i];
+          fdct16_f32(v);
+          for (int j = 0; j < 16; ++j) (rows ? b[i][j] : b[j][i]) = v[j];
+        }
+      }
+      float* o = out + ((size_t)by * nbx + bx) * 256;
+      for (int i = 0; i < 256; ++i) o[i] = b[i / 16][i % 16];
+    }
+  return 0;
+}
+
+}  // namespace jds

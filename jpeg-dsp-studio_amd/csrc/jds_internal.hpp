@@ -72,6 +72,21 @@ struct Side {
   hipEvent_t fork = nullptr, join = nullptr;
 };
 
+// Buffers of the certified 16x16 forward (jds_fast16.hip): per-frame fp32
+// tables (FastQ16), the fp32 Gaussian taps, per-tile statistics partials
+// (NSTAT u32 per tile), the list of blocks the exact fix-up recomputes, and
+// counters [0] list length, [1] fix-up tickets (both
+// re-armed by k_fix_fwd16), [2] the last run's list length.  Zeroed at plan
+// creation.
+struct Fwd16Fast {
+  const void* fq16;
+  const float* gk32;
+  uint32_t* part;
+  uint2* fixlist;
+  unsigned* counters;
+  int fix_all;  // test: list every block
+};
+
 // Counters of the certified fast inverse (jds_inv_fast.hip).
 // * count[0..1]: tiles recomputed exactly in a run.  They alternate between
 //   runs (`parity`): a run counts into count[parity] and zeroes

@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get('JDS_LIB_PATH') or os.path.join(_HERE, 'libjds.so')
 JDS_OK, JDS_EINVAL, JDS_ENOTSUP, JDS_EHIP, JDS_ENOMEM = 0, -1, -2, -3, -4
 SS_444, SS_422, SS_420 = 0, 1, 2
 MODE_CODES = {'4:4:4': SS_444, '4:2:2': SS_422, '4:2:0': SS_420}
-RUN_SSE, RUN_FWD, RUN_INV, RUN_EXACT, RUN_EXACT_INV, RUN_INV_FIXALL = 1, 2, 4, 8, 16, 32
+RUN_SSE, RUN_FWD, RUN_INV, RUN_EXACT, RUN_EXACT_INV, RUN_INV_FIXALL, RUN_FWD_FIXALL = 1, 2, 4, 8, 16, 32, 64
 
 
 class Params(C.Structure):
@@ -102,6 +102,8 @@ _SIGS = {
     'jds_selftest_dct16x16': (C.c_int, [_P, _P, C.c_int64, C.c_int32]),
     'jds_selftest_area_tab': (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P]),
     'jds_selftest_fwd32': (C.c_int, [C.c_int32, C.c_int32, _P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P,
+                                     _P]),
+    'jds_selftest_fwd16': (C.c_int, [C.c_int32, C.c_int32, _P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P,
                                      _P]),
 }
 _OPTIONAL_SIGS: dict = {}
@@ -293,7 +295,7 @@ class Plan:
         check(lib().jds_plan_run(self.handle, rgb_dev, out_dev, coeffs_dev, stats_dev, flags, stream))
 
     def fix_counts(self):
-        """[forward blocks, inverse pixels] sent to the exact fp64 fix-up by the last run."""
+        """[forward blocks, inverse tiles] sent to the exact fp64 fix-up by the last run."""
         c = np.zeros(2, np.uint32)
         check(lib().jds_plan_fix_counts(self.handle, c.ctypes.data))
         return c

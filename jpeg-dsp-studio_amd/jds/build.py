@@ -20,8 +20,8 @@ LIB = os.path.join(HERE, 'libjds.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('JDS_OFFLOAD_ARCH', 'gfx950')
 
-SOURCES = ['jds_codec.hip', 'jds_gen.hip', 'jds_b16.hip', 'jds_inv.hip', 'jds_inv_fast.hip', 'jds_fast.hip', 'jds_stages.hip', 'jds_ssim.hip', 'jds_entropy.hip', 'jds_abi.hip']
-HEADERS = ['jds_dct8.hpp', 'jds_dct16.hpp', 'jds_internal.hpp', 'jds_device.hpp', 'jds_inv_common.hpp', 'jds_inv_exact.hpp']
+SOURCES = ['jds_codec.hip', 'jds_gen.hip', 'jds_b16.hip', 'jds_inv.hip', 'jds_inv_fast.hip', 'jds_fast.hip', 'jds_fast16.hip', 'jds_stages.hip', 'jds_ssim.hip', 'jds_entropy.hip', 'jds_abi.hip']
+HEADERS = ['jds_dct8.hpp', 'jds_dct16.hpp', 'jds_internal.hpp', 'jds_device.hpp', 'jds_inv_common.hpp', 'jds_inv_exact.hpp', 'jds_fwd_common.hpp']
 
 
 def _inputs():

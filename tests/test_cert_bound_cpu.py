@@ -8,7 +8,9 @@ fp32 chain, restated on the host (jds_selftest_fwd32), runs on structured
 worst cases -- saturated colours, all-0 / all-255, checkerboards at several
 phases, one-pixel spikes, hard colour edges under the prefilter -- and the
 exact reference coefficients come from the oracle (the reference's fp64 chain,
-engines/color_space.py + engines/dct_engine.py).  Asserted: the measured error
+engines/color_space.py + engines/dct_engine.py).  The same for the 16x16
+forward (csrc/jds_fast16.hip, jds_selftest_fwd16; table kron(Q8, ones(2,2))).
+Asserted: the measured error
 stays below the bound (ratio < 1) for both pass orders, and every coefficient
 the certificate accepts at Q in {1, 50, 95, 100} rounds exactly like the
 reference's np.round(c / Q) (engines/quantizer.py:22-24)."""
@@ -28,7 +30,7 @@ def L():
 
 def _images():
     rng = np.random.default_rng(123)
-    H, W = 32, 48
+    H, W = 32, 64  # every plane a multiple of 16 (the 16x16 variant) at every subsampling
     imgs = {}
     imgs['black'] = np.zeros((H, W, 3), np.uint8)
     imgs['white'] = np.full((H, W, 3), 255, np.uint8)
@@ -61,6 +63,7 @@ def _images():
 
 
 IMAGES = _images()
+BLOCKS = {8: 'jds_selftest_fwd32', 16: 'jds_selftest_fwd16'}
 
 
 def _exact_planes(img, mode, pf):
@@ -78,9 +81,10 @@ def _thr(E, Q):
     return f
 
 
+@pytest.mark.parametrize('bs', [8, 16])
 @pytest.mark.parametrize('mode,pf', [('4:2:0', True), ('4:2:0', False), ('4:2:2', True), ('4:2:2', False),
                                      ('4:4:4', False)])
-def test_fp32_forward_error_within_certified_bound(L, mode, pf):
+def test_fp32_forward_error_within_certified_bound(L, mode, pf, bs):
     gk = cpu_ref.gaussian_kernel3(0.75)
     code = {'4:4:4': 0, '4:2:2': 1, '4:2:0': 2}[mode]
     worst = 0.0
@@ -89,11 +93,11 @@ def test_fp32_forward_error_within_certified_bound(L, mode, pf):
         img = np.ascontiguousarray(img)
         planes = _exact_planes(img, mode, pf)
         for plane in range(3):
-            exact = cpu_ref.encode_blocks(cpu_ref.split_blocks(planes[plane], 8)).reshape(-1, 64)
+            exact = cpu_ref.encode_blocks(cpu_ref.split_blocks(planes[plane], bs)).reshape(-1, bs * bs)
             for rows_first in (1, 0):
                 c32 = np.empty(exact.shape, np.float32)
-                bound = np.empty(64, np.float64)
-                rc = L.jds_selftest_fwd32(code, int(pf), gk.ctypes.data, img.ctypes.data, img.shape[0],
+                bound = np.empty(bs * bs, np.float64)
+                rc = getattr(L, BLOCKS[bs])(code, int(pf), gk.ctypes.data, img.ctypes.data, img.shape[0],
                                           img.shape[1], plane, rows_first, c32.ctypes.data, bound.ctypes.data)
                 assert rc == 0
                 ratio = np.abs(c32.astype(np.float64) - exact) / bound
@@ -101,7 +105,8 @@ def test_fp32_forward_error_within_certified_bound(L, mode, pf):
                 assert ratio.max() < 1.0, (name, plane, rows_first, float(ratio.max()))
                 # the certificate at several qualities: accepted roundings are the reference's
                 for q in (1, 50, 95, 100):
-                    Q = cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q).reshape(-1)
+                    Q = cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q)
+                    Q = (np.kron(Q, np.ones((2, 2))) if bs == 16 else Q).reshape(-1)  # include/jds.h: Q16
                     rq = (1.0 / Q).astype(np.float32)
                     t = c32 * rq
                     r = np.rint(t)
@@ -110,6 +115,6 @@ def test_fp32_forward_error_within_certified_bound(L, mode, pf):
                     ref_q = np.round(exact / Q)
                     accepted += int(ok.sum())
                     wrong += int(np.sum(ok & (r != ref_q)))
-    print(f'{mode} pf={pf}: worst |c32 - c_exact| / E = {worst:.4f}; {accepted} certified roundings, {wrong} wrong')
+    print(f'{bs}x{bs} {mode} pf={pf}: worst |c32 - c_exact| / E = {worst:.4f}; {accepted} certified roundings, {wrong} wrong')
     assert wrong == 0
     assert accepted > 0
