@@ -32,7 +32,11 @@
 
 namespace jds {
 
-constexpr int BS16 = 264;  // doubles per 16x16 block in LDS (256 + 8 pad)
+// doubles per 16x16 block in LDS: rows of 17 (a lane's row of 16 lands on 16
+// distinct bank pairs; two blocks sit 32 banks apart, so 32 lanes of b64
+// accesses -- rows or columns -- are conflict-free)
+constexpr int BS16 = 272;
+constexpr int RS16 = 17;  // row stride
 
 template <int MODE>
 struct Cfg16 {
@@ -224,7 +228,7 @@ k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   double* s_blk = s_u + blk * BS16;
   if (valid) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s_blk[i * 16 + line] = v[i];
+    for (int i = 0; i < 16; ++i) s_blk[i * RS16 + line] = v[i];
   }
   __syncthreads();
 
@@ -232,7 +236,7 @@ k_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   if (valid) {
     const int u = line;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = s_blk[u * 16 + k];
+    for (int k = 0; k < 16; ++k) v[k] = s_blk[u * RS16 + k];
     dct2_line16(v);
     // quantizer.py:22-24: rint of the true IEEE quotient.  t = fl(v * fl(1/Q))
     // lies within 3 * 2^-53 |v/Q| of fl(v/Q), so unless t is within |t| 2^-50
@@ -315,19 +319,19 @@ __device__ __forceinline__ void idct16_rows(const Row16& rw, const double* __res
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int16_t qv = (int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
-      s_b[line * 16 + k] = (double)qv * q16_of(q8, line, k);  // quantizer.py:27-29
+      s_b[line * RS16 + k] = (double)qv * q16_of(q8, line, k);  // quantizer.py:27-29
     }
   }
   __builtin_amdgcn_wave_barrier();  // no LDS access moves across (the exchange is wave-local)
   double c[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) c[i] = s_b[i * 16 + line];
+  for (int i = 0; i < 16; ++i) c[i] = s_b[i * RS16 + line];
   dct3_line16(c);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) s_b[i * 16 + line] = c[i];
+  for (int i = 0; i < 16; ++i) s_b[i * RS16 + line] = c[i];
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int k = 0; k < 16; ++k) c[k] = s_b[line * 16 + k];
+  for (int k = 0; k < 16; ++k) c[k] = s_b[line * RS16 + k];
   dct3_line16(c);
 #pragma unroll
   for (int k = 0; k < 16; ++k) {

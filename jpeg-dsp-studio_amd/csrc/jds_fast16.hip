@@ -389,8 +389,14 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 // blocks away from the image edges stage their source window once (fp64
 // colour, then the row pass, in LDS) -- the same fp64 operations as sample64,
 // which the other blocks call per sample.
+#ifndef JDS_FIX16_WPE
+#define JDS_FIX16_WPE 3
+#endif
+#ifndef JDS_FIX16_GRID
+#define JDS_FIX16_GRID 3072  // 3 per SIMD (LDS and VGPRs allow it at 4:2:2)
+#endif
 template <int MODE, bool PF>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(JDS_FIX16_WPE)))
 k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
             const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
             const uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, unsigned* __restrict__ fixlen,
@@ -423,9 +429,16 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       o1 = dst[1];
     }
     const int wy0 = SY * 16 * gy - 1, wx0 = 32 * gx - 1;
+#ifdef JDS_P16FIX_NOSAMPLE
+    s_b[t] = (double)t; s_b[t + 64] = 1.0; s_b[t + 128] = 2.0; s_b[t + 192] = 3.0;
+#endif
     const bool staged = CPLANE && plane != 0 && gy * 16 + 16 <= g.hc && gx * 16 + 16 <= g.wc && wy0 >= 0 &&
                         wx0 >= 0 && wy0 + WRR <= g.H && wx0 + WCC <= g.W;
+#ifdef JDS_P16FIX_NOSAMPLE
+    if (false) {
+#else
     if (staged) {  // uniform per workgroup
+#endif
       constexpr int NWL = (WRR * WCC + 63) / 64;
       uint32_t px[NWL];
 #pragma unroll
@@ -477,6 +490,9 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
         s_b[i * 17 + j] = v - 128.0;
       }
     } else {
+#ifdef JDS_P16FIX_NOSAMPLE
+      if (false)
+#endif
 #pragma unroll
       for (int l = 0; l < 4; ++l) {
         const int i = (t >> 4) + 4 * l, j = t & 15;
@@ -488,7 +504,9 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
     if (t < 16) {  // axis 0, column t
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = s_b[r * 17 + t];
+#ifndef JDS_P16FIX_NODCT
       dct2_line16(v);
+#endif
 #pragma unroll
       for (int r = 0; r < 16; ++r) s_b[r * 17 + t] = v[r];
     }
@@ -497,7 +515,9 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       const int u = t;
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) v[cc] = s_b[u * 17 + cc];
+#ifndef JDS_P16FIX_NODCT
       dct2_line16(v);
+#endif
       const uint32_t ow[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
       uint32_t nw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
       long long dnz = 0, dmb = 0;
@@ -509,7 +529,11 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
         const int qn = (int)__builtin_rint(v[cc] / (32.0 * fq[frame].q[(u >> 1) * 8 + (cc >> 1)]));
         const int qo = (int16_t)((ow[cc >> 1] >> ((cc & 1) * 16)) & 0xffffu);
         nw[cc >> 1] |= (uint32_t)(uint16_t)qn << ((cc & 1) * 16);
+#ifdef JDS_P16FIX_NOSTAT
+        if (qn == 0x7fffffff) {
+#else
         if (qn != qo) {
+#endif
           const int mo = qo < 0 ? -qo : qo, mn = qn < 0 ? -qn : qn;
           if (mo) {
             --dnz;
@@ -548,7 +572,7 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
 // ------------------------------------------------------------ launchers --
 
 hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s);
-constexpr int FIX16_GRID = 2048;  // k_fix_fwd16 workgroups (8 per CU by LDS at 4:2:0)
+constexpr int FIX16_GRID = JDS_FIX16_GRID;  // k_fix_fwd16 workgroups
 
 template <int MODE, bool PF>
 static hipError_t fast16_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
