@@ -161,6 +161,7 @@ struct jds_plan {
   unsigned inv_runs = 0;  // fast-inverse runs so far: picks the list counter (InvFix::parity)
   bool last_inv_fast = false;  // the last run's inverse was the certified fast one
   bool last_fwd16_fast = false;  // 16x16: the last forward was the certified fp32 one
+  unsigned fwd16_runs = 0;       // 16x16 certified forward runs so far: picks the list counter
   InvFix inv_fix() const {
     return {(unsigned*)invfix.p, (unsigned*)invfix.p + 16, 0, (int)(inv_runs & 1u), (int)(inv_runs % 3u),
             (int)(inv_runs % 16u == 15u)};
@@ -589,12 +590,15 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
     // the certified fp32 forward unless JDS_RUN_EXACT (k_fix_fwd16 re-arms its counters)
     const Fwd16Fast ff{p->fq32.p, (const float*)p->gk32.p, (uint32_t*)p->part32.p, (uint2*)p->fixlist.p,
                        (unsigned*)p->counters.p,
-                       (flags & JDS_RUN_FWD_FIXALL) ? 1 : 0};
+                       (flags & JDS_RUN_FWD_FIXALL) ? 1 : 0, (int)(p->fwd16_runs & 1u)};
     if (phases & 1) HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
     HIP_TRY(launch_codec16(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                            (const double*)p->gk.p, stats, (double*)p->part.p, (double*)p->planes.p,
                            (flags & JDS_RUN_SSE) != 0, nullptr, nullptr, s, nullptr, phases, exact ? nullptr : &ff));
-    if (phases & 1) p->last_fwd16_fast = !exact;
+    if (phases & 1) {
+      p->last_fwd16_fast = !exact;
+      if (!exact) p->fwd16_runs++;
+    }
     return JDS_OK;
   }
   if (phases & 1) {

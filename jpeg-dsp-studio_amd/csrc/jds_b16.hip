@@ -783,7 +783,7 @@ hipError_t launch_finalize(const Geo& g, int n, jds_frame_stats* st, const doubl
 hipError_t launch_fast_fwd16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
                              const FrameQ* fq, const void* fq16, const double* gk, const float* gk32,
                              jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* counters, int fix_all,
-                             hipStream_t s);
+                             int parity, hipStream_t s);
 
 // tiles of the fused 16x16 inverse (sse_y partials per tile); 0 for 4:4:4
 int inv16_tiles(int mode, int H, int W) {
@@ -814,7 +814,7 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
     if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
     if (ff)  // certified fp32 forward + exact fix-up of the listed blocks (jds_fast16.hip)
       e = launch_fast_fwd16(MODE, pf, g, n, rgb, coeffs, fq, ff->fq16, gk, ff->gk32, st, ff->part, ff->fixlist, ff->counters,
-                            ff->fix_all, s);
+                            ff->fix_all, ff->parity, s);
     else if (MODE != M444 && pf)
       hipLaunchKernelGGL((k_fwd16<MODE, (MODE != M444)>), grid, dim3(C::TF), 0, s, g, rgb, coeffs, fq, gk, st);
     else

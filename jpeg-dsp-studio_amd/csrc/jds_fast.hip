@@ -716,9 +716,14 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
     int q[8];
     quant8(v, rq, thr, true, q, ls, s_st);
-    int16_t* tq = reinterpret_cast<int16_t*>(src);  // row k at byte offset k * rs * 4
+    // int16 transpose in place (row k at byte offset k * rs * 4).  Rotating
+    // full-width rows across the wave's 8 blocks (so a block's 8 lanes read 8
+    // bank groups instead of one) measured 6 us slower: the address math
+    // costs more than the conflicts.
+    int16_t* tq = reinterpret_cast<int16_t*>(src);
 #pragma unroll
     for (int k = 0; k < 8; ++k) tq[k * rs * 2 + line] = (int16_t)q[k];
+    __builtin_amdgcn_wave_barrier();  // other lanes' rows: the LDS keeps the wave's order
     const uint4 row = *reinterpret_cast<const uint4*>(tq + line * rs * 2);
 #ifndef JDS_PROBE_NOSTORE
     *reinterpret_cast<uint4*>(dst + line * 8) = row;

@@ -154,7 +154,8 @@ template <int MODE, bool PF>
 __global__ void __launch_bounds__(Cfg16F<MODE>::TF)
 k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
          const FastQ16* __restrict__ fq16, const float* __restrict__ gk32, uint32_t* __restrict__ part,
-         uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, const unsigned cap, const int fix_all) {
+         uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, unsigned* __restrict__ fixnext,
+         const unsigned cap, const int fix_all) {
   using C = Cfg16F<MODE>;
   constexpr int WR = C::TH + 2, WC = C::TW + 2, WN = WR * WC;
   constexpr bool CPLANE = (MODE != M444) && PF;
@@ -195,6 +196,7 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     }
   }
   if (tid <= NSTAT) s_st[tid] = 0u;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *fixnext = 0u;  // the next run's list
   const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
   __syncthreads();
 
@@ -203,6 +205,14 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     G = (float)((v >> 8) & 255u);
     B = (float)((v >> 16) & 255u);
   };
+  // chroma planes: each window row holds its even columns, then its odd ones
+  // (the sample loop reads columns 2m+1 and 2m+2 of lane m: unit stride)
+  static_assert(WC % 2 == 0, "even window width");
+#ifndef JDS_NO_CSPLIT
+  auto cidx = [](int r, int c) { return r * WC + (c & 1) * (WC / 2) + (c >> 1); };
+#else
+  auto cidx = [](int r, int c) { return r * WC + c; };
+#endif
   if constexpr (CPLANE) {  // full-resolution chroma, then the prefilter's row pass in place
     float* s_cb = s_u;
     float* s_cr = s_u + WN;
@@ -212,8 +222,9 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       if (i < WN) {
         float R, G, B;
         rgbf(s_rgb[i], R, G, B);
-        s_cb[i] = cb32(R, G, B);
-        s_cr[i] = cr32(R, G, B);
+        const int r = i / WC, c = i - r * WC;
+        s_cb[cidx(r, c)] = cb32(R, G, B);
+        s_cr[cidx(r, c)] = cr32(R, G, B);
       }
     }
     __syncthreads();
@@ -225,10 +236,9 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       const int i = tid + j * C::TF;
       if (i < NRP) {
         const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
-        const float* b = s_cb + r * WC + c;
-        const float* q = s_cr + r * WC + c;
-        tb[j] = fmaf(k2, b[1], fmaf(k1, b[0], k0 * b[-1]));  // the 8x8 kernels' row chain
-        tr[j] = fmaf(k2, q[1], fmaf(k1, q[0], k0 * q[-1]));
+        const int il = cidx(r, c - 1), i0 = cidx(r, c), ir = cidx(r, c + 1);
+        tb[j] = fmaf(k2, s_cb[ir], fmaf(k1, s_cb[i0], k0 * s_cb[il]));  // the 8x8 kernels' row chain
+        tr[j] = fmaf(k2, s_cr[ir], fmaf(k1, s_cr[i0], k0 * s_cr[il]));
       }
     }
     __syncthreads();
@@ -237,8 +247,8 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       const int i = tid + j * C::TF;
       if (i < NRP) {
         const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
-        s_cb[r * WC + c] = tb[j];
-        s_cr[r * WC + c] = tr[j];
+        s_cb[cidx(r, c)] = tb[j];
+        s_cr[cidx(r, c)] = tr[j];
       }
     }
     __syncthreads();
@@ -285,12 +295,12 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
         for (int a = 0; a < C::SY; ++a) {
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
-            const int w = (wr0 + a) * WC + wc0 + b;
             if constexpr (CPLANE) {
+              const int w = cidx(wr0 + a, wc0 + b);
               s[a][b] = fmaf(k0, s_pl[w + WC] + s_pl[w - WC], k1 * s_pl[w]);  // the 8x8 kernels' column chain
             } else {
               float R, G, B;
-              rgbf(s_rgb[w], R, G, B);
+              rgbf(s_rgb[(wr0 + a) * WC + wc0 + b], R, G, B);
               s[a][b] = plane == 1 ? cb32(R, G, B) : cr32(R, G, B);
             }
           }
@@ -368,7 +378,11 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     const bool mine = valid && line == 0 && ((fm >> (lane & ~15)) & 0xffffull);
     const unsigned long long lm = __ballot(mine);
     unsigned base = 0u;
+#ifdef JDS_P16_FLAGSPREAD  // tools/probe: the appends spread over 13 counters (timing only)
+    if (lane == __ffsll((long long)lm) - 1) base = atomicAdd(fixcount + 3 + (blockIdx.x % 13), (unsigned)__popcll(lm));
+#else
     if (lane == __ffsll((long long)lm) - 1) base = atomicAdd(fixcount, (unsigned)__popcll(lm));
+#endif
     base = __shfl(base, __ffsll((long long)lm) - 1, 64);
     if (mine) {
       const unsigned slot = base + (unsigned)__popcll(lm & ((1ull << lane) - 1ull));
@@ -380,153 +394,210 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 
 // ---------------------------------------------------------------- fix-up --
 //
-// One listed block per 64-thread workgroup iteration (a fixed grid strides
-// over the list; the forward launch completed before): every thread forms 4
-// samples of the padded plane exactly, 16 lanes run pocketfft's 16-point
-// DCT-II along axis 0 then axis 1 (jds_dct16.hpp: 32x the reference's values),
-// the quotient by 32 Q16 rounds half-even (k_fwd16's quantiser), and the
-// statistics change by the difference to the stored row.  Prefiltered chroma
-// blocks away from the image edges stage their source window once (fp64
-// colour, then the row pass, in LDS) -- the same fp64 operations as sample64,
-// which the other blocks call per sample.
+// Each 64-lane workgroup takes four listed blocks at a time, 16 lanes (one
+// column each) per block; a fixed grid strides over the list (the forward
+// launch completed before).  A lane forms its column's 16 samples exactly in
+// registers (fix_column: the fp64 operations of sample64 / k_fwd16), runs
+// pocketfft's 16-point DCT-II on them (axis 0, jds_dct16.hpp: 32x the
+// reference's values), the block is transposed through LDS, the row lanes run
+// the axis-1 transform, the quotient by 32 Q16 rounds half-even (k_fwd16's
+// quantiser), and the statistics change by the difference to the stored row.
+
+__device__ __forceinline__ double chroma_px(uint32_t R, uint32_t G, uint32_t B, int plane) {
+  return plane == 1 ? chroma_b((double)R, (double)G, (double)B) : chroma_r((double)R, (double)G, (double)B);
+}
+
+// Four pixels x0 - 1 .. x0 + 2 of one image row: 12 bytes from byte offset a,
+// read as the 4-aligned 16-byte span around them (inside the row: the caller
+// keeps x0 + 3 < W).  Raw dwords first (issued one row ahead), chroma after.
+struct Raw4 {
+  uint32_t w0, w1, w2, w3, sh;
+};
+__device__ __forceinline__ Raw4 load_row4(const uint8_t* p, long long) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
+  return Raw4{w[0], w[1], w[2], w[3], (uint32_t)((uintptr_t)p & 3)};
+}
+// the prefilter's row pass at x0 (ra) and x0 + 1 (rb): cv2 RowFilter<double>
+__device__ __forceinline__ void row_pass_pair(const Raw4& w, int plane, const double (&k)[3], double& ra,
+                                              double& rb) {
+  const uint32_t d0 = __builtin_amdgcn_alignbyte(w.w1, w.w0, w.sh), d1 = __builtin_amdgcn_alignbyte(w.w2, w.w1, w.sh),
+                 d2 = __builtin_amdgcn_alignbyte(w.w3, w.w2, w.sh);
+  const double c0 = chroma_px(d0 & 255u, (d0 >> 8) & 255u, (d0 >> 16) & 255u, plane);
+  const double c1 = chroma_px(d0 >> 24, d1 & 255u, (d1 >> 8) & 255u, plane);
+  const double c2 = chroma_px((d1 >> 16) & 255u, d1 >> 24, d2 & 255u, plane);
+  const double c3 = chroma_px((d2 >> 8) & 255u, (d2 >> 16) & 255u, d2 >> 24, plane);
+  double t = k[0] * c0;
+  t = t + k[1] * c1;
+  ra = t + k[2] * c2;
+  t = k[0] * c1;
+  t = t + k[1] * c2;
+  rb = t + k[2] * c3;
+}
+
+// v[i] = sample(gy*16 + i, gx*16 + line) - 128 of the padded plane, exactly
+// (col: the lane's column of the block's LDS tile, scratch for the interior
+// prefiltered walk).
+template <int MODE, bool PF>
+__device__ __forceinline__ void fix_column(const uint8_t* __restrict__ img, const Geo& g, int plane, int gy, int gx,
+                                           int line, const double (&k)[3], double (&v)[16], double* col) {
+  constexpr int SY = Cfg16F<MODE>::SY;
+  if (plane == 0 || MODE == M444) {
+    const int x = reflect_pad(gx * 16 + line, g.W);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int y = reflect_pad(gy * 16 + i, g.H);
+      const uint8_t* p = img + ((size_t)y * g.W + x) * 3;
+      const double R = p[0], G = p[1], B = p[2];
+      v[i] = (plane == 0 ? luma(R, G, B) : (plane == 1 ? chroma_b(R, G, B) : chroma_r(R, G, B))) - 128.0;
+    }
+    return;
+  }
+  const int sc = gx * 16 + line, x0 = 2 * sc;
+  if constexpr (PF) {
+    // interior: the prefilter's rows rolled down the column (full-resolution
+    // rows SY*16*gy - 1 .. SY*16*gy + 16*SY), each row pass computed once
+    const bool interior = gy * 16 + 16 <= g.hc && gx * 16 + 16 <= g.wc && gy > 0 && gx > 0 &&
+                          SY * 16 * gy + 16 * SY < g.H && 32 * gx + 34 < g.W;  // uniform per 16-lane group
+    if (interior) {
+      // window row r = full-resolution row SY*16*gy - 1 + r (r < NR); sample i
+      // reads rows SY*i .. SY*i + SY + 1.  The rows are walked in order, P
+      // rows' loads in flight, the last SY + 2 row passes in a shift register;
+      // a sample is formed once its last row is in and parked in the block's
+      // LDS column (runtime index).
+      constexpr int NR = 16 * SY + 2, P = 8, RING = SY + 2;
+      const long long stride = (long long)g.W * 3;
+      const uint8_t* rowp = img + ((long long)(SY * 16 * gy - 1) * g.W + x0 - 1) * 3;
+      Raw4 raw[P];
+#pragma unroll
+      for (int j = 0; j < P; ++j) raw[j] = load_row4(rowp + j * stride, 0);
+      double ra[RING], rb[RING];
+#pragma unroll 1
+      for (int r0 = 0; r0 < NR; r0 += P) {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int r = r0 + j;
+          if (r < NR) {  // uniform
+#pragma unroll
+            for (int q = 0; q + 1 < RING; ++q) {
+              ra[q] = ra[q + 1];
+              rb[q] = rb[q + 1];
+            }
+            row_pass_pair(raw[j], plane, k, ra[RING - 1], rb[RING - 1]);
+            if (r + P < NR) raw[j] = load_row4(rowp + (r + P) * stride, 0);
+            // P is even, so r's parity is j's: the SY = 2 emission test folds
+            if (r >= SY + 1 && (SY == 1 || (j & 1) == 1)) {
+              const int i = (r - SY - 1) / SY;
+              double sm[SY][2];
+#pragma unroll
+              for (int q = 0; q < SY; ++q) {  // ring[q + 1] = full-resolution row SY*(gy*16+i) + q
+                const double da = k[1] * ra[q + 1] + 0.0;  // SymmColumnFilter<double>
+                sm[q][0] = da + k[0] * (ra[q + 2] + ra[q]);
+                const double db = k[1] * rb[q + 1] + 0.0;
+                sm[q][1] = db + k[0] * (rb[q + 2] + rb[q]);
+              }
+              double m;
+              if constexpr (SY == 2)
+                m = (((sm[0][0] + sm[0][1]) + sm[1][0]) + sm[1][1]) * 0.25;
+              else
+                m = (sm[0][0] + sm[0][1]) * 0.5;
+              col[i * 17] = m - 128.0;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = col[i * 17];
+      return;
+    }
+#pragma unroll 2
+    for (int i = 0; i < 16; ++i) v[i] = sample64<MODE, PF>(img, g, plane, gy * 16 + i, sc, k) - 128.0;
+    return;
+  } else {  // INTER_AREA mean without the prefilter
+    const int xr = reflect_pad(sc, g.wc);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int sr = reflect_pad(gy * 16 + i, g.hc);
+      double s[SY][2];
+#pragma unroll
+      for (int a = 0; a < SY; ++a) {
+        const uint8_t* p = img + ((size_t)(SY * sr + a) * g.W + 2 * xr) * 3;
+        s[a][0] = chroma_px(p[0], p[1], p[2], plane);
+        s[a][1] = chroma_px(p[3], p[4], p[5], plane);
+      }
+      double m;
+      if constexpr (SY == 2)
+        m = (((s[0][0] + s[0][1]) + s[1][0]) + s[1][1]) * 0.25;
+      else
+        m = (s[0][0] + s[0][1]) * 0.5;
+      v[i] = m - 128.0;
+    }
+  }
+}
+
 #ifndef JDS_FIX16_WPE
 #define JDS_FIX16_WPE 3
 #endif
 #ifndef JDS_FIX16_GRID
-#define JDS_FIX16_GRID 3072  // 3 per SIMD (LDS and VGPRs allow it at 4:2:2)
+#define JDS_FIX16_GRID 4096
 #endif
 template <int MODE, bool PF>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(JDS_FIX16_WPE)))
 k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
             const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
-            const uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount, unsigned* __restrict__ fixlen,
+            const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, unsigned* __restrict__ fixlen,
             const unsigned cap) {
-  constexpr bool CPLANE = (MODE != M444) && PF;
-  constexpr int SY = Cfg16F<MODE>::SY;
-  constexpr int WRR = 16 * SY + 2, WCC = 34;  // prefilter source window of one chroma block
-  __shared__ double s_b[16 * 17];
-  __shared__ double s_w[CPLANE ? WRR * WCC : 1];         // fp64 chroma of the window
-  __shared__ double s_rf[CPLANE ? WRR * (WCC - 2) : 1];  // after the row pass
-  const int t = threadIdx.x;
+  __shared__ double s_b[4 * 272];  // four blocks, rows of 17 (jds_b16.hip's BS16 layout)
+  const int lane = threadIdx.x, grp = lane >> 4, line = lane & 15;
+#ifdef JDS_P16_FIXNONE  // tools/probe: an empty list (timing only)
+  const unsigned c = *fixcount * 0u;
+#else
   const unsigned c = *fixcount;
+#endif
   const unsigned count = c < cap ? c : cap;
   const double k[3] = {gk[0], gk[1], gk[2]};
-  for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
-    const uint2 ent = fixlist[e];
-    const int frame = (int)ent.x;
-    const int plane = (int)(ent.y >> 24);
-    const int bidx = (int)(ent.y & 0xffffffu);
-    const int nbx = plane ? g.ncx : g.nbx;
-    const int gy = bidx / nbx, gx = bidx - gy * nbx;
-    const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
-    // lanes 0-15 (row u = t): the stored row, fetched now (its latency hides under the sampling)
-    const long long off = (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
-                          (long long)bidx * 256 + (t & 15) * 16;
-    uint4* dst = reinterpret_cast<uint4*>(coeffs + off);
+  double* const sb = s_b + grp * 272;
+  for (unsigned e0 = blockIdx.x * 4u; e0 < count; e0 += gridDim.x * 4u) {
+    const unsigned e = e0 + (unsigned)grp;
+    const bool act = e < count;  // uniform per 16-lane group
+    int frame = 0, plane = 0, bidx = 0, gy = 0, gx = 0;
     uint4 o0 = make_uint4(0u, 0u, 0u, 0u), o1 = o0;
-    if (t < 16) {
+    uint4* dst = nullptr;
+    double v[16];
+    if (act) {
+      const uint2 ent = fixlist[e];
+      frame = (int)ent.x;
+      plane = (int)(ent.y >> 24);
+      bidx = (int)(ent.y & 0xffffffu);
+      const int nbx = plane ? g.ncx : g.nbx;
+      gy = bidx / nbx;
+      gx = bidx - gy * nbx;
+      // row `line` of the stored block, fetched first (its latency hides under the sampling)
+      const long long off = (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
+                            (long long)bidx * 256 + line * 16;
+      dst = reinterpret_cast<uint4*>(coeffs + off);
       o0 = dst[0];
       o1 = dst[1];
+      fix_column<MODE, PF>(rgb + (size_t)frame * g.H * g.W * 3, g, plane, gy, gx, line, k, v, sb + line);
+      dct2_line16(v);  // axis 0, column `line`
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sb[r * 17 + line] = v[r];
     }
-    const int wy0 = SY * 16 * gy - 1, wx0 = 32 * gx - 1;
-#ifdef JDS_P16FIX_NOSAMPLE
-    s_b[t] = (double)t; s_b[t + 64] = 1.0; s_b[t + 128] = 2.0; s_b[t + 192] = 3.0;
-#endif
-    const bool staged = CPLANE && plane != 0 && gy * 16 + 16 <= g.hc && gx * 16 + 16 <= g.wc && wy0 >= 0 &&
-                        wx0 >= 0 && wy0 + WRR <= g.H && wx0 + WCC <= g.W;
-#ifdef JDS_P16FIX_NOSAMPLE
-    if (false) {
-#else
-    if (staged) {  // uniform per workgroup
-#endif
-      constexpr int NWL = (WRR * WCC + 63) / 64;
-      uint32_t px[NWL];
+    __builtin_amdgcn_wave_barrier();  // the exchange is wave-local; the LDS keeps a wave's order
+    if (act) {  // axis 1, row u = line; requantize and correct the statistics
+      const int u = line;
 #pragma unroll
-      for (int l = 0; l < NWL; ++l) {
-        const int q = t + 64 * l;
-        px[l] = 0u;
-        if (q < WRR * WCC) {
-          const int r = q / WCC, cc = q - r * WCC;
-          const uint8_t* p = img + ((size_t)(wy0 + r) * g.W + wx0 + cc) * 3;
-          px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
-        }
-      }
-#pragma unroll
-      for (int l = 0; l < NWL; ++l) {
-        const int q = t + 64 * l;
-        if (q < WRR * WCC) {
-          double R, G, B;
-          unpack(px[l], R, G, B);
-          s_w[q] = plane == 1 ? chroma_b(R, G, B) : chroma_r(R, G, B);
-        }
-      }
-      __syncthreads();
-      for (int q = t; q < WRR * (WCC - 2); q += 64) {  // cv2 RowFilter<double>
-        const int r = q / (WCC - 2), cc = q - r * (WCC - 2) + 1;
-        const double* w = s_w + r * WCC + cc;
-        double a = k[0] * w[-1];
-        a = a + k[1] * w[0];
-        s_rf[q] = a + k[2] * w[1];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int l = 0; l < 4; ++l) {
-        const int i = (t >> 4) + 4 * l, j = t & 15;
-        double sm[SY][2];
-#pragma unroll
-        for (int a = 0; a < SY; ++a) {
-#pragma unroll
-          for (int bb = 0; bb < 2; ++bb) {
-            const double* f = s_rf + (SY * i + a + 1) * (WCC - 2) + 2 * j + bb;
-            const double d = k[1] * f[0] + 0.0;  // SymmColumnFilter<double>
-            sm[a][bb] = d + k[0] * (f[WCC - 2] + f[-(WCC - 2)]);
-          }
-        }
-        double v;
-        if constexpr (SY == 2)
-          v = (((sm[0][0] + sm[0][1]) + sm[1][0]) + sm[1][1]) * 0.25;
-        else
-          v = (sm[0][0] + sm[0][1]) * 0.5;
-        s_b[i * 17 + j] = v - 128.0;
-      }
-    } else {
-#ifdef JDS_P16FIX_NOSAMPLE
-      if (false)
-#endif
-#pragma unroll
-      for (int l = 0; l < 4; ++l) {
-        const int i = (t >> 4) + 4 * l, j = t & 15;
-        s_b[i * 17 + j] = sample64<MODE, PF>(img, g, plane, gy * 16 + i, gx * 16 + j, k) - 128.0;
-      }
-    }
-    __syncthreads();
-    double v[16];
-    if (t < 16) {  // axis 0, column t
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = s_b[r * 17 + t];
-#ifndef JDS_P16FIX_NODCT
+      for (int cc = 0; cc < 16; ++cc) v[cc] = sb[u * 17 + cc];
       dct2_line16(v);
-#endif
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s_b[r * 17 + t] = v[r];
-    }
-    __syncthreads();
-    if (t < 16) {  // axis 1, row u = t; requantize and correct the statistics
-      const int u = t;
-#pragma unroll
-      for (int cc = 0; cc < 16; ++cc) v[cc] = s_b[u * 17 + cc];
-#ifndef JDS_P16FIX_NODCT
-      dct2_line16(v);
-#endif
       const uint32_t ow[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
       uint32_t nw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
       long long dnz = 0, dmb = 0;
       jds_frame_stats* fs = st + frame;
+      const double* q8 = fq[frame].q + (u >> 1) * 8;
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) {
         // quantizer.py:22-24: the true quotient of the reference's coefficient
         // (v / 32, exact) by Q16 = Q8[u/2][cc/2]
-        const int qn = (int)__builtin_rint(v[cc] / (32.0 * fq[frame].q[(u >> 1) * 8 + (cc >> 1)]));
+        const int qn = (int)__builtin_rint(v[cc] / (32.0 * q8[cc >> 1]));
         const int qo = (int16_t)((ow[cc >> 1] >> ((cc & 1) * 16)) & 0xffffu);
         nw[cc >> 1] |= (uint32_t)(uint16_t)qn << ((cc & 1) * 16);
 #ifdef JDS_P16FIX_NOSTAT
@@ -554,57 +625,51 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       if (dnz) atomicAdd((unsigned long long*)&fs->nonzero, (unsigned long long)dnz);
       if (dmb) atomicAdd((unsigned long long*)&fs->magnitude_bits, (unsigned long long)dmb);
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();  // the next iteration's column writes after these row reads
   }
-  // the last workgroup re-arms the counter (its count kept in fixlen for
-  // jds_plan_fix_counts): every workgroup read it before taking a ticket
-  __syncthreads();
-  if (t == 0) {
-    const unsigned tk = atomicAdd(fixcount + 1, 1u);
-    if (tk == gridDim.x - 1) {
-      *fixlen = c;
-      fixcount[0] = 0u;
-      fixcount[1] = 0u;
-    }
-  }
+  // the run's list length for jds_plan_fix_counts (the counter itself is
+  // zeroed by the run after next's forward; no ticket: 4096 workgroups
+  // serialising on one device-scope atomic took ~150 us)
+  if (blockIdx.x == 0 && lane == 0) *fixlen = c;
 }
 
 // ------------------------------------------------------------ launchers --
 
 hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s);
-constexpr int FIX16_GRID = JDS_FIX16_GRID;  // k_fix_fwd16 workgroups
+constexpr int FIX16_GRID = JDS_FIX16_GRID;  // k_fix_fwd16 workgroups (x 4 blocks in flight)
 
 template <int MODE, bool PF>
 static hipError_t fast16_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
                            const void* fq16, const double* gk, const float* gk32, jds_frame_stats* st,
-                           uint32_t* part, uint2* fixlist, unsigned* counters, int fix_all, hipStream_t s) {
+                           uint32_t* part, uint2* fixlist, unsigned* counters, int fix_all, int parity,
+                           hipStream_t s) {
   using C = Cfg16F<MODE>;
   const unsigned cap = (unsigned)((g.cpf / 256) * n);
   const int tiles = g.tiles_y * g.tiles_x;
   hipLaunchKernelGGL((k_fwd16f<MODE, PF>), dim3(tiles, n), dim3(C::TF), 0, s, g, rgb, coeffs, (const FastQ16*)fq16,
-                     gk32, part, fixlist, counters, cap, fix_all);
+                     gk32, part, fixlist, counters + parity, counters + (parity ^ 1), cap, fix_all);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_fix_fwd16<MODE, PF>), dim3(FIX16_GRID), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
-                     counters, counters + 2, cap);
+                     counters + parity, counters + 2, cap);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return launch_fwd_reduce(n, st, part, tiles, s);  // the per-tile partials (order-free: u64 atomics)
 }
 
-// counters: [0] list length (live), [1] fix-up tickets, [2] the last run's length
+// counters: [0..1] list lengths (this run appends to [parity]), [2] the run's length
 hipError_t launch_fast_fwd16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs,
                              const FrameQ* fq, const void* fq16, const double* gk, const float* gk32,
                              jds_frame_stats* st, uint32_t* part, uint2* fixlist, unsigned* counters, int fix_all,
-                             hipStream_t s) {
+                             int parity, hipStream_t s) {
   switch (mode) {
     case M420:
-      return pf ? fast16_t<M420, true>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s)
-                : fast16_t<M420, false>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s);
+      return pf ? fast16_t<M420, true>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, parity, s)
+                : fast16_t<M420, false>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, parity, s);
     case M422:
-      return pf ? fast16_t<M422, true>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s)
-                : fast16_t<M422, false>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s);
+      return pf ? fast16_t<M422, true>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, parity, s)
+                : fast16_t<M422, false>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, parity, s);
     default:
-      return fast16_t<M444, false>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, s);
+      return fast16_t<M444, false>(g, n, rgb, coeffs, fq, fq16, gk, gk32, st, part, fixlist, counters, fix_all, parity, s);
   }
 }
 

@@ -75,8 +75,9 @@ struct Side {
 // Buffers of the certified 16x16 forward (jds_fast16.hip): per-frame fp32
 // tables (FastQ16), the fp32 Gaussian taps, per-tile statistics partials
 // (NSTAT u32 per tile), the list of blocks the exact fix-up recomputes, and
-// counters [0] list length, [1] fix-up tickets (both
-// re-armed by k_fix_fwd16), [2] the last run's list length.  Zeroed at plan
+// counters: [0..1] list lengths, alternating between runs (`parity`: a run
+// appends to [parity] and zeroes [parity ^ 1], which the previous run's
+// fix-up has consumed), [2] the last run's list length.  Zeroed at plan
 // creation.
 struct Fwd16Fast {
   const void* fq16;
@@ -85,6 +86,7 @@ struct Fwd16Fast {
   uint2* fixlist;
   unsigned* counters;
   int fix_all;  // test: list every block
+  int parity;
 };
 
 // Counters of the certified fast inverse (jds_inv_fast.hip).
