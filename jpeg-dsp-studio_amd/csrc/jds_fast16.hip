@@ -13,6 +13,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "jds_dct16.hpp"
 #include "jds_device.hpp"
 #include "jds_fwd_common.hpp"
@@ -417,21 +419,32 @@ __device__ __forceinline__ Raw4 load_row4(const uint8_t* p, long long) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
   return Raw4{w[0], w[1], w[2], w[3], (uint32_t)((uintptr_t)p & 3)};
 }
-// the prefilter's row pass at x0 (ra) and x0 + 1 (rb): cv2 RowFilter<double>
-__device__ __forceinline__ void row_pass_pair(const Raw4& w, int plane, const double (&k)[3], double& ra,
-                                              double& rb) {
+__device__ __forceinline__ void decode_row4(const Raw4& w, int plane, double (&c)[4]) {
   const uint32_t d0 = __builtin_amdgcn_alignbyte(w.w1, w.w0, w.sh), d1 = __builtin_amdgcn_alignbyte(w.w2, w.w1, w.sh),
                  d2 = __builtin_amdgcn_alignbyte(w.w3, w.w2, w.sh);
-  const double c0 = chroma_px(d0 & 255u, (d0 >> 8) & 255u, (d0 >> 16) & 255u, plane);
-  const double c1 = chroma_px(d0 >> 24, d1 & 255u, (d1 >> 8) & 255u, plane);
-  const double c2 = chroma_px((d1 >> 16) & 255u, d1 >> 24, d2 & 255u, plane);
-  const double c3 = chroma_px((d2 >> 8) & 255u, (d2 >> 16) & 255u, d2 >> 24, plane);
-  double t = k[0] * c0;
-  t = t + k[1] * c1;
-  ra = t + k[2] * c2;
-  t = k[0] * c1;
-  t = t + k[1] * c2;
-  rb = t + k[2] * c3;
+  c[0] = chroma_px(d0 & 255u, (d0 >> 8) & 255u, (d0 >> 16) & 255u, plane);
+  c[1] = chroma_px(d0 >> 24, d1 & 255u, (d1 >> 8) & 255u, plane);
+  c[2] = chroma_px((d1 >> 16) & 255u, d1 >> 24, d2 & 255u, plane);
+  c[3] = chroma_px((d2 >> 8) & 255u, (d2 >> 16) & 255u, d2 >> 24, plane);
+}
+// the same four pixels at reflected columns xs[] of image row y (edge blocks)
+struct Px4 {
+  uint8_t b[12];
+};
+__device__ __forceinline__ Px4 load_px4(const uint8_t* img, const Geo& g, int y, const int (&xs)[4]) {
+  Px4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint8_t* p = img + ((size_t)y * g.W + xs[j]) * 3;
+    o.b[3 * j] = p[0];
+    o.b[3 * j + 1] = p[1];
+    o.b[3 * j + 2] = p[2];
+  }
+  return o;
+}
+__device__ __forceinline__ void decode_px4(const Px4& w, int plane, double (&c)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c[j] = chroma_px(w.b[3 * j], w.b[3 * j + 1], w.b[3 * j + 2], plane);
 }
 
 // v[i] = sample(gy*16 + i, gx*16 + line) - 128 of the padded plane, exactly
@@ -454,56 +467,80 @@ __device__ __forceinline__ void fix_column(const uint8_t* __restrict__ img, cons
   }
   const int sc = gx * 16 + line, x0 = 2 * sc;
   if constexpr (PF) {
-    // interior: the prefilter's rows rolled down the column (full-resolution
-    // rows SY*16*gy - 1 .. SY*16*gy + 16*SY), each row pass computed once
-    const bool interior = gy * 16 + 16 <= g.hc && gx * 16 + 16 <= g.wc && gy > 0 && gx > 0 &&
-                          SY * 16 * gy + 16 * SY < g.H && 32 * gx + 34 < g.W;  // uniform per 16-lane group
-    if (interior) {
-      // window row r = full-resolution row SY*16*gy - 1 + r (r < NR); sample i
-      // reads rows SY*i .. SY*i + SY + 1.  The rows are walked in order, P
-      // rows' loads in flight, the last SY + 2 row passes in a shift register;
-      // a sample is formed once its last row is in and parked in the block's
-      // LDS column (runtime index).
-      constexpr int NR = 16 * SY + 2, P = 8, RING = SY + 2;
-      const long long stride = (long long)g.W * 3;
-      const uint8_t* rowp = img + ((long long)(SY * 16 * gy - 1) * g.W + x0 - 1) * 3;
-      Raw4 raw[P];
+    // the prefilter's rows walked down the column: window row r = full-
+    // resolution row SY*16*gy - 1 + r (r < NR); sample i reads rows SY*i ..
+    // SY*i + SY + 1.  Rows are walked in order with P rows' loads in flight,
+    // the last SY + 2 row passes in a shift register; a sample is formed once
+    // its last row is in and parked in the block's LDS column (runtime index).
+    // Blocks inside the image read 4-aligned dword spans; blocks on the image
+    // edge read bytes with BORDER_REFLECT_101 (cv2's filter border) -- every
+    // block but those holding np.pad rows/columns, whose sample rows are not
+    // monotone (sample64 per sample).
+    const bool padded = gy * 16 + 16 > g.hc || gx * 16 + 16 > g.wc;  // uniform per 16-lane group
+    if (!padded) {
+      constexpr int NR = 16 * SY + 2, RING = SY + 2;
+      auto walk = [&](auto load, auto decode, auto& raw, auto P_) {
+        constexpr int P = decltype(P_)::value;
 #pragma unroll
-      for (int j = 0; j < P; ++j) raw[j] = load_row4(rowp + j * stride, 0);
-      double ra[RING], rb[RING];
+        for (int j = 0; j < P; ++j) raw[j] = load(j);
+        double ra[RING], rb[RING];
 #pragma unroll 1
-      for (int r0 = 0; r0 < NR; r0 += P) {
+        for (int r0 = 0; r0 < NR; r0 += P) {
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-          const int r = r0 + j;
-          if (r < NR) {  // uniform
+          for (int j = 0; j < P; ++j) {
+            const int r = r0 + j;
+            if (r < NR) {  // uniform
 #pragma unroll
-            for (int q = 0; q + 1 < RING; ++q) {
-              ra[q] = ra[q + 1];
-              rb[q] = rb[q + 1];
-            }
-            row_pass_pair(raw[j], plane, k, ra[RING - 1], rb[RING - 1]);
-            if (r + P < NR) raw[j] = load_row4(rowp + (r + P) * stride, 0);
-            // P is even, so r's parity is j's: the SY = 2 emission test folds
-            if (r >= SY + 1 && (SY == 1 || (j & 1) == 1)) {
-              const int i = (r - SY - 1) / SY;
-              double sm[SY][2];
-#pragma unroll
-              for (int q = 0; q < SY; ++q) {  // ring[q + 1] = full-resolution row SY*(gy*16+i) + q
-                const double da = k[1] * ra[q + 1] + 0.0;  // SymmColumnFilter<double>
-                sm[q][0] = da + k[0] * (ra[q + 2] + ra[q]);
-                const double db = k[1] * rb[q + 1] + 0.0;
-                sm[q][1] = db + k[0] * (rb[q + 2] + rb[q]);
+              for (int q = 0; q + 1 < RING; ++q) {
+                ra[q] = ra[q + 1];
+                rb[q] = rb[q + 1];
               }
-              double m;
-              if constexpr (SY == 2)
-                m = (((sm[0][0] + sm[0][1]) + sm[1][0]) + sm[1][1]) * 0.25;
-              else
-                m = (sm[0][0] + sm[0][1]) * 0.5;
-              col[i * 17] = m - 128.0;
+              double c[4];
+              decode(raw[j], c);
+              if (r + P < NR) raw[j] = load(r + P);
+              double t = k[0] * c[0];  // cv2 RowFilter<double> at x0 and x0 + 1
+              t = t + k[1] * c[1];
+              ra[RING - 1] = t + k[2] * c[2];
+              t = k[0] * c[1];
+              t = t + k[1] * c[2];
+              rb[RING - 1] = t + k[2] * c[3];
+              // P is even, so r's parity is j's: the SY = 2 emission test folds
+              if (r >= SY + 1 && (SY == 1 || (j & 1) == 1)) {
+                const int i = (r - SY - 1) / SY;
+                double sm[SY][2];
+#pragma unroll
+                for (int q = 0; q < SY; ++q) {  // ring[q + 1] = full-resolution row SY*(gy*16+i) + q
+                  const double da = k[1] * ra[q + 1] + 0.0;  // SymmColumnFilter<double>
+                  sm[q][0] = da + k[0] * (ra[q + 2] + ra[q]);
+                  const double db = k[1] * rb[q + 1] + 0.0;
+                  sm[q][1] = db + k[0] * (rb[q + 2] + rb[q]);
+                }
+                double m;
+                if constexpr (SY == 2)
+                  m = (((sm[0][0] + sm[0][1]) + sm[1][0]) + sm[1][1]) * 0.25;
+                else
+                  m = (sm[0][0] + sm[0][1]) * 0.5;
+                col[i * 17] = m - 128.0;
+              }
             }
           }
         }
+      };
+      const int yw0 = SY * 16 * gy - 1;
+      const bool interior = gy > 0 && gx > 0 && yw0 + NR <= g.H && 32 * gx + 34 < g.W;  // uniform per group
+      if (interior) {
+        const long long stride = (long long)g.W * 3;
+        const uint8_t* rowp = img + ((long long)yw0 * g.W + x0 - 1) * 3;
+        Raw4 raw[8];
+        walk([&](int r) { return load_row4(rowp + r * stride, 0); },
+             [&](const Raw4& w, double (&c)[4]) { decode_row4(w, plane, c); }, raw,
+             std::integral_constant<int, 8>());
+      } else {
+        const int xs[4] = {reflect101(x0 - 1, g.W), x0, x0 + 1, reflect101(x0 + 2, g.W)};
+        Px4 raw[4];
+        walk([&](int r) { return load_px4(img, g, reflect101(yw0 + r, g.H), xs); },
+             [&](const Px4& w, double (&c)[4]) { decode_px4(w, plane, c); }, raw,
+             std::integral_constant<int, 4>());
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = col[i * 17];
@@ -577,8 +614,15 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       dst = reinterpret_cast<uint4*>(coeffs + off);
       o0 = dst[0];
       o1 = dst[1];
+#ifdef JDS_P16FIX_NOSAMPLE  // tools/probe: constant samples (timing only)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = (double)(i * 3 + line + (int)(o0.x & 7u));
+#else
       fix_column<MODE, PF>(rgb + (size_t)frame * g.H * g.W * 3, g, plane, gy, gx, line, k, v, sb + line);
+#endif
+#ifndef JDS_P16FIX_NODCT
       dct2_line16(v);  // axis 0, column `line`
+#endif
 #pragma unroll
       for (int r = 0; r < 16; ++r) sb[r * 17 + line] = v[r];
     }
@@ -587,7 +631,9 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       const int u = line;
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) v[cc] = sb[u * 17 + cc];
+#ifndef JDS_P16FIX_NODCT
       dct2_line16(v);
+#endif
       const uint32_t ow[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
       uint32_t nw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
       long long dnz = 0, dmb = 0;
@@ -597,7 +643,11 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       for (int cc = 0; cc < 16; ++cc) {
         // quantizer.py:22-24: the true quotient of the reference's coefficient
         // (v / 32, exact) by Q16 = Q8[u/2][cc/2]
+#ifdef JDS_P16FIX_NODIV  // tools/probe: a product instead of the division (timing only)
+        const int qn = (int)__builtin_rint(v[cc] * q8[cc >> 1]);
+#else
         const int qn = (int)__builtin_rint(v[cc] / (32.0 * q8[cc >> 1]));
+#endif
         const int qo = (int16_t)((ow[cc >> 1] >> ((cc & 1) * 16)) & 0xffffu);
         nw[cc >> 1] |= (uint32_t)(uint16_t)qn << ((cc & 1) * 16);
 #ifdef JDS_P16FIX_NOSTAT
