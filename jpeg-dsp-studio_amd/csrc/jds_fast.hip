@@ -933,11 +933,13 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     uint4* dst = reinterpret_cast<uint4*>(coeffs + off);
     uint4 old = make_uint4(0u, 0u, 0u, 0u);
     if (t < 8) old = *dst;
-    // prefiltered chroma of a block away from every edge: stage the source
-    // window once (colour, then the row pass, in LDS), same fp64 operations
+    // prefiltered chroma of a block without np.pad samples: stage the source
+    // window once (colour, then the row pass, in LDS), same fp64 operations as
+    // sample64; window rows/columns outside the image are cv2's
+    // BORDER_REFLECT_101 pixels, so edge blocks stage too (sample64 per sample
+    // chains ~4 dependent load rounds per thread: such blocks set the tail)
     const int wy0 = SY * 8 * gy - 1, wx0 = 16 * gx - 1;
-    const bool staged = CPLANE && plane != 0 && gy * 8 + 8 <= g.hc && gx * 8 + 8 <= g.wc && wy0 >= 0 &&
-                        wx0 >= 0 && wy0 + WRR <= g.H && wx0 + WCC <= g.W;
+    const bool staged = CPLANE && plane != 0 && gy * 8 + 8 <= g.hc && gx * 8 + 8 <= g.wc;
     if (staged) {  // uniform per workgroup
       // every window load in flight before the first use (one memory latency)
       constexpr int NWL = (WRR * WCC + 63) / 64;
@@ -948,7 +950,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
         px[l] = 0u;
         if (q < WRR * WCC) {
           const int r = q / WCC, c = q - r * WCC;
-          const uint8_t* p = img + ((size_t)(wy0 + r) * g.W + wx0 + c) * 3;
+          const uint8_t* p = img + ((size_t)reflect101(wy0 + r, g.H) * g.W + reflect101(wx0 + c, g.W)) * 3;
           px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
         }
       }
