@@ -177,31 +177,6 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
   const FastQ16& fq = fq16[frame];
 
-  {  // every window load in flight before the first LDS store
-    constexpr int NL = (WN + C::TF - 1) / C::TF;
-    uint32_t px[NL];
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      const int i = tid + l * C::TF;
-      px[l] = 0u;
-      if (i < WN) {
-        const int r = i / WC, c = i - r * WC;
-        const int yy = reflect101(y0 - 1 + r, g.H), xx = reflect101(x0 - 1 + c, g.W);
-        const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
-        px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
-      }
-    }
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      const int i = tid + l * C::TF;
-      if (i < WN) s_rgb[i] = px[l];
-    }
-  }
-  if (tid <= NSTAT) s_st[tid] = 0u;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *fixnext = 0u;  // the next run's list
-  const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
-  __syncthreads();
-
   auto rgbf = [](uint32_t v, float& R, float& G, float& B) {
     R = (float)(v & 255u);
     G = (float)((v >> 8) & 255u);
@@ -215,47 +190,150 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 #else
   auto cidx = [](int r, int c) { return r * WC + c; };
 #endif
-  if constexpr (CPLANE) {  // full-resolution chroma, then the prefilter's row pass in place
-    float* s_cb = s_u;
-    float* s_cr = s_u + WN;
+  if (tid <= NSTAT) s_st[tid] = 0u;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *fixnext = 0u;  // the next run's list
+  const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
+
+  // Tiles whose columns lie inside the image (no np.pad samples; only the
+  // 1-px ring may reflect), rows 16-B aligned: one thread per 16-pixel row
+  // segment loads 48 B, packs the pixels for the luma / 4:4:4 / unfiltered
+  // samples and -- prefiltered chroma -- converts colour and runs the row
+  // pass in registers (neighbours from the adjacent lanes), writing the
+  // filtered planes directly.  Same fp32 operations as the general path.
+  constexpr int SEGS = C::TW / 16;
+  static_assert(WR * SEGS <= C::TF, "one thread per row segment");
+  const bool fast_stage = (g.W % 16) == 0 && x0 >= 0 && x0 + C::TW <= g.W && y0 >= 0 && y0 + C::TH <= g.H;
+  if (fast_stage) {  // uniform per workgroup
+    const int r = tid / SEGS, c = tid - r * SEGS;
+    if (r < WR) {
+      const int yy = reflect101(y0 - 1 + r, g.H);
+      const uint8_t* row = img + (size_t)yy * g.W * 3;
+      const uint4* p4 = reinterpret_cast<const uint4*>(row + (size_t)(x0 + 16 * c) * 3);
+      const bool luma_row = r >= 1 && r <= C::TH;
+      const bool need = CPLANE || luma_row;  // uniform per 4-lane row group
+      uint32_t w[12] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+      uint4 ring = make_uint4(0u, 0u, 0u, 0u);
+      if (need) {
+        const uint4 a0 = p4[0], a1 = p4[1], a2 = p4[2];
+        w[0] = a0.x; w[1] = a0.y; w[2] = a0.z; w[3] = a0.w;
+        w[4] = a1.x; w[5] = a1.y; w[6] = a1.z; w[7] = a1.w;
+        w[8] = a2.x; w[9] = a2.y; w[10] = a2.z; w[11] = a2.w;
+        if (CPLANE && c == 0 && x0 > 0) ring = p4[-1];                      // bytes 13..15: pixel x0 - 1
+        if (CPLANE && c == SEGS - 1 && x0 + C::TW < g.W) ring = p4[3];   // bytes 0..2: pixel x0 + TW
+      }
+      uint32_t px[16];
 #pragma unroll
-    for (int l = 0; l < (WN + C::TF - 1) / C::TF; ++l) {
-      const int i = tid + l * C::TF;
-      if (i < WN) {
-        float R, G, B;
-        rgbf(s_rgb[i], R, G, B);
-        const int r = i / WC, c = i - r * WC;
-        s_cb[cidx(r, c)] = cb32(R, G, B);
-        s_cr[cidx(r, c)] = cr32(R, G, B);
+      for (int j = 0; j < 16; ++j) {
+        const int b = 3 * j;
+        const uint32_t lo = w[b >> 2], hi = (b >> 2) + 1 < 12 ? w[(b >> 2) + 1] : 0u;
+        px[j] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(b & 3)) & 0xffffffu;
+      }
+      if (luma_row) {  // luma (and 4:4:4 / unfiltered chroma) samples: rows 1..TH, columns 1..TW
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s_rgb[r * WC + 1 + 16 * c + j] = px[j];
+      }
+      if constexpr (CPLANE) {
+        float cb[16], cr[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          float R, G, B;
+          rgbf(px[j], R, G, B);
+          cb[j] = cb32(R, G, B);
+          cr[j] = cr32(R, G, B);
+        }
+        float lb = __shfl_up(cb[15], 1, SEGS), lr = __shfl_up(cr[15], 1, SEGS);
+        float rb = __shfl_down(cb[0], 1, SEGS), rr = __shfl_down(cr[0], 1, SEGS);
+        if (c == 0) {  // pixel x0 - 1; pixel 1 at the image edge (BORDER_REFLECT_101)
+          const float R = (float)((ring.w >> 8) & 255u), G = (float)((ring.w >> 16) & 255u), B = (float)(ring.w >> 24);
+          lb = x0 == 0 ? cb[1] : cb32(R, G, B);
+          lr = x0 == 0 ? cr[1] : cr32(R, G, B);
+        }
+        if (c == SEGS - 1) {  // pixel x0 + TW; pixel W - 2 at the image edge
+          const float R = (float)(ring.x & 255u), G = (float)((ring.x >> 8) & 255u), B = (float)((ring.x >> 16) & 255u);
+          const bool edge = x0 + C::TW == g.W;
+          rb = edge ? cb[14] : cb32(R, G, B);
+          rr = edge ? cr[14] : cr32(R, G, B);
+        }
+        float* s_cb = s_u;
+        float* s_cr = s_u + WN;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float bl = j == 0 ? lb : cb[j - 1], br = j == 15 ? rb : cb[j + 1];
+          const float ql = j == 0 ? lr : cr[j - 1], qr = j == 15 ? rr : cr[j + 1];
+          s_cb[cidx(r, 1 + 16 * c + j)] = fmaf(k2, br, fmaf(k1, cb[j], k0 * bl));  // the row chain
+          s_cr[cidx(r, 1 + 16 * c + j)] = fmaf(k2, qr, fmaf(k1, cr[j], k0 * ql));
+        }
       }
     }
     __syncthreads();
-    constexpr int NRP = WR * (WC - 2);
-    constexpr int PER = (NRP + C::TF - 1) / C::TF;
-    float tb[PER], tr[PER];
+  } else {
+    {  // every window load in flight before the first LDS store
+      constexpr int NL = (WN + C::TF - 1) / C::TF;
+      uint32_t px[NL];
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int i = tid + j * C::TF;
-      if (i < NRP) {
-        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
-        const int il = cidx(r, c - 1), i0 = cidx(r, c), ir = cidx(r, c + 1);
-        tb[j] = fmaf(k2, s_cb[ir], fmaf(k1, s_cb[i0], k0 * s_cb[il]));  // the 8x8 kernels' row chain
-        tr[j] = fmaf(k2, s_cr[ir], fmaf(k1, s_cr[i0], k0 * s_cr[il]));
+      for (int l = 0; l < NL; ++l) {
+        const int i = tid + l * C::TF;
+        px[l] = 0u;
+        if (i < WN) {
+          const int r = i / WC, c = i - r * WC;
+          const int yy = reflect101(y0 - 1 + r, g.H), xx = reflect101(x0 - 1 + c, g.W);
+          const uint8_t* p = img + ((size_t)yy * g.W + xx) * 3;
+          px[l] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        const int i = tid + l * C::TF;
+        if (i < WN) s_rgb[i] = px[l];
       }
     }
     __syncthreads();
+    if constexpr (CPLANE) {  // full-resolution chroma, then the prefilter's row pass in place
+      float* s_cb = s_u;
+      float* s_cr = s_u + WN;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int i = tid + j * C::TF;
-      if (i < NRP) {
-        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
-        s_cb[cidx(r, c)] = tb[j];
-        s_cr[cidx(r, c)] = tr[j];
+      for (int l = 0; l < (WN + C::TF - 1) / C::TF; ++l) {
+        const int i = tid + l * C::TF;
+        if (i < WN) {
+          float R, G, B;
+          rgbf(s_rgb[i], R, G, B);
+          const int r = i / WC, c = i - r * WC;
+          s_cb[cidx(r, c)] = cb32(R, G, B);
+          s_cr[cidx(r, c)] = cr32(R, G, B);
+        }
       }
+      __syncthreads();
+      constexpr int NRP = WR * (WC - 2);
+      constexpr int PER = (NRP + C::TF - 1) / C::TF;
+      float tb[PER], tr[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int i = tid + j * C::TF;
+        if (i < NRP) {
+          const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
+          const int il = cidx(r, c - 1), i0 = cidx(r, c), ir = cidx(r, c + 1);
+          tb[j] = fmaf(k2, s_cb[ir], fmaf(k1, s_cb[i0], k0 * s_cb[il]));  // the 8x8 kernels' row chain
+          tr[j] = fmaf(k2, s_cr[ir], fmaf(k1, s_cr[i0], k0 * s_cr[il]));
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int i = tid + j * C::TF;
+        if (i < NRP) {
+          const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
+          s_cb[cidx(r, c)] = tb[j];
+          s_cr[cidx(r, c)] = tr[j];
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 
+#ifdef JDS_P16_ST1  // tools/probe: stop after staging (timing only)
+  if (s_u[tid] == 1234.5f && s_rgb[tid] == 77u) coeffs[tid] = 1;
+  return;
+#endif
   const int blk = tid >> 4, line = tid & 15;
   int plane, gy, gx;
   if (blk < C::NYB) {
@@ -313,7 +391,9 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
           v[i] = (s[0][0] + s[0][1]) * 0.5f - 128.0f;
       }
     }
+#ifndef JDS_P16_NODCT
     fdct16_f32(v);  // axis 0 (columns) first
+#endif
   }
   if constexpr (CPLANE) __syncthreads();  // the block buffer aliases the chroma planes
   float* s_blk = s_u + blk * BS16F;
@@ -330,12 +410,18 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     const int u = line;
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = s_blk[u * 17 + k];
+#ifndef JDS_P16_NODCT
     fdct16_f32(v);
+#endif
     const float* thr = fq.thr[plane ? 1 : 0];
     int q[16];
     unsigned nrare = 0u;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
+#ifdef JDS_P16_NOQ  // tools/probe: truncation instead of the certified quantiser (timing only)
+      q[k] = (int)v[k];
+      continue;
+#endif
       const float t = v[k] * fq.rq[u * 16 + k];
       const float r = rintf(t);
       // |t - r| is exact (Sterbenz); thr holds 0.5 - E/Q - slack, rounded down
