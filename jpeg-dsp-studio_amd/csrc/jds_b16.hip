@@ -774,6 +774,244 @@ k_inv16f(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, con
   }
 }
 
+// ------------------------------------------- fused inverse, one window (4:2:x) --
+//
+// k_inv16s<MODE, XTRA>: k_inv16f with the two chroma windows built one after
+// the other in the same LDS: Cb window -> luma IDCT, B bytes and the G partial
+// Y - 0.344136 (Cb - 128) per pixel (registers) -> Cr window -> R, G bytes and
+// the stores.  The reference evaluates G = Y - a (Cb - 128) - b (Cr - 128)
+// left to right, so the partial is the same double; every other operation is
+// k_inv16f's.  One fp64 window instead of two: 3 workgroups per CU at 4:2:2
+// instead of 2 (k_inv16f: 69 KB of LDS).
+template <int MODE, int XTRA>
+__global__ void __launch_bounds__(Inv16<MODE>::NT)
+k_inv16s(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+         const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
+         double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb) {
+  using I = Inv16<MODE>;
+  __shared__ __attribute__((aligned(16))) double s_b[I::NG * BS16];
+  __shared__ double s_cw[I::CWR * I::CWC];
+  __shared__ double s_q[64];
+  __shared__ double s_red[I::NT / 64];
+  __shared__ unsigned long long s_sse;
+
+  const int tid = threadIdx.x, grp = tid >> 4, line = tid & 15;
+  const int frame = blockIdx.y, tile = blockIdx.x;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int Y0 = ty * I::TH, X0 = tx * I::TW;
+  const int16_t* cf = coeffs + (size_t)frame * g.cpf;
+  if (tid < 64) s_q[tid] = fq[frame].q[tid];
+  if (XTRA && tid == 0) s_sse = 0ull;
+  __syncthreads();
+
+  const int cwy0 = Y0 / I::SY - I::RY, cwx0 = X0 / 2 - 1;
+  const int cby0 = (Y0 / I::SY) / 16 - I::RY, cbx0 = (X0 / 2) / 16 - 1;
+  double* const sb = s_b + grp * BS16;
+  // every coefficient row of the lane (both planes' chroma blocks and its luma
+  // block) requested before the first transform: one memory latency
+  constexpr int NCR = (I::NCB + I::NG - 1) / I::NG;  // chroma rounds per plane
+  Row16 crow[2][NCR];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll
+    for (int k = 0; k < NCR; ++k) {
+      const int bi = k * I::NG + grp;
+      const int by = cby0 + bi / I::CBC, bx = cbx0 + bi % I::CBC;
+      if (bi < I::NCB && by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx)
+        crow[p][k] = load_row16(cf + (p ? g.off_cr : g.off_cb) + ((long long)by * g.ncx + bx) * 256, line);
+    }
+  }
+  const int by = Y0 / 16 + grp / I::YBC, bx = X0 / 16 + grp % I::YBC;
+  Row16 lrow;
+  if (by < g.nby && bx < g.nbx) lrow = load_row16(cf + ((long long)by * g.nbx + bx) * 256, line);
+
+  auto build = [&](int p) {  // plane p's window: IDCT16 of the blocks the tile reaches (+ ring)
+#pragma unroll
+    for (int k = 0; k < NCR; ++k) {
+      const int bi = k * I::NG + grp;
+      if (bi < I::NCB) {
+        const int cy = cby0 + bi / I::CBC, cx = cbx0 + bi % I::CBC;
+        if (cy >= 0 && cx >= 0 && cy < g.ncy && cx < g.ncx) {  // uniform per 16-lane group
+          double r[16];
+          idct16_rows(crow[p][k], s_q, sb, line, r);
+          const int wr = cy * 16 + line - cwy0;
+          if ((unsigned)wr < (unsigned)I::CWR) {
+            double* w = &s_cw[wr * I::CWC];
+            const int wc0 = cx * 16 - cwx0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+              if ((unsigned)(wc0 + j) < (unsigned)I::CWC) w[wc0 + j] = r[j];
+          }
+        }
+      }
+    }
+  };
+  // one plane's upsampled chroma at pixels x0 .. x0 + 7 of row (wq, wt): k_inv16f's taps
+  auto upsample = [&](int x0, int wq, int wt, double (&C)[8]) {
+    const int c0 = x0 / 2 - 1 - cwx0;
+    double h0[8];
+#pragma unroll
+    for (int rr = 0; rr < I::SY; ++rr) {
+      const double* sp = &s_cw[(rr ? wt : wq) * I::CWC + c0];
+      double q75[5];
+#pragma unroll
+      for (int j = 1; j < 5; ++j) q75[j] = sp[j] * 0.75;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double e = fma(sp[i], 0.25, q75[i + 1]), o = fma(sp[i + 2], 0.25, q75[i + 1]);
+        if (rr == 0) {
+          h0[2 * i] = e;
+          h0[2 * i + 1] = o;
+        } else {
+          C[2 * i] = fma(h0[2 * i], 0.25, e * 0.75);
+          C[2 * i + 1] = fma(h0[2 * i + 1], 0.25, o * 0.75);
+        }
+      }
+    }
+    if constexpr (I::SY == 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) C[k] = h0[k];
+    }
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int kl = side == 0 ? (x0 == 0 ? 0 : -1) : (g.W - 1 - x0 < 8 ? g.W - 1 - x0 : -1);
+      if (kl >= 0) {
+        const int e = (side == 0 ? 0 : g.wc - 1) - cwx0;
+        double v = s_cw[wq * I::CWC + e];
+        if constexpr (I::SY == 2) v = fma(v, 0.25, s_cw[wt * I::CWC + e] * 0.75);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) C[k] = k == kl ? v : C[k];
+      }
+    }
+  };
+
+  // ---- 1. Cb window ----
+  build(0);
+  __syncthreads();
+  // ---- 2. luma row, Cb terms ----
+  const int y = by * 16 + line;
+  const bool act = by < g.nby && bx < g.nbx;  // uniform per 16-lane group
+  const bool rowok = act && y < g.H;
+  double Yv[16], Gt[16], Bv[XTRA > 1 ? 16 : 1];
+  uint32_t bbyte[16];
+  int wq = 0, wt = 0;
+  if (act) idct16_rows(lrow, s_q, sb, line, Yv);
+  if (rowok) {
+    if constexpr (I::SY == 2) {  // cv2 INTER_LINEAR rows: wq weight 1/4, wt weight 3/4 (k_inv2)
+      float fy = (float)((y + 0.5) * g.up_sy - 0.5);
+      const int sy = (int)floorf(fy);
+      fy -= (float)sy;
+      const int r0 = clampi(clampi(sy, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+      const int r1 = clampi(clampi(sy + 1, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+      const bool q0 = fy == 0.75f;
+      wq = q0 ? r0 : r1;
+      wt = q0 ? r1 : r0;
+    } else {
+      wq = y - cwy0;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int x0 = bx * 16 + 8 * h;
+      if (x0 < g.W) {
+        double C[8];
+        upsample(x0, wq, wt, C);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {  // color_space.py:17-24: the Cb terms of G and B
+          const double Yk = Yv[8 * h + k];
+          Gt[8 * h + k] = Yk - 0.344136 * (C[k] - 128.0);
+          const double B = Yk + 1.772 * (C[k] - 128.0);
+          bbyte[8 * h + k] = (uint32_t)clampi((int)B, 0, 255);
+          if constexpr (XTRA > 1) Bv[8 * h + k] = B;
+        }
+      }
+    }
+  }
+  __syncthreads();  // every Cb read done
+  // ---- 3. Cr window ----
+  build(1);
+  __syncthreads();
+  // ---- 4. Cr terms, store ----
+  unsigned long long sse = 0ull;
+  double ssy = 0.0;
+  const uint8_t* in_f = XTRA ? rgb_in + (size_t)frame * g.H * g.W * 3 : nullptr;
+  uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
+  if (rowok) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int x0 = bx * 16 + 8 * h;
+      if (x0 >= g.W) break;
+      double C[8];
+      upsample(x0, wq, wt, C);
+      const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
+      uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
+      uint32_t pk[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+      double R[8], G[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // color_space.py:17-24, pipeline.py:93-95
+        const double Yk = Yv[8 * h + k];
+        R[k] = Yk + 1.402 * (C[k] - 128.0);
+        G[k] = Gt[8 * h + k] - 0.714136 * (C[k] - 128.0);
+        const int b = 3 * k;
+        pk[b >> 2] |= (uint32_t)clampi((int)R[k], 0, 255) << (8 * (b & 3));
+        pk[(b + 1) >> 2] |= (uint32_t)clampi((int)G[k], 0, 255) << (8 * ((b + 1) & 3));
+        pk[(b + 2) >> 2] |= bbyte[8 * h + k] << (8 * ((b + 2) & 3));
+      }
+      if (nx == 8 && ((((uintptr_t)o) & 7u) == 0)) {
+        uint2* o2 = reinterpret_cast<uint2*>(o);
+        o2[0] = make_uint2(pk[0], pk[1]);
+        o2[1] = make_uint2(pk[2], pk[3]);
+        o2[2] = make_uint2(pk[4], pk[5]);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 24; ++b)
+          if (b < 3 * nx) o[b] = (uint8_t)(pk[b >> 2] >> (8 * (b & 3)));
+      }
+      if constexpr (XTRA > 0) {
+        const uint8_t* src = in_f + ((size_t)y * g.W + x0) * 3;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (k < nx) {
+            const int o0 = src[3 * k], o1 = src[3 * k + 1], o2 = src[3 * k + 2];
+            const int b = 3 * k;
+            const int ur = (pk[b >> 2] >> (8 * (b & 3))) & 255, ug = (pk[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 255,
+                      ub = (pk[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 255;
+            const int d0 = o0 - ur, d1 = o1 - ug, d2 = o2 - ub;
+            sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
+            const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
+            const double yo = luma(R0, G0, B0);
+            const double yr = luma((double)ur, (double)ug, (double)ub);
+            const double dy = yo - yr;
+            ssy = ssy + dy * dy;
+            if constexpr (XTRA > 1) {
+              const size_t pix = (size_t)y * g.W + x0 + k;
+              err_y[pix] = fabs(yo - Yv[8 * h + k]);  // pipeline.py:120
+              err_rgb[pix] = ((fabs(R0 - fmin(fmax(R[k], 0.0), 255.0)) + fabs(G0 - fmin(fmax(G[k], 0.0), 255.0))) +
+                              fabs(B0 - fmin(fmax(Bv[8 * h + k], 0.0), 255.0))) / 3.0;  // pipeline.py:121
+            }
+          }
+        }
+      }
+    }
+  }
+  if constexpr (XTRA > 0) {
+    unsigned long long sv = sse;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sv += __shfl_xor(sv, o, 64);
+    if ((tid & 63) == 0) atomicAdd(&s_sse, sv);
+    double d = ssy;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d = d + __shfl_xor(d, o, 64);
+    if ((tid & 63) == 0) s_red[tid >> 6] = d;
+    __syncthreads();
+    if (tid == 0) {
+      double a = 0.0;
+      for (int i = 0; i < I::NT / 64; ++i) a = a + s_red[i];
+      sse_y_part[(size_t)frame * gridDim.x + tile] = a;
+      atomicAdd((unsigned long long*)&st[frame].sse_rgb, s_sse);
+    }
+  }
+}
+
 // ------------------------------------------------------------ launchers --
 
 hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uint32_t* part, int ptiles,
@@ -831,15 +1069,21 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
       const int tx = (g.W + I::TW - 1) / I::TW;
       tiles = ((g.H + I::TH - 1) / I::TH) * tx;
       const dim3 gi(tiles, n), bi(I::NT);
+#ifndef JDS_INV16_TWO_WINDOWS
+#define K_INV16 k_inv16s
+#else
+#define K_INV16 k_inv16f
+#endif
       if (err_y)
-        hipLaunchKernelGGL((k_inv16f<MODE, 2>), gi, bi, 0, s, g, tx, coeffs, fq, rin, rgb_out, st, part, err_y,
+        hipLaunchKernelGGL((K_INV16<MODE, 2>), gi, bi, 0, s, g, tx, coeffs, fq, rin, rgb_out, st, part, err_y,
                            err_rgb);
       else if (rin)
-        hipLaunchKernelGGL((k_inv16f<MODE, 1>), gi, bi, 0, s, g, tx, coeffs, fq, rin, rgb_out, st, part, nullptr,
+        hipLaunchKernelGGL((K_INV16<MODE, 1>), gi, bi, 0, s, g, tx, coeffs, fq, rin, rgb_out, st, part, nullptr,
                            nullptr);
       else
-        hipLaunchKernelGGL((k_inv16f<MODE, 0>), gi, bi, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, nullptr,
+        hipLaunchKernelGGL((K_INV16<MODE, 0>), gi, bi, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, nullptr,
                            nullptr);
+#undef K_INV16
       if ((e = hipGetLastError()) != hipSuccess) return e;
     } else {
       const int cblocks = 2 * g.ncy * g.ncx;
