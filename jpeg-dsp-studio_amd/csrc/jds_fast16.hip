@@ -46,21 +46,39 @@ static constexpr float W16[16][8] = {
     {0x1.1be3520000000p-5f, -0x1.a4608a0000000p-4f, 0x1.5553e40000000p-3f, -0x1.cb598c0000000p-3f, 0x1.17dc140000000p-2f, -0x1.3f4a240000000p-2f, 0x1.5a730c0000000p-2f, -0x1.684b9c0000000p-2f},
 };
 
-// 8 add/sub + 16 eight-term FMA chains (the host bound follows this sequence)
+// Per pass: s_i = x_i + x_{15-i}, d_i = x_i - x_{15-i} (i < 8); the fp32 even
+// rows are exactly symmetric (W16[2m][7-i] = (-1)^m W16[2m][i]), so the even
+// outputs are 4-term chains over e_i = s_i + s_{7-i} (m even) or
+// o_i = s_i - s_{7-i} (m odd), i < 4; the odd outputs 8-term chains over d.
+// 24 add/sub + 8 x 4 + 8 x 8 multiply-adds (pass_bound16 follows this).
 __host__ __device__ __forceinline__ void fdct16_f32(float (&x)[16]) {
-  float sd[2][8];
+  float sv[8], dv[8], ev[4], ov[4];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    sd[0][i] = x[i] + x[15 - i];
-    sd[1][i] = x[i] - x[15 - i];
+    sv[i] = x[i] + x[15 - i];
+    dv[i] = x[i] - x[15 - i];
   }
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const float* v = sd[k & 1];
-    float a = W16[k][0] * v[0];
+  for (int i = 0; i < 4; ++i) {
+    ev[i] = sv[i] + sv[7 - i];
+    ov[i] = sv[i] - sv[7 - i];
+  }
 #pragma unroll
-    for (int i = 1; i < 8; ++i) a = fmaf(W16[k][i], v[i], a);
-    x[k] = a;
+  for (int m = 0; m < 8; ++m) {
+    const float* v = (m & 1) ? ov : ev;
+    const float* w = W16[2 * m];
+    float a = w[0] * v[0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) a = fmaf(w[i], v[i], a);
+    x[2 * m] = a;
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const float* w = W16[2 * m + 1];
+    float a = w[0] * dv[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) a = fmaf(w[i], dv[i], a);
+    x[2 * m + 1] = a;
   }
 }
 
@@ -165,9 +183,19 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   constexpr int BLK_D = C::NB * BS16F;
   constexpr int U_D = PLANE_D > BLK_D ? PLANE_D : BLK_D;
 
-  __shared__ uint32_t s_rgb[WN];
+  __shared__ __attribute__((aligned(16))) uint32_t s_rgb[WN];  // 16-B aligned: the tables' float4s alias it
   __shared__ __attribute__((aligned(16))) float s_u[U_D];
   __shared__ unsigned s_st[NSTAT + 1];  // rare histogram bins (+ stats_flush16's ticket)
+#ifndef JDS_Q16_GLOBAL
+  // the frame's tables, rows of 20 floats (a row's four 16-B reads by the 16
+  // row lanes hit distinct bank groups; lanes of other blocks broadcast):
+  // rq, thr luma, thr chroma.  With the prefilter planes (the LDS-heavy
+  // modes) they go into s_rgb once the sampling is done; otherwise their own.
+  constexpr int QR = 20, TABF = 3 * 16 * QR;
+  static_assert(WN >= TABF, "tables fit the RGB window");
+  __shared__ __attribute__((aligned(16))) float s_tab_own[CPLANE ? 4 : TABF];
+  float* const s_tab = CPLANE ? reinterpret_cast<float*>(s_rgb) : s_tab_own;
+#endif
 
   const int tid = threadIdx.x;
   const int frame = blockIdx.y;
@@ -191,6 +219,15 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   auto cidx = [](int r, int c) { return r * WC + c; };
 #endif
   if (tid <= NSTAT) s_st[tid] = 0u;
+#ifndef JDS_Q16_GLOBAL
+  float4 tabv = make_float4(0.f, 0.f, 0.f, 0.f);  // 3 tables x 16 rows x 4 float4: one per thread < 192
+  const int tab_t = tid >> 6, tab_r = (tid >> 2) & 15, tab_q = tid & 3;
+  if (tid < 192) {
+    const float* src = tab_t == 0 ? fq.rq : fq.thr[tab_t - 1];
+    tabv = reinterpret_cast<const float4*>(src + tab_r * 16)[tab_q];
+    if constexpr (!CPLANE) *reinterpret_cast<float4*>(&s_tab[tab_t * 16 * QR + tab_r * QR + 4 * tab_q]) = tabv;
+  }
+#endif
   if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *fixnext = 0u;  // the next run's list
   const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
 
@@ -366,7 +403,7 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       const float* s_pl = s_u + (plane == 1 ? 0 : WN);
       const int sc = reflect_pad(gx * 16 + line, g.wc);
       const int wc0 = C::SX * sc - x0 + 1;
-#pragma unroll 4
+#pragma unroll 4  // full unrolling (window rows reused across samples) costs 20-50 VGPRs: occupancy 5 -> 3-4
       for (int i = 0; i < 16; ++i) {
         const int sr = reflect_pad(gy * 16 + i, g.hc);
         const int wr0 = C::SY * sr - y0 + 1;
@@ -395,7 +432,12 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     fdct16_f32(v);  // axis 0 (columns) first
 #endif
   }
-  if constexpr (CPLANE) __syncthreads();  // the block buffer aliases the chroma planes
+  if constexpr (CPLANE) {
+    __syncthreads();  // the block buffer aliases the chroma planes; s_rgb is free
+#ifndef JDS_Q16_GLOBAL
+    if (tid < 192) *reinterpret_cast<float4*>(&s_tab[tab_t * 16 * QR + tab_r * QR + 4 * tab_q]) = tabv;
+#endif
+  }
   float* s_blk = s_u + blk * BS16F;
   if (valid) {
 #pragma unroll
@@ -413,7 +455,19 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 #ifndef JDS_P16_NODCT
     fdct16_f32(v);
 #endif
-    const float* thr = fq.thr[plane ? 1 : 0];
+#ifndef JDS_Q16_GLOBAL
+    float rqv[16], thv[16];
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+      const float4 a = *reinterpret_cast<const float4*>(&s_tab[u * QR + 4 * qd]);
+      const float4 b = *reinterpret_cast<const float4*>(&s_tab[(plane ? 2 : 1) * 16 * QR + u * QR + 4 * qd]);
+      rqv[4 * qd] = a.x; rqv[4 * qd + 1] = a.y; rqv[4 * qd + 2] = a.z; rqv[4 * qd + 3] = a.w;
+      thv[4 * qd] = b.x; thv[4 * qd + 1] = b.y; thv[4 * qd + 2] = b.z; thv[4 * qd + 3] = b.w;
+    }
+#else
+    const float* thv = fq.thr[plane ? 1 : 0] + u * 16;
+    const float* rqv = fq.rq + u * 16;
+#endif
     int q[16];
     unsigned nrare = 0u;
 #pragma unroll
@@ -422,10 +476,10 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       q[k] = (int)v[k];
       continue;
 #endif
-      const float t = v[k] * fq.rq[u * 16 + k];
+      const float t = v[k] * rqv[k];
       const float r = rintf(t);
       // |t - r| is exact (Sterbenz); thr holds 0.5 - E/Q - slack, rounded down
-      flag |= fabsf(t - r) >= fmaf(fabsf(t), -0x1p-22f, thr[u * 16 + k]) ? 1u : 0u;
+      flag |= fabsf(t - r) >= fmaf(fabsf(t), -0x1p-22f, thv[k]) ? 1u : 0u;
       q[k] = (int)r;
       nz += r != 0.0f ? 1u : 0u;
       mb += (unsigned)__builtin_amdgcn_frexp_expf(r);  // bit length of |q|
@@ -811,22 +865,31 @@ hipError_t launch_fast_fwd16(int mode, bool pf, const Geo& g, int n, const uint8
 
 // ---------------------------------------------------- host: the bounds --
 //
-// fast_fwd_bounds with 16-point passes: each output is an 8-term FMA chain
-// over s_i / d_i (|.| <= 2X, error 2e + 2uX); its error is
-// b_k (2e + 2uX) + 2uX (b_k + P_k) with b_k = sum_i |W16_ki| and P_k the sum
-// of the chain's partial sums of |W16_k0..7| (covering the fp32
-// representation error of W16 and every rounding of the chain).
+// fast_fwd_bounds with 16-point passes (fdct16_f32's sequence).  A chain
+// over n inputs of magnitude <= M and error <= eps, with weights W (fp32),
+// has error <= b eps + u M (b + P): b = sum |W| (the inputs' error, and the
+// fp32 representation error of W: <= u |W| M per term), P = the sum of the
+// chain's partial sums of |W| (each step rounds a partial sum <= M * prefix).
+// Inputs |x| <= X, error e: s_i, d_i have |.| <= 2X, error 2e + 2uX;
+// e_i, o_i |.| <= 4X, error 4e + 8uX.
+static void chain_bound(const float* w, int n, double M, double eps, double* Mout, double* eout) {
+  const double u = 0x1p-24;
+  double b = 0, P = 0, pre = 0;
+  for (int i = 0; i < n; ++i) {
+    b += fabs((double)w[i]);
+    pre += fabs((double)w[i]);
+    P += pre;
+  }
+  *Mout = M * b;
+  *eout = b * eps + u * M * (b + P);
+}
 static void pass_bound16(double X, double e, double* Xout, double* eout) {
   const double u = 0x1p-24;
   for (int k = 0; k < 16; ++k) {
-    double b = 0, P = 0, pre = 0;
-    for (int i = 0; i < 8; ++i) {
-      b += fabs((double)W16[k][i]);
-      pre += fabs((double)W16[k][i]);
-      P += pre;
-    }
-    Xout[k] = 2 * X * b;
-    eout[k] = b * (2 * e + 2 * u * X) + 2 * u * X * (b + P);
+    if (k & 1)
+      chain_bound(W16[k], 8, 2 * X, 2 * e + 2 * u * X, &Xout[k], &eout[k]);
+    else
+      chain_bound(W16[k], 4, 4 * X, 4 * e + 8 * u * X, &Xout[k], &eout[k]);
   }
 }
 
