@@ -458,8 +458,11 @@ def main():
         else:
             kname = f'k_inv16f<{mcode},0>' if mcode else f'k_chroma16<{mcode}> + k_inv16<{mcode}>'
     else:
+        # the plan's inverse choice (jds_abi.hip inv_fast_ok): the certified fast
+        # kernel for 4:2:x with a DC quantiser <= 60, k_inv2 otherwise
+        inv_fast = mcode != 0 and float(qt[0][0]) <= 60.0
         kname = (f'k_fwd32i<{mcode},{pfs}> + k_fwd32<{mcode},{pfs}> (border tiles) + k_fix_fwd'
-                 if dom == 'k_fwd' else f'k_inv2<{mcode},0>')
+                 if dom == 'k_fwd' else (f'k_inv_fast<{mcode},0>' if inv_fast else f'k_inv2<{mcode},0>'))
     traffic = None
     tf = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tf):

@@ -160,6 +160,13 @@ struct jds_plan {
   DevBuf invfix;  // certified fast inverse: run and per-item counters (InvFix, jds_inv_fast.hip)
   unsigned inv_runs = 0;  // fast-inverse runs so far: picks the list counter (InvFix::parity)
   bool last_inv_fast = false;  // the last run's inverse was the certified fast one
+  // Where the certified fast inverse pays (measured, 1 MI355X): 4:2:x plans
+  // whose tables are not coarse.  Coarse tables (DC quantiser > 60: quality
+  // below ~14 on the standard table) put most tiles on the exact path
+  // (reconstructions land on integers), where k_inv2 beats k_inv_fast's
+  // in-kernel fallback (4K 4:2:0: Q10 373 vs 396 us; Q20 376 vs 347); at 4:4:4
+  // k_inv2 is faster outright (512x512 x 256: 337 vs 391 us).
+  bool inv_fast_ok = true;
   bool last_fwd16_fast = false;  // 16x16: the last forward was the certified fp32 one
   unsigned fwd16_runs = 0;       // 16x16 certified forward runs so far: picks the list counter
   InvFix inv_fix() const {
@@ -434,6 +441,8 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
     return fail(JDS_ENOMEM, "host allocation failed");
   }
   for (int i = 0; i < n; ++i) memcpy(p->qt + 64 * i, params[i].qtable, 64 * sizeof(double));
+  p->inv_fast_ok = mode != JDS_SS_444;
+  for (int i = 0; i < n; ++i) p->inv_fast_ok = p->inv_fast_ok && params[i].qtable[0] <= 60.0;
   p->mode = mode;
   p->pf = pf;
   p->g = g;
@@ -618,7 +627,8 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   }
   InvFix fx = p->inv_fix();
   fx.fix_all = (flags & JDS_RUN_INV_FIXALL) ? 1 : 0;
-  const bool exact_inv = exact || (flags & JDS_RUN_EXACT_INV) != 0;
+  const bool exact_inv =
+      exact || (flags & JDS_RUN_EXACT_INV) != 0 || (!p->inv_fast_ok && !(flags & JDS_RUN_INV_FAST));
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,

@@ -213,7 +213,36 @@ __device__ __forceinline__ void flag_block_bits(const LaneStats& ls, bool valid,
 // s_st holds NSTAT + 1 words: the last is the waves' ticket counter.
 constexpr int NW_MAX = 8;  // waves per forward workgroup (TF <= 512)
 
-__device__ __forceinline__ void stats_flush(LaneStats ls, bool valid, unsigned* s_st, uint32_t* __restrict__ slot) {
+// Two forms, picked per kernel configuration (stats_flush<TF>): the barrier
+// form (wave reductions, LDS atomics, one workgroup barrier) measured faster
+// with 8 waves per workgroup (4:2:2: k_fwd32i 379 vs 418 us per 16 x 4K),
+// the ticket form below with 6 (4:2:0: 325 vs 333 us per 64 x 1080p).
+#ifndef JDS_FLUSH_BARRIER_TF
+#define JDS_FLUSH_BARRIER_TF 512  // workgroups of at least this many threads take the barrier form
+#endif
+__device__ __forceinline__ void stats_flush_barrier(LaneStats ls, bool valid, unsigned* s_st,
+                                                    uint32_t* __restrict__ slot) {
+  if (!valid) ls = LaneStats();
+  const unsigned e = ls.hn & 0x0f0f0f0fu, o = (ls.hn >> 4) & 0x0f0f0f0fu;
+  const unsigned w0 = __reduce_add_sync(~0ull, e & 0x00ff00ffu), w1 = __reduce_add_sync(~0ull, (e >> 8) & 0x00ff00ffu);
+  const unsigned w2 = __reduce_add_sync(~0ull, o & 0x00ff00ffu), w3 = __reduce_add_sync(~0ull, (o >> 8) & 0x00ff00ffu);
+  const unsigned wmb = __reduce_add_sync(~0ull, ls.mb), wnz = __reduce_add_sync(~0ull, ls.nz);
+  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&s_st[0], wnz);
+    atomicAdd(&s_st[1], wmb + wnz);
+    const unsigned zeros = 8u * nvalid - wnz;
+    const unsigned c[8] = {w0 & 0xffffu, w2 & 0xffffu, w1 & 0xffffu, (w3 & 0xffffu) - zeros,
+                           w0 >> 16,     w2 >> 16,     w1 >> 16,     w3 >> 16};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (c[j]) atomicAdd(&s_st[2 + 22 + j], c[j]);
+  }
+  __syncthreads();
+  if (threadIdx.x < NSTAT) slot[threadIdx.x] = s_st[threadIdx.x];
+}
+__device__ __forceinline__ void stats_flush_ticket(LaneStats ls, bool valid, unsigned* s_st,
+                                                   uint32_t* __restrict__ slot) {
   __shared__ __attribute__((aligned(16))) unsigned s_wave[NW_MAX][4][4];  // [wave][row][word]
   __shared__ unsigned s_nvalid[NW_MAX];
   if (!valid) ls = LaneStats();
@@ -272,6 +301,13 @@ __device__ __forceinline__ void stats_flush(LaneStats ls, bool valid, unsigned* 
     }
     slot[t] = tot;
   }
+}
+template <int TF>
+__device__ __forceinline__ void stats_flush(LaneStats ls, bool valid, unsigned* s_st, uint32_t* __restrict__ slot) {
+  if constexpr (TF >= JDS_FLUSH_BARRIER_TF)
+    stats_flush_barrier(ls, valid, s_st, slot);
+  else
+    stats_flush_ticket(ls, valid, s_st, slot);
 }
 
 // ---- general tiles ------------------------------------------------------------
@@ -512,7 +548,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
     *reinterpret_cast<uint4*>(coeffs + (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
                               (long long)bidx * 64 + u * 8) = pack_q(q);
   flag_block_list(ls, valid, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
-  stats_flush(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
+  stats_flush<C::TF>(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
 }
 
 // ---- interior tiles ------------------------------------------------------------
@@ -788,7 +824,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   }
   if constexpr (!MQ) {
     flag_block_list(ls, true, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
-    stats_flush(ls, true, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
+    stats_flush<C::TF>(ls, true, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
   }
 }
 

@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get('JDS_LIB_PATH') or os.path.join(_HERE, 'libjds.so')
 JDS_OK, JDS_EINVAL, JDS_ENOTSUP, JDS_EHIP, JDS_ENOMEM = 0, -1, -2, -3, -4
 SS_444, SS_422, SS_420 = 0, 1, 2
 MODE_CODES = {'4:4:4': SS_444, '4:2:2': SS_422, '4:2:0': SS_420}
-RUN_SSE, RUN_FWD, RUN_INV, RUN_EXACT, RUN_EXACT_INV, RUN_INV_FIXALL, RUN_FWD_FIXALL = 1, 2, 4, 8, 16, 32, 64
+RUN_SSE, RUN_FWD, RUN_INV, RUN_EXACT, RUN_EXACT_INV, RUN_INV_FIXALL, RUN_FWD_FIXALL, RUN_INV_FAST = 1, 2, 4, 8, 16, 32, 64, 128
 
 
 class Params(C.Structure):

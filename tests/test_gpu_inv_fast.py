@@ -6,7 +6,10 @@ through a different fp64 operation order and certifies every truncation with
 a rigorous bound (tools/inv_bound.py); tiles with an uncertain sample go
 through the exact kernel (k_inv2_list).  Bar: bit-identical bytes, SSE and
 luma SSE with the default (fast), JDS_RUN_EXACT_INV (exact) and
-JDS_RUN_INV_FIXALL (fast, then every tile recomputed by the list kernel)."""
+JDS_RUN_INV_FIXALL (fast, then every tile recomputed by the exact tile code).
+Plans pick k_inv2 at 4:4:4 and for coarse tables (measured faster there);
+these tests force the fast kernel with JDS_RUN_INV_FAST, and the default
+route is checked separately."""
 import numpy as np
 import pytest
 
@@ -68,13 +71,14 @@ def test_fast_inverse_equals_exact_inverse_random(h, w, mode, pf):
     from jds import _abi
     qs = [1, 10, 50, 95, 100]
     frames = np.stack([cpu_ref.random_image(h, w, 700 + i) for i in range(len(qs))])
-    fast, exact, fixall = _plan(frames, qs, mode, pf, [0, _abi.RUN_EXACT_INV, _abi.RUN_INV_FIXALL])
+    F = _abi.RUN_INV_FAST  # the plan would pick k_inv2 for these qualities / 4:4:4
+    fast, exact, fixall = _plan(frames, qs, mode, pf, [F, _abi.RUN_EXACT_INV, F | _abi.RUN_INV_FIXALL])
     _same(fast, exact)
     _same(fixall, exact)
     assert fixall[3][1] > 0  # every tile was listed
     ref = cpu_ref.compress_reconstruct(frames[2], 50, 8, mode, pf, metrics=False)
     assert np.array_equal(fast[0][2], ref['reconstructed'])
-    fs, es = _plan(frames, qs, mode, pf, [_abi.RUN_SSE, _abi.RUN_SSE | _abi.RUN_EXACT_INV])
+    fs, es = _plan(frames, qs, mode, pf, [_abi.RUN_SSE | F, _abi.RUN_SSE | _abi.RUN_EXACT_INV])
     _same(fs, es, sse=True)
 
 
@@ -105,7 +109,7 @@ def test_fast_inverse_structured_images(name, mode):
     from jds import _abi
     img = STRUCTURED[name]()
     frames = np.stack([img, img])
-    fast, exact = _plan(frames, [50, 90], mode, mode != '4:4:4', [0, _abi.RUN_EXACT_INV])
+    fast, exact = _plan(frames, [50, 90], mode, mode != '4:4:4', [_abi.RUN_INV_FAST, _abi.RUN_EXACT_INV])
     _same(fast, exact)
     ref = cpu_ref.compress_reconstruct(img, 90, 8, mode, mode != '4:4:4', metrics=False)
     assert np.array_equal(fast[0][1], ref['reconstructed'])
@@ -114,8 +118,9 @@ def test_fast_inverse_structured_images(name, mode):
 def test_fast_inverse_checkerboard_golden_needs_fixups():
     """cfg1: every sample of value 30 decodes to 29.999... in the reference
     (SURVEY §8(a)(13)); the fast kernel must hand those tiles to the exact one."""
+    from jds import _abi
     img = cpu_ref.generate_colored_checkerboard(512)
-    (out, cf, st, fix), = _plan(img[None], [50], '4:4:4', False, [0])
+    (out, cf, st, fix), = _plan(img[None], [50], '4:4:4', False, [_abi.RUN_INV_FAST])
     assert fix[1] > 0
     g = golden()['cfg1_checker512_q50_444']
     assert sha(out[0]) == g['sha_recon']
@@ -136,5 +141,19 @@ def test_fast_inverse_arbitrary_int16_coefficients(scale):
         geo_cpf = _abi.geometry(_abi.make_params(50, cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, 50), mode,
                                                  False, codec.gaussian_kernel3()), h, w).coeffs_per_frame
         cf = np.clip(rng.normal(0, scale, (3, geo_cpf)), -32768, 32767).astype(np.int16)
-        fast, exact = _plan(frames, [5, 50, 100], mode, False, [0, _abi.RUN_EXACT_INV], coeffs=cf)
+        fast, exact = _plan(frames, [5, 50, 100], mode, False, [_abi.RUN_INV_FAST, _abi.RUN_EXACT_INV], coeffs=cf)
         _same(fast, exact)
+
+
+@pytest.mark.parametrize('mode,q,fast', [('4:2:0', 50, True), ('4:2:2', 20, True), ('4:2:0', 10, False),
+                                         ('4:4:4', 50, False)])
+def test_default_inverse_route(mode, q, fast):
+    """The plan's own choice (fast inverse for 4:2:x with fine tables, k_inv2
+    otherwise) gives the exact kernel's bytes; the fix-up counter shows which
+    kernel ran (k_inv2 reports none)."""
+    from jds import _abi
+    frames = np.stack([cpu_ref.generate_colored_checkerboard(256)] * 2)  # ties: the fast kernel lists tiles
+    dflt, exact = _plan(frames, [q, q], mode, mode != '4:4:4', [0, _abi.RUN_EXACT_INV])
+    _same(dflt, exact)
+    if not fast:
+        assert dflt[3][1] == 0
