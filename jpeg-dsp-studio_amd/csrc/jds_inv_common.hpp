@@ -42,9 +42,15 @@ __device__ __forceinline__ int tslot(int r, int c) { return r * 8 + ((((c >> 1) 
 // The same with the column's coefficients already loaded (software
 // prefetch: the loads of the next block are issued before this one's math).
 // (held sign-extended: signed 16-bit loads, no per-use extension)
+#ifndef JDS_COL16_INT
+struct Col16 {  // int16 elements: loaded two per VGPR (k_inv2 373 -> 363 us at 4K Q10 vs int)
+  int16_t q[8];
+};
+#else
 struct Col16 {
   int q[8];
 };
+#endif
 // Blocks outside the grid (`ok` false) read block 0 of the plane instead: the
 // caller never transforms them, and unmasked loads need no per-load branches.
 __device__ __forceinline__ Col16 load_col(const int16_t* __restrict__ plane, long long boff, int v, bool ok) {
