@@ -186,16 +186,22 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   __shared__ __attribute__((aligned(16))) uint32_t s_rgb[WN];  // 16-B aligned: the tables' float4s alias it
   __shared__ __attribute__((aligned(16))) float s_u[U_D];
   __shared__ unsigned s_st[NSTAT + 1];  // rare histogram bins (+ stats_flush16's ticket)
-#ifndef JDS_Q16_GLOBAL
   // the frame's tables, rows of 20 floats (a row's four 16-B reads by the 16
   // row lanes hit distinct bank groups; lanes of other blocks broadcast):
   // rq, thr luma, thr chroma.  With the prefilter planes (the LDS-heavy
   // modes) they go into s_rgb once the sampling is done; otherwise their own.
+  // 4:2:0 with the prefilter reads them from global memory instead: holding
+  // them in registers across its sampling cost a wave per SIMD (94 -> 100
+  // VGPRs); staging them saves ~6 us elsewhere.
+#ifndef JDS_Q16_GLOBAL
+  constexpr bool QLDS = !(MODE == M420 && CPLANE);
+#else
+  constexpr bool QLDS = false;
+#endif
   constexpr int QR = 20, TABF = 3 * 16 * QR;
   static_assert(WN >= TABF, "tables fit the RGB window");
-  __shared__ __attribute__((aligned(16))) float s_tab_own[CPLANE ? 4 : TABF];
+  __shared__ __attribute__((aligned(16))) float s_tab_own[(CPLANE || !QLDS) ? 4 : TABF];
   float* const s_tab = CPLANE ? reinterpret_cast<float*>(s_rgb) : s_tab_own;
-#endif
 
   const int tid = threadIdx.x;
   const int frame = blockIdx.y;
@@ -219,15 +225,13 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   auto cidx = [](int r, int c) { return r * WC + c; };
 #endif
   if (tid <= NSTAT) s_st[tid] = 0u;
-#ifndef JDS_Q16_GLOBAL
   float4 tabv = make_float4(0.f, 0.f, 0.f, 0.f);  // 3 tables x 16 rows x 4 float4: one per thread < 192
   const int tab_t = tid >> 6, tab_r = (tid >> 2) & 15, tab_q = tid & 3;
-  if (tid < 192) {
+  if (QLDS && tid < 192) {
     const float* src = tab_t == 0 ? fq.rq : fq.thr[tab_t - 1];
     tabv = reinterpret_cast<const float4*>(src + tab_r * 16)[tab_q];
     if constexpr (!CPLANE) *reinterpret_cast<float4*>(&s_tab[tab_t * 16 * QR + tab_r * QR + 4 * tab_q]) = tabv;
   }
-#endif
   if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *fixnext = 0u;  // the next run's list
   const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
 
@@ -388,12 +392,15 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   const int bidx = gy * nbx + gx;
 
   float v[16];
-  if (valid) {
+  // the samples of column `line`; tiles on the fast staging path hold no
+  // np.pad samples, so their rows are linear in i (immediate LDS offsets)
+  auto sample_col = [&](auto interior_tag) {
+    constexpr bool INT = decltype(interior_tag)::value;
     if (plane == 0 || MODE == M444) {
-      const int sx = reflect_pad(gx * 16 + line, g.W) - x0 + 1;
+      const int sx = (INT ? gx * 16 + line : reflect_pad(gx * 16 + line, g.W)) - x0 + 1;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int sy = reflect_pad(gy * 16 + i, g.H) - y0 + 1;
+        const int sy = (INT ? gy * 16 + i : reflect_pad(gy * 16 + i, g.H)) - y0 + 1;
         float R, G, B;
         rgbf(s_rgb[sy * WC + sx], R, G, B);
         v[i] = plane == 0 ? luma32m(R, G, B) : (plane == 1 ? cb32(R, G, B) : cr32(R, G, B)) - 128.0f;
@@ -401,11 +408,11 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     } else {
       // INTER_AREA mean of the (prefiltered) full-resolution chroma
       const float* s_pl = s_u + (plane == 1 ? 0 : WN);
-      const int sc = reflect_pad(gx * 16 + line, g.wc);
+      const int sc = INT ? gx * 16 + line : reflect_pad(gx * 16 + line, g.wc);
       const int wc0 = C::SX * sc - x0 + 1;
 #pragma unroll 4  // full unrolling (window rows reused across samples) costs 20-50 VGPRs: occupancy 5 -> 3-4
       for (int i = 0; i < 16; ++i) {
-        const int sr = reflect_pad(gy * 16 + i, g.hc);
+        const int sr = INT ? gy * 16 + i : reflect_pad(gy * 16 + i, g.hc);
         const int wr0 = C::SY * sr - y0 + 1;
         float s[C::SY][2];
 #pragma unroll
@@ -428,15 +435,19 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
           v[i] = (s[0][0] + s[0][1]) * 0.5f - 128.0f;
       }
     }
+  };
+  if (valid) {
+    if (fast_stage)  // uniform per workgroup
+      sample_col(std::integral_constant<bool, true>());
+    else
+      sample_col(std::integral_constant<bool, false>());
 #ifndef JDS_P16_NODCT
     fdct16_f32(v);  // axis 0 (columns) first
 #endif
   }
   if constexpr (CPLANE) {
     __syncthreads();  // the block buffer aliases the chroma planes; s_rgb is free
-#ifndef JDS_Q16_GLOBAL
-    if (tid < 192) *reinterpret_cast<float4*>(&s_tab[tab_t * 16 * QR + tab_r * QR + 4 * tab_q]) = tabv;
-#endif
+    if (QLDS && tid < 192) *reinterpret_cast<float4*>(&s_tab[tab_t * 16 * QR + tab_r * QR + 4 * tab_q]) = tabv;
   }
   float* s_blk = s_u + blk * BS16F;
   if (valid) {
@@ -455,19 +466,22 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 #ifndef JDS_P16_NODCT
     fdct16_f32(v);
 #endif
-#ifndef JDS_Q16_GLOBAL
     float rqv[16], thv[16];
+    if constexpr (QLDS) {
 #pragma unroll
-    for (int qd = 0; qd < 4; ++qd) {
-      const float4 a = *reinterpret_cast<const float4*>(&s_tab[u * QR + 4 * qd]);
-      const float4 b = *reinterpret_cast<const float4*>(&s_tab[(plane ? 2 : 1) * 16 * QR + u * QR + 4 * qd]);
-      rqv[4 * qd] = a.x; rqv[4 * qd + 1] = a.y; rqv[4 * qd + 2] = a.z; rqv[4 * qd + 3] = a.w;
-      thv[4 * qd] = b.x; thv[4 * qd + 1] = b.y; thv[4 * qd + 2] = b.z; thv[4 * qd + 3] = b.w;
+      for (int qd = 0; qd < 4; ++qd) {
+        const float4 a = *reinterpret_cast<const float4*>(&s_tab[u * QR + 4 * qd]);
+        const float4 b = *reinterpret_cast<const float4*>(&s_tab[(plane ? 2 : 1) * 16 * QR + u * QR + 4 * qd]);
+        rqv[4 * qd] = a.x; rqv[4 * qd + 1] = a.y; rqv[4 * qd + 2] = a.z; rqv[4 * qd + 3] = a.w;
+        thv[4 * qd] = b.x; thv[4 * qd + 1] = b.y; thv[4 * qd + 2] = b.z; thv[4 * qd + 3] = b.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        rqv[k] = fq.rq[u * 16 + k];
+        thv[k] = fq.thr[plane ? 1 : 0][u * 16 + k];
+      }
     }
-#else
-    const float* thv = fq.thr[plane ? 1 : 0] + u * 16;
-    const float* rqv = fq.rq + u * 16;
-#endif
     int q[16];
     unsigned nrare = 0u;
 #pragma unroll

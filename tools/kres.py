@@ -5,8 +5,11 @@ import re, subprocess, sys, os
 src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ''
 inc = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'include')
+# the library's own flags (jds/build.py), plus KRES_FLAGS (e.g. "-DJDS_Q16_GLOBAL")
+extra = os.environ.get('KRES_FLAGS', '').split()
 r = subprocess.run(['/opt/rocm/bin/hipcc', '-std=c++17', '-O3', '--offload-arch=gfx950', '-fPIC', '-c', src,
-                    '-o', '/tmp/_kres.o', '-I', inc, '-Rpass-analysis=kernel-resource-usage'],
+                    '-fno-slp-vectorize', '-ffp-contract=off', '-o', '/tmp/_kres.o', '-I', inc,
+                    '-I', os.path.dirname(os.path.abspath(src)), *extra, '-Rpass-analysis=kernel-resource-usage'],
                    capture_output=True, text=True)
 if r.returncode:
     print(r.stderr[-4000:]); sys.exit(1)
