@@ -896,7 +896,10 @@ k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ 
 //   lengths in LDS (dynamic, 4 (n + 1) bytes) and maps its entry index to
 //   (item, slot) by binary search.
 template <int MODE, bool PF>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
+#ifndef JDS_FIX_WPE
+#define JDS_FIX_WPE 5
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(JDS_FIX_WPE)))
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
           const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq, const int n_flat) {
@@ -976,7 +979,11 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     // chains ~4 dependent load rounds per thread: such blocks set the tail)
     const int wy0 = SY * 8 * gy - 1, wx0 = 16 * gx - 1;
     const bool staged = CPLANE && plane != 0 && gy * 8 + 8 <= g.hc && gx * 8 + 8 <= g.wc;
+#ifdef JDS_PFIX_NOSAMPLE  // tools/probe: constant samples (timing only)
+    if (false) {
+#else
     if (staged) {  // uniform per workgroup
+#endif
       // every window load in flight before the first use (one memory latency)
       constexpr int NWL = (WRR * WCC + 63) / 64;
       uint32_t px[NWL];
@@ -1025,7 +1032,11 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
         v = (sm[0][0] + sm[0][1]) * 0.5;
       s_b[t] = v - 128.0;
     } else {
+#ifdef JDS_PFIX_NOSAMPLE
+      s_b[t] = (double)(t + (int)(old.x & 7u));
+#else
       s_b[t] = sample64<MODE, PF>(img, g, plane, gy * 8 + i, gx * 8 + j, k) - 128.0;
+#endif
     }
     __syncthreads();
     double v[8];
@@ -1051,7 +1062,11 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
         const int qn = (int)__builtin_rint(v[c] / fq[frame].q16[u * 8 + c]);
         const int qo = (int16_t)((ow[c >> 1] >> ((c & 1) * 16)) & 0xffffu);
         nw[c >> 1] |= (uint32_t)(uint16_t)qn << ((c & 1) * 16);
+#ifdef JDS_PFIX_NOSTAT
+        if (qn == 0x7fffffff) {
+#else
         if (qn != qo) {
+#endif
           const int mo = qo < 0 ? -qo : qo, mn = qn < 0 ? -qn : qn;
           if (mo) {
             --dnz;
