@@ -59,7 +59,7 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
     from jds import _abi, codec
     from engines.quantizer import scale_quant_matrix
     from utils.constants import JPEG_LUMA_Q50
-    from utils.metrics import bitrate_from_counts
+    from utils.metrics import bitrate_from_counts, psnr_from_mse
 
     dev = torch.device('cuda', device)
     fr = frames if isinstance(frames, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frames))
@@ -89,10 +89,12 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
             s = stats[f, qi]
             br = bitrate_from_counts(int(s['nonzero']), float(s['magnitude_bits']), int(s['total_coeffs']), (H, W), 8)
             mse = float(s['sse_rgb']) / (H * W * 3)
+            mse_y = float(s['sse_y']) / (H * W)  # fp64 luma SSE in tile order (NumPy's mean: pairwise)
             items.append({'frame': f, 'quality': q, 'nonzero': int(s['nonzero']),
                           'magnitude_bits': int(s['magnitude_bits']), 'total_coeffs': int(s['total_coeffs']),
                           'hist': s['hist'].astype(np.int64), 'sse_rgb': int(s['sse_rgb']),
                           'psnr_rgb': float('inf') if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse)),
+                          'mse_y': mse_y, 'psnr_y': psnr_from_mse(mse_y),
                           'bpp': br['bpp'], 'compression_ratio': br['compression_ratio']})
     return items
 

@@ -92,11 +92,16 @@ def test_sweep_device_chunks_more_than_eight_qualities():
     items = sweep_device(frames, qs, '4:2:2', False)
     assert [(it['frame'], it['quality']) for it in items] == [(f, q) for f in range(2) for q in qs]
     for it in items[::4]:
-        ref = cpu_ref.compress_reconstruct(frames[it['frame']], it['quality'], 8, '4:2:2', False, metrics=False)
+        ref = cpu_ref.compress_reconstruct(frames[it['frame']], it['quality'], 8, '4:2:2', False, metrics=True)
         assert it['nonzero'] == ref['bitrate']['nonzero_count']
         assert np.array_equal(it['hist'], ref['hist'])
         f = frames[it['frame']]
         assert it['sse_rgb'] == int(((f.astype(np.int64) - ref['reconstructed']) ** 2).sum())
+        # the CompressionResult metrics a BatchSweepWorker item carries (gui/worker.py:62-68):
+        # PSNR from the exact integer SSE (same float64 value as skimage's), luma PSNR from
+        # the fp64 luma SSE summed in tile order (NumPy sums pairwise: a few ulps apart)
+        assert it['psnr_rgb'] == pytest.approx(ref['metrics']['psnr_rgb'], rel=1e-12)
+        assert it['psnr_y'] == pytest.approx(ref['metrics']['psnr_y'], rel=1e-12)
 
 
 def test_sweep_plan_rejects_bad_shapes():
