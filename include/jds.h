@@ -160,6 +160,14 @@ int jds_compress_reconstruct(jds_ctx* ctx, const jds_params* p, const uint8_t* r
  * Bit-identical to skimage + scipy.ndimage + NumPy reductions.  H, W >= 7. */
 int jds_psnr_ssim(jds_ctx* ctx, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out);
 
+/* The same on device-resident images (a_dev, b_dev: HxWx3 uint8 in device
+ * memory of ctx's device, e.g. a plan's input frames and outputs), run on the
+ * context's stream after a device-wide wait for earlier work; out on the host.
+ * Serves the batch sweep's per-item CompressionResult metrics
+ * (gui/worker.py:62-68 -> utils/metrics.py:9-28) without host copies
+ * (SURVEY.md section 5 interface sketch: jds_ssim_dev). */
+int jds_psnr_ssim_dev(jds_ctx* ctx, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W, double* out);
+
 /* Per-stage functions of the engines.* API (engines/__init__.py:10-27), on host
  * fp64 arrays staged through the context's device memory.  Synchronous.
  *   rgb_to_ycbcr / ycbcr_to_rgb: n_pixels x 3 (engines/color_space.py:8-24)

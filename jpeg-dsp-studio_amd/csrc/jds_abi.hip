@@ -770,7 +770,8 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
   return JDS_OK;
 }
 
-int jds_psnr_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out) {
+// jds_psnr_ssim / jds_psnr_ssim_dev: argument checks shared by both
+static int psnr_ssim_args(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out) {
   if (!c || !a || !b || !out) return fail(JDS_EINVAL, "null argument");
   if (H < 7 || W < 7)
     return fail(JDS_EINVAL,
@@ -779,20 +780,20 @@ int jds_psnr_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int
                 "smaller side of your images. If your images are multichannel (with color channels), set "
                 "channel_axis to the axis number corresponding to the channels.");
   if (H * W > (int64_t)1 << 28) return fail(JDS_EINVAL, "image too large");
-  HIP_TRY(hipSetDevice(c->device));
+  return JDS_OK;
+}
+
+// SSIM / MSE of two device-resident images (the context's stream)
+static int psnr_ssim_device(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out) {
   const size_t nb = (size_t)H * W * 3;
-  HIP_TRY(c->img_a.ensure(nb));
-  HIP_TRY(c->img_b.ensure(nb));
   HIP_TRY(c->ss_out.ensure(5 * sizeof(double) + sizeof(unsigned long long)));
   hipStream_t s = c->stream;
-  HIP_TRY(hipMemcpyAsync(c->img_a.p, a, nb, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(c->img_b.p, b, nb, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(c->ss_out.p, 0, 5 * sizeof(double) + sizeof(unsigned long long), s));
   double* dres = (double*)c->ss_out.p;
   unsigned long long* dsse = (unsigned long long*)(dres + 5);
-  int rc = run_ssim(c, (const uint8_t*)c->img_a.p, (const uint8_t*)c->img_b.p, (int)H, (int)W, dres);
+  int rc = run_ssim(c, a, b, (int)H, (int)W, dres);
   if (rc) return rc;
-  HIP_TRY(launch_sse_u8((const uint8_t*)c->img_a.p, (const uint8_t*)c->img_b.p, (long long)nb, dsse, s));
+  HIP_TRY(launch_sse_u8(a, b, (long long)nb, dsse, s));
   double res[5];
   unsigned long long sse = 0;
   HIP_TRY(hipMemcpyAsync(res, dres, sizeof res, hipMemcpyDeviceToHost, s));
@@ -801,6 +802,26 @@ int jds_psnr_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int
   for (int i = 0; i < 5; ++i) out[i] = res[i];
   out[5] = (double)sse / (double)nb;  // exact: integer sum, one division (np.mean)
   return JDS_OK;
+}
+
+int jds_psnr_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out) {
+  int rc = psnr_ssim_args(c, a, b, H, W, out);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t nb = (size_t)H * W * 3;
+  HIP_TRY(c->img_a.ensure(nb));
+  HIP_TRY(c->img_b.ensure(nb));
+  HIP_TRY(hipMemcpyAsync(c->img_a.p, a, nb, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->img_b.p, b, nb, hipMemcpyHostToDevice, c->stream));
+  return psnr_ssim_device(c, (const uint8_t*)c->img_a.p, (const uint8_t*)c->img_b.p, H, W, out);
+}
+
+int jds_psnr_ssim_dev(jds_ctx* c, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W, double* out) {
+  int rc = psnr_ssim_args(c, a_dev, b_dev, H, W, out);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());  // the images come from other streams (plan runs, torch)
+  return psnr_ssim_device(c, a_dev, b_dev, H, W, out);
 }
 
 // ----------------------------------------------------- per-stage API --

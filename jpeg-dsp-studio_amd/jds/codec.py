@@ -83,6 +83,15 @@ def psnr_ssim_raw(a: np.ndarray, b: np.ndarray, device: int = 0) -> np.ndarray:
     return out
 
 
+def psnr_ssim_dev(a_ptr: int, b_ptr: int, H: int, W: int, device: int = 0) -> np.ndarray:
+    """jds_psnr_ssim_dev: psnr_ssim_raw's six values for two HxWx3 uint8 images
+    already in device memory (raw device pointers, e.g. torch tensors' data_ptr())."""
+    out = np.empty(6, np.float64)
+    with lease(device) as ctx:
+        check(lib().jds_psnr_ssim_dev(ctx.handle, int(a_ptr), int(b_ptr), int(H), int(W), out.ctypes.data))
+    return out
+
+
 # ----------------------------------------------------------- per-stage ops
 
 def _f64(a) -> np.ndarray:

@@ -49,12 +49,15 @@ def shard(n: int, rank: int, world: int) -> range:
 
 
 def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilter: bool = True,
-                 device: int = 0, tables: Optional[np.ndarray] = None) -> List[dict]:
+                 device: int = 0, tables: Optional[np.ndarray] = None, ssim: bool = False) -> List[dict]:
     """All (frame, quality) items of `frames` (uint8 [F, H, W, 3], NumPy or a torch
     tensor on the device) through quality-sweep plans (jds_plan_create_q: the
     colour / prefilter / subsample / DCT front end runs once per frame and is
     quantised for up to 8 tables at a time).  Items are ordered frame-major.
-    Returns one dict per item."""
+    Returns one dict per item.  ssim=True adds the SSIM fields of the
+    reference's per-item CompressionResult (ssim_rgb, ssim_y; gui/worker.py:62-68
+    -> utils/metrics.py:9-28) from the device-resident reconstructions
+    (jds_psnr_ssim_dev: bit-identical to skimage, the heaviest per-item tail)."""
     import torch
     from jds import _abi, codec
     from engines.quantizer import scale_quant_matrix
@@ -68,6 +71,7 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
     qs = [int(q) for q in qualities]
     gk = codec.gaussian_kernel3()
     stats = np.zeros((F, len(qs)), dtype=_abi.STATS_DTYPE)
+    ssims = np.full((F, len(qs), 2), np.nan)
     for c0 in range(0, len(qs), 8):
         qc = qs[c0:c0 + 8]
         qt = [scale_quant_matrix(JPEG_LUMA_Q50, q) if tables is None else tables[c0 + i] for i, q in enumerate(qc)]
@@ -81,6 +85,11 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
             plan.run(fr.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), _abi.RUN_SSE, 0)
             torch.cuda.synchronize(dev)
             stats[:, c0:c0 + len(qc)] = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(F, len(qc))
+            if ssim:
+                for f in range(F):
+                    for i in range(len(qc)):
+                        r = codec.psnr_ssim_dev(fr[f].data_ptr(), out[f * len(qc) + i].data_ptr(), H, W, device)
+                        ssims[f, c0 + i] = (float(np.mean(r[:3])), r[3])  # channel_axis=2: mean of R, G, B
         finally:
             plan.close()
     items = []
@@ -96,6 +105,8 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
                           'psnr_rgb': float('inf') if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse)),
                           'mse_y': mse_y, 'psnr_y': psnr_from_mse(mse_y),
                           'bpp': br['bpp'], 'compression_ratio': br['compression_ratio']})
+            if ssim:
+                items[-1].update(ssim_rgb=float(ssims[f, qi, 0]), ssim_y=float(ssims[f, qi, 1]))
     return items
 
 

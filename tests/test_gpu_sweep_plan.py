@@ -104,6 +104,23 @@ def test_sweep_device_chunks_more_than_eight_qualities():
         assert it['psnr_y'] == pytest.approx(ref['metrics']['psnr_y'], rel=1e-12)
 
 
+def test_sweep_device_ssim_fields():
+    """ssim=True: the reference CompressionResult's SSIM fields per item, from the
+    device-resident reconstructions (jds_psnr_ssim_dev), against the oracle's
+    skimage restatement and the host-copy entry point."""
+    from jds import codec
+    from jds.sweep import sweep_device
+    frames = np.stack([cpu_ref.random_image(40, 56, s) for s in (11, 12)])
+    qs = [10, 50, 90]
+    items = sweep_device(frames, qs, '4:2:0', True, ssim=True)
+    for it in items:
+        ref = cpu_ref.compress_reconstruct(frames[it['frame']], it['quality'], 8, '4:2:0', True, metrics=True)
+        assert it['ssim_rgb'] == pytest.approx(ref['metrics']['ssim_rgb'], rel=1e-12)
+        assert it['ssim_y'] == pytest.approx(ref['metrics']['ssim_y'], rel=1e-12)
+        host = codec.psnr_ssim_raw(frames[it['frame']], ref['reconstructed'])
+        assert it['ssim_y'] == host[3]
+
+
 def test_sweep_plan_rejects_bad_shapes():
     from jds import _abi, codec
     q = cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, 50)
