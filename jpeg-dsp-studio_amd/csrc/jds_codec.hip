@@ -560,13 +560,8 @@ __global__ void __launch_bounds__(512) k_fwd_reduce(jds_frame_stats* st, const u
 
 // End of the forward phase: per-frame constants and the histogram's zero bin.
 __global__ void k_fwd_finish(const Geo g, jds_frame_stats* st) {
-  const int f = blockIdx.x;
   if (threadIdx.x != 0) return;
-  jds_frame_stats* s = st + f;
-  s->total_coeffs = (uint64_t)g.cpf;
-  s->block_overhead_bits = 2ull * (uint64_t)g.nby * (uint64_t)g.nbx;
-  s->pixels = (uint64_t)g.H * (uint64_t)g.W;
-  s->hist[25] += (uint64_t)g.cpf - s->nonzero;  // zeros fall in bin 25 ([0, 4))
+  finalize_frame(g, st + blockIdx.x, 1);
 }
 
 hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s) {
@@ -592,10 +587,7 @@ __global__ void k_finalize(const Geo g, jds_frame_stats* st, const double* __res
   const int f = blockIdx.x;
   if (threadIdx.x != 0) return;
   jds_frame_stats* s = st + f;
-  s->total_coeffs = (uint64_t)g.cpf;
-  s->block_overhead_bits = 2ull * (uint64_t)g.nby * (uint64_t)g.nbx;
-  s->pixels = (uint64_t)g.H * (uint64_t)g.W;
-  if (zero_bin) s->hist[25] += (uint64_t)g.cpf - s->nonzero;  // zeros fall in bin 25 ([0, 4))
+  finalize_frame(g, s, zero_bin);
   if (with_sse) {
     double a = 0.0;
     for (int t = 0; t < tiles; ++t) a = a + sse_y_part[(size_t)f * tiles + t];
@@ -635,7 +627,7 @@ static hipError_t launch_inv_t(const Geo& g, int n, const int16_t* coeffs, const
 int inv_tiles(int mode, int H, int W);
 hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
                            const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part,
-                           const InvFix& fx, hipStream_t s, int in_div);
+                           const InvFix& fx, hipStream_t s, int in_div, int fin);
 hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
                        const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y,
                        double* err_rgb, hipStream_t s, int in_div);
@@ -693,14 +685,18 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
   }
   if (phases & 2) {
     int tiles = g.tiles_y * g.tiles_x;
+    bool fused_fin = false;
     if (!(phases & 4)) {  // jds_inv.hip (default); bit 2 selects the original k_inv
       // certified fast inverse (jds_inv_fast.hip) unless the caller wants the
       // exact kernels, the IntermediateData maps or the SSE: with the SSE terms
       // (sweeps) the fast kernel measured slower than k_inv2<MODE, 1> (register
       // pressure of both paths in one kernel), so those runs stay exact
-      if (fx && !err_y && !rin)
-        e = launch_inv_fast(mode, g, n, coeffs, fq, rin, rgb_out, st, part, *fx, s, in_div);
-      else
+      if (fx && !err_y && !rin) {
+        // no SSE terms: the fast kernel does k_finalize's per-frame work itself
+        fused_fin = !sel;
+        e = launch_inv_fast(mode, g, n, coeffs, fq, rin, rgb_out, st, part, *fx, s, in_div,
+                            fused_fin ? ((phases & 8) ? 1 : 0) : -1);
+      } else
         e = launch_inv2(mode, g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, s, in_div);
       tiles = inv_tiles(mode, g.H, g.W);
     } else switch (mode) {
@@ -720,9 +716,11 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
       if ((e = hipGetLastError()) != hipSuccess) return e;
       if (!(phases & 4) && (e = launch_sel_recon(coeffs, fq, sel, sel_blk, s)) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, tiles,
-                       (int)(rin != nullptr), (phases & 8) ? 1 : 0);
-    e = hipGetLastError();
+    if (!fused_fin) {
+      hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, tiles,
+                         (int)(rin != nullptr), (phases & 8) ? 1 : 0);
+      e = hipGetLastError();
+    }
   }
   return e;
 }

@@ -24,6 +24,13 @@
 
 #pragma clang fp contract(off)
 
+// first/last tile rows in k_fwd32i (fold_rows); A/B: -DJDS_FOLD_MODE=0 gives
+// them a border launch.  A uniform per-tile flag that skips the masks on the
+// other rows measured no better (339.6 vs 337.1 us per 64 x 1080p).
+#ifndef JDS_FOLD_MODE
+#define JDS_FOLD_MODE 1
+#endif
+
 namespace jds {
 
 // orthonormal 8-point DCT matrix entries rounded to fp32:
@@ -726,6 +733,9 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   }
   const int gy = plane == 0 ? m0y * C::SY + by_t : m0y + by_t;
   const int gx = plane == 0 ? m0x * C::SX + bx_t : m0x + bx_t;
+  // the first and last tile rows may hold whole MCU rows outside the padded
+  // planes (rect admits them when fold_rows_ok holds): those blocks do not exist
+  const bool valid = (unsigned)gy < (unsigned)(plane ? g.ncy : g.nby);
   const int bidx = gy * (plane ? g.ncx : g.nbx) + gx;
   int16_t* dst = coeffs + (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
                  (long long)bidx * 64;
@@ -741,8 +751,10 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     for (int i = 0; i < 8; ++i) v[i] = src[i * rs + line];
     fdct8_f32(v);
     if constexpr (MQ) {  // shared front end: coefficient (k, line) for k_quant_mq
+      if (valid) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) dctb[k * 8 + line] = v[k];
+        for (int k = 0; k < 8; ++k) dctb[k * 8 + line] = v[k];
+      }
       return;
     }
     const float4* rq4 = reinterpret_cast<const float4*>(s_rqT + line * 8);
@@ -751,7 +763,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     const float rq[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
     const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
     int q[8];
-    quant8(v, rq, thr, true, q, ls, s_st);
+    quant8(v, rq, thr, valid, q, ls, s_st);
     // int16 transpose in place (row k at byte offset k * rs * 4).  Rotating
     // full-width rows across the wave's 8 blocks (so a block's 8 lanes read 8
     // bank groups instead of one) measured 6 us slower: the address math
@@ -762,7 +774,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     __builtin_amdgcn_wave_barrier();  // other lanes' rows: the LDS keeps the wave's order
     const uint4 row = *reinterpret_cast<const uint4*>(tq + line * rs * 2);
 #ifndef JDS_PROBE_NOSTORE
-    *reinterpret_cast<uint4*>(dst + line * 8) = row;
+    if (valid) *reinterpret_cast<uint4*>(dst + line * 8) = row;
 #else
     if (row.x == 0x7eadbeefu && row.y == 0x1234567u) *reinterpret_cast<uint4*>(dst + line * 8) = row;
 #endif
@@ -776,7 +788,11 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       // the row-filtered (or raw) planes, then the row DCT
       const float* P = plane == 1 ? s_cb : s_cr;
       const int i = line;
-      const int pr = C::SY * (by_t * 8 + i);  // first pixel row of the sample row (tile-relative)
+      // sample row of the plane; np.pad rows (>= hc, last tile row only) reflect
+      // onto rows of the same tile (fold_rows_ok)
+      int gs = gy * 8 + i;
+      gs = (gs < g.hc || !valid) ? gs : 2 * (g.hc - 1) - gs;
+      const int pr = C::SY * (gs - m0y * 8);  // first pixel row of the sample row (tile-relative)
       const int xc = 2 * bx_t * 8;            // first pixel column of the block
       float v[8];
 #pragma unroll
@@ -823,8 +839,8 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     column(P + by_t * 8 * TW + bx_t * 8, TW, plane);
   }
   if constexpr (!MQ) {
-    flag_block_list(ls, true, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
-    stats_flush<C::TF>(ls, true, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
+    flag_block_list(ls, valid, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
+    stats_flush<C::TF>(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
   }
 }
 
@@ -1204,6 +1220,39 @@ k_quant_mq(const Geo g, const int nq, const float* __restrict__ dct32, int16_t* 
 
 hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uint32_t* part, int ptiles,
                              hipStream_t s);
+// The first and last tile rows hold whole MCU rows outside the padded planes
+// (tiles are bottom-aligned: ty_off MCU rows above the image; a partial last
+// MCU row below it, e.g. 1080p 4:2:0).  k_fwd32i takes them too -- one launch
+// instead of a border launch of a few thousand workgroups; measured per 64 x
+// 1080p: k_fwd32i 327.7 + k_fwd32 26.7 -> 337.1 us; per 16 x 4K 4:2:0: 331.8 +
+// 14.6 -> 339.1 us -- when
+//  * H % 8 == 0: a luma block lies wholly in the image or does not exist;
+//  * np.pad's reflected chroma rows of the last block row (hc .. 8 ncy - 1 ->
+//    2 (hc - 1) - row) come from sample rows whose pixel rows (and the
+//    prefilter's ring) lie in the same tile window;
+//  * the window rows BORDER_REFLECT_101 maps (-yrow, 2H - 2 - yrow) stay in
+//    the image.
+// Blocks outside the planes are masked (k_fwd32i `valid`).
+template <int MODE>
+static void fold_rows(const Geo& g, int4& rect) {
+  using C = Cfg<MODE>;
+  if (g.H % 8 != 0 || g.H < C::TH + 2) return;
+  if (rect.x == 1) {
+    const int y0 = -g.ty_off * C::MH;  // tile row 0
+    if (1 - y0 <= g.H - 1) rect.x = 0;
+  }
+  if (rect.y == g.tiles_y - 2) {
+    const int y0 = ((g.tiles_y - 1) * C::MY - g.ty_off) * C::MH;
+    bool ok = y0 >= 1 && y0 + C::TH <= 2 * g.H - 2;
+    const int hp = g.ncy * 8;  // padded chroma rows
+    if (MODE != M444 && hp > g.hc) {
+      const int rmin = 2 * (g.hc - 1) - (hp - 1);
+      ok = ok && rmin >= 0 && C::SY * rmin >= y0;
+    }
+    if (ok) rect.y = g.tiles_y - 1;
+  }
+}
+
 // k_fix_fwd workgroups in all (x items, grid-stride over each item's list):
 // typical lists (0.4 % of 3M blocks at Q50) need one block per workgroup
 constexpr int FIX_GRID = 16384;
@@ -1225,6 +1274,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   rect.z = (g.tx_off * C::MW > 0) ? 1 : 0;
   rect.w = (g.W / C::MW + g.tx_off) / C::MX - 1;
   const bool split = (g.W % 8) == 0 && g.H >= 2 && g.W >= 2 && rect.y >= rect.x && rect.w >= rect.z;
+  if (split && JDS_FOLD_MODE >= 1) fold_rows<MODE>(g, rect);
   hipError_t e;
   if (split) {
     const int nin = (rect.y - rect.x + 1) * (rect.w - rect.z + 1), nout = g.tiles_y * g.tiles_x - nin;

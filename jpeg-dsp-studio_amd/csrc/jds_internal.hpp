@@ -139,6 +139,15 @@ struct Cfg {
   static constexpr int TI = 384;                      // inverse threads
 };
 
+// Per-frame constants of the statistics and, when the forward deferred it,
+// the histogram's zero bin (k_fwd_finish, k_finalize, k_inv_fast's fused tail).
+__device__ inline void finalize_frame(const Geo& g, jds_frame_stats* s, int zero_bin) {
+  s->total_coeffs = (uint64_t)g.cpf;
+  s->block_overhead_bits = 2ull * (uint64_t)g.nby * (uint64_t)g.nbx;
+  s->pixels = (uint64_t)g.H * (uint64_t)g.W;
+  if (zero_bin) s->hist[25] += (uint64_t)g.cpf - s->nonzero;  // zeros fall in bin 25 ([0, 4))
+}
+
 // Workgroup (x, f) of a (ceil(ptiles / 64), n) x 512 launch: sums tiles
 // [64x, 64x + 64) of frame f's per-tile statistics partials (nonzero,
 // magnitude bits, hist[50] as u32 per tile) into the frame stats, 8 groups x 64

@@ -445,11 +445,15 @@ __global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per
 k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
            const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
            double* __restrict__ sse_y_part, unsigned* __restrict__ fixcount, unsigned* __restrict__ next_count,
-           unsigned* __restrict__ item_cnt, const int rot, const int probe, const int in_div, const int fix_all) {
+           unsigned* __restrict__ item_cnt, const int rot, const int probe, const int in_div, const int fix_all,
+           const int fin) {
   // the transpose buffer and chroma window are the exact fallback's own
   __shared__ __attribute__((aligned(16))) InvShared<MODE, XTRA> sh;
   const int tid = threadIdx.x;
   const int frame = blockIdx.y, tile = blockIdx.x;
+  // k_finalize's work for runs without SSE terms (fin >= 0; fin = 1 adds the
+  // zero bin the forward deferred): one launch fewer per run
+  if (fin >= 0 && tile == 0 && tid == 0) finalize_frame(g, st + frame, fin);
   // per-item adaptivity (InvFix): the previous run's recomputed tiles of this item
   const unsigned n_items = gridDim.y, ntile = gridDim.x;
   unsigned* cnt_prev = item_cnt + ((rot + 2) % 3) * n_items;
@@ -480,7 +484,7 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
 template <int MODE>
 static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq, const uint8_t* rgb_in,
                              uint8_t* rgb_out, jds_frame_stats* st, double* part, const InvFix& fx, hipStream_t s,
-                             int in_div) {
+                             int in_div, int fin) {
   const int ty = (g.H + Inv<MODE>::TH - 1) / Inv<MODE>::TH, tx = (g.W + Inv<MODE>::TW - 1) / Inv<MODE>::TW;
   const dim3 grid(ty * tx, n), blk(Inv<MODE>::NT);
   // count[parity] was zeroed by the previous run; this run zeroes the other
@@ -488,17 +492,17 @@ static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const F
   unsigned* nxt = fx.count + (fx.parity ^ 1);
   (void)rgb_in;  // SSE runs take the exact kernel (launch_codec)
   hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, cnt, nxt,
-                     fx.item, fx.rot, fx.probe, in_div, fx.fix_all);
+                     fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
   return hipGetLastError();
 }
 
 hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
                            const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part,
-                           const InvFix& fx, hipStream_t s, int in_div) {
+                           const InvFix& fx, hipStream_t s, int in_div, int fin) {
   switch (mode) {
-    case M420: return inv_fast_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div);
-    case M422: return inv_fast_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div);
-    default: return inv_fast_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div);
+    case M420: return inv_fast_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div, fin);
+    case M422: return inv_fast_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div, fin);
+    default: return inv_fast_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div, fin);
   }
 }
 

@@ -183,7 +183,11 @@ def _plan_run(frames, qs, mode, pf, flags):
                                           (256, 384, '4:4:4', False), (130, 98, '4:2:0', False),
                                           (64, 48, '4:2:2', False), (360, 648, '4:2:0', False),
                                           (200, 328, '4:2:2', True), (184, 260, '4:4:4', False),
-                                          (226, 516, '4:2:0', True), (98, 196, '4:2:2', False)])
+                                          (226, 516, '4:2:0', True), (98, 196, '4:2:2', False),
+                                          # first/last tile rows with MCU rows outside the planes
+                                          # folded into the interior launch (fold_rows in jds_fast.hip)
+                                          (72, 128, '4:4:4', False), (104, 192, '4:2:0', True),
+                                          (88, 128, '4:2:0', True), (72, 256, '4:2:2', True)])
 def test_fast_path_equals_exact_path_and_oracle(h, w, mode, pf):
     """Certified fp32 + fp64 fix-up (default) == all-fp64 kernels == oracle, bit for bit."""
     from jds import _abi
