@@ -42,7 +42,7 @@ hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
                            jds_frame_stats* st, uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount,
                            float* dct32,
-                           hipStream_t s, const Side* side, bool finish);
+                           hipStream_t s, const Side* side, bool finish, int par);
 int quant_mq_tiles(const Geo& g);
 int inv16_tiles(int mode, int H, int W);
 constexpr int MAXQ_SHARED = 8;  // jds_fast.hip MAXQ
@@ -169,6 +169,8 @@ struct jds_plan {
   bool inv_fast_ok = true;
   bool last_fwd16_fast = false;  // 16x16: the last forward was the certified fp32 one
   unsigned fwd16_runs = 0;       // 16x16 certified forward runs so far: picks the list counter
+  unsigned fwd8_runs = 0;        // 8x8 single-quality certified forward runs: picks the counter bank
+  int last_fwd8_bank = -1;       // bank of the last such run (jds_plan_fix_counts), -1: none
   InvFix inv_fix() const {
     return {(unsigned*)invfix.p, (unsigned*)invfix.p + 16, 0, (int)(inv_runs & 1u), (int)(inv_runs % 3u),
             (int)(inv_runs % 16u == 15u)};
@@ -542,7 +544,7 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
 
 int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   if (!p || !counts) return fail(JDS_EINVAL, "null argument");
-  // counters[n, 2n): blocks the last run's k_fix_fwd recomputed, per item;
+  // counters[bank n, bank n + n): blocks the last run's k_fix_fwd recomputed, per item;
   // invfix[0]: tiles the last run's certified inverse handed to the exact kernel
   counts[0] = counts[1] = 0u;
   if (p->g.bs == 16) {  // counters[2]: blocks the last certified 16x16 forward recomputed
@@ -557,8 +559,11 @@ int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   if (!c) return fail(JDS_ENOMEM, "fix_counts: host allocation");
   // the last run may be in flight on any stream: wait for the device first
   hipError_t e = hipDeviceSynchronize();
+  // single-quality plans: the live counter bank of the last certified run;
+  // sweep plans: the list lengths k_fwd_reduce_fix built at [n, 2n)
+  const int bank = p->nq > 1 ? 1 : (p->last_fwd8_bank < 0 ? 1 : p->last_fwd8_bank);
   if (e == hipSuccess)
-    e = hipMemcpy(c, (const uint32_t*)p->counters.p + p->n, 4 * (size_t)p->n, hipMemcpyDeviceToHost);
+    e = hipMemcpy(c, (const uint32_t*)p->counters.p + bank * p->n, 4 * (size_t)p->n, hipMemcpyDeviceToHost);
   // the last fast-inverse run appended to counter (inv_runs - 1) & 1
   if (e == hipSuccess && p->last_inv_fast)
     e = hipMemcpy(c + p->n, (const uint32_t*)p->invfix.p + ((p->inv_runs + 1u) & 1u), 4, hipMemcpyDeviceToHost);
@@ -566,7 +571,7 @@ int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
     free(c);
     return fail(JDS_EHIP, "fix_counts: %s", hipGetErrorString(e));
   }
-  for (int i = 0; i < p->n; ++i) counts[0] += c[i];
+  for (int i = 0; i < p->n; ++i) counts[0] += std::min(c[i], (uint32_t)(p->g.cpf / 64));  // (k_fix_fwd's clamp)
   counts[1] = p->last_inv_fast ? c[p->n] : 0u;
   free(c);
   return JDS_OK;
@@ -623,7 +628,9 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
                               (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint32_t*)p->part32.p,
                               (uint32_t*)p->fixbits.p, (uint2*)p->fixlist.p, (unsigned*)p->counters.p,
                               (float*)p->dct32.p, s, &p->side,
-                              phases == 1));  // forward + inverse: k_finalize adds the zero bin
+                              phases == 1,  // forward + inverse: k_finalize adds the zero bin
+                              (int)(p->fwd8_runs & 1u)));
+    if (!exact && p->nq == 1) p->last_fwd8_bank = (int)(p->fwd8_runs++ & 1u);
   }
   InvFix fx = p->inv_fix();
   fx.fix_all = (flags & JDS_RUN_INV_FIXALL) ? 1 : 0;

@@ -355,7 +355,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   if (stz != nullptr && blockIdx.x == 0) {
     uint64_t* z = reinterpret_cast<uint64_t*>(stz + (size_t)frame * nzq);
     for (int i = tid; i < nzq * (int)(sizeof(jds_frame_stats) / 8); i += blockDim.x) z[i] = 0ull;
-    if (tid < nzq) fixcount[gridDim.y * nzq + frame * nzq + tid] = 0u;  // and the items' final fix-up counts
+    if (MQ && tid < nzq) fixcount[gridDim.y * nzq + frame * nzq + tid] = 0u;  // and the items' list lengths
   }
   if (border) {  // tiles outside the interior rectangle rect = (ty_lo, ty_hi, tx_lo, tx_hi) only
     int e = blockIdx.x;
@@ -603,7 +603,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   if (stz != nullptr && blockIdx.x == 0) {
     uint64_t* z = reinterpret_cast<uint64_t*>(stz + (size_t)frame * nzq);
     for (int i = tid; i < nzq * (int)(sizeof(jds_frame_stats) / 8); i += blockDim.x) z[i] = 0ull;
-    if (tid < nzq) fixcount[gridDim.y * nzq + frame * nzq + tid] = 0u;  // and the items' final fix-up counts
+    if (MQ && tid < nzq) fixcount[gridDim.y * nzq + frame * nzq + tid] = 0u;  // and the items' list lengths
   }
   const int ty = rect.x + (int)blockIdx.x / ncol, tx = rect.z + (int)blockIdx.x % ncol;
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
@@ -855,17 +855,9 @@ __global__ void __launch_bounds__(512)
 k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ part, int ptiles,
                  uint32_t* __restrict__ fixbits, uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount) {
   reduce_partials(st, part, ptiles);
-  // fixcount[0, n): live counters the single-quality front ends appended to;
-  // fixcount[n, 2n): this run's list lengths (k_fix_fwd, jds_plan_fix_counts)
+  // sweep plans only (single-quality plans reduce in k_fix_fwd): list lengths
+  // accumulate at fixcount[n + item]
   unsigned* const fixlen = fixcount + gridDim.y;
-  if (fixbits == nullptr) {  // single-quality front ends appended to the lists themselves
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      const unsigned cap = (unsigned)(g.cpf / 64);
-      fixlen[blockIdx.y] = min(fixcount[blockIdx.y], cap);
-      fixcount[blockIdx.y] = 0u;  // re-armed for the next run
-    }
-    return;
-  }
   const int item = blockIdx.y, wpi = fix_wpi(g), lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int per = (wpi + gridDim.x - 1) / gridDim.x, w_end = min(wpi, (blockIdx.x + 1) * per);
   const long long nyb = (long long)g.nby * g.nbx, ncb = (long long)g.ncy * g.ncx, cap = g.cpf / 64;
@@ -918,7 +910,8 @@ template <int MODE, bool PF>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(JDS_FIX_WPE)))
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
-          const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq, const int n_flat) {
+          const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq, const int n_flat,
+          unsigned* __restrict__ rearm) {
   constexpr bool CPLANE = (MODE != M444) && PF;
   constexpr int SY = Cfg<MODE>::SY;
   constexpr int WRR = 8 * SY + 2, WCC = 18;  // prefilter source window of one chroma block
@@ -953,12 +946,16 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     list = fixlist;
     next = make_uint2(0u, 0u);
   } else {
-    // length fixcount[item] (k_fwd_reduce_fix); the first entry is read beside
-    // it (in bounds, maybe stale when blockIdx.x >= count, then unused): one
-    // memory latency instead of two
-    count = fixcount[blockIdx.y];
+    // length fixcount[item] (single-quality plans: the live counter the front
+    // end appended to; sweeps: k_fwd_reduce_fix's list length); the first
+    // entry is read beside it (in bounds, maybe stale when blockIdx.x >= count,
+    // then unused): one memory latency instead of two
+    count = min(fixcount[blockIdx.y], cap);
     list = fixlist + (size_t)blockIdx.y * cap;
     next = blockIdx.x < cap ? list[blockIdx.x] : make_uint2(0u, 0u);
+    // single-quality plans: the other counter bank, which the next run appends
+    // to, is re-armed here
+    if (rearm != nullptr && blockIdx.x == 0 && t == 0) rearm[blockIdx.y] = 0u;
   }
   const double k[3] = {gk[0], gk[1], gk[2]};
   for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
@@ -1253,6 +1250,7 @@ static void fold_rows(const Geo& g, int4& rect) {
   }
 }
 
+hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s);
 // k_fix_fwd workgroups in all (x items, grid-stride over each item's list):
 // typical lists (0.4 % of 3M blocks at Q50) need one block per workgroup
 constexpr int FIX_GRID = 16384;
@@ -1261,10 +1259,12 @@ template <int MODE, bool PF>
 static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
                              const FastQ* fq32, const double* gk, const float* gk32, jds_frame_stats* st,
                              uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount, float* dct32, hipStream_t s,
-                             const Side* side, bool finish) {
+                             const Side* side, bool finish, int par) {
   using C = Cfg<MODE>;
   const bool mq = nq > 1;  // sweep plan: front end once per frame into dct32, then k_quant_mq
   const int nf = n / nq;   // frames (n = items)
+  // single quality: the front end appends to live counter bank `par` (of two)
+  unsigned* const fc = mq ? fixcount : fixcount + par * n;
   // Tiles lying wholly inside the image (no padding blocks, no phantom MCUs;
   // only the 1-px ring may reflect) form a rectangle of tile indices and take
   // k_fwd32i; the rest run in k_fwd32 beside it on the side stream.
@@ -1289,7 +1289,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
                            part, fixlist, fixcount, 1, rect, dct32, nullptr, nq);
       else
         hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(nout, n), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32, part,
-                           fixlist, fixcount, 1, rect, nullptr, nullptr, 1);
+                           fixlist, fc, 1, rect, nullptr, nullptr, 1);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (fork && (e = hipEventRecord(side->join, sb)) != hipSuccess) return e;
@@ -1298,7 +1298,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
                          part, fixlist, fixcount, rect, dct32, st, nq);
     else
       hipLaunchKernelGGL((k_fwd32i<MODE, PF>), dim3(nin, n), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32, part,
-                         fixlist, fixcount, rect, nullptr, st, 1);
+                         fixlist, fc, rect, nullptr, st, 1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (fork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
   } else {
@@ -1307,7 +1307,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
                          coeffs, fq32, gk32, part, fixlist, fixcount, 0, rect, dct32, st, nq);
     else
       hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(g.tiles_y * g.tiles_x, n), dim3(C::TF), 0, s, g, rgb, coeffs,
-                         fq32, gk32, part, fixlist, fixcount, 0, rect, nullptr, st, 1);
+                         fq32, gk32, part, fixlist, fc, 0, rect, nullptr, st, 1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   int ptiles = g.tiles_y * g.tiles_x;
@@ -1316,18 +1316,30 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     hipLaunchKernelGGL(k_quant_mq, dim3(ptiles, nf), dim3(256), 0, s, g, nq, dct32, coeffs, fq32, part, fixbits);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  // partials -> frame statistics (reset by the front-end launch above), list
-  // lengths to fixcount[n + item] (sweep plans: bitmaps -> lists)
-  hipLaunchKernelGGL(k_fwd_reduce_fix, dim3((ptiles + 63) / 64, n), dim3(512), 0, s, g, st, part, ptiles,
-                     mq ? fixbits : nullptr, fixlist, fixcount);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (mq && n < 8192) {  // sweep: one flat grid over every item's list (list starts in <= 32 KB of LDS)
-    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(FIX_GRID), dim3(64), sizeof(unsigned) * (n + 1), s, g, rgb,
-                       coeffs, fq, gk, st, fixlist, fixcount + n, nq, n);
-  } else {
-    const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
+  const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
+  if (!mq) {
+    // single quality: the statistics partials into the frame stats (reset by
+    // the front-end launch above); k_fix_fwd reads the live counter bank `par`
+    // the front end appended to and re-arms the other bank.  (Reducing the
+    // partials inside k_fix_fwd instead of this launch measured slower: 49.4
+    // vs 29.1 + 5.4 us per 64 x 1080p.)
+    if ((e = launch_fwd_reduce(n, st, part, ptiles, s)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
-                       fixcount + n, nq, 0);
+                       fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
+  }
+  // sweeps: partials -> frame statistics, bitmaps -> lists with their lengths
+  // at fixcount[n + item] (zeroed by the front-end launch)
+  hipLaunchKernelGGL(k_fwd_reduce_fix, dim3((ptiles + 63) / 64, n), dim3(512), 0, s, g, st, part, ptiles,
+                     fixbits, fixlist, fixcount);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (n < 8192) {  // one flat grid over every item's list (list starts in <= 32 KB of LDS)
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(FIX_GRID), dim3(64), sizeof(unsigned) * (n + 1), s, g, rgb,
+                       coeffs, fq, gk, st, fixlist, fixcount + n, nq, n, nullptr);
+  } else {
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
+                       fixcount + n, nq, 0, nullptr);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
@@ -1336,17 +1348,17 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
                            jds_frame_stats* st, uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount, float* dct32,
-                           hipStream_t s, const Side* side, bool finish) {
+                           hipStream_t s, const Side* side, bool finish, int par) {
   const FastQ* f = (const FastQ*)fq32;
   switch (mode) {
     case M420:
-      return pf ? fast_fwd_t<M420, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish)
-                : fast_fwd_t<M420, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish);
+      return pf ? fast_fwd_t<M420, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par)
+                : fast_fwd_t<M420, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par);
     case M422:
-      return pf ? fast_fwd_t<M422, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish)
-                : fast_fwd_t<M422, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish);
+      return pf ? fast_fwd_t<M422, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par)
+                : fast_fwd_t<M422, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par);
     default:
-      return fast_fwd_t<M444, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish);
+      return fast_fwd_t<M444, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par);
   }
 }
 
