@@ -430,7 +430,7 @@ def main():
     # Per-kernel launch durations from a serial calibration pass (outside the
     # timed region): with pipelining the forward and inverse launches overlap,
     # so their in-stream durations would not describe either kernel alone.
-    # Forward phase = k_fwd32i + k_fwd32 (border tiles) + k_fix_fwd + reductions.
+    # Forward phase = k_fwd32i (+ k_fwd32 border tiles) + k_fwd_reduce + k_fix_fwd.
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     torch.cuda.synchronize(dev)
     for k in range(args.steps):
@@ -461,7 +461,8 @@ def main():
         # the plan's inverse choice (jds_abi.hip inv_fast_ok): the certified fast
         # kernel for 4:2:x with a DC quantiser <= 60, k_inv2 otherwise
         inv_fast = mcode != 0 and float(qt[0][0]) <= 60.0
-        kname = (f'k_fwd32i<{mcode},{pfs}> + k_fwd32<{mcode},{pfs}> (border tiles) + k_fix_fwd'
+        # (k_fwd32 runs only for border tiles k_fwd32i cannot take: fold_rows in jds_fast.hip)
+        kname = (f'k_fwd32i<{mcode},{pfs}> (+ k_fwd32 border tiles if any) + k_fwd_reduce + k_fix_fwd'
                  if dom == 'k_fwd' else (f'k_inv_fast<{mcode},0>' if inv_fast else f'k_inv2<{mcode},0>'))
     traffic = None
     tf = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
