@@ -34,7 +34,7 @@ bench = json.loads(open(os.path.join(src, 'bench.json')).read().strip().splitlin
 json.dump(bench, open(os.path.join(prof, f'{name}_bench.json'), 'w'), indent=1)
 shutil.copy(os.path.join(src, 'stats', 'run_kernel_stats.csv'), os.path.join(prof, f'{name}_kernel_stats.csv'))
 
-FWD = ('k_fwd32i', 'k_fwd32<', 'k_fix_fwd', 'k_fwd_reduce_fix', 'k_fwd16', 'k_fwd<', 'k_fwdq', 'k_quant_mq')
+FWD = ('k_fwd32i', 'k_fwd32<', 'k_fix_fwd', 'k_fwd_reduce', 'k_fwd16', 'k_fwd<', 'k_fwdq', 'k_quant_mq')
 INV = ('k_inv2', 'k_inv<', 'k_inv_fast', 'k_inv16', 'k_chroma16', 'k_inv32', 'k_fix_inv')
 pmc = collections.defaultdict(dict)
 for ctr in ('fetch', 'write'):
