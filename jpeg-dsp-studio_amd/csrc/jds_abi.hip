@@ -38,6 +38,7 @@ hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsign
 size_t mag_scratch_bytes(long long nblocks, int max_chunks);
 hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* chunk_sum, int max_chunks,
                           double* out, hipStream_t s);
+void combined_taps32(const double* gk, float* out5);
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
                            jds_frame_stats* st, uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount,
@@ -506,7 +507,10 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
       float* f = (float*)(h32 + fqs * i);
       fast_fwd_thresholds(params[i].qtable, mode, pf, params[i].gauss, f, f + 64);
     }
-    const float gk32[3] = {(float)params[0].gauss[0], (float)params[0].gauss[1], (float)params[0].gauss[2]};
+    // taps and k_fwd32i's combined taps (Gaussian then 2-sample area: k0, k0+k1, k1+k2, k2)
+    const double* gs = params[0].gauss;
+    float gk32[5];
+    combined_taps32(gs, gk32);
     const size_t nblk = (size_t)n * (size_t)(g.cpf / 64);
     const size_t ptiles = (size_t)(n_q > 1 ? quant_mq_tiles(g) : g.tiles_y * g.tiles_x);
     if ((e = p->fq32.ensure(fqs * n)) != hipSuccess || (e = p->gk32.ensure(sizeof gk32)) != hipSuccess ||

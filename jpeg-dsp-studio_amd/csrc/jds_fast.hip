@@ -83,6 +83,13 @@ constexpr int BS32 = 72;  // floats per 8x8 block in LDS (column writes conflict
 template <int SY>
 __device__ __forceinline__ int csw(int row) { return (row / SY) & 3; }
 
+// The prefiltered planes hold pair sums (8 float4 slots per 128-B row): the
+// 8 lanes of a chroma block read rows SY apart at the same slots, which rows
+// two apart put on the same banks; XOR-ing the slot with the row's sample
+// index mod 8 spreads them over 8 slots.
+template <int SY>
+__device__ __forceinline__ int psw(int row) { return (row / SY) & 7; }
+
 __device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[6], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255u; }
 
 // Per-lane statistics of the quantised coefficients.  Integer counters keep
@@ -590,7 +597,10 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   constexpr int CR = SUB ? (CPLANE ? WR : TH) : TH;  // chroma plane rows
   constexpr int NCD = SUB ? 2 * C::NCB : 1;          // chroma row-DCT blocks (SUB)
   __shared__ __attribute__((aligned(16))) float s_y[TH * TW];       // luma after the row DCT
-  __shared__ __attribute__((aligned(16))) float s_c[2 * CR * TW];   // chroma planes (4:4:4: after the row DCT)
+  // chroma planes (4:4:4: after the row DCT; prefiltered 4:2:x: the horizontal
+  // pair sums, TW / 2 per row)
+  constexpr int CW = CPLANE ? TW / 2 : TW;
+  __shared__ __attribute__((aligned(16))) float s_c[2 * CR * CW];
   __shared__ __attribute__((aligned(16))) float s_cd[NCD * BS32];   // chroma blocks after the row DCT
   __shared__ __attribute__((aligned(16))) float s_rqT[64];          // 1/Q transposed: [v][k]
   __shared__ __attribute__((aligned(16))) float s_thT[2][64];
@@ -618,7 +628,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   if (tid <= NSTAT) s_st[tid] = 0u;
   const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
   float* s_cb = s_c;
-  float* s_cr = s_c + CR * TW;
+  float* s_cr = s_c + CR * CW;
 
   // ---- 1. row segments --------------------------------------------------------
   if (tid < WR * SEG) {
@@ -684,21 +694,22 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
           rb = right_edge ? cb[6] : cb32(R, G, B);
           rr = right_edge ? cr[6] : cr32(R, G, B);
         }
-        float ob[8], orr[8];
+        // Gaussian row pass and the area's horizontal pair sum in one chain:
+        // H_j = (k0, k0+k1, k1+k2, k2) . x_{2j-1 .. 2j+2} (fwd_input_error)
+        const float h0 = k0, h1 = gk32[3], h2 = gk32[4], h3 = k2;
+        float ob[4], orr[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float bl = k == 0 ? lb : cb[k - 1], br = k == 7 ? rb : cb[k + 1];
-          const float ql = k == 0 ? lr : cr[k - 1], qr = k == 7 ? rr : cr[k + 1];
-          ob[k] = fmaf(k2, br, fmaf(k1, cb[k], k0 * bl));
-          orr[k] = fmaf(k2, qr, fmaf(k1, cr[k], k0 * ql));
+        for (int j = 0; j < 4; ++j) {
+          const float bl = j == 0 ? lb : cb[2 * j - 1], br = j == 3 ? rb : cb[2 * j + 2];
+          const float ql = j == 0 ? lr : cr[2 * j - 1], qr = j == 3 ? rr : cr[2 * j + 2];
+          ob[j] = fmaf(h3, br, fmaf(h2, cb[2 * j + 1], fmaf(h1, cb[2 * j], h0 * bl)));
+          orr[j] = fmaf(h3, qr, fmaf(h2, cr[2 * j + 1], fmaf(h1, cr[2 * j], h0 * ql)));
         }
-        const int hs = csw<C::SY>(r);
-        float4* db = reinterpret_cast<float4*>(s_cb + r * TW);
-        float4* dr = reinterpret_cast<float4*>(s_cr + r * TW);
-        db[(2 * c) ^ hs] = make_float4(ob[0], ob[1], ob[2], ob[3]);
-        db[(2 * c + 1) ^ hs] = make_float4(ob[4], ob[5], ob[6], ob[7]);
-        dr[(2 * c) ^ hs] = make_float4(orr[0], orr[1], orr[2], orr[3]);
-        dr[(2 * c + 1) ^ hs] = make_float4(orr[4], orr[5], orr[6], orr[7]);
+        const int hs = psw<C::SY>(r);
+        float4* db = reinterpret_cast<float4*>(s_cb + r * CW);
+        float4* dr = reinterpret_cast<float4*>(s_cr + r * CW);
+        db[c ^ hs] = make_float4(ob[0], ob[1], ob[2], ob[3]);
+        dr[c ^ hs] = make_float4(orr[0], orr[1], orr[2], orr[3]);
       } else {
         if (r >= 1 && r <= TH) {
           const int hs = csw<C::SY>(r - 1);
@@ -795,6 +806,28 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       const int pr = C::SY * (gs - m0y * 8);  // first pixel row of the sample row (tile-relative)
       const int xc = 2 * bx_t * 8;            // first pixel column of the block
       float v[8];
+      if constexpr (CPLANE) {
+        // the 8 samples' pair sums on the window rows of the sample row (pixel
+        // row + 1): 4:2:0 the combined taps down 4 rows, *0.25; 4:2:2 the
+        // Gaussian's column form over 3 rows, *0.5 (both exact scalings)
+        float R[C::SY + 2][8];
+        const int f0 = 2 * bx_t;  // float4 slot of the block's first pair sum
+#pragma unroll
+        for (int j = 0; j < C::SY + 2; ++j) {
+          const int hs = psw<C::SY>(pr + j);
+          const float4* s4 = reinterpret_cast<const float4*>(P + (pr + j) * CW);
+          const float4 x = s4[f0 ^ hs], y = s4[(f0 + 1) ^ hs];
+          R[j][0] = x.x; R[j][1] = x.y; R[j][2] = x.z; R[j][3] = x.w;
+          R[j][4] = y.x; R[j][5] = y.y; R[j][6] = y.z; R[j][7] = y.w;
+        }
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          if constexpr (C::SY == 2)
+            v[jj] = fmaf(k2, R[3][jj], fmaf(gk32[4], R[2][jj], fmaf(gk32[3], R[1][jj], k0 * R[0][jj]))) * 0.25f - 128.0f;
+          else
+            v[jj] = fmaf(k0, R[2][jj] + R[0][jj], k1 * R[1][jj]) * 0.5f - 128.0f;
+        }
+      } else {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {  // 4 samples (8 pixel columns) at a time
         float rows[C::SY + 2][8];
@@ -825,6 +858,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
           else
             v[4 * h + jj] = (s[0][0] + s[0][1]) * 0.5f - 128.0f;
         }
+      }
       }
       fdct8_f32(v);
       float4* d4 = reinterpret_cast<float4*>(s_cd + (blk - C::NYB) * BS32 + i * 8);
@@ -1390,6 +1424,36 @@ void pass_bound(double X, double e, const double* Xin, const double* ein, double
   }
 }
 
+// fp32 taps for the kernels: the Gaussian's k0, k1, k2 (k_fwd32, k_fix_fwd's
+// sampling is fp64) and the combined taps of Gaussian + 2-sample area sum
+// (k_fwd32i: x_{2j-1..2j+2} weighted k0, k0+k1, k1+k2, k2).
+void combined_taps32(const double* gk, float* out5) {
+  out5[0] = (float)gk[0];
+  out5[1] = (float)gk[1];
+  out5[2] = (float)gk[2];
+  out5[3] = (float)(gk[0] + gk[1]);
+  out5[4] = (float)(gk[1] + gk[2]);
+}
+
+// Error of one combined-tap chain fmaf(h3, x3, fmaf(h2, x2, fmaf(h1, x1, h0 * x0)))
+// over inputs |x| <= X with error e each: the taps' own fp32 representation
+// error against the real sums, the inputs' errors and one rounding per step.
+static double combined_chain_error(const double* gk, double X, double e) {
+  const double u = 0x1p-24;
+  float h[5];
+  combined_taps32(gk, h);
+  const double hf[4] = {h[0], h[3], h[4], h[2]};
+  const double hx[4] = {gk[0], gk[0] + gk[1], gk[1] + gk[2], gk[2]};
+  double sh = 0, dh = 0, pre = 0, P = 0;
+  for (int i = 0; i < 4; ++i) {
+    sh += fabs(hf[i]);
+    dh += fabs(hf[i] - hx[i]);
+    pre += fabs(hf[i]);
+    P += pre;  // |partial result| after step i <= X * (sum of |h| so far)
+  }
+  return sh * e + dh * X + u * X * P + 1e-12;
+}
+
 double fwd_input_error(int plane, int mode, bool pf, const double* gk) {
   const double u = 0x1p-24;
   // luma32: fmaf(kb, B, fmaf(kg, G, kr*R)); constants in fp32; then -128
@@ -1400,17 +1464,28 @@ double fwd_input_error(int plane, int mode, bool pf, const double* gk) {
   const double dkr = fabs((double)-0.081312f + 0.081312) + fabs((double)-0.418688f + 0.418688);
   const double ec = 255 * (dkb > dkr ? dkb : dkr) + 2 * u * 256 + 1e-12;  // before -128
   double e = ec;
+  double e_comb = 0.0;  // k_fwd32i's combined-tap chain (prefiltered chroma)
   if (mode != M444 && pf) {
     const double k0 = gk[0], k1 = gk[1], k2 = gk[2];
     const double k0f = (float)k0, k1f = (float)k1, k2f = (float)k2;
     const double dk = fabs(k0f - k0) + fabs(k1f - k1) + fabs(k2f - k2);
-    // row: fmaf(k2, S1, fmaf(k1, S0, k0*S_1)); |S| <= 256, taps sum to 1
+    // k_fwd32 (per pixel): row fmaf(k2, S1, fmaf(k1, S0, k0*S_1)); |S| <= 256, taps sum to 1
     const double er = (k0f + k1f + k2f) * e + dk * 256 + u * 256 * (k0 + (k0 + k1) + 1.0) + 1e-12;
     // column: fmaf(k0, T+1 + T-1, k1*T0)
     e = (k1f + 2 * k0f) * er + dk * 512 + u * (512 + k1 * 256 + 256) + 1e-12;
+    // k_fwd32i: horizontal pair sums H = combined chain over 4 chroma samples
+    // (|H| <= 512), then 4:2:0: the combined chain down 4 rows of H (|.| <= 1024)
+    // and *0.25 (exact); 4:2:2: the column form over H (magnitudes doubled) and
+    // *0.5 (exact)
+    const double eh = combined_chain_error(gk, 256, ec);
+    if (mode == M420)
+      e_comb = combined_chain_error(gk, 512, eh) / 4;
+    else
+      e_comb = ((k1f + 2 * k0f) * eh + dk * 1024 + u * (1024 + k1 * 512 + 512) + 1e-12) / 2;
   }
   if (mode == M420) e = e + u * (512 + 768 + 1024) / 4;  // ((a+b)+c)+d, *0.25 exact
   if (mode == M422) e = e + u * 512 / 2;                  // (a+b), *0.5 exact
+  if (e_comb > e) e = e_comb;                             // the bound covers both chains
   return e + u * 128;                                     // -128
 }
 
@@ -1489,9 +1564,24 @@ int fwd32_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, in
     const float bl = chroma(y, refl101(x - 1, W)), c = chroma(y, x), br = chroma(y, refl101(x + 1, W));
     return fmaf(k2, br, fmaf(k1, c, k0 * bl));
   };
+  float h[5];
+  combined_taps32(gk, h);
+  auto pairf = [&](int y, int j) {  // k_fwd32i: combined taps over chroma columns 2j-1 .. 2j+2 of row y
+    const float x0 = chroma(y, refl101(2 * j - 1, W)), x1 = chroma(y, 2 * j), x2 = chroma(y, 2 * j + 1),
+                x3 = chroma(y, refl101(2 * j + 2, W));
+    return fmaf(h[2], x3, fmaf(h[4], x2, fmaf(h[3], x1, h[0] * x0)));
+  };
   auto sample = [&](int y, int x) -> float {  // plane sample (y, x), level-shifted
     if (plane == 0) return luma32m(px(y, x, 0), px(y, x, 1), px(y, x, 2));
     if (mode == M444) return chroma(y, x) - 128.0f;
+    if (pf && rows_first) {  // k_fwd32i
+      if (sy == 2) {
+        const float r0 = pairf(refl101(2 * y - 1, H), x), r1 = pairf(2 * y, x), r2 = pairf(2 * y + 1, x),
+                    r3 = pairf(refl101(2 * y + 2, H), x);
+        return fmaf(h[2], r3, fmaf(h[4], r2, fmaf(h[3], r1, h[0] * r0))) * 0.25f - 128.0f;
+      }
+      return fmaf(k0, pairf(refl101(y + 1, H), x) + pairf(refl101(y - 1, H), x), k1 * pairf(y, x)) * 0.5f - 128.0f;
+    }
     float s[2][2];
     for (int a = 0; a < sy; ++a)
       for (int b = 0; b < 2; ++b) {
