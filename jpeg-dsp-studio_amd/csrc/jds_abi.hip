@@ -49,7 +49,7 @@ int inv16_tiles(int mode, int H, int W);
 constexpr int MAXQ_SHARED = 8;  // jds_fast.hip MAXQ
 void fast_fwd_bounds(int mode, bool pf, const double* gk, double* E);
 int fwd32_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
-                     bool rows_first, float* out);
+                     int flags, float* out);
 void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
 size_t fast_q_size();
 hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse, hipStream_t s);
@@ -77,7 +77,7 @@ void fast_fwd16_bounds(int mode, bool pf, const double* gk, double* E);
 void fast_fwd16_thresholds(const double* Q8, int mode, bool pf, const double* gk, void* out);
 size_t fast_q16_size();
 int fwd16_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
-                     bool rows_first, float* out);
+                     int flags, float* out);
 }
 
 // skimage: C1 = (K1 * R) ** 2, C2 = (K2 * R) ** 2 with R = data_range = 255
@@ -481,7 +481,8 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
       return fail(JDS_ENOMEM, "host allocation failed");
     }
     for (int i = 0; i < n; ++i) fast_fwd16_thresholds(params[i].qtable, mode, pf, params[i].gauss, h16 + fqs * i);
-    const float gk32[3] = {(float)params[0].gauss[0], (float)params[0].gauss[1], (float)params[0].gauss[2]};
+    float gk32[5];  // taps + the combined taps of k_fwd16f's fast staging
+    combined_taps32(params[0].gauss, gk32);
     const size_t nblk = (size_t)n * (size_t)(g.cpf / 256);
     if ((e = p->planes.ensure(mode == JDS_SS_444 ? sizeof(double) * 2 * (size_t)n * g.hc * g.wc : 8)) !=
             hipSuccess ||
@@ -1110,7 +1111,7 @@ int jds_selftest_fwd32(int32_t subsampling, int32_t prefilter, const double* gau
   double E[128];
   fast_fwd_bounds(subsampling, pf, gauss, E);
   memcpy(bound, E + (plane ? 64 : 0), 64 * sizeof(double));
-  if (fwd32_host_plane(subsampling, pf, gauss, rgb, (int)H, (int)W, plane, rows_first != 0, coeffs))
+  if (fwd32_host_plane(subsampling, pf, gauss, rgb, (int)H, (int)W, plane, rows_first, coeffs))
     return fail(JDS_EINVAL, "plane size must be a multiple of 8");
   return JDS_OK;
 }
@@ -1124,7 +1125,7 @@ int jds_selftest_fwd16(int32_t subsampling, int32_t prefilter, const double* gau
   double E[512];
   fast_fwd16_bounds(subsampling, pf, gauss, E);
   memcpy(bound, E + (plane ? 256 : 0), 256 * sizeof(double));
-  if (fwd16_host_plane(subsampling, pf, gauss, rgb, (int)H, (int)W, plane, rows_first != 0, coeffs))
+  if (fwd16_host_plane(subsampling, pf, gauss, rgb, (int)H, (int)W, plane, rows_first, coeffs))
     return fail(JDS_EINVAL, "plane size must be a multiple of 16");
   return JDS_OK;
 }

@@ -1550,7 +1550,9 @@ static int refl101(int i, int n) {
 }
 
 int fwd32_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
-                     bool rows_first, float* out) {
+                     int flags, float* out) {
+  // flags bit 0: rows first (k_fwd32i's order); bit 1: the combined-tap chroma chain (k_fwd32i)
+  const bool rows_first = (flags & 1) != 0, comb = (flags & 2) != 0;
   const int sy = mode == M420 ? 2 : 1, sx = mode == M444 ? 1 : 2;
   const int ph = plane == 0 ? H : H / sy, pw = plane == 0 ? W : W / sx;
   if (ph % 8 || pw % 8) return -1;
@@ -1574,7 +1576,7 @@ int fwd32_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, in
   auto sample = [&](int y, int x) -> float {  // plane sample (y, x), level-shifted
     if (plane == 0) return luma32m(px(y, x, 0), px(y, x, 1), px(y, x, 2));
     if (mode == M444) return chroma(y, x) - 128.0f;
-    if (pf && rows_first) {  // k_fwd32i
+    if (pf && comb) {  // k_fwd32i
       if (sy == 2) {
         const float r0 = pairf(refl101(2 * y - 1, H), x), r1 = pairf(2 * y, x), r2 = pairf(2 * y + 1, x),
                     r3 = pairf(refl101(2 * y + 2, H), x);

@@ -182,6 +182,7 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   constexpr int PLANE_D = CPLANE ? 2 * WN : 0;
   constexpr int BLK_D = C::NB * BS16F;
   constexpr int U_D = PLANE_D > BLK_D ? PLANE_D : BLK_D;
+  constexpr int HW = C::TW / 2;  // pair sums per window row (fast staging path)
 
   __shared__ __attribute__((aligned(16))) uint32_t s_rgb[WN];  // 16-B aligned: the tables' float4s alias it
   __shared__ __attribute__((aligned(16))) float s_u[U_D];
@@ -295,15 +296,25 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
           rb = edge ? cb[14] : cb32(R, G, B);
           rr = edge ? cr[14] : cr32(R, G, B);
         }
+        // the Gaussian row pass and the area's horizontal pair sum as one chain
+        // (k_fwd32i's combined taps, fwd_input_error): TW / 2 pair sums per row
         float* s_cb = s_u;
-        float* s_cr = s_u + WN;
+        float* s_cr = s_u + WR * HW;
+        const float h1 = gk32[3], h2 = gk32[4];
+        float ob[8], orr[8];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float bl = j == 0 ? lb : cb[j - 1], br = j == 15 ? rb : cb[j + 1];
-          const float ql = j == 0 ? lr : cr[j - 1], qr = j == 15 ? rr : cr[j + 1];
-          s_cb[cidx(r, 1 + 16 * c + j)] = fmaf(k2, br, fmaf(k1, cb[j], k0 * bl));  // the row chain
-          s_cr[cidx(r, 1 + 16 * c + j)] = fmaf(k2, qr, fmaf(k1, cr[j], k0 * ql));
+        for (int j = 0; j < 8; ++j) {
+          const float bl = j == 0 ? lb : cb[2 * j - 1], br = j == 7 ? rb : cb[2 * j + 2];
+          const float ql = j == 0 ? lr : cr[2 * j - 1], qr = j == 7 ? rr : cr[2 * j + 2];
+          ob[j] = fmaf(k2, br, fmaf(h2, cb[2 * j + 1], fmaf(h1, cb[2 * j], k0 * bl)));
+          orr[j] = fmaf(k2, qr, fmaf(h2, cr[2 * j + 1], fmaf(h1, cr[2 * j], k0 * ql)));
         }
+        float4* db = reinterpret_cast<float4*>(s_cb + r * HW + 8 * c);
+        float4* dr = reinterpret_cast<float4*>(s_cr + r * HW + 8 * c);
+        db[0] = make_float4(ob[0], ob[1], ob[2], ob[3]);
+        db[1] = make_float4(ob[4], ob[5], ob[6], ob[7]);
+        dr[0] = make_float4(orr[0], orr[1], orr[2], orr[3]);
+        dr[1] = make_float4(orr[4], orr[5], orr[6], orr[7]);
       }
     }
     __syncthreads();
@@ -404,6 +415,20 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
         float R, G, B;
         rgbf(s_rgb[sy * WC + sx], R, G, B);
         v[i] = plane == 0 ? luma32m(R, G, B) : (plane == 1 ? cb32(R, G, B) : cr32(R, G, B)) - 128.0f;
+      }
+    } else if (CPLANE && INT) {
+      // pair sums of window rows 2r-1 .. 2r+2 (4:2:0: the combined taps, *0.25)
+      // or r-1 .. r+1 (4:2:2: the Gaussian's column form, *0.5) of sample row r
+      const float* s_pl = s_u + (plane == 1 ? 0 : WR * HW) + (gx * 16 + line - x0 / C::SX);
+      const float h1 = gk32[3], h2 = gk32[4];
+#pragma unroll 4
+      for (int i = 0; i < 16; ++i) {
+        const int wr0 = C::SY * (gy * 16 + i) - y0 + 1;  // window row of the sample's first pixel row
+        const float* col = s_pl + wr0 * HW;
+        if constexpr (C::SY == 2)
+          v[i] = fmaf(k2, col[2 * HW], fmaf(h2, col[HW], fmaf(h1, col[0], k0 * col[-HW]))) * 0.25f - 128.0f;
+        else
+          v[i] = fmaf(k0, col[HW] + col[-HW], k1 * col[0]) * 0.5f - 128.0f;
       }
     } else {
       // INTER_AREA mean of the (prefiltered) full-resolution chroma
@@ -948,8 +973,10 @@ size_t fast_q16_size() { return sizeof(FastQ16); }
 // Test-only: the fp32 chain of k_fwd16f for every 16x16 block of one plane of
 // an H x W RGB image (plane size a multiple of 16), in either pass order
 // (rows_first 0 = the kernel's columns first), before quantisation.
+void combined_taps32(const double* gk, float* out5);
 int fwd16_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
-                     bool rows_first, float* out) {
+                     int flags, float* out) {
+  const bool rows_first = (flags & 1) != 0, comb = (flags & 2) != 0;  // comb: k_fwd16f's fast staging
   const int sy = mode == M420 ? 2 : 1, sx = mode == M444 ? 1 : 2;
   const int ph = plane == 0 ? H : H / sy, pw = plane == 0 ? W : W / sx;
   if (ph % 16 || pw % 16) return -1;
@@ -967,9 +994,22 @@ int fwd16_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, in
   auto rowf = [&](int y, int x) {
     return fmaf(k2, chroma(y, refl(x + 1, W)), fmaf(k1, chroma(y, x), k0 * chroma(y, refl(x - 1, W))));
   };
+  float h[5];
+  combined_taps32(gk, h);
+  auto pairf = [&](int y, int j) {  // combined taps over chroma columns 2j-1 .. 2j+2 of row y
+    return fmaf(h[2], chroma(y, refl(2 * j + 2, W)),
+                fmaf(h[4], chroma(y, 2 * j + 1), fmaf(h[3], chroma(y, 2 * j), h[0] * chroma(y, refl(2 * j - 1, W)))));
+  };
   auto sample = [&](int y, int x) -> float {
     if (plane == 0) return luma32m(px(y, x, 0), px(y, x, 1), px(y, x, 2));
     if (mode == M444) return chroma(y, x) - 128.0f;
+    if (pf && comb) {
+      if (sy == 2)
+        return fmaf(h[2], pairf(refl(2 * y + 2, H), x),
+                    fmaf(h[4], pairf(2 * y + 1, x), fmaf(h[3], pairf(2 * y, x), h[0] * pairf(refl(2 * y - 1, H), x)))) *
+                   0.25f - 128.0f;
+      return fmaf(k0, pairf(refl(y + 1, H), x) + pairf(refl(y - 1, H), x), k1 * pairf(y, x)) * 0.5f - 128.0f;
+    }
     float s[2][2];
     for (int a = 0; a < sy; ++a)
       for (int b = 0; b < 2; ++b) {

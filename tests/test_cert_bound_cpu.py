@@ -94,7 +94,7 @@ def test_fp32_forward_error_within_certified_bound(L, mode, pf, bs):
         planes = _exact_planes(img, mode, pf)
         for plane in range(3):
             exact = cpu_ref.encode_blocks(cpu_ref.split_blocks(planes[plane], bs)).reshape(-1, bs * bs)
-            for rows_first in (1, 0):
+            for rows_first in (1, 0, 3, 2):  # bit 0: pass order, bit 1: combined-tap chroma chain
                 c32 = np.empty(exact.shape, np.float32)
                 bound = np.empty(bs * bs, np.float64)
                 rc = getattr(L, BLOCKS[bs])(code, int(pf), gk.ctypes.data, img.ctypes.data, img.shape[0],
