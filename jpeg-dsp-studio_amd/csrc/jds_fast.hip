@@ -458,18 +458,22 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
       }
     }
     __syncthreads();
-    constexpr int NRP = WR * (WC - 2);
+    // k_fwd32i's combined taps: the Gaussian row pass and the area's pair sum
+    // in one chain, H_j over window columns 2j .. 2j+3 (pixels 2j-1 .. 2j+2 of
+    // the tile), into rows of TW / 2 at the start of the planes' space
+    constexpr int NRP = WR * (C::TW / 2);
     constexpr int PER = (NRP + C::TF - 1) / C::TF;
+    const float h1 = gk32[3], h2 = gk32[4];
     float tb[PER], tr[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int i = tid + j * C::TF;
       if (i < NRP) {
-        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
+        const int r = i / (C::TW / 2), c = 2 * (i - r * (C::TW / 2));
         const float* b = s_cb + r * WC + c;
         const float* q = s_cr + r * WC + c;
-        tb[j] = fmaf(k2, b[1], fmaf(k1, b[0], k0 * b[-1]));
-        tr[j] = fmaf(k2, q[1], fmaf(k1, q[0], k0 * q[-1]));
+        tb[j] = fmaf(k2, b[3], fmaf(h2, b[2], fmaf(h1, b[1], k0 * b[0])));
+        tr[j] = fmaf(k2, q[3], fmaf(h2, q[2], fmaf(h1, q[1], k0 * q[0])));
       }
     }
     __syncthreads();
@@ -477,9 +481,8 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
     for (int j = 0; j < PER; ++j) {
       const int i = tid + j * C::TF;
       if (i < NRP) {
-        const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
-        s_cb[r * WC + c] = tb[j];
-        s_cr[r * WC + c] = tr[j];
+        s_cb[i] = tb[j];
+        s_cr[i] = tr[j];
       }
     }
     __syncthreads();
@@ -496,6 +499,21 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
         unpack32(s_rgb[sy * WC + sx], R, G, B);
         v[i] = (plane == 0 ? luma32(R, G, B) : (plane == 1 ? cb32(R, G, B) : cr32(R, G, B))) - 128.0f;
       }
+    } else if constexpr (CPLANE) {
+      // pair sums of the sample's column on window rows (pixel row + 1)
+      // 2r .. 2r+3 (4:2:0: combined taps, *0.25) or r .. r+2 (4:2:2: the
+      // Gaussian's column form, *0.5), np.pad samples by reflected index
+      constexpr int HW = C::TW / 2;
+      const float* s_pl = s_u + (plane == 1 ? 0 : WN) + (reflect_pad(gx * 8 + line, g.wc) - x0 / C::SX);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int wr0 = C::SY * reflect_pad(gy * 8 + i, g.hc) - y0 + 1;  // window row of the first pixel row
+        const float* col = s_pl + wr0 * HW;
+        if constexpr (C::SY == 2)
+          v[i] = fmaf(k2, col[2 * HW], fmaf(gk32[4], col[HW], fmaf(gk32[3], col[0], k0 * col[-HW]))) * 0.25f - 128.0f;
+        else
+          v[i] = fmaf(k0, col[HW] + col[-HW], k1 * col[0]) * 0.5f - 128.0f;
+      }
     } else {
       const float* s_pl = s_u + (plane == 1 ? 0 : WN);
       const int sc = reflect_pad(gx * 8 + line, g.wc);
@@ -510,9 +528,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
             const int w = (wr0 + a) * WC + wc0 + b;
-            if constexpr (CPLANE) {
-              s[a][b] = fmaf(k0, s_pl[w + WC] + s_pl[w - WC], k1 * s_pl[w]);
-            } else {
+            {  // unfiltered chroma
               float R, G, B;
               unpack32(s_rgb[w], R, G, B);
               s[a][b] = plane == 1 ? cb32(R, G, B) : cr32(R, G, B);
@@ -1454,7 +1470,7 @@ static double combined_chain_error(const double* gk, double X, double e) {
   return sh * e + dh * X + u * X * P + 1e-12;
 }
 
-double fwd_input_error(int plane, int mode, bool pf, const double* gk) {
+double fwd_input_error(int plane, int mode, bool pf, const double* gk, int chains) {
   const double u = 0x1p-24;
   // luma32: fmaf(kb, B, fmaf(kg, G, kr*R)); constants in fp32; then -128
   const double dkl = fabs((double)0.299f - 0.299) + fabs((double)0.587f - 0.587) + fabs((double)0.114f - 0.114);
@@ -1473,7 +1489,8 @@ double fwd_input_error(int plane, int mode, bool pf, const double* gk) {
     const double er = (k0f + k1f + k2f) * e + dk * 256 + u * 256 * (k0 + (k0 + k1) + 1.0) + 1e-12;
     // column: fmaf(k0, T+1 + T-1, k1*T0)
     e = (k1f + 2 * k0f) * er + dk * 512 + u * (512 + k1 * 256 + 256) + 1e-12;
-    // k_fwd32i: horizontal pair sums H = combined chain over 4 chroma samples
+    // k_fwd32i, k_fwd32 and k_fwd16f's fast staging: horizontal pair sums H =
+    // combined chain over 4 chroma samples
     // (|H| <= 512), then 4:2:0: the combined chain down 4 rows of H (|.| <= 1024)
     // and *0.25 (exact); 4:2:2: the column form over H (magnitudes doubled) and
     // *0.5 (exact)
@@ -1485,7 +1502,8 @@ double fwd_input_error(int plane, int mode, bool pf, const double* gk) {
   }
   if (mode == M420) e = e + u * (512 + 768 + 1024) / 4;  // ((a+b)+c)+d, *0.25 exact
   if (mode == M422) e = e + u * 512 / 2;                  // (a+b), *0.5 exact
-  if (e_comb > e) e = e_comb;                             // the bound covers both chains
+  // the bound covers the chains named (8x8: combined taps only; 16x16: both)
+  if (mode != M444 && pf) e = (chains & 1) ? ((chains & 2) && e_comb > e ? e_comb : e) : e_comb;
   return e + u * 128;                                     // -128
 }
 
@@ -1499,7 +1517,7 @@ void fast_fwd_bounds(int mode, bool pf, const double* gk, double* E) {
       {FW[6][0], FW[6][1], FW[6][2], FW[6][3]}, {FW[7][0], FW[7][1], FW[7][2], FW[7][3]},
   };
   for (int p = 0; p < 2; ++p) {
-    const double e_in = fwd_input_error(p, mode, pf, gk);
+    const double e_in = fwd_input_error(p, mode, pf, gk, 2);  // k_fwd32i and k_fwd32: combined taps
     double X1[8], e1[8];
     pass_bound(128.0, e_in, nullptr, nullptr, X1, e1, W);
     double E2[8][8];  // [first-pass frequency][second-pass frequency]

@@ -103,6 +103,8 @@ __device__ __forceinline__ void row_sums4(unsigned (&v)[4]) {
 void pass_bound(double X, double e, const double* Xin, const double* ein, double* Xout, double* eout,
                 const double W[8][4]);
 // |x_fp32 - x_exact| bound of the level-shifted samples entering the DCT.
-double fwd_input_error(int plane, int mode, bool pf, const double* gk);
+// chains (prefiltered chroma): bit 0 the per-pixel Gaussian then area chain,
+// bit 1 the combined taps; the bound covers every chain named
+double fwd_input_error(int plane, int mode, bool pf, const double* gk, int chains = 3);
 
 }  // namespace jds
