@@ -158,19 +158,22 @@ __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int 
   }
 }
 
-// Byte and certificate of one output value v in one fp64 add: y = v + 1.5 * 2^20
+// Byte and certificate of one output value v from y = v + 1.5 * 2^20
 // has a fixed exponent for |v| < 2^19, so its high word is 0x41380000 +
 // floor(v') and its low word is frac(v') * 2^32, where v' = y - 1.5 * 2^20 is v
 // rounded to a multiple of 2^-32 (|v' - v| <= 2^-33, added to the bound).
 // med3 of the high word against [0x41380000, 0x413800FF] leaves
 // clamp(floor(v'), 0, 255) in its low byte (the reference's clip +
 // astype(uint8), pipeline.py:95); the smallest and largest low words seen
-// tell how close any value came to an integer.
+// tell how close any value came to an integer.  The colour terms add onto
+// Y + MAGIC (one add per pixel instead of one per channel): each of the <= 3
+// roundings on the way (Y + MAGIC, then one or two fmas) lands on the same
+// 2^-32 grid, |error| <= 2^-33 each, so the certificate adds 2^-31 (the
+// colour fma's own rounding stays in K_CONST, now an over-estimate).
 constexpr double MAGIC = 0x1.8p+20;
 constexpr uint32_t MAGIC_HI = 0x41380000u;
 
-__device__ __forceinline__ uint32_t byte_cert(double v, uint32_t& lo_min, uint32_t& lo_max) {
-  const double y = v + MAGIC;
+__device__ __forceinline__ uint32_t byte_cert_y(double y, uint32_t& lo_min, uint32_t& lo_max) {
   const uint32_t lo = (uint32_t)__double2loint(y), hi = (uint32_t)__double2hiint(y);
   lo_min = lo_min < lo ? lo_min : lo;
   lo_max = lo_max > lo ? lo_max : lo;
@@ -321,17 +324,18 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
         chroma8_fast<MODE>(s_cw[0], x0, cwx0, wq, wt, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
+          Yv[k] = Yv[k] + MAGIC;  // (byte_cert_y's grid, shared by the three channels)
           const double B = Yv[k] + C[k] * 1.772;
           Gt[k] = Yv[k] + C[k] * -0.344136;
-          cb[3 * k + 2] = byte_cert(B, lo_min, lo_max);
+          cb[3 * k + 2] = byte_cert_y(B, lo_min, lo_max);
         }
         chroma8_fast<MODE>(s_cw[1], x0, cwx0, wq, wt, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const double R = Yv[k] + C[k] * 1.402;
           const double G = Gt[k] + C[k] * -0.714136;
-          cb[3 * k] = byte_cert(R, lo_min, lo_max);
-          cb[3 * k + 1] = byte_cert(G, lo_min, lo_max);
+          cb[3 * k] = byte_cert_y(R, lo_min, lo_max);
+          cb[3 * k + 1] = byte_cert_y(G, lo_min, lo_max);
         }
 #pragma unroll
         for (int w = 0; w < 6; ++w) pk[w] = pack4(cb[4 * w], cb[4 * w + 1], cb[4 * w + 2], cb[4 * w + 3]);
@@ -418,8 +422,9 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       mx = mx > s_lmax[i] ? mx : s_lmax[i];
       q = fmax(q, s_dq[i]);
     }
-    // |v_fast - v_ref| <= E, plus the magic add's rounding (2^-33); T in units of 2^-32
-    const double E = K_LIN * (q * s_qmax) + K_CONST + 0x1p-33;
+    // |v_fast - v_ref| <= E, plus <= 3 roundings on the magic grid (2^-33 each:
+    // byte_cert); T in units of 2^-32
+    const double E = K_LIN * (q * s_qmax) + K_CONST + 0x1p-31;
     const double T = ceil(E * 0x1p+32) + 1.0;
     const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
     sh.redo = uncertain || fix_all;
