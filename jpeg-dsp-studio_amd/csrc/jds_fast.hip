@@ -1489,7 +1489,7 @@ double fwd_input_error(int plane, int mode, bool pf, const double* gk, int chain
     const double er = (k0f + k1f + k2f) * e + dk * 256 + u * 256 * (k0 + (k0 + k1) + 1.0) + 1e-12;
     // column: fmaf(k0, T+1 + T-1, k1*T0)
     e = (k1f + 2 * k0f) * er + dk * 512 + u * (512 + k1 * 256 + 256) + 1e-12;
-    // k_fwd32i, k_fwd32 and k_fwd16f's fast staging: horizontal pair sums H =
+    // k_fwd32i, k_fwd32 and k_fwd16f: horizontal pair sums H =
     // combined chain over 4 chroma samples
     // (|H| <= 512), then 4:2:0: the combined chain down 4 rows of H (|.| <= 1024)
     // and *0.25 (exact); 4:2:2: the column form over H (magnitudes doubled) and
@@ -1502,7 +1502,8 @@ double fwd_input_error(int plane, int mode, bool pf, const double* gk, int chain
   }
   if (mode == M420) e = e + u * (512 + 768 + 1024) / 4;  // ((a+b)+c)+d, *0.25 exact
   if (mode == M422) e = e + u * 512 / 2;                  // (a+b), *0.5 exact
-  // the bound covers the chains named (8x8: combined taps only; 16x16: both)
+  // the bound covers the chains named (every certified forward kernel now
+  // uses the combined taps: callers pass 2)
   if (mode != M444 && pf) e = (chains & 1) ? ((chains & 2) && e_comb > e ? e_comb : e) : e_comb;
   return e + u * 128;                                     // -128
 }

@@ -355,17 +355,20 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
         }
       }
       __syncthreads();
-      constexpr int NRP = WR * (WC - 2);
+      // the combined-tap pair sums of the fast path (window columns 2j .. 2j+3),
+      // same layout: rows of HW at the start of each plane's space
+      constexpr int NRP = WR * HW;
       constexpr int PER = (NRP + C::TF - 1) / C::TF;
+      const float h1 = gk32[3], h2 = gk32[4];
       float tb[PER], tr[PER];
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
         const int i = tid + j * C::TF;
         if (i < NRP) {
-          const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
-          const int il = cidx(r, c - 1), i0 = cidx(r, c), ir = cidx(r, c + 1);
-          tb[j] = fmaf(k2, s_cb[ir], fmaf(k1, s_cb[i0], k0 * s_cb[il]));  // the 8x8 kernels' row chain
-          tr[j] = fmaf(k2, s_cr[ir], fmaf(k1, s_cr[i0], k0 * s_cr[il]));
+          const int r = i / HW, c = 2 * (i - r * HW);
+          const int i0 = cidx(r, c), i1 = cidx(r, c + 1), i2 = cidx(r, c + 2), i3 = cidx(r, c + 3);
+          tb[j] = fmaf(k2, s_cb[i3], fmaf(h2, s_cb[i2], fmaf(h1, s_cb[i1], k0 * s_cb[i0])));
+          tr[j] = fmaf(k2, s_cr[i3], fmaf(h2, s_cr[i2], fmaf(h1, s_cr[i1], k0 * s_cr[i0])));
         }
       }
       __syncthreads();
@@ -373,9 +376,8 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       for (int j = 0; j < PER; ++j) {
         const int i = tid + j * C::TF;
         if (i < NRP) {
-          const int r = i / (WC - 2), c = i - r * (WC - 2) + 1;
-          s_cb[cidx(r, c)] = tb[j];
-          s_cr[cidx(r, c)] = tr[j];
+          s_u[i] = tb[j];
+          s_u[WR * HW + i] = tr[j];
         }
       }
       __syncthreads();
@@ -416,14 +418,17 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
         rgbf(s_rgb[sy * WC + sx], R, G, B);
         v[i] = plane == 0 ? luma32m(R, G, B) : (plane == 1 ? cb32(R, G, B) : cr32(R, G, B)) - 128.0f;
       }
-    } else if (CPLANE && INT) {
+    } else if (CPLANE) {
       // pair sums of window rows 2r-1 .. 2r+2 (4:2:0: the combined taps, *0.25)
       // or r-1 .. r+1 (4:2:2: the Gaussian's column form, *0.5) of sample row r
-      const float* s_pl = s_u + (plane == 1 ? 0 : WR * HW) + (gx * 16 + line - x0 / C::SX);
+      // (np.pad samples by reflected index off the fast staging path)
+      const int sc = INT ? gx * 16 + line : reflect_pad(gx * 16 + line, g.wc);
+      const float* s_pl = s_u + (plane == 1 ? 0 : WR * HW) + (sc - x0 / C::SX);
       const float h1 = gk32[3], h2 = gk32[4];
 #pragma unroll 4
       for (int i = 0; i < 16; ++i) {
-        const int wr0 = C::SY * (gy * 16 + i) - y0 + 1;  // window row of the sample's first pixel row
+        const int sr = INT ? gy * 16 + i : reflect_pad(gy * 16 + i, g.hc);
+        const int wr0 = C::SY * sr - y0 + 1;  // window row of the sample's first pixel row
         const float* col = s_pl + wr0 * HW;
         if constexpr (C::SY == 2)
           v[i] = fmaf(k2, col[2 * HW], fmaf(h2, col[HW], fmaf(h1, col[0], k0 * col[-HW]))) * 0.25f - 128.0f;
@@ -431,8 +436,7 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
           v[i] = fmaf(k0, col[HW] + col[-HW], k1 * col[0]) * 0.5f - 128.0f;
       }
     } else {
-      // INTER_AREA mean of the (prefiltered) full-resolution chroma
-      const float* s_pl = s_u + (plane == 1 ? 0 : WN);
+      // INTER_AREA mean of the unfiltered full-resolution chroma
       const int sc = INT ? gx * 16 + line : reflect_pad(gx * 16 + line, g.wc);
       const int wc0 = C::SX * sc - x0 + 1;
 #pragma unroll 4  // full unrolling (window rows reused across samples) costs 20-50 VGPRs: occupancy 5 -> 3-4
@@ -443,15 +447,10 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 #pragma unroll
         for (int a = 0; a < C::SY; ++a) {
 #pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            if constexpr (CPLANE) {
-              const int w = cidx(wr0 + a, wc0 + b);
-              s[a][b] = fmaf(k0, s_pl[w + WC] + s_pl[w - WC], k1 * s_pl[w]);  // the 8x8 kernels' column chain
-            } else {
-              float R, G, B;
-              rgbf(s_rgb[(wr0 + a) * WC + wc0 + b], R, G, B);
-              s[a][b] = plane == 1 ? cb32(R, G, B) : cr32(R, G, B);
-            }
+          for (int b = 0; b < 2; ++b) {  // unfiltered chroma
+            float R, G, B;
+            rgbf(s_rgb[(wr0 + a) * WC + wc0 + b], R, G, B);
+            s[a][b] = plane == 1 ? cb32(R, G, B) : cr32(R, G, B);
           }
         }
         if constexpr (C::SY == 2)
@@ -934,7 +933,7 @@ static void pass_bound16(double X, double e, double* Xout, double* eout) {
 
 void fast_fwd16_bounds(int mode, bool pf, const double* gk, double* E /*2 x 256*/) {
   for (int p = 0; p < 2; ++p) {
-    const double e_in = fwd_input_error(p, mode, pf, gk);
+    const double e_in = fwd_input_error(p, mode, pf, gk, 2);  // both staging paths: combined taps
     double X1[16], e1[16];
     pass_bound16(128.0, e_in, X1, e1);
     double E2[16][16];

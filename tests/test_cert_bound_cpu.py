@@ -94,9 +94,9 @@ def test_fp32_forward_error_within_certified_bound(L, mode, pf, bs):
         planes = _exact_planes(img, mode, pf)
         for plane in range(3):
             exact = cpu_ref.encode_blocks(cpu_ref.split_blocks(planes[plane], bs)).reshape(-1, bs * bs)
-            # bit 0: pass order, bit 1: combined-tap chroma chain (both 8x8 kernels use
-            # it and their bound covers it alone; 16x16's bound covers both chains)
-            for rows_first in ((3, 2) if bs == 8 else (1, 0, 3, 2)):
+            # bit 0: pass order, bit 1: the combined-tap chroma chain (every certified
+            # forward kernel uses it; the bounds cover it alone)
+            for rows_first in (3, 2):
                 c32 = np.empty(exact.shape, np.float32)
                 bound = np.empty(bs * bs, np.float64)
                 rc = getattr(L, BLOCKS[bs])(code, int(pf), gk.ctypes.data, img.ctypes.data, img.shape[0],
