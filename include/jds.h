@@ -230,7 +230,8 @@ int jds_selftest_dct16x16(const double* in, double* out, int64_t n, int32_t inve
  * block of one plane (0 Y, 1 Cb, 2 Cr) of an H x W RGB image whose plane size is
  * a multiple of 8.  rows_first bit 0: pass order (1 = k_fwd32i's rows first,
  * 0 = k_fwd32's columns first); bit 1: prefiltered chroma through the combined
- * Gaussian + area taps (k_fwd32i) instead of the per-pixel chains (k_fwd32);
+ * Gaussian + area taps (what every certified forward kernel computes; 0 = the
+ * per-pixel Gaussian then area chains, an fp32 restatement kept for comparison);
  * coefficients before quantisation (n_blocks x 64 f32, raster block order);
  * bound[64] = the rigorous bound on |c_fp32 - c_exact| the kernels certify
  * with (fast_fwd_bounds).  Lets the CPU suite test the bound adversarially. */
@@ -238,7 +239,7 @@ int jds_selftest_fwd32(int32_t subsampling, int32_t prefilter, const double* gau
                        int64_t W, int32_t plane, int32_t rows_first, float* coeffs, double* bound);
 /* The same for the certified 16x16 forward (jds_fast16.hip: fdct16_f32, plane
  * size a multiple of 16; rows_first bit 0 as above, 0 = k_fwd16f's order; bit 1:
- * the combined taps of k_fwd16f's fast staging path): n_blocks x 256 f32
+ * the combined taps, as k_fwd16f computes them): n_blocks x 256 f32
  * coefficients and bound[256] (fast_fwd16_bounds). */
 int jds_selftest_fwd16(int32_t subsampling, int32_t prefilter, const double* gauss, const uint8_t* rgb, int64_t H,
                        int64_t W, int32_t plane, int32_t rows_first, float* coeffs, double* bound);
