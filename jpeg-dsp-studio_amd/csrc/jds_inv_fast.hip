@@ -109,7 +109,11 @@ __device__ __forceinline__ void fast_col(const Col16& in, const double* __restri
   for (int r = 0; r < 8; ++r) dst[tslot(r, v)] = c[r];
 }
 
-// Axis-1 pass of row u, clip to [0, 255] (dct_engine.py:27).
+// Axis-1 pass of row u, clip to [LO, LO + 255] (dct_engine.py:27; chroma runs
+// without the +128 and clips to [-128, 127]: the window's shifted samples
+// directly, clip(x + 128, 0, 255) - 128 = clip(x, -128, 127) with one rounding
+// fewer, inside tools/inv_bound.py's model of the shifted form).
+template <int LO = 0>
 __device__ __forceinline__ void fast_row(const double* __restrict__ src, int u, double (&c)[8]) {
   const int sw = u & 3;
 #pragma unroll
@@ -120,7 +124,7 @@ __device__ __forceinline__ void fast_row(const double* __restrict__ src, int u, 
   }
   aan8(c);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) c[k] = fmin(fmax(c[k], 0.0), 255.0);
+  for (int k = 0; k < 8; ++k) c[k] = fmin(fmax(c[k], (double)LO), (double)(LO + 255));
 }
 
 // One plane's upsampled (chroma - 128) at the lane's 8 pixels (cv2
@@ -251,24 +255,24 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       const Col16 cur = cq;
       if (p == 0) cq = load_col(cf + g.off_cr, boff, lv, bvalid);
       if (bvalid) {
-        fast_col(cur, s_qs, lv, dc_add, s_mid + lb * MS, dq);
+        fast_col(cur, s_qs, lv, 0.0, s_mid + lb * MS, dq);  // (chroma: no +128, see fast_row)
         if (need) {
           double c[8];
-          fast_row(s_mid + lb * MS, lv, c);
+          fast_row<-128>(s_mid + lb * MS, lv, c);
           double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWC];
           const int wc0 = bx * 8 - cwx0;
 #pragma unroll
           for (int k = 0; k < 8; ++k)
-            if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k] - 128.0;
+            if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k];
           if constexpr (I::SX == 2) {
             // cv2's clamped taps at the image's left / right edge pixels read the
             // edge column alone: replicate it into the ring (and past the
             // plane's right end, where pixels beyond the image read too)
-            if (bx == 0 && wc0 >= 1) w[wc0 - 1] = c[0] - 128.0;
+            if (bx == 0 && wc0 >= 1) w[wc0 - 1] = c[0];
             const int ke = g.wc - 1 - bx * 8;
             if ((unsigned)ke < 8u) {
               const double e = (ke == 0 ? c[0] : ke == 1 ? c[1] : ke == 2 ? c[2] : ke == 3 ? c[3]
-                                : ke == 4 ? c[4] : ke == 5 ? c[5] : ke == 6 ? c[6] : c[7]) - 128.0;
+                                : ke == 4 ? c[4] : ke == 5 ? c[5] : ke == 6 ? c[6] : c[7]);
               for (int col = wc0 + ke + 1; col < I::CWC; ++col) w[col] = e;
             }
           }
