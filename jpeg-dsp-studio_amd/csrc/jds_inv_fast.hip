@@ -93,14 +93,16 @@ __device__ __forceinline__ void aan8(double (&v)[8]) {
 
 // Axis-0 pass of column v of one block: dequantise with the folded table
 // (DC + dc_add: 128 on column 0, 0 elsewhere), AAN, into the transpose buffer.
-// dq tracks max |q| of the column.
+// qhi / qlo track the largest and smallest q the lane read (integer max3 /
+// min3 chains: cheaper than an fp64 max of |q| per coefficient).
 __device__ __forceinline__ void fast_col(const Col16& in, const double* __restrict__ qs, int v, double dc_add,
-                                         double* __restrict__ dst, double& dq) {
+                                         double* __restrict__ dst, int& qhi, int& qlo) {
   double c[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const double qd = (double)in.q[r];
-    dq = fmax(dq, fabs(qd));
+    qhi = max(qhi, (int)in.q[r]);
+    qlo = min(qlo, (int)in.q[r]);
     c[r] = qd * qs[r * 8 + v];
   }
   c[0] = c[0] + dc_add;
@@ -224,7 +226,7 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   if (XTRA && tid == 0) s_sse = 0ull;
   __syncthreads();
 
-  double dq = 0.0;  // max |q| this lane read
+  int qhi = 0, qlo = 0;  // max / min q this lane read (max |q| = max(qhi, -qlo))
   const double dc_add = lv == 0 ? 128.0 : 0.0;
 
   // ---- 1. chroma window: (clip(IDCT) - 128) of the blocks the tile reaches --
@@ -255,7 +257,7 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       const Col16 cur = cq;
       if (p == 0) cq = load_col(cf + g.off_cr, boff, lv, bvalid);
       if (bvalid) {
-        fast_col(cur, s_qs, lv, 0.0, s_mid + lb * MS, dq);  // (chroma: no +128, see fast_row)
+        fast_col(cur, s_qs, lv, 0.0, s_mid + lb * MS, qhi, qlo);  // (chroma: no +128, see fast_row)
         if (need) {
           double c[8];
           fast_row<-128>(s_mid + lb * MS, lv, c);
@@ -302,7 +304,7 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       const bool ok1 = luma_blk(r + 1, by1, bx1);
       lq = load_col(cf, ((long long)by1 * g.nbx + bx1) * 64, lv, ok1);
     }
-    if (bvalid) fast_col(cur, s_qs, lv, dc_add, s_mid + lb * MS, dq);
+    if (bvalid) fast_col(cur, s_qs, lv, dc_add, s_mid + lb * MS, qhi, qlo);
     const int y = by * 8 + lv, x0 = bx * 8;
     if (bvalid && y < g.H && x0 < g.W) {
       double Yv[8];
@@ -395,12 +397,13 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   }
 
   // ---- 3. certification: the tile's closest approach to an integer vs its bound
+  int qm = max(qhi, -qlo);  // max |q| this lane read
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t a = __shfl_xor(lo_min, o, 64), b = __shfl_xor(lo_max, o, 64);
     lo_min = lo_min < a ? lo_min : a;
     lo_max = lo_max > b ? lo_max : b;
-    dq = fmax(dq, __shfl_xor(dq, o, 64));
+    qm = max(qm, __shfl_xor(qm, o, 64));
   }
   if constexpr (XTRA > 0) {
     unsigned long long s = sse;
@@ -415,7 +418,7 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   if ((tid & 63) == 0) {
     s_lmin[tid >> 6] = lo_min;
     s_lmax[tid >> 6] = lo_max;
-    s_dq[tid >> 6] = dq;
+    s_dq[tid >> 6] = (double)qm;
   }
   __syncthreads();
   if (tid == 0) {
