@@ -91,11 +91,12 @@ __device__ __forceinline__ void aan8(double (&v)[8]) {
   v[4] = e3 - o4;
 }
 
-// Axis-0 pass of column v of one block: dequantise with the folded table
-// (DC + dc_add: 128 on column 0, 0 elsewhere), AAN, into the transpose buffer.
+// Axis-0 pass of column v of one block: dequantise with the folded table,
+// AAN, into the transpose buffer (no +128: fast_row clips to [-128, 127] and
+// the luma's +128 rides on the magic constant, see byte_cert_y).
 // qhi / qlo track the largest and smallest q the lane read (integer max3 /
 // min3 chains: cheaper than an fp64 max of |q| per coefficient).
-__device__ __forceinline__ void fast_col(const Col16& in, const double* __restrict__ qs, int v, double dc_add,
+__device__ __forceinline__ void fast_col(const Col16& in, const double* __restrict__ qs, int v,
                                          double* __restrict__ dst, int& qhi, int& qlo) {
   double c[8];
 #pragma unroll
@@ -105,16 +106,16 @@ __device__ __forceinline__ void fast_col(const Col16& in, const double* __restri
     qlo = min(qlo, (int)in.q[r]);
     c[r] = qd * qs[r * 8 + v];
   }
-  c[0] = c[0] + dc_add;
   aan8(c);
 #pragma unroll
   for (int r = 0; r < 8; ++r) dst[tslot(r, v)] = c[r];
 }
 
-// Axis-1 pass of row u, clip to [LO, LO + 255] (dct_engine.py:27; chroma runs
-// without the +128 and clips to [-128, 127]: the window's shifted samples
-// directly, clip(x + 128, 0, 255) - 128 = clip(x, -128, 127) with one rounding
-// fewer, inside tools/inv_bound.py's model of the shifted form).
+// Axis-1 pass of row u, clip to [LO, LO + 255] (dct_engine.py:27).  Both planes
+// run without the reference's +128 and clip to [-128, 127] (clip(x + 128, 0,
+// 255) - 128 = clip(x, -128, 127)): the chroma window holds the shifted samples
+// directly and the luma's +128 rides on the magic constant; fewer roundings and
+// smaller magnitudes than the +128-folded form tools/inv_bound.py models.
 template <int LO = 0>
 __device__ __forceinline__ void fast_row(const double* __restrict__ src, int u, double (&c)[8]) {
   const int sw = u & 3;
@@ -227,7 +228,6 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   __syncthreads();
 
   int qhi = 0, qlo = 0;  // max / min q this lane read (max |q| = max(qhi, -qlo))
-  const double dc_add = lv == 0 ? 128.0 : 0.0;
 
   // ---- 1. chroma window: (clip(IDCT) - 128) of the blocks the tile reaches --
   const int cby0 = Y0 / (8 * I::SY) - I::RY, cbx0 = X0 / (8 * I::SX) - I::RX;
@@ -257,7 +257,7 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       const Col16 cur = cq;
       if (p == 0) cq = load_col(cf + g.off_cr, boff, lv, bvalid);
       if (bvalid) {
-        fast_col(cur, s_qs, lv, 0.0, s_mid + lb * MS, qhi, qlo);  // (chroma: no +128, see fast_row)
+        fast_col(cur, s_qs, lv, s_mid + lb * MS, qhi, qlo);
         if (need) {
           double c[8];
           fast_row<-128>(s_mid + lb * MS, lv, c);
@@ -304,11 +304,11 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       const bool ok1 = luma_blk(r + 1, by1, bx1);
       lq = load_col(cf, ((long long)by1 * g.nbx + bx1) * 64, lv, ok1);
     }
-    if (bvalid) fast_col(cur, s_qs, lv, dc_add, s_mid + lb * MS, qhi, qlo);
+    if (bvalid) fast_col(cur, s_qs, lv, s_mid + lb * MS, qhi, qlo);
     const int y = by * 8 + lv, x0 = bx * 8;
     if (bvalid && y < g.H && x0 < g.W) {
       double Yv[8];
-      fast_row(s_mid + lb * MS, lv, Yv);
+      fast_row<-128>(s_mid + lb * MS, lv, Yv);  // Y - 128
       int wq, wt = 0;
       if constexpr (I::SY == 2) {
         // output row 2m: rows (m-1, m) weighted (1/4, 3/4); row 2m+1: (m+1, m)
@@ -330,7 +330,7 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
         chroma8_fast<MODE>(s_cw[0], x0, cwx0, wq, wt, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          Yv[k] = Yv[k] + MAGIC;  // (byte_cert_y's grid, shared by the three channels)
+          Yv[k] = Yv[k] + (MAGIC + 128.0);  // Y on byte_cert_y's grid, shared by the three channels
           const double B = Yv[k] + C[k] * 1.772;
           Gt[k] = Yv[k] + C[k] * -0.344136;
           cb[3 * k + 2] = byte_cert_y(B, lo_min, lo_max);
