@@ -244,6 +244,20 @@ int jds_selftest_fwd32(int32_t subsampling, int32_t prefilter, const double* gau
 int jds_selftest_fwd16(int32_t subsampling, int32_t prefilter, const double* gauss, const uint8_t* rgb, int64_t H,
                        int64_t W, int32_t plane, int32_t rows_first, float* coeffs, double* bound);
 
+/* Test-only: the certified fast inverse's arithmetic (jds_inv_fast.hip,
+ * k_inv_fast: folded dequantisation, AAN IDCT on both axes, clip to [-128, 127],
+ * vertical then difference-form chroma blends, colour terms on the 2^-32 magic
+ * grid) evaluated on the host with the kernel's own helpers, for an H x W image
+ * (even H at 4:2:0, even W at 4:2:x) from coefficients in the
+ * IntermediateData.all_quantized_coeffs layout and one 8x8 quant table.
+ * fuse: 0 = every multiply-add rounded twice, 1 = every one fused (the device
+ * compiler may pick either per site).  values: H*W*3 f64, the value v' the
+ * certificate judges (RGB order); bytes: H*W*3, the kernel's byte for it.
+ * Lets the CPU suite test tools/inv_bound.py's bound (K_LIN / K_CONST)
+ * adversarially against the oracle's pre-truncation values. */
+int jds_selftest_inv_fast(int32_t subsampling, const int16_t* coeffs, const double* qtable, int64_t H, int64_t W,
+                          int32_t fuse, double* values, uint8_t* bytes);
+
 /* Test-only: the host-built cv2 INTER_AREA table of one axis (OpenCV
  * computeResizeAreaTab, used by the odd-size path) for src -> dst samples:
  * per destination index its tap count n[d] (<= 4) and taps si[4d..], a[4d..].

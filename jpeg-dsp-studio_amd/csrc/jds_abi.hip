@@ -51,6 +51,7 @@ void fast_fwd_bounds(int mode, bool pf, const double* gk, double* E);
 int fwd32_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
                      int flags, float* out);
 void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
+int inv_fast_host(int mode, const int16_t* cf, const double* Q, int H, int W, int fuse, double* vout, uint8_t* bout);
 size_t fast_q_size();
 hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse, hipStream_t s);
 hipError_t stage_subsample(const double* in, double* tmp, double* tmp2, double* out, int H, int W, int sy,
@@ -1127,6 +1128,16 @@ int jds_selftest_fwd16(int32_t subsampling, int32_t prefilter, const double* gau
   memcpy(bound, E + (plane ? 256 : 0), 256 * sizeof(double));
   if (fwd16_host_plane(subsampling, pf, gauss, rgb, (int)H, (int)W, plane, rows_first, coeffs))
     return fail(JDS_EINVAL, "plane size must be a multiple of 16");
+  return JDS_OK;
+}
+
+int jds_selftest_inv_fast(int32_t subsampling, const int16_t* coeffs, const double* qtable, int64_t H, int64_t W,
+                          int32_t fuse, double* values, uint8_t* bytes) {
+  if (!coeffs || !qtable || !values || !bytes || H < 1 || W < 1 || H > 4096 || W > 4096 ||
+      subsampling < JDS_SS_444 || subsampling > JDS_SS_420)
+    return fail(JDS_EINVAL, "bad argument");
+  if (inv_fast_host(subsampling, coeffs, qtable, (int)H, (int)W, fuse, values, bytes))
+    return fail(JDS_EINVAL, "odd chroma geometry: the certified inverse runs even sizes only");
   return JDS_OK;
 }
 

@@ -8,17 +8,23 @@
 // and :63-65).  The exact kernel (jds_inv.hip, k_inv2) replays every one of
 // those roundings.  This kernel computes the same real numbers in fp64 with a
 // cheaper order:
-//   * AAN IDCT (5 multiplies per 8-point line) with the AAN scales, the 1/8
-//     normalisation and the +128 folded into the dequantisation (one fma per
-//     coefficient: q * Qs[u][v], DC + 128);
-//   * chroma shifted by -128 once per window sample, so the colour transform is
-//     one fma per channel term (R = Y + 1.402 Cr', ...);
+//   * AAN IDCT (5 multiplies per 8-point line) with the AAN scales and the 1/8
+//     normalisation folded into the dequantisation (one product per
+//     coefficient: q * Qs[u][v]), no +128: both planes clip to [-128, 127];
 //   * the bilinear upsample as a vertical blend of the lane's 6 chroma columns
-//     followed by shared 3/4 products (3 operations per pixel and plane).
+//     followed by a difference-form horizontal blend (3 operations per pixel
+//     and plane);
+//   * the colour terms added onto Y + 1.5 * 2^20 + 128 (one fma per term), so
+//     each output lands on a grid of spacing 2^-32 whose words give both the
+//     byte and the certificate (byte_cert_y).
 // Every output value v_fast then differs from v_ref by at most
-// E = K_LIN * Dmax + K_CONST, where Dmax bounds |q * Q| over the coefficients the
-// tile reads (tools/inv_bound.py derives K_LIN / K_CONST rigorously for both
-// operation orders, with every fused multiply-add counted as two roundings).
+// E = K_LIN * Dmax + K_CONST + 2^-31, where Dmax bounds |q * Q| over the
+// coefficients the tile reads and 2^-31 covers the <= 3 roundings on the grid
+// (tools/inv_bound.py derives K_LIN / K_CONST rigorously for both operation
+// orders as they stand in this file, every fused multiply-add counted as two
+// roundings; tests/test_inv_bound_cpu.py pins the constants below to it and
+// runs this file's chain on the host, jds_selftest_inv_fast, against the
+// oracle on adversarial inputs).
 // If no integer lies within E of v_fast, trunc(clip(v_fast)) ==
 // trunc(clip(v_ref)): the byte is certified.  Each lane tracks the smallest
 // distance to an integer over its samples and the largest |q|; a workgroup
@@ -36,6 +42,10 @@
 // in LDS, Y in registers, one lane per 8-pixel row, 24-byte stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+
+#include <cmath>
+#include <vector>
 
 #include "jds_device.hpp"
 #include "jds_internal.hpp"
@@ -48,38 +58,53 @@
 
 namespace jds {
 
-// tools/inv_bound.py: e_fast + e_ref <= K_LIN * Dmax + K_CONST (x2 safety included)
-constexpr double K_LIN = 1.422823e-12 * 1.01;
-constexpr double K_CONST = 3.188096e-12 * 1.01;
+// tools/inv_bound.py (the v24 chain as it stands in this file): e_fast + e_ref
+// <= K_LIN * Dmax + K_CONST off the magic grid, x2 safety included
+// (tests/test_inv_bound_cpu.py asserts kernel >= model)
+constexpr double K_LIN = 1.103043e-12 * 1.01;
+constexpr double K_CONST = 1.081459e-12 * 1.01;
 
-// AAN scale factors a_k = sqrt(2) cos(k pi / 16), a_0 = 1 (correctly rounded)
-__constant__ double c_aan[8] = {1.0,
-                                0x1.63150b15e8536p+0,
-                                0x1.4e7ae9144f0fcp+0,
-                                0x1.2d062ef88e319p+0,
-                                1.0,
-                                0x1.92469c0dcf32dp-1,
-                                0x1.1517a7bdb3895p-1,
-                                0x1.1a855dec071b5p-2};
+// AAN scale factors a_k = sqrt(2) cos(k pi / 16), a_0 = 1 (correctly rounded;
+// tools/inv_bound.py reads them from this list and prices their representation
+// errors)
+#define JDS_AAN_LIST                                                                                 \
+  1.0, 0x1.63150b15e8536p+0, 0x1.4e7ae9144f0fcp+0, 0x1.2d062ef88e319p+0, 1.0, 0x1.92469c0dcf32dp-1, \
+      0x1.1517a7bdb3895p-1, 0x1.1a855dec071b5p-2
+__constant__ double c_aan[8] = {JDS_AAN_LIST};
+static const double h_aan[8] = {JDS_AAN_LIST};  // the host restatement's copy
 constexpr double F_SQ2 = 0x1.6a09e667f3bcdp+0;   // sqrt(2)
 constexpr double F_A2C2 = 0x1.d906bcf328d46p+0;  // 2 cos(pi/8)
 constexpr double F_K10 = 0x1.1517a7bdb3895p+0;   // 2 (cos(pi/8) - cos(3pi/8))
 constexpr double F_K12 = 0x1.4e7ae9144f0fcp+1;   // 2 (cos(pi/8) + cos(3pi/8))
 
+// The chain's multiply-adds go through a policy so that the host restatement
+// (jds_selftest_inv_fast, tests/test_inv_bound_cpu.py) runs the same source:
+// on the device MadDev writes a * b + c and the compiler fuses what it likes
+// under this unit's fp contract(fast) (the bound covers either way); the host
+// runs it unfused (MadSep: x86-64 has no FMA at the default target) and fully
+// fused (MadFma: std::fma at every site).
+struct MadDev {
+  __host__ __device__ static double mad(double a, double b, double c) { return a * b + c; }
+};
+struct MadFma {
+  static double mad(double a, double b, double c) { return std::fma(a, b, c); }
+};
+
 // One 8-point AAN IDCT line on scaled inputs (inputs pre-multiplied by
 // a_u / sqrt(8) per axis; outputs are the orthonormal IDCT).  The operation
 // sequence is the one tools/inv_bound.py::aan_line models.
-__device__ __forceinline__ void aan8(double (&v)[8]) {
+template <class M = MadDev>
+__host__ __device__ __forceinline__ void aan8(double (&v)[8]) {
   const double t10 = v[0] + v[4], t11 = v[0] - v[4];
   const double t13 = v[2] + v[6];
-  const double t12 = (v[2] - v[6]) * F_SQ2 - t13;
+  const double t12 = M::mad(v[2] - v[6], F_SQ2, -t13);
   const double e0 = t10 + t13, e3 = t10 - t13, e1 = t11 + t12, e2 = t11 - t12;
   const double z13 = v[5] + v[3], z10 = v[5] - v[3], z11 = v[1] + v[7], z12 = v[1] - v[7];
   const double o7 = z11 + z13;
   const double o11 = (z11 - z13) * F_SQ2;
   const double z5 = (z10 + z12) * F_A2C2;
-  const double o10 = z5 - z12 * F_K10;
-  const double o12 = z5 - z10 * F_K12;
+  const double o10 = M::mad(-z12, F_K10, z5);
+  const double o12 = M::mad(-z10, F_K12, z5);
   const double o6 = o12 - o7, o5 = o11 - o6, o4 = o10 - o5;
   v[0] = e0 + o7;
   v[7] = e0 - o7;
@@ -90,6 +115,24 @@ __device__ __forceinline__ void aan8(double (&v)[8]) {
   v[3] = e3 + o4;
   v[4] = e3 - o4;
 }
+
+// cv2 INTER_LINEAR's blends at an exact 2x scale, in the certified order:
+// vertical a * 1/4 + b * 3/4 (a the "quarter" row), horizontal in difference
+// form near + (far - near) * (+-1/4)
+template <class M = MadDev>
+__host__ __device__ __forceinline__ double vblend(double a, double b) { return M::mad(a, 0.25, b * 0.75); }
+template <class M = MadDev>
+__host__ __device__ __forceinline__ double hblend(double d, double w, double near) { return M::mad(d, w, near); }
+
+// The colour terms onto Y + MAGIC + 128 (byte_cert_y's grid): out = B, Gt, R, G
+template <class M = MadDev>
+__host__ __device__ __forceinline__ double col_b(double yv, double cb) { return M::mad(cb, 1.772, yv); }
+template <class M = MadDev>
+__host__ __device__ __forceinline__ double col_gt(double yv, double cb) { return M::mad(cb, -0.344136, yv); }
+template <class M = MadDev>
+__host__ __device__ __forceinline__ double col_r(double yv, double cr) { return M::mad(cr, 1.402, yv); }
+template <class M = MadDev>
+__host__ __device__ __forceinline__ double col_g(double gt, double cr) { return M::mad(cr, -0.714136, gt); }
 
 // Axis-0 pass of column v of one block: dequantise with the folded table,
 // AAN, into the transpose buffer (no +128: fast_row clips to [-128, 127] and
@@ -150,7 +193,7 @@ __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int 
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       if constexpr (I::SY == 2)
-        vb[j] = cw[wq * I::CWC + c0 + j] * 0.25 + cw[wt * I::CWC + c0 + j] * 0.75;
+        vb[j] = vblend(cw[wq * I::CWC + c0 + j], cw[wt * I::CWC + c0 + j]);
       else
         vb[j] = cw[wq * I::CWC + c0 + j];
     }
@@ -159,8 +202,8 @@ __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int 
     for (int j = 0; j < 5; ++j) d[j] = vb[j] - vb[j + 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      C[2 * i] = d[i] * 0.25 + vb[i + 1];           // (1/4, 3/4) on (m-1, m)
-      C[2 * i + 1] = d[i + 1] * -0.25 + vb[i + 1];  // (3/4, 1/4) on (m, m+1)
+      C[2 * i] = hblend(d[i], 0.25, vb[i + 1]);       // (1/4, 3/4) on (m-1, m)
+      C[2 * i + 1] = hblend(d[i + 1], -0.25, vb[i + 1]);  // (3/4, 1/4) on (m, m+1)
     }
   }
 }
@@ -175,8 +218,9 @@ __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int 
 // tell how close any value came to an integer.  The colour terms add onto
 // Y + MAGIC (one add per pixel instead of one per channel): each of the <= 3
 // roundings on the way (Y + MAGIC, then one or two fmas) lands on the same
-// 2^-32 grid, |error| <= 2^-33 each, so the certificate adds 2^-31 (the
-// colour fma's own rounding stays in K_CONST, now an over-estimate).
+// 2^-32 grid, |error| <= 2^-33 each, so the certificate adds 2^-31
+// (tools/inv_bound.py prices everything off the grid: the products C * k fused
+// or rounded, and the constants' representation errors).
 constexpr double MAGIC = 0x1.8p+20;
 constexpr uint32_t MAGIC_HI = 0x41380000u;
 
@@ -331,15 +375,15 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           Yv[k] = Yv[k] + (MAGIC + 128.0);  // Y on byte_cert_y's grid, shared by the three channels
-          const double B = Yv[k] + C[k] * 1.772;
-          Gt[k] = Yv[k] + C[k] * -0.344136;
+          const double B = col_b(Yv[k], C[k]);
+          Gt[k] = col_gt(Yv[k], C[k]);
           cb[3 * k + 2] = byte_cert_y(B, lo_min, lo_max);
         }
         chroma8_fast<MODE>(s_cw[1], x0, cwx0, wq, wt, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const double R = Yv[k] + C[k] * 1.402;
-          const double G = Gt[k] + C[k] * -0.714136;
+          const double R = col_r(Yv[k], C[k]);
+          const double G = col_g(Gt[k], C[k]);
           cb[3 * k] = byte_cert_y(R, lo_min, lo_max);
           cb[3 * k + 1] = byte_cert_y(G, lo_min, lo_max);
         }
@@ -516,6 +560,99 @@ hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs,
     case M422: return inv_fast_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div, fin);
     default: return inv_fast_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div, fin);
   }
+}
+
+// ------------------------------------------- host: the chain (tests only) --
+//
+// k_inv_fast's arithmetic evaluated on the host for a whole image, with the
+// kernel's own helpers (aan8, vblend, hblend, col_*): dequantisation with the
+// folded table, AAN along axis 0 then axis 1, clip to [-128, 127], the
+// vertical then difference-form horizontal chroma blends with cv2's clamped
+// taps (the kernel's replicated window ring gives the same operands), the
+// colour terms on the magic grid and byte_cert_y's byte.  fuse = 0: every
+// multiply-add rounded twice (MadDev on x86-64); 1: every one fused (MadFma).
+// values[] = v' = y - MAGIC (exact), the value the certificate judges.
+template <class M>
+static void inv_fast_host_t(int mode, const int16_t* cf, const double* Q, int H, int W, double* vout,
+                            uint8_t* bout) {
+  const int sy = mode == M420 ? 2 : 1, sx = mode == M444 ? 1 : 2;
+  double qs[64];
+  for (int i = 0; i < 64; ++i) qs[i] = Q[i] * h_aan[i >> 3] * h_aan[i & 7] * 0.125;
+  std::vector<double> pl[3];
+  int ph[3], pw[3], st[3];
+  size_t off = 0;
+  for (int p = 0; p < 3; ++p) {
+    ph[p] = p ? H / sy : H;
+    pw[p] = p ? W / sx : W;
+    const int nby = (ph[p] + 7) / 8, nbx = (pw[p] + 7) / 8;
+    st[p] = nbx * 8;
+    pl[p].assign((size_t)nby * 8 * st[p], 0.0);
+    for (int by = 0; by < nby; ++by)
+      for (int bx = 0; bx < nbx; ++bx) {
+        const int16_t* b = cf + off + ((size_t)by * nbx + bx) * 64;
+        double mid[8][8];
+        for (int v = 0; v < 8; ++v) {  // fast_col
+          double c[8];
+          for (int r = 0; r < 8; ++r) c[r] = (double)b[r * 8 + v] * qs[r * 8 + v];
+          aan8<M>(c);
+          for (int r = 0; r < 8; ++r) mid[r][v] = c[r];
+        }
+        for (int u = 0; u < 8; ++u) {  // fast_row<-128>
+          double c[8];
+          for (int k = 0; k < 8; ++k) c[k] = mid[u][k];
+          aan8<M>(c);
+          for (int k = 0; k < 8; ++k) pl[p][(size_t)(by * 8 + u) * st[p] + bx * 8 + k] = fmin(fmax(c[k], -128.0), 127.0);
+        }
+      }
+    off += (size_t)nby * nbx * 64;
+  }
+  auto S = [&](int p, int r, int c) {  // clamped taps (cv2) = the kernel's ring / clampi rows
+    r = r < 0 ? 0 : (r > ph[p] - 1 ? ph[p] - 1 : r);
+    c = c < 0 ? 0 : (c > pw[p] - 1 ? pw[p] - 1 : c);
+    return pl[p][(size_t)r * st[p] + c];
+  };
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) {
+      double C[3];
+      for (int p = 1; p < 3; ++p) {
+        if (sx == 1) {
+          C[p] = S(p, y, x);
+          continue;
+        }
+        auto vb = [&](int col) {
+          if (sy == 2) {
+            const int m = y >> 1, rq = (y & 1) ? m + 1 : m - 1;
+            return vblend<M>(S(p, rq, col), S(p, m, col));
+          }
+          return S(p, y, col);
+        };
+        const int m = x >> 1;
+        C[p] = (x & 1) == 0 ? hblend<M>(vb(m - 1) - vb(m), 0.25, vb(m)) : hblend<M>(vb(m) - vb(m + 1), -0.25, vb(m));
+      }
+      const double Yv = S(0, y, x) + (MAGIC + 128.0);
+      const double B = col_b<M>(Yv, C[1]), Gt = col_gt<M>(Yv, C[1]);
+      const double R = col_r<M>(Yv, C[2]), G = col_g<M>(Gt, C[2]);
+      const double o[3] = {R, G, B};
+      for (int ch = 0; ch < 3; ++ch) {
+        uint64_t bits;
+        memcpy(&bits, &o[ch], 8);
+        const uint32_t hi = (uint32_t)(bits >> 32);
+        const uint32_t c = hi < MAGIC_HI ? MAGIC_HI : (hi > MAGIC_HI + 255u ? MAGIC_HI + 255u : hi);
+        const size_t i = ((size_t)y * W + x) * 3 + ch;
+        vout[i] = o[ch] - MAGIC;
+        bout[i] = (uint8_t)(c & 255u);
+      }
+    }
+}
+
+int inv_fast_host(int mode, const int16_t* cf, const double* Q, int H, int W, int fuse, double* vout, uint8_t* bout) {
+  const int sy = mode == M420 ? 2 : 1, sx = mode == M444 ? 1 : 2;
+  if (H % sy || W % sx) return -1;  // the tiled kernels' even geometries
+  if (fuse)
+    inv_fast_host_t<MadFma>(mode, cf, Q, H, W, vout, bout);
+  else
+    inv_fast_host_t<MadDev>(mode, cf, Q, H, W, vout, bout);
+  return 0;
 }
 
 }  // namespace jds
