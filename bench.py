@@ -57,6 +57,9 @@ def parse():
                     help='CPU budget over the 4 legs (faithful / vectorised x 1 core / pool)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
+    ap.add_argument('--no-north-star', action='store_true',
+                    help='skip the north-star leg (16 x 3840x2160, Q=50, 4:2:0, prefilter) that the default run '
+                         'measures after the headline configs[1] line')
     ap.add_argument('--no-host-path', action='store_true',
                     help='skip the PCIe-inclusive engines.compress_reconstruct measurement (1080p, host arrays)')
     ap.add_argument('--sweep', action='store_true',
@@ -205,7 +208,12 @@ def cpu_baseline(frames_host, quality, mode, pf, budget_s, block=8):
                       f'through oracle/cpu_ref.py ({best_k}), {best["seconds"]} s, no SSIM/maps',
             'legs': legs, 'cpu_model': _cpu_model(), 'host_cores_visible': os.cpu_count(),
             'reference_per_block_loop_note': 'faithful = engines/pipeline.py:47-82 loop structure (one scipy '
-                                             'call per 8x8 block); vectorised = batched dctn over (n, 8, 8)'}
+                                             'call per 8x8 block); vectorised = batched dctn over (n, 8, 8)',
+            'reconciliation': 'BASELINE.md section 2 measured the reference itself at 0.87-0.97 Mpix/s (1080p cfg2, '
+                              '1 core, no SSIM) on the survey container\'s Xeon; the faithful leg on that same '
+                              'container type runs 0.76-0.81 Mpix/s (2.55-2.74 s per 1080p frame, DESIGN.md section 4), '
+                              'so the legs here differ from it by the host CPU (this box: ' + _cpu_model() + '), '
+                              'not by the work timed'}
 
 
 def host_path(quality, mode, pf, H=1080, W=1920, reps=5):
@@ -320,6 +328,23 @@ def sweep_main(args):
                          'items_per_step': items, 'items_per_s': round(items * args.steps / elapsed, 1),
                          'front_end': 'replicated per item' if rep else 'shared per frame (jds_plan_create_q)',
                          'parallelism': f'frame-shard x{world}', **dist_info(world, backend)}}
+    # the per-item statistics of every rank reach every rank (distributed_sweep's
+    # all_gather_object, gui/worker.py:55-74's result list), once, outside the
+    # timed region: the record shows the gather ran and what it carried
+    from jds.sweep import distributed_sweep
+    st_np = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(F, nq)
+
+    def mine_items(frames, qs, tabs):
+        assert len(frames) == F and np.array_equal(tabs, tables)
+        return [{'frame': frames[f], 'quality': q, 'nonzero': int(st_np[f, i]['nonzero']),
+                 'magnitude_bits': int(st_np[f, i]['magnitude_bits']), 'sse_rgb': int(st_np[f, i]['sse_rgb'])}
+                for f in range(F) for i, q in enumerate(qs)]
+    tg = time.perf_counter()
+    gathered = distributed_sweep(F * world, SWEEP_QS, mine_items)
+    result['gather'] = {'collective': 'broadcast (tables) + all_gather_object (per-item stats)' if world > 1
+                        else 'none (one rank)', 'items_gathered': len(gathered), 'items_expected': F * nq * world,
+                        'frames_covered': sorted({it['frame'] for it in gathered}) == list(range(F * world)),
+                        'seconds': round(time.perf_counter() - tg, 4), **dist_info(world, backend)}
     if rank == 0 and not args.no_parity:
         from oracle import cpu_ref
         stats = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(-1)
@@ -338,44 +363,36 @@ def sweep_main(args):
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
-    if args.sweep:
-        return sweep_main(args)
-    import numpy as np
+def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block=8, qtable=None, seed=1000):
+    """One measured configuration: B device-resident frames per GPU, W untimed
+    warmup steps (continued to PREWARM_S of load), then exactly K timed steps
+    bracketed by barrier + synchronize, max over ranks; then a serial
+    calibration pass timing each phase with HIP events on its launch stream.
+    Returns (result dict, state) -- state keeps the plans and buffers for the
+    legs that follow (entropy, parity); the caller closes the plans."""
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    local, backend = init_dist(world, local)
-    dev = torch.device('cuda', local)
-    torch.cuda.set_device(dev)
-
     from jds import _abi, codec
     from engines.quantizer import scale_quant_matrix
     from utils.constants import JPEG_LUMA_Q50
 
-    B, H, W = args.frames, args.height, args.width
-    qt = scale_quant_matrix(JPEG_LUMA_Q50, args.quality)
-    prm = _abi.make_params(args.quality, qt, args.mode, bool(args.prefilter), codec.gaussian_kernel3(), args.block)
+    qt = scale_quant_matrix(JPEG_LUMA_Q50, quality) if qtable is None else qtable
+    prm = _abi.make_params(quality, qt, mode, bool(pf), codec.gaussian_kernel3(), block)
     # image stream: NS buffer sets (plan + frames + outputs); with pipelining the
     # forward of batch k+1 (set (k+1) % 2) runs beside the inverse of batch k on
     # a second stream, and batch k+2 reuses set k % 2 once batch k's inverse is done
     NS = 2 if args.pipeline else 1
-    plans = [_abi.Plan(_abi.context(local), [prm] * B, H, W) for _ in range(NS)]
+    plans = [_abi.Plan(_abi.context(dev.index), [prm] * B, H, W) for _ in range(NS)]
     geo = plans[0].geometry
     cpf = geo.coeffs_per_frame
 
     # device-resident synthetic frames (uniform random RGB), distinct per rank and set
     gen = torch.Generator(device=dev)
-    gen.manual_seed(1000 + rank)
+    gen.manual_seed(seed + rank)
     rgbs = [torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=gen) for _ in range(NS)]
     outs = [torch.empty_like(r) for r in rgbs]
     coefs = [torch.empty((B, cpf), dtype=torch.int16, device=dev) for _ in range(NS)]
     stats_l = [torch.zeros((B, _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev) for _ in range(NS)]
-    rgb, out, coeffs, stats = rgbs[0], outs[0], coefs[0], stats_l[0]
     s_f = torch.cuda.Stream(dev)  # forward launches (and their events)
     s_i = torch.cuda.Stream(dev) if NS > 1 else s_f  # inverse launches
     torch.cuda.synchronize(dev)  # inputs were produced on the default stream
@@ -438,7 +455,6 @@ def main():
     torch.cuda.synchronize(dev)
     t_fwd = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     t_inv = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
-    plan = plans[0]
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev, backend)
 
@@ -450,9 +466,9 @@ def main():
     dom = 'k_fwd' if t_fwd >= t_inv else 'k_inv'
     t_dom = max(t_fwd, t_inv)
     achieved = (bytes_fwd if dom == 'k_fwd' else bytes_inv) / (t_dom * 1e-3) / 1e9
-    mcode = {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[args.mode]
-    pfs = 'true' if (args.prefilter and mcode != 0) else 'false'
-    if args.block == 16:
+    mcode = {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[mode]
+    pfs = 'true' if (pf and mcode != 0) else 'false'
+    if block == 16:
         if dom == 'k_fwd':
             kname = f'k_fwd16<{mcode},{pfs}>' if args.exact else f'k_fwd16f<{mcode},{pfs}> + k_fix_fwd16<{mcode},{pfs}>'
         else:
@@ -469,8 +485,7 @@ def main():
     if os.path.exists(tf):
         try:
             rec = json.load(open(tf))
-            base = (f'{W}x{H}_q{args.quality}_{args.mode}_pf{int(bool(args.prefilter))}'
-                    + ('_B16' if args.block == 16 else '') + '_b')
+            base = (f'{W}x{H}_q{quality}_{mode}_pf{int(bool(pf))}' + ('_B16' if block == 16 else '') + '_b')
             nl = B  # frames per launch
             if base + str(nl) in rec:
                 traffic = rec[base + str(nl)].get(dom)
@@ -483,7 +498,7 @@ def main():
             traffic = None
 
     result = {
-        'metric': metric_name(args.quality, args.mode),
+        'metric': metric_name(quality, mode),
         'value': round(value, 2),
         'unit': 'Mpixels/s',
         'n_gpus': world,
@@ -496,9 +511,8 @@ def main():
         'vs_baseline': None,
         'dtype': 'f32+f64',  # forward: fp32 certified + fp64 fix-up; inverse: fp64 (u8 in/out, int16 coefficients)
         'data': 'synthetic (uniform random RGB generated on device)',
-        'config': {'workload': f'{W}x{H} RGB, Q={args.quality}, {args.mode}, prefilter={"on" if args.prefilter else "off"}, '
-                               f'{args.block}x{args.block} blocks ('
-                               + workload_label(H, W, args.quality, args.mode, args.prefilter, args.block) + ')',
+        'config': {'workload': f'{W}x{H} RGB, Q={quality}, {mode}, prefilter={"on" if pf else "off"}, '
+                               f'{block}x{block} blocks (' + workload_label(H, W, quality, mode, pf, block) + ')',
                    'frames_per_gpu_per_step': B, 'global_batch_frames': B * world,
                    'pipeline': ('image stream: forward of batch k+1 beside the inverse of batch k (two streams, '
                                 'two buffer sets)' if NS > 1 else 'serial forward then inverse per step'),
@@ -512,9 +526,61 @@ def main():
                      'limiter': 'VALU issue, not HBM: the forward computes in certified fp32, the bit-exact '
                                 'inverse in fp64 (DESIGN.md section 4, profiles/*_pmc_summary.json)'},
         'kernels_ms': {'k_fwd': round(t_fwd, 4), 'k_inv': round(t_inv, 4)},
-        'fixups_last_step': {'fwd_blocks': int(plans[0].fix_counts()[0])},
+        'fixups_last_step': {'fwd_blocks': int(plans[0].fix_counts()[0]), 'inv_tiles': int(plans[0].fix_counts()[1])},
         'pipeline_roofline_frac': round(value / world * 1e6 * (6 + 2 * S) / (HBM_PEAK_GBS * 1e9), 4),
     }
+    state = {'plans': plans, 'rgb': rgbs[0], 'out': outs[0], 'coeffs': coefs[0], 'stats': stats_l[0], 's_f': s_f,
+             'cpf': cpf, 'qt': qt}
+    return result, state
+
+
+def frame0_parity(state, quality, mode, pf, block):
+    """Frame 0 against the oracle (outside the timed region): coefficient and
+    byte mismatches, PSNR and its difference from the reference's."""
+    import numpy as np
+    from oracle import cpu_ref
+    f0 = state['rgb'][0].cpu().numpy()
+    ref = cpu_ref.compress_reconstruct(f0, quality, block, mode, bool(pf), metrics=False, stretch=block == 16)
+    rec0, cf0 = state['out'][0].cpu().numpy(), state['coeffs'][0].cpu().numpy()
+    mse = np.mean((f0.astype(np.float64) - rec0) ** 2)
+    mse_ref = np.mean((f0.astype(np.float64) - ref['reconstructed']) ** 2)
+    return {'frame': 0, 'coeff_mismatch': int(np.sum(cf0 != ref['coeffs'])),
+            'recon_mismatch_bytes': int(np.sum(rec0 != ref['reconstructed'])),
+            'psnr_rgb': float(10 * np.log10(255 ** 2 / mse)),
+            'dpsnr_rgb_vs_ref': float(10 * np.log10(255 ** 2 / mse) - 10 * np.log10(255 ** 2 / mse_ref))}
+
+
+NORTH_STAR = dict(B=16, H=2160, W=3840, quality=50, mode='4:2:0', pf=1)  # BASELINE.json north_star point
+
+
+def main():
+    args = parse()
+    if args.sweep:
+        return sweep_main(args)
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    local, backend = init_dist(world, local)
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    from jds import _abi
+    from jds.sweep import broadcast_tables
+
+    B, H, W = args.frames, args.height, args.width
+    # rank 0's quant table reaches every rank in one broadcast (RCCL over xGMI
+    # at N > 1, the north star's exchange; outside the timed region)
+    qt = broadcast_tables([args.quality])[0]
+    result, state = run_point(args, dev, world, backend, rank, B, H, W, args.quality, args.mode, args.prefilter,
+                              args.block, qt)
+    result['config']['quant_table'] = ('rank 0 -> all ranks, one broadcast of 64 float64 '
+                                       f'({"RCCL over xGMI" if backend == "nccl" else backend})' if world > 1
+                                       else 'local (one rank)')
+    plans, rgb, coeffs, stats, s_f, cpf = (state[k] for k in ('plans', 'rgb', 'coeffs', 'stats', 's_f', 'cpf'))
+    px_per_step = B * H * W
 
     if not args.no_entropy and args.block == 8:
         # JPEG entropy coding of the step's coefficients (jds_entropy.hip), timed on
@@ -550,17 +616,7 @@ def main():
 
     if rank == 0 and not args.no_parity:
         # PSNR / bytes vs the reference restatement on frame 0 (outside the timed region)
-        from oracle import cpu_ref
-        f0 = rgb[0].cpu().numpy()
-        ref = cpu_ref.compress_reconstruct(f0, args.quality, args.block, args.mode, bool(args.prefilter),
-                                           metrics=False, stretch=args.block == 16)
-        rec0, cf0 = out[0].cpu().numpy(), coeffs[0].cpu().numpy()
-        mse = np.mean((f0.astype(np.float64) - rec0) ** 2)
-        mse_ref = np.mean((f0.astype(np.float64) - ref['reconstructed']) ** 2)
-        result['parity'] = {'frame': 0, 'coeff_mismatch': int(np.sum(cf0 != ref['coeffs'])),
-                            'recon_mismatch_bytes': int(np.sum(rec0 != ref['reconstructed'])),
-                            'psnr_rgb': float(10 * np.log10(255 ** 2 / mse)),
-                            'dpsnr_rgb_vs_ref': float(10 * np.log10(255 ** 2 / mse) - 10 * np.log10(255 ** 2 / mse_ref))}
+        result['parity'] = frame0_parity(state, args.quality, args.mode, args.prefilter, args.block)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         n = max(1, min(B, 64))
         host = rgb[:n].cpu().numpy()
@@ -568,10 +624,32 @@ def main():
                                               args.cpu_baseline_seconds, args.block)
     else:
         result['cpu_baseline'] = None
-    if rank == 0 and not args.no_host_path and args.block == 8:
-        result['host_path'] = host_path(args.quality, args.mode, args.prefilter)
     for p_ in plans:
         p_.close()
+    del state, rgb, coeffs, stats
+
+    default_point = (H, W, args.quality, args.mode, bool(args.prefilter), args.block) == (1080, 1920, 50, '4:2:0',
+                                                                                          True, 8)
+    if default_point and not args.no_north_star:
+        # the north-star point (BASELINE.json north_star: 4K / Q=50 / 4:2:0), same
+        # timing method, same ranks: the driver's default run carries it
+        ns = NORTH_STAR
+        nqt = broadcast_tables([ns['quality']])[0]
+        r_ns, st_ns = run_point(args, dev, world, backend, rank, ns['B'], ns['H'], ns['W'], ns['quality'],
+                                ns['mode'], ns['pf'], 8, nqt, seed=3000)
+        keep = ('metric', 'value', 'unit', 'ms_per_step', 'warmup_steps_run', 'roofline', 'kernels_ms',
+                'fixups_last_step', 'pipeline_roofline_frac')
+        result['north_star'] = {k: r_ns[k] for k in keep}
+        result['north_star']['config'] = {'workload': r_ns['config']['workload'],
+                                          'frames_per_gpu_per_step': ns['B'], 'steps': args.steps}
+        result['north_star']['target_pipeline_roofline_frac'] = 0.60
+        if rank == 0 and not args.no_parity:
+            result['north_star']['parity'] = frame0_parity(st_ns, ns['quality'], ns['mode'], ns['pf'], 8)
+        for p_ in st_ns['plans']:
+            p_.close()
+        del st_ns
+    if rank == 0 and not args.no_host_path and args.block == 8:
+        result['host_path'] = host_path(args.quality, args.mode, args.prefilter)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

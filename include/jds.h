@@ -168,6 +168,22 @@ int jds_psnr_ssim(jds_ctx* ctx, const uint8_t* a, const uint8_t* b, int64_t H, i
  * (SURVEY.md section 5 interface sketch: jds_ssim_dev). */
 int jds_psnr_ssim_dev(jds_ctx* ctx, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W, double* out);
 
+/* jds_psnr_ssim_dev without the device-wide wait: the context's stream waits
+ * only for the work queued so far on `after` (a hipStream_t, e.g. the plan
+ * run's stream; NULL = the caller has already synchronised the images), so
+ * leased contexts of other threads keep running.  out on the host. */
+int jds_psnr_ssim_dev_after(jds_ctx* ctx, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W,
+                            double* out, void* after);
+
+/* NumPy's float32 sum of magnitude_bits over device-resident int16
+ * coefficients (utils/metrics.py:77-78: np.sum(np.ceil(np.log2(|q| + 1)) + 1)
+ * over the nonzero q, float32 accumulation in NumPy's 8192-element buffered
+ * pairwise order; the host path's k_mag_f32 chain): what bpp and
+ * compression_ratio are computed from once the exact sum passes 2^24.
+ * n_coeffs: a multiple of 64 (one frame's IntermediateData layout); `after` as
+ * above.  *out on the host. */
+int jds_magnitude_bits_f32_dev(jds_ctx* ctx, const int16_t* coeffs_dev, int64_t n_coeffs, double* out, void* after);
+
 /* Per-stage functions of the engines.* API (engines/__init__.py:10-27), on host
  * fp64 arrays staged through the context's device memory.  Synchronous.
  *   rgb_to_ycbcr / ycbcr_to_rgb: n_pixels x 3 (engines/color_space.py:8-24)

@@ -837,6 +837,46 @@ int jds_psnr_ssim_dev(jds_ctx* c, const uint8_t* a_dev, const uint8_t* b_dev, in
   return psnr_ssim_device(c, a_dev, b_dev, H, W, out);
 }
 
+// the context's stream waits for what `after` has queued so far (one event)
+static int wait_after(jds_ctx* c, void* after) {
+  if (!after) return JDS_OK;
+  hipEvent_t e;
+  HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  hipError_t err = hipEventRecord(e, (hipStream_t)after);
+  if (err == hipSuccess) err = hipStreamWaitEvent(c->stream, e, 0);
+  hipError_t d = hipEventDestroy(e);  // released once the wait has completed
+  if (err != hipSuccess) return fail(JDS_EHIP, "HIP error: %s", hipGetErrorString(err));
+  if (d != hipSuccess) return fail(JDS_EHIP, "HIP error: %s", hipGetErrorString(d));
+  return JDS_OK;
+}
+
+int jds_psnr_ssim_dev_after(jds_ctx* c, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W,
+                            double* out, void* after) {
+  int rc = psnr_ssim_args(c, a_dev, b_dev, H, W, out);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  if ((rc = wait_after(c, after))) return rc;
+  return psnr_ssim_device(c, a_dev, b_dev, H, W, out);
+}
+
+int jds_magnitude_bits_f32_dev(jds_ctx* c, const int16_t* coeffs_dev, int64_t n_coeffs, double* out, void* after) {
+  if (!c || !coeffs_dev || !out || n_coeffs < 0 || n_coeffs % 64) return fail(JDS_EINVAL, "bad argument");
+  if (n_coeffs > ((int64_t)1 << 31)) return fail(JDS_EINVAL, "too many coefficients");
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = wait_after(c, after);
+  if (rc) return rc;
+  hipStream_t s = c->stream;
+  const long long nblk = n_coeffs / 64;
+  const int max_chunks = (int)((n_coeffs + 8191) / 8192) + 1;
+  HIP_TRY(c->chunks.ensure(mag_scratch_bytes(nblk, max_chunks)));
+  HIP_TRY(c->ss_out.ensure(5 * sizeof(double) + sizeof(unsigned long long)));
+  double* d = (double*)c->ss_out.p;
+  HIP_TRY(launch_mag_f32(coeffs_dev, nblk, (unsigned*)c->chunks.p, max_chunks, d, s));
+  HIP_TRY(hipMemcpyAsync(out, d, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return JDS_OK;
+}
+
 // ----------------------------------------------------- per-stage API --
 
 static int stage_io(jds_ctx* c, int idx, const void* host, size_t bytes, void** dev) {

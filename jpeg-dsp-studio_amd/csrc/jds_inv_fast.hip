@@ -120,9 +120,9 @@ __host__ __device__ __forceinline__ void aan8(double (&v)[8]) {
 // vertical a * 1/4 + b * 3/4 (a the "quarter" row), horizontal in difference
 // form near + (far - near) * (+-1/4)
 template <class M = MadDev>
-__host__ __device__ __forceinline__ double vblend(double a, double b) { return M::mad(a, 0.25, b * 0.75); }
+__host__ __device__ __forceinline__ double fvblend(double a, double b) { return M::mad(a, 0.25, b * 0.75); }
 template <class M = MadDev>
-__host__ __device__ __forceinline__ double hblend(double d, double w, double near) { return M::mad(d, w, near); }
+__host__ __device__ __forceinline__ double fhblend(double d, double w, double near) { return M::mad(d, w, near); }
 
 // The colour terms onto Y + MAGIC + 128 (byte_cert_y's grid): out = B, Gt, R, G
 template <class M = MadDev>
@@ -193,7 +193,7 @@ __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int 
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       if constexpr (I::SY == 2)
-        vb[j] = vblend(cw[wq * I::CWC + c0 + j], cw[wt * I::CWC + c0 + j]);
+        vb[j] = fvblend(cw[wq * I::CWC + c0 + j], cw[wt * I::CWC + c0 + j]);
       else
         vb[j] = cw[wq * I::CWC + c0 + j];
     }
@@ -202,8 +202,8 @@ __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int 
     for (int j = 0; j < 5; ++j) d[j] = vb[j] - vb[j + 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      C[2 * i] = hblend(d[i], 0.25, vb[i + 1]);       // (1/4, 3/4) on (m-1, m)
-      C[2 * i + 1] = hblend(d[i + 1], -0.25, vb[i + 1]);  // (3/4, 1/4) on (m, m+1)
+      C[2 * i] = fhblend(d[i], 0.25, vb[i + 1]);       // (1/4, 3/4) on (m-1, m)
+      C[2 * i + 1] = fhblend(d[i + 1], -0.25, vb[i + 1]);  // (3/4, 1/4) on (m, m+1)
     }
   }
 }
@@ -530,9 +530,11 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
                               next_count, cnt_now, in_div, fix_all);
   }
   // one call site of the exact tile code: items in exact mode, uncertain tiles
+#ifndef JDS_PROBE_NOFALLBACK  // tools/stage_budget.py: the fast path's code alone
   if (item_exact || sh.redo)  // (uniform)
     inv2_tile<MODE, XTRA>(sh, g, tiles_x, ntile, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part, nullptr,
                           nullptr, in_div);
+#endif
 }
 
 // ------------------------------------------------------------ launchers --
@@ -565,7 +567,7 @@ hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs,
 // ------------------------------------------- host: the chain (tests only) --
 //
 // k_inv_fast's arithmetic evaluated on the host for a whole image, with the
-// kernel's own helpers (aan8, vblend, hblend, col_*): dequantisation with the
+// kernel's own helpers (aan8, fvblend, fhblend, col_*): dequantisation with the
 // folded table, AAN along axis 0 then axis 1, clip to [-128, 127], the
 // vertical then difference-form horizontal chroma blends with cv2's clamped
 // taps (the kernel's replicated window ring gives the same operands), the
@@ -622,12 +624,12 @@ static void inv_fast_host_t(int mode, const int16_t* cf, const double* Q, int H,
         auto vb = [&](int col) {
           if (sy == 2) {
             const int m = y >> 1, rq = (y & 1) ? m + 1 : m - 1;
-            return vblend<M>(S(p, rq, col), S(p, m, col));
+            return fvblend<M>(S(p, rq, col), S(p, m, col));
           }
           return S(p, y, col);
         };
         const int m = x >> 1;
-        C[p] = (x & 1) == 0 ? hblend<M>(vb(m - 1) - vb(m), 0.25, vb(m)) : hblend<M>(vb(m) - vb(m + 1), -0.25, vb(m));
+        C[p] = (x & 1) == 0 ? fhblend<M>(vb(m - 1) - vb(m), 0.25, vb(m)) : fhblend<M>(vb(m) - vb(m + 1), -0.25, vb(m));
       }
       const double Yv = S(0, y, x) + (MAGIC + 128.0);
       const double B = col_b<M>(Yv, C[1]), Gt = col_gt<M>(Yv, C[1]);

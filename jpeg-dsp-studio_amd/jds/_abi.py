@@ -87,6 +87,8 @@ _SIGS = {
                                            C.POINTER(SelectedBlock), C.POINTER(C.c_int32)]),
     'jds_psnr_ssim': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, _P]),
     'jds_psnr_ssim_dev': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, _P]),
+    'jds_psnr_ssim_dev_after': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, _P, _P]),
+    'jds_magnitude_bits_f32_dev': (C.c_int, [_P, _P, C.c_int64, _P, _P]),
     'jds_stage_rgb_to_ycbcr': (C.c_int, [_P, _P, _P, C.c_int64]),
     'jds_stage_ycbcr_to_rgb': (C.c_int, [_P, _P, _P, C.c_int64]),
     'jds_stage_subsample': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P]),

@@ -83,13 +83,30 @@ def psnr_ssim_raw(a: np.ndarray, b: np.ndarray, device: int = 0) -> np.ndarray:
     return out
 
 
-def psnr_ssim_dev(a_ptr: int, b_ptr: int, H: int, W: int, device: int = 0) -> np.ndarray:
+def psnr_ssim_dev(a_ptr: int, b_ptr: int, H: int, W: int, device: int = 0, after=-1) -> np.ndarray:
     """jds_psnr_ssim_dev: psnr_ssim_raw's six values for two HxWx3 uint8 images
-    already in device memory (raw device pointers, e.g. torch tensors' data_ptr())."""
+    already in device memory (raw device pointers, e.g. torch tensors' data_ptr()).
+    after: -1 = wait for the whole device (jds_psnr_ssim_dev); None = the caller
+    has synchronised the images; a stream handle = wait only for that stream's
+    queued work (jds_psnr_ssim_dev_after)."""
     out = np.empty(6, np.float64)
     with lease(device) as ctx:
-        check(lib().jds_psnr_ssim_dev(ctx.handle, int(a_ptr), int(b_ptr), int(H), int(W), out.ctypes.data))
+        if after == -1:
+            check(lib().jds_psnr_ssim_dev(ctx.handle, int(a_ptr), int(b_ptr), int(H), int(W), out.ctypes.data))
+        else:
+            check(lib().jds_psnr_ssim_dev_after(ctx.handle, int(a_ptr), int(b_ptr), int(H), int(W), out.ctypes.data,
+                                                after or None))
     return out
+
+
+def magnitude_bits_f32_dev(coeffs_ptr: int, n_coeffs: int, device: int = 0, after=None) -> float:
+    """jds_magnitude_bits_f32_dev: NumPy's float32 np.sum of magnitude_bits
+    (utils/metrics.py:77-78) over n_coeffs device-resident int16 coefficients."""
+    out = C.c_double()
+    with lease(device) as ctx:
+        check(lib().jds_magnitude_bits_f32_dev(ctx.handle, int(coeffs_ptr), int(n_coeffs), C.byref(out),
+                                               after or None))
+    return float(out.value)
 
 
 # ----------------------------------------------------------- per-stage ops

@@ -54,10 +54,13 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
     tensor on the device) through quality-sweep plans (jds_plan_create_q: the
     colour / prefilter / subsample / DCT front end runs once per frame and is
     quantised for up to 8 tables at a time).  Items are ordered frame-major.
-    Returns one dict per item.  ssim=True adds the SSIM fields of the
+    Returns one dict per item; bpp / compression_ratio come from NumPy's float32
+    magnitude-bits sum (jds_magnitude_bits_f32_dev), as the reference computes
+    them (utils/metrics.py:77-78).  ssim=True adds the SSIM fields of the
     reference's per-item CompressionResult (ssim_rgb, ssim_y; gui/worker.py:62-68
     -> utils/metrics.py:9-28) from the device-resident reconstructions
-    (jds_psnr_ssim_dev: bit-identical to skimage, the heaviest per-item tail)."""
+    (jds_psnr_ssim_dev_after: bit-identical to skimage, the heaviest per-item
+    tail) and takes mse_y / psnr_y from the same bit-exact reduction."""
     import torch
     from jds import _abi, codec
     from engines.quantizer import scale_quant_matrix
@@ -71,7 +74,8 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
     qs = [int(q) for q in qualities]
     gk = codec.gaussian_kernel3()
     stats = np.zeros((F, len(qs)), dtype=_abi.STATS_DTYPE)
-    ssims = np.full((F, len(qs), 2), np.nan)
+    ssims = np.full((F, len(qs), 3), np.nan)  # ssim_rgb, ssim_y, mse_y (bit-exact, jds_psnr_ssim_dev)
+    magf = np.zeros((F, len(qs)))  # NumPy float32 magnitude_bits per item (bpp, compression_ratio)
     for c0 in range(0, len(qs), 8):
         qc = qs[c0:c0 + 8]
         qt = [scale_quant_matrix(JPEG_LUMA_Q50, q) if tables is None else tables[c0 + i] for i, q in enumerate(qc)]
@@ -85,22 +89,29 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
             plan.run(fr.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), _abi.RUN_SSE, 0)
             torch.cuda.synchronize(dev)
             stats[:, c0:c0 + len(qc)] = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(F, len(qc))
-            if ssim:
-                for f in range(F):
-                    for i in range(len(qc)):
-                        r = codec.psnr_ssim_dev(fr[f].data_ptr(), out[f * len(qc) + i].data_ptr(), H, W, device)
-                        ssims[f, c0 + i] = (float(np.mean(r[:3])), r[3])  # channel_axis=2: mean of R, G, B
+            cpf = plan.geometry.coeffs_per_frame
+            for f in range(F):
+                for i in range(len(qc)):
+                    # the images and coefficients are complete (synchronised above)
+                    magf[f, c0 + i] = codec.magnitude_bits_f32_dev(cf[f * len(qc) + i].data_ptr(), cpf, device, None)
+                    if ssim:
+                        r = codec.psnr_ssim_dev(fr[f].data_ptr(), out[f * len(qc) + i].data_ptr(), H, W, device, None)
+                        ssims[f, c0 + i] = (float(np.mean(r[:3])), r[3], r[4])  # channel_axis=2: mean of R, G, B
         finally:
             plan.close()
     items = []
     for f in range(F):
         for qi, q in enumerate(qs):
             s = stats[f, qi]
-            br = bitrate_from_counts(int(s['nonzero']), float(s['magnitude_bits']), int(s['total_coeffs']), (H, W), 8)
+            # bpp from NumPy's float32 sum (the reference's np.sum, exact below 2^24)
+            br = bitrate_from_counts(int(s['nonzero']), float(magf[f, qi]), int(s['total_coeffs']), (H, W), 8)
             mse = float(s['sse_rgb']) / (H * W * 3)
-            mse_y = float(s['sse_y']) / (H * W)  # fp64 luma SSE in tile order (NumPy's mean: pairwise)
+            # mse_y: with ssim, the bit-exact NumPy mean (jds_psnr_ssim_dev); otherwise the
+            # fp64 luma SSE summed in tile order -- NumPy's pairwise mean to ~1e-15 relative
+            mse_y = float(ssims[f, qi, 2]) if ssim else float(s['sse_y']) / (H * W)
             items.append({'frame': f, 'quality': q, 'nonzero': int(s['nonzero']),
-                          'magnitude_bits': int(s['magnitude_bits']), 'total_coeffs': int(s['total_coeffs']),
+                          'magnitude_bits': int(s['magnitude_bits']), 'magnitude_bits_f32': float(magf[f, qi]),
+                          'total_coeffs': int(s['total_coeffs']),
                           'hist': s['hist'].astype(np.int64), 'sse_rgb': int(s['sse_rgb']),
                           'psnr_rgb': float('inf') if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse)),
                           'mse_y': mse_y, 'psnr_y': psnr_from_mse(mse_y),

@@ -151,6 +151,21 @@ def test_per_stage_api_matches_oracle():
     assert np.array_equal(E.idct2(d), sfft.idctn(d, type=2, norm='ortho', axes=(1, 2)))
 
 
+@pytest.mark.parametrize('h,w,H,W', [(20, 28, 40, 56), (540, 960, 1080, 1920), (19, 27, 37, 53), (7, 9, 13, 17),
+                                      (32, 48, 32, 96)])
+def test_upsample_chroma_nearest_matches_oracle(h, w, H, W):
+    """upsample_chroma(..., method='nearest') (reference engines/color_space.py:63,
+    cv2.INTER_NEAREST) through the per-stage kernel vs the oracle's resizeNN
+    restatement: a gather, so equality is exact."""
+    import engines as E
+    rng = np.random.default_rng(h * 1000 + w)
+    cb, cr = rng.uniform(0, 255, (h, w)), rng.uniform(0, 255, (h, w))
+    got = E.upsample_chroma(cb, cr, (H, W), method='nearest')
+    want = cpu_ref.upsample_chroma(cb, cr, (H, W), method='nearest')
+    assert got[0].shape == (H, W)
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+
+
 def test_4k_420_full_size_bit_exact():
     img = cpu_ref.random_image(2160, 3840, 21)
     res, inter = run(img, 50, '4:2:0', False)

@@ -102,6 +102,8 @@ def test_sweep_device_chunks_more_than_eight_qualities():
         # the fp64 luma SSE summed in tile order (NumPy sums pairwise: a few ulps apart)
         assert it['psnr_rgb'] == pytest.approx(ref['metrics']['psnr_rgb'], rel=1e-12)
         assert it['psnr_y'] == pytest.approx(ref['metrics']['psnr_y'], rel=1e-12)
+        # bpp / ratio from NumPy's float32 magnitude-bits sum, as the reference computes them
+        assert it['bpp'] == ref['bitrate']['bpp'] and it['compression_ratio'] == ref['bitrate']['compression_ratio']
 
 
 def test_sweep_device_ssim_fields():
@@ -119,6 +121,27 @@ def test_sweep_device_ssim_fields():
         assert it['ssim_y'] == pytest.approx(ref['metrics']['ssim_y'], rel=1e-12)
         host = codec.psnr_ssim_raw(frames[it['frame']], ref['reconstructed'])
         assert it['ssim_y'] == host[3]
+        # with ssim, mse_y is the bit-exact NumPy mean, so psnr_y is the reference's double
+        assert it['mse_y'] == host[4] and it['psnr_y'] == ref['metrics']['psnr_y']
+        assert it['bpp'] == ref['bitrate']['bpp']
+
+
+def test_magnitude_bits_f32_dev_matches_numpy_float32_sum():
+    """jds_magnitude_bits_f32_dev on device coefficients == NumPy's float32
+    np.sum of the reference's magnitude bits (utils/metrics.py:77-78), also past
+    2^24 where float32 no longer holds the exact integer sum."""
+    import torch
+    from jds import codec
+    rng = np.random.default_rng(4)
+    for n_blocks in (1, 1000, 300000):
+        q = rng.integers(-2047, 2048, n_blocks * 64).astype(np.int16)
+        q[rng.random(q.size) < 0.3] = 0
+        nz = q[q != 0]
+        want = float(np.sum(np.ceil(np.log2(np.abs(nz).astype(np.float32) + 1)) + 1, dtype=np.float32))
+        d = torch.from_numpy(q).to('cuda:0')
+        torch.cuda.synchronize()
+        got = codec.magnitude_bits_f32_dev(d.data_ptr(), q.size, 0, None)
+        assert got == want, (n_blocks, got, want)
 
 
 def test_sweep_plan_rejects_bad_shapes():

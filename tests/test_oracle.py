@@ -89,3 +89,24 @@ def test_faithful_per_block_loop_equals_vectorised(mode, pf):
     b = cpu_ref.compress_reconstruct(img, 40, 8, mode, pf, metrics=False)
     assert np.array_equal(a['coeffs'], b['coeffs'])
     assert np.array_equal(a['reconstructed'], b['reconstructed'])
+
+
+def test_resize_nearest_restatement_properties():
+    """cv2 INTER_NEAREST (resizeNN) as restated for upsample_chroma(method=
+    'nearest') (reference engines/color_space.py:63).  cv2 is not importable
+    here, so the restatement is parity-unpinned; what is pinned: at an exact 2x
+    scale every output is the input sample (y // 2, x // 2) (OpenCV's
+    documented nearest mapping), outputs are always input values, and at odd
+    sizes the source index is floor(d * (1 / (dst / src))) clamped."""
+    rng = np.random.default_rng(3)
+    c = rng.standard_normal((7, 9))
+    up = cpu_ref.resize_nearest(c, 14, 18)
+    yy, xx = np.mgrid[0:14, 0:18]
+    assert np.array_equal(up, c[yy // 2, xx // 2])
+    odd = cpu_ref.resize_nearest(c, 13, 17)
+    assert np.isin(odd, c).all()
+    sx = [min(int(np.floor(x * (1.0 / (17 / 9)))), 8) for x in range(17)]
+    sy = [min(int(np.floor(y * (1.0 / (13 / 7)))), 6) for y in range(13)]
+    assert np.array_equal(odd, c[np.ix_(sy, sx)])
+    cb, cr = cpu_ref.upsample_chroma(c, -c, (14, 18), method='nearest')
+    assert np.array_equal(cb, up) and np.array_equal(cr, -up)

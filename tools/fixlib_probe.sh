@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); mkdir -p gpurun_out; export TMPDIR=/tmp; cd /tmp
 for L in ${LIBS:-A W5 W6 W7}; do
   JDS_LIB_PATH=$ROOT/tools/bin/ab/libjds_$L.so timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/fl$L" -o run --output-format csv \
-    -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-entropy > "$ROOT/gpurun_out/fl$L.log" 2>&1 || exit $?
+    -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-north-star --no-entropy > "$ROOT/gpurun_out/fl$L.log" 2>&1 || exit $?
   python3 - "$ROOT/gpurun_out/fl$L/run_kernel_stats.csv" "$L" <<'PY'
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):

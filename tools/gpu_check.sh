@@ -21,7 +21,7 @@ fi
 if [ "$STAGE" = all ] || [ "$STAGE" = prof ]; then
   cd /tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv \
-    -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-parity \
+    -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-north-star --no-parity \
     > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"; [ $rc -eq 0 ] || exit $rc
 fi

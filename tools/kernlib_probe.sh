@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); mkdir -p gpurun_out; export TMPDIR=/tmp; cd /tmp
 for L in ${LIBS:-A B}; do
   JDS_LIB_PATH=$ROOT/tools/bin/ab/libjds_$L.so timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/kl$L" -o run --output-format csv \
-    -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ${ENT_FLAG---no-entropy} ${BENCH_ARGS:-} > "$ROOT/gpurun_out/kl$L.log" 2>&1 || exit $?
+    -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-north-star ${ENT_FLAG---no-entropy} ${BENCH_ARGS:-} > "$ROOT/gpurun_out/kl$L.log" 2>&1 || exit $?
   python3 - "$ROOT/gpurun_out/kl$L/run_kernel_stats.csv" "$L" "${KPAT:-k_}" <<'PY'
 import csv, re, sys
 for r in csv.DictReader(open(sys.argv[1])):

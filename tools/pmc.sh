@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-parity}"
+ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-north-star --no-parity}"
 cd /tmp
 timeout -k 10 120 rocprofv3 -L > "$ROOT/gpurun_out/pmc/counters_list.txt" 2>&1 || true
 i=0

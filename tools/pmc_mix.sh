@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); mkdir -p gpurun_out/pmcmix; export TMPDIR=/tmp
-ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-entropy}"
+ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-north-star --no-parity --no-entropy}"
 cd /tmp
 i=0
 while read -r group; do

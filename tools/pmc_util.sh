@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=gpurun_out/${PMC_TAG:-pmcutil}; mkdir -p $OUT; export TMPDIR=/tmp
-ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-entropy --no-host-path}"
+ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-north-star --no-parity --no-entropy --no-host-path}"
 cd /tmp
 i=0
 while read -r group; do

@@ -16,16 +16,16 @@ timeout -k 10 400 python bench.py --steps 20 --warmup 3 --no-entropy "$@" > "$OU
 rc=$?; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; stop bench $rc; }
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv \
-  -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-parity --no-entropy "$@" \
+  -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-north-star --no-parity --no-entropy "$@" \
   > "$OUT/stats.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || stop stats $rc
 [ "${NO_PMC:-0}" = 1 ] && { echo done; exit 0; }
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
-  -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-entropy "$@" \
+  -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-north-star --no-parity --no-entropy "$@" \
   > "$OUT/fetch.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || stop fetch $rc
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
-  -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-entropy "$@" \
+  -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-north-star --no-parity --no-entropy "$@" \
   > "$OUT/write.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || stop write $rc
 echo done

@@ -11,11 +11,11 @@ rc=$?; tail -1 gpurun_out/smoke_$TAG.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_$TAG.err; exit $rc; }
 python3 -c "import json;d=json.load(open('gpurun_out/bench_$TAG.json'));print('bench', d['value'], d['ms_per_step'], d['kernels_ms'], d['roofline']['frac'], d['fixups_last_step'])"
-timeout -k 10 300 python bench.py --sweep --no-cpu-baseline > gpurun_out/sweep_$TAG.json 2> gpurun_out/sweep_$TAG.err
+timeout -k 10 300 python bench.py --sweep --no-cpu-baseline --no-north-star > gpurun_out/sweep_$TAG.json 2> gpurun_out/sweep_$TAG.err
 rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/sweep_$TAG.err; exit $rc; }
 python3 -c "import json;d=json.load(open('gpurun_out/sweep_$TAG.json'));print('sweep', d['value'], d['ms_per_step'], d.get('parity'))"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run --output-format csv \
-  -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-entropy --no-host-path --no-parity > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1
+  -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-north-star --no-entropy --no-host-path --no-parity > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || { tail -5 "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log"; exit $rc; }
 echo done

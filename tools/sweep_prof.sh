@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; ROOT=$(pwd); mkdir -p gpurun_out; e
 for v in "$@"; do
   lib=$ROOT/tools/bin/ab/libjds_$v.so; [ "$v" = base ] && lib=$ROOT/jpeg-dsp-studio_amd/jds/libjds.so
   (cd /tmp && JDS_LIB_PATH=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/sprof_$v" -o run \
-    --output-format csv -- python3 "$ROOT/bench.py" --sweep --no-cpu-baseline > "$ROOT/gpurun_out/sprof_$v.log" 2>&1) || { echo "$v failed"; exit 1; }
+    --output-format csv -- python3 "$ROOT/bench.py" --sweep --no-cpu-baseline --no-north-star > "$ROOT/gpurun_out/sprof_$v.log" 2>&1) || { echo "$v failed"; exit 1; }
   f=$(find "$ROOT/gpurun_out/sprof_$v" -name '*kernel_stats.csv' | head -1)
   python3 - "$f" "$v" <<'PY'
 import csv, sys
