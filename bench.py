@@ -51,6 +51,9 @@ def parse():
     ap.add_argument('--block', type=int, default=8, choices=(8, 16),
                     help='16 = the configs[4] 16x16 stretch path (jds_fast16.hip certified fp32 forward, '
                          'jds_b16.hip fp64 inverse)')
+    ap.add_argument('--inv-fast', action='store_true',
+                    help='A/B: force the certified fast inverse (JDS_RUN_INV_FAST) where the plan would pick k_inv2 '
+                         '(4:4:4, coarse tables)')
     ap.add_argument('--exact', action='store_true',
                     help='all-fp64 kernels (JDS_RUN_EXACT) instead of the certified fast ones (A/B)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=20.0,
@@ -401,7 +404,7 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
     fwd_done = [torch.cuda.Event() for _ in range(NS)]
     used = [False] * NS
 
-    xflags = _abi.RUN_EXACT if args.exact else 0
+    xflags = (_abi.RUN_EXACT if args.exact else 0) | (_abi.RUN_INV_FAST if args.inv_fast else 0)
 
     def ptrs(b):
         return (rgbs[b].data_ptr(), outs[b].data_ptr(), coefs[b].data_ptr(), stats_l[b].data_ptr())
@@ -476,7 +479,7 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
     else:
         # the plan's inverse choice (jds_abi.hip inv_fast_ok): the certified fast
         # kernel for 4:2:x with a DC quantiser <= 60, k_inv2 otherwise
-        inv_fast = mcode != 0 and float(qt[0][0]) <= 60.0
+        inv_fast = (mcode != 0 and float(qt[0][0]) <= 60.0) or (args.inv_fast and not args.exact)
         # (k_fwd32 runs only for border tiles k_fwd32i cannot take: fold_rows in jds_fast.hip)
         kname = (f'k_fwd32i<{mcode},{pfs}> (+ k_fwd32 border tiles if any) + k_fwd_reduce + k_fix_fwd'
                  if dom == 'k_fwd' else (f'k_inv_fast<{mcode},0>' if inv_fast else f'k_inv2<{mcode},0>'))

@@ -128,6 +128,10 @@ struct jds_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  // host path: the device -> host copies run on a stream of their own beside
+  // the statistics kernels (SSIM, float32 magnitude bits) of the same call
+  hipStream_t xfer = nullptr;
+  hipEvent_t xfer_ev = nullptr;
   // host-path scratch
   DevBuf rgb, out, coeffs, stats, part, fq, gk, erry, errrgb, sel;
   DevBuf ss_planes, ss_map, ss_chunks, ss_out, img_a, img_b;
@@ -376,6 +380,11 @@ void jds_ctx_destroy(jds_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  if (c->xfer) {
+    (void)hipStreamSynchronize(c->xfer);
+    (void)hipStreamDestroy(c->xfer);
+  }
+  if (c->xfer_ev) (void)hipEventDestroy(c->xfer_ev);
   DevBuf* bufs[] = {&c->rgb,     &c->out,    &c->coeffs,    &c->stats,  &c->part,  &c->fq,   &c->gk,  &c->erry,
                     &c->errrgb,  &c->sel,    &c->ss_planes, &c->ss_map, &c->ss_chunks, &c->ss_out, &c->img_a, &c->img_b};
   for (DevBuf* b : bufs) b->release();
@@ -749,12 +758,15 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
                        (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
                        (double*)c->part.p, true, maps ? (double*)c->erry.p : nullptr,
                        maps ? (double*)c->errrgb.p : nullptr, dsel, sel_blk, s, c->ev, 3, 1, &gb));
-  HIP_TRY(hipMemcpyAsync(rgb_out, c->out.p, nimg, hipMemcpyDeviceToHost, s));
-  if (coeffs) HIP_TRY(hipMemcpyAsync(coeffs, c->coeffs.p, ncf * sizeof(int16_t), hipMemcpyDeviceToHost, s));
-  if (maps) {
-    HIP_TRY(hipMemcpyAsync(error_map_y, c->erry.p, npx * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(error_map_rgb, c->errrgb.p, npx * sizeof(double), hipMemcpyDeviceToHost, s));
+  // the outputs are final here: their copies to the caller's (pageable) arrays
+  // go on the transfer stream, so the statistics kernels queued below on `s`
+  // run while the host thread stages the copies
+  if (!c->xfer) {
+    HIP_TRY(hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->xfer_ev, hipEventDisableTiming));
   }
+  HIP_TRY(hipEventRecord(c->xfer_ev, s));
+  HIP_TRY(hipStreamWaitEvent(c->xfer, c->xfer_ev, 0));
   {
     // NumPy float32 magnitude_bits (utils/metrics.py:77-78)
     const long long nblk = g.cpf / 64;
@@ -768,8 +780,16 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
     if ((rc = run_ssim(c, (const uint8_t*)c->rgb.p, (const uint8_t*)c->out.p, (int)H, (int)W, &dst->ssim[0])))
       return rc;
   }
+  hipStream_t x = c->xfer;
+  HIP_TRY(hipMemcpyAsync(rgb_out, c->out.p, nimg, hipMemcpyDeviceToHost, x));
+  if (coeffs) HIP_TRY(hipMemcpyAsync(coeffs, c->coeffs.p, ncf * sizeof(int16_t), hipMemcpyDeviceToHost, x));
+  if (maps) {
+    HIP_TRY(hipMemcpyAsync(error_map_y, c->erry.p, npx * sizeof(double), hipMemcpyDeviceToHost, x));
+    HIP_TRY(hipMemcpyAsync(error_map_rgb, c->errrgb.p, npx * sizeof(double), hipMemcpyDeviceToHost, x));
+  }
   if (dsel) HIP_TRY(hipMemcpyAsync(sel, dsel, sizeof(jds_selected_block), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(stats, c->stats.p, sizeof(jds_frame_stats), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(x));
   HIP_TRY(hipStreamSynchronize(s));
   if (!(H >= 7 && W >= 7)) {
     for (int i = 0; i < 4; ++i) stats->ssim[i] = __builtin_nan("");
