@@ -128,6 +128,37 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
   }
 }
 
+// 4:4:4 colour of 8 pixels from the clipped fp64 planes in NumPy's order
+// (color_space.py:17-24: each expression left to right, contraction off),
+// clip + astype(uint8) (pipeline.py:95) into packed output bytes: the exact
+// path of k_inv_fast444's per-wave fallback (k_inv2's colour with no
+// upsample), in two halves so that Cb's registers are free before Cr's pass:
+// _cb writes B and G's first term Gt = Y - 0.344136 (Cb - 128), _cr adds R and
+// G = Gt - 0.714136 (Cr - 128).
+__device__ __forceinline__ void colour8_exact_cb(const double (&Yv)[8], const double (&Cb)[8], double (&Gt)[8],
+                                                 uint32_t (&pk)[6]) {
+#pragma unroll
+  for (int w = 0; w < 6; ++w) pk[w] = 0u;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const double B = Yv[k] + 1.772 * (Cb[k] - 128.0);
+    Gt[k] = Yv[k] - 0.344136 * (Cb[k] - 128.0);
+    const int b = 3 * k + 2;
+    pk[b >> 2] |= (uint32_t)clampi((int)B, 0, 255) << (8 * (b & 3));
+  }
+}
+__device__ __forceinline__ void colour8_exact_cr(const double (&Yv)[8], const double (&Gt)[8], const double (&Cr)[8],
+                                                 uint32_t (&pk)[6]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const double R = Yv[k] + 1.402 * (Cr[k] - 128.0);
+    const double G = Gt[k] - 0.714136 * (Cr[k] - 128.0);
+    const int b = 3 * k;
+    pk[b >> 2] |= (uint32_t)clampi((int)R, 0, 255) << (8 * (b & 3));
+    pk[(b + 1) >> 2] |= (uint32_t)clampi((int)G, 0, 255) << (8 * ((b + 1) & 3));
+  }
+}
+
 // XTRA: 0 = RGB only, 1 = + exact integer SSE and luma SSE partials,
 //       2 = + IntermediateData error maps (pipeline.py:117-122)
 // (XTRA = 2 is the single-frame host path: it trades occupancy for registers

@@ -537,6 +537,156 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
 #endif
 }
 
+// ------------------------------------------------- 4:4:4, wave-local --
+//
+// k_inv_fast444: without chroma subsampling every output sample reads only the
+// co-located block of each plane, so the inverse needs no chroma window, no
+// ring and no workgroup barrier: a wave owns 8 blocks (raster order over the
+// block grid), a block's 8 lanes run the column pass (lane = column), the
+// wave-local transpose and the row pass (lane = row) for Y, Cb and Cr in turn,
+// and each lane converts, certifies and stores its 8-pixel row.  The
+// certificate is k_inv_fast's (E = K_LIN * Dmax + K_CONST + 2^-31), with Dmax
+// over the block's own three planes; a wave with any uncertain value redoes
+// its 8 blocks in the exact replayed order (idct_col / idct_row /
+// colour8_exact, jds_inv_exact.hpp) and overwrites their rows.  (k_inv_fast's
+// tiled 4:4:4 form measured slower than k_inv2: 383 vs 332 us per 256 x 512^2,
+// its per-tile fixed costs spread over 2048 pixels.)
+constexpr int I444_WAVES = 4;
+
+__global__ void __launch_bounds__(64 * I444_WAVES)
+k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+              uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st, unsigned* __restrict__ fixcount,
+              unsigned* __restrict__ next_count, unsigned* __restrict__ item_cnt, const int rot, const int fix_all,
+              const int fin) {
+  __shared__ __attribute__((aligned(16))) double s_mid[8 * I444_WAVES * MS];
+  __shared__ double s_qs[64];
+  __shared__ int s_qi[64];
+  __shared__ double s_qmax;
+  const int tid = threadIdx.x, lv = tid & 7, lb = tid >> 3;
+  const int frame = blockIdx.y;
+  if (fin >= 0 && blockIdx.x == 0 && tid == 0) finalize_frame(g, st + frame, fin);
+  const unsigned n_items = gridDim.y;
+  unsigned* cnt_now = item_cnt + rot * n_items;
+  if (blockIdx.x == 0 && tid == 0) {
+    item_cnt[((rot + 1) % 3) * n_items + frame] = 0u;  // the next run's
+    if (frame == 0) *next_count = 0u;                  // the next run counts from zero
+  }
+  if (tid < 64) {
+    const double q = fq[frame].q[tid];
+    s_qs[tid] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
+    s_qi[tid] = (int)q;
+    double m = q;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (tid == 0) s_qmax = m;
+  }
+  __syncthreads();
+  const long long nblk = (long long)g.nby * g.nbx;
+  const long long blk = (long long)blockIdx.x * (8 * I444_WAVES) + lb;
+  const bool bvalid = blk < nblk;
+  const long long bq = bvalid ? blk : 0;
+  const int by = (int)(bq / g.nbx), bx = (int)(bq - (long long)by * g.nbx);
+  const int16_t* cf = coeffs + (size_t)frame * g.cpf;
+  double* slot = s_mid + lb * MS;
+  const Col16 qy = load_col(cf, bq * 64, lv, bvalid);
+  const Col16 qb = load_col(cf + g.off_cb, bq * 64, lv, bvalid);
+  const Col16 qr = load_col(cf + g.off_cr, bq * 64, lv, bvalid);
+  const int y = by * 8 + lv, x0 = bx * 8;
+  const bool row_ok = bvalid && y < g.H;
+  const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
+  uint8_t* o = rgb_out + (size_t)frame * g.H * g.W * 3 + ((size_t)y * g.W + x0) * 3;
+  const bool wide = nx == 8 && ((((uintptr_t)o) & 7u) == 0);
+  auto store = [&](const uint32_t (&pk)[6]) {
+    if (!row_ok) return;
+    if (wide) {
+      uint2* o2 = reinterpret_cast<uint2*>(o);
+      o2[0] = make_uint2(pk[0], pk[1]);
+      o2[1] = make_uint2(pk[2], pk[3]);
+      o2[2] = make_uint2(pk[4], pk[5]);
+    } else {
+#pragma unroll
+      for (int b = 0; b < 24; ++b)
+        if (b < 3 * nx) o[b] = (uint8_t)(pk[b >> 2] >> (8 * (b & 3)));
+    }
+  };
+
+  // ---- the certified fast pass ---------------------------------------------
+  int qhi = 0, qlo = 0;
+  uint32_t lo_min = 0xffffffffu, lo_max = 0u;
+  {
+    // chroma planes first, luma last, then the colour terms pixel by pixel
+    // (bytes packed as they come: fewer live registers than plane by plane)
+    double Cb[8], Cr[8], Yv[8];
+    fast_col(qb, s_qs, lv, slot, qhi, qlo);
+    __builtin_amdgcn_wave_barrier();
+    fast_row<-128>(slot, lv, Cb);  // Cb - 128
+    __builtin_amdgcn_wave_barrier();
+    fast_col(qr, s_qs, lv, slot, qhi, qlo);
+    __builtin_amdgcn_wave_barrier();
+    fast_row<-128>(slot, lv, Cr);  // Cr - 128
+    __builtin_amdgcn_wave_barrier();
+    fast_col(qy, s_qs, lv, slot, qhi, qlo);
+    __builtin_amdgcn_wave_barrier();
+    fast_row<-128>(slot, lv, Yv);  // Y - 128
+    uint32_t cb[24];  // channel words (byte in bits 0-7), output order R0 G0 B0 R1 ...
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const double y = Yv[k] + (MAGIC + 128.0);
+      cb[3 * k] = byte_cert_y(col_r(y, Cr[k]), lo_min, lo_max);
+      cb[3 * k + 1] = byte_cert_y(col_g(col_gt(y, Cb[k]), Cr[k]), lo_min, lo_max);
+      cb[3 * k + 2] = byte_cert_y(col_b(y, Cb[k]), lo_min, lo_max);
+    }
+    uint32_t pk[6];
+#pragma unroll
+    for (int w = 0; w < 6; ++w) pk[w] = pack4(cb[4 * w], cb[4 * w + 1], cb[4 * w + 2], cb[4 * w + 3]);
+    store(pk);
+  }
+  // the block's Dmax over its three planes (its 8 lanes), then this lane's margin
+  int qm = max(qhi, -qlo);
+#pragma unroll
+  for (int m = 1; m < 8; m <<= 1) qm = max(qm, __shfl_xor(qm, m, 64));
+  const double E = K_LIN * ((double)qm * s_qmax) + K_CONST + 0x1p-31;
+  const double T = ceil(E * 0x1p+32) + 1.0;
+  const bool unc = row_ok && ((double)lo_min <= T || (double)lo_max >= 0x1p+32 - 1.0 - T);
+#ifndef JDS_PROBE_NOFALLBACK
+  if (__ballot(unc || fix_all) == 0ull) return;  // (uniform) the wave's rows are certified
+
+  // ---- exact fallback: the wave's 8 blocks in the reference's order ---------
+  if ((tid & 63) == 0) {
+    atomicAdd(fixcount, 1u);  // waves recomputed (jds_plan_fix_counts)
+    atomicAdd(cnt_now + frame, 1u);
+  }
+  __builtin_amdgcn_wave_barrier();
+  {
+    // (the coefficients reloaded: keeping them live through the fast pass costs
+    // the common case registers; the empty asm hides the pointer's identity so
+    // the compiler cannot forward the first loads' values)
+    const int16_t* cf2 = cf;
+    asm volatile("" : "+v"(cf2));
+    double Yv[8], C[8], Gt[8];
+    uint32_t pk[6];
+    idct_col(load_col(cf2, bq * 64, lv, bvalid), s_qi, lv, slot);
+    __builtin_amdgcn_wave_barrier();
+    idct_row(slot, lv, Yv);
+    __builtin_amdgcn_wave_barrier();
+    idct_col(load_col(cf2 + g.off_cb, bq * 64, lv, bvalid), s_qi, lv, slot);
+    __builtin_amdgcn_wave_barrier();
+    idct_row(slot, lv, C);
+    __builtin_amdgcn_wave_barrier();
+    colour8_exact_cb(Yv, C, Gt, pk);
+    idct_col(load_col(cf2 + g.off_cr, bq * 64, lv, bvalid), s_qi, lv, slot);
+    __builtin_amdgcn_wave_barrier();
+    idct_row(slot, lv, C);
+    colour8_exact_cr(Yv, Gt, C, pk);
+    store(pk);
+  }
+#else
+  (void)unc;
+  (void)cnt_now;
+  (void)fixcount;
+#endif
+}
+
 // ------------------------------------------------------------ launchers --
 
 template <int MODE>
@@ -560,7 +710,17 @@ hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs,
   switch (mode) {
     case M420: return inv_fast_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div, fin);
     case M422: return inv_fast_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div, fin);
-    default: return inv_fast_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, fx, s, in_div, fin);
+    default: {
+      // 4:4:4: the wave-local kernel (SSE runs take the exact kernel, launch_codec)
+      (void)rgb_in;
+      (void)part;
+      (void)in_div;
+      const long long nblk = (long long)g.nby * g.nbx;
+      const dim3 grid((unsigned)((nblk + 8 * I444_WAVES - 1) / (8 * I444_WAVES)), n), blk(64 * I444_WAVES);
+      hipLaunchKernelGGL(k_inv_fast444, grid, blk, 0, s, g, coeffs, fq, rgb_out, st, fx.count + fx.parity,
+                         fx.count + (fx.parity ^ 1), fx.item, fx.rot, fx.fix_all, fin);
+      return hipGetLastError();
+    }
   }
 }
 

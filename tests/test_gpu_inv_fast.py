@@ -7,9 +7,9 @@ a rigorous bound (tools/inv_bound.py); tiles with an uncertain sample go
 through the exact kernel (k_inv2_list).  Bar: bit-identical bytes, SSE and
 luma SSE with the default (fast), JDS_RUN_EXACT_INV (exact) and
 JDS_RUN_INV_FIXALL (fast, then every tile recomputed by the exact tile code).
-Plans pick k_inv2 at 4:4:4 and for coarse tables (measured faster there);
-these tests force the fast kernel with JDS_RUN_INV_FAST, and the default
-route is checked separately."""
+Plans pick k_inv2 for coarse 4:2:x tables (measured faster there) and the
+wave-local k_inv_fast444 at 4:4:4; these tests force the fast kernels with
+JDS_RUN_INV_FAST, and the default route is checked separately."""
 import numpy as np
 import pytest
 
@@ -71,7 +71,7 @@ def test_fast_inverse_equals_exact_inverse_random(h, w, mode, pf):
     from jds import _abi
     qs = [1, 10, 50, 95, 100]
     frames = np.stack([cpu_ref.random_image(h, w, 700 + i) for i in range(len(qs))])
-    F = _abi.RUN_INV_FAST  # the plan would pick k_inv2 for these qualities / 4:4:4
+    F = _abi.RUN_INV_FAST  # the plan would pick k_inv2 for some of these 4:2:x qualities
     fast, exact, fixall = _plan(frames, qs, mode, pf, [F, _abi.RUN_EXACT_INV, F | _abi.RUN_INV_FIXALL])
     _same(fast, exact)
     _same(fixall, exact)
@@ -146,14 +146,17 @@ def test_fast_inverse_arbitrary_int16_coefficients(scale):
 
 
 @pytest.mark.parametrize('mode,q,fast', [('4:2:0', 50, True), ('4:2:2', 20, True), ('4:2:0', 10, False),
-                                         ('4:4:4', 50, False)])
+                                         ('4:4:4', 50, True), ('4:4:4', 10, True)])
 def test_default_inverse_route(mode, q, fast):
-    """The plan's own choice (fast inverse for 4:2:x with fine tables, k_inv2
-    otherwise) gives the exact kernel's bytes; the fix-up counter shows which
-    kernel ran (k_inv2 reports none)."""
+    """The plan's own choice (fast inverse at 4:4:4 and for 4:2:x with fine
+    tables, k_inv2 otherwise) gives the exact kernel's bytes; the fix-up
+    counter shows which kernel ran (k_inv2 reports none, the fast kernels list
+    the checkerboard's ties)."""
     from jds import _abi
     frames = np.stack([cpu_ref.generate_colored_checkerboard(256)] * 2)  # ties: the fast kernel lists tiles
     dflt, exact = _plan(frames, [q, q], mode, mode != '4:4:4', [0, _abi.RUN_EXACT_INV])
     _same(dflt, exact)
     if not fast:
         assert dflt[3][1] == 0
+    else:
+        assert dflt[3][1] > 0
