@@ -53,7 +53,9 @@ def parse():
                          'jds_b16.hip fp64 inverse)')
     ap.add_argument('--inv-fast', action='store_true',
                     help='A/B: force the certified fast inverse (JDS_RUN_INV_FAST) where the plan would pick k_inv2 '
-                         '(4:4:4, coarse tables)')
+                         '(coarse tables) or k_inv16s (16x16 blocks: k_inv16_fast)')
+    ap.add_argument('--exact-inv', action='store_true',
+                    help='A/B: force the exact replayed-order inverse (JDS_RUN_EXACT_INV: k_inv2 / k_inv16s)')
     ap.add_argument('--exact', action='store_true',
                     help='all-fp64 kernels (JDS_RUN_EXACT) instead of the certified fast ones (A/B)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=20.0,
@@ -404,7 +406,8 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
     fwd_done = [torch.cuda.Event() for _ in range(NS)]
     used = [False] * NS
 
-    xflags = (_abi.RUN_EXACT if args.exact else 0) | (_abi.RUN_INV_FAST if args.inv_fast else 0)
+    xflags = ((_abi.RUN_EXACT if args.exact else 0) | (_abi.RUN_INV_FAST if args.inv_fast else 0) |
+              (_abi.RUN_EXACT_INV if args.exact_inv else 0))
 
     def ptrs(b):
         return (rgbs[b].data_ptr(), outs[b].data_ptr(), coefs[b].data_ptr(), stats_l[b].data_ptr())
@@ -475,14 +478,19 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
         if dom == 'k_fwd':
             kname = f'k_fwd16<{mcode},{pfs}>' if args.exact else f'k_fwd16f<{mcode},{pfs}> + k_fix_fwd16<{mcode},{pfs}>'
         else:
-            kname = f'k_inv16f<{mcode},0>' if mcode else f'k_chroma16<{mcode}> + k_inv16<{mcode}>'
+            # the plan's 16x16 inverse: exact k_inv16s; the certified k_inv16_fast with --inv-fast
+            kname = ((f'k_inv16_fast<{mcode}>' if args.inv_fast and not (args.exact or args.exact_inv)
+                      else f'k_inv16s<{mcode},0>') if mcode
+                     else f'k_chroma16<{mcode}> + k_inv16<{mcode}>')
     else:
         # the plan's inverse choice (jds_abi.hip inv_fast_ok): the certified fast
-        # kernel for 4:2:x with a DC quantiser <= 60, k_inv2 otherwise
-        inv_fast = (mcode != 0 and float(qt[0][0]) <= 60.0) or (args.inv_fast and not args.exact)
+        # kernel for 4:2:x with a DC quantiser <= 60 and the wave-local
+        # k_inv_fast444 at every 4:4:4 quality, k_inv2 otherwise
+        inv_fast = (mcode == 0 or float(qt[0][0]) <= 60.0 or args.inv_fast) and not (args.exact or args.exact_inv)
         # (k_fwd32 runs only for border tiles k_fwd32i cannot take: fold_rows in jds_fast.hip)
         kname = (f'k_fwd32i<{mcode},{pfs}> (+ k_fwd32 border tiles if any) + k_fwd_reduce + k_fix_fwd'
-                 if dom == 'k_fwd' else (f'k_inv_fast<{mcode},0>' if inv_fast else f'k_inv2<{mcode},0>'))
+                 if dom == 'k_fwd' else ((('k_inv_fast444' if mcode == 0 else f'k_inv_fast<{mcode},0>') if inv_fast
+                                          else f'k_inv2<{mcode},0>')))
     traffic = None
     tf = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tf):

@@ -274,6 +274,12 @@ int jds_selftest_fwd16(int32_t subsampling, int32_t prefilter, const double* gau
 int jds_selftest_inv_fast(int32_t subsampling, const int16_t* coeffs, const double* qtable, int64_t H, int64_t W,
                           int32_t fuse, double* values, uint8_t* bytes);
 
+/* Test-only: the same for 16x16 blocks (k_inv16_fast's chain: fidct16 lines,
+ * coefficients in 16x16 blocks, Q16[u][v] = qtable[u/2][v/2]); pins
+ * tools/inv_bound.py --b16's K_LIN16 / K_CONST16 on the CPU. */
+int jds_selftest_inv_fast16(int32_t subsampling, const int16_t* coeffs, const double* qtable, int64_t H, int64_t W,
+                            int32_t fuse, double* values, uint8_t* bytes);
+
 /* Test-only: the host-built cv2 INTER_AREA table of one axis (OpenCV
  * computeResizeAreaTab, used by the odd-size path) for src -> dst samples:
  * per destination index its tap count n[d] (<= 4) and taps si[4d..], a[4d..].

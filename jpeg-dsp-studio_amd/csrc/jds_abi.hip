@@ -51,7 +51,8 @@ void fast_fwd_bounds(int mode, bool pf, const double* gk, double* E);
 int fwd32_host_plane(int mode, bool pf, const double* gk, const uint8_t* rgb, int H, int W, int plane,
                      int flags, float* out);
 void fast_fwd_thresholds(const double* Q, int mode, bool pf, const double* gk, float* rq, float* thr);
-int inv_fast_host(int mode, const int16_t* cf, const double* Q, int H, int W, int fuse, double* vout, uint8_t* bout);
+int inv_fast_host(int mode, const int16_t* cf, const double* Q, int H, int W, int fuse, int block, double* vout,
+                  uint8_t* bout);
 size_t fast_q_size();
 hipError_t stage_rgb_ycc(const double* in, double* out, long long n, int inverse, hipStream_t s);
 hipError_t stage_subsample(const double* in, double* tmp, double* tmp2, double* out, int H, int W, int sy,
@@ -73,7 +74,7 @@ hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* cons
 hipError_t launch_codec16(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                           int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st, double* part,
                           double* planes, bool want_sse, double* err_y, double* err_rgb, hipStream_t s,
-                          hipEvent_t* ev, int phases, const Fwd16Fast* ff);
+                          hipEvent_t* ev, int phases, const Fwd16Fast* ff, const InvFix* fx);
 void fast_fwd16_bounds(int mode, bool pf, const double* gk, double* E);
 void fast_fwd16_thresholds(const double* Q8, int mode, bool pf, const double* gk, void* out);
 size_t fast_q16_size();
@@ -170,8 +171,9 @@ struct jds_plan {
   // whose tables are not coarse.  Coarse tables (DC quantiser > 60: quality
   // below ~14 on the standard table) put most tiles on the exact path
   // (reconstructions land on integers), where k_inv2 beats k_inv_fast's
-  // in-kernel fallback (4K 4:2:0: Q10 373 vs 396 us; Q20 376 vs 347); at 4:4:4
-  // k_inv2 is faster outright (512x512 x 256: 337 vs 391 us).
+  // in-kernel fallback (4K 4:2:0: Q10 373 vs 396 us; Q20 376 vs 347).  At
+  // 4:4:4 the wave-local k_inv_fast444 is faster at every quality (512x512 x
+  // 256: 167.5 vs k_inv2's 331.8 us).
   bool inv_fast_ok = true;
   bool last_fwd16_fast = false;  // 16x16: the last forward was the certified fp32 one
   unsigned fwd16_runs = 0;       // 16x16 certified forward runs so far: picks the list counter
@@ -501,6 +503,8 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
             hipSuccess ||
         (e = p->fq32.ensure(fqs * n)) != hipSuccess || (e = p->gk32.ensure(sizeof gk32)) != hipSuccess ||
         (e = p->fixlist.ensure(8 * nblk)) != hipSuccess || (e = p->counters.ensure(64)) != hipSuccess ||
+        (e = p->invfix.ensure(64 + 12 * (size_t)n)) != hipSuccess ||
+        (e = hipMemset(p->invfix.p, 0, 64 + 12 * (size_t)n)) != hipSuccess ||
         (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * g.tiles_y * g.tiles_x)) != hipSuccess ||
         (e = hipMemcpy(p->fq32.p, h16, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess ||
@@ -566,9 +570,12 @@ int jds_plan_fix_counts(const jds_plan* p, uint32_t* counts) {
   // invfix[0]: tiles the last run's certified inverse handed to the exact kernel
   counts[0] = counts[1] = 0u;
   if (p->g.bs == 16) {  // counters[2]: blocks the last certified 16x16 forward recomputed
-    if (!p->last_fwd16_fast) return JDS_OK;
     hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(counts, (const uint32_t*)p->counters.p + 2, 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && p->last_fwd16_fast)
+      e = hipMemcpy(counts, (const uint32_t*)p->counters.p + 2, 4, hipMemcpyDeviceToHost);
+    // and the tiles the last k_inv16_fast run handed to the exact tile body
+    if (e == hipSuccess && p->last_inv_fast)
+      e = hipMemcpy(counts + 1, (const uint32_t*)p->invfix.p + ((p->inv_runs + 1u) & 1u), 4, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return fail(JDS_EHIP, "fix_counts: %s", hipGetErrorString(e));
     return JDS_OK;
   }
@@ -624,12 +631,25 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
                        (unsigned*)p->counters.p,
                        (flags & JDS_RUN_FWD_FIXALL) ? 1 : 0, (int)(p->fwd16_runs & 1u)};
     if (phases & 1) HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
+    // the certified fast inverse (k_inv16_fast) on request (JDS_RUN_INV_FAST)
+    // for 4:2:x runs without SSE terms: measured level with the exact k_inv16s
+    // (configs[4]: 524-526 vs 520-522 us, same box), both held by their LDS
+    // footprint to 3 workgroups per CU, so the plan keeps the exact kernel
+    InvFix fx16 = p->inv_fix();
+    fx16.fix_all = (flags & JDS_RUN_INV_FIXALL) ? 1 : 0;
+    const bool fast_inv16 = (phases & 2) && (flags & JDS_RUN_INV_FAST) && !exact && !(flags & JDS_RUN_EXACT_INV) &&
+                            !(flags & JDS_RUN_SSE) && p->mode != JDS_SS_444 && p->invfix.p;
     HIP_TRY(launch_codec16(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                            (const double*)p->gk.p, stats, (double*)p->part.p, (double*)p->planes.p,
-                           (flags & JDS_RUN_SSE) != 0, nullptr, nullptr, s, nullptr, phases, exact ? nullptr : &ff));
+                           (flags & JDS_RUN_SSE) != 0, nullptr, nullptr, s, nullptr, phases, exact ? nullptr : &ff,
+                           fast_inv16 ? &fx16 : nullptr));
     if (phases & 1) {
       p->last_fwd16_fast = !exact;
       if (!exact) p->fwd16_runs++;
+    }
+    if (phases & 2) {
+      p->last_inv_fast = fast_inv16;
+      if (fast_inv16) p->inv_runs++;
     }
     return JDS_OK;
   }
@@ -755,7 +775,7 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
     HIP_TRY(launch_codec16(mode, pf, g, 1, (const uint8_t*)c->rgb.p, (uint8_t*)c->out.p, (int16_t*)c->coeffs.p,
                            (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
                            (double*)c->part.p, (double*)c->planes.p, true, maps ? (double*)c->erry.p : nullptr,
-                           maps ? (double*)c->errrgb.p : nullptr, s, c->ev, 3, nullptr));
+                           maps ? (double*)c->errrgb.p : nullptr, s, c->ev, 3, nullptr, nullptr));
   } else
   HIP_TRY(launch_codec(mode, pf, g, 1, (const uint8_t*)c->rgb.p, (uint8_t*)c->out.p, (int16_t*)c->coeffs.p,
                        (const FrameQ*)c->fq.p, (const double*)c->gk.p, (jds_frame_stats*)c->stats.p,
@@ -1199,7 +1219,17 @@ int jds_selftest_inv_fast(int32_t subsampling, const int16_t* coeffs, const doub
   if (!coeffs || !qtable || !values || !bytes || H < 1 || W < 1 || H > 4096 || W > 4096 ||
       subsampling < JDS_SS_444 || subsampling > JDS_SS_420)
     return fail(JDS_EINVAL, "bad argument");
-  if (inv_fast_host(subsampling, coeffs, qtable, (int)H, (int)W, fuse, values, bytes))
+  if (inv_fast_host(subsampling, coeffs, qtable, (int)H, (int)W, fuse, 8, values, bytes))
+    return fail(JDS_EINVAL, "odd chroma geometry: the certified inverse runs even sizes only");
+  return JDS_OK;
+}
+
+int jds_selftest_inv_fast16(int32_t subsampling, const int16_t* coeffs, const double* qtable, int64_t H, int64_t W,
+                            int32_t fuse, double* values, uint8_t* bytes) {
+  if (!coeffs || !qtable || !values || !bytes || H < 1 || W < 1 || H > 4096 || W > 4096 ||
+      subsampling < JDS_SS_444 || subsampling > JDS_SS_420)
+    return fail(JDS_EINVAL, "bad argument");
+  if (inv_fast_host(subsampling, coeffs, qtable, (int)H, (int)W, fuse, 16, values, bytes))
     return fail(JDS_EINVAL, "odd chroma geometry: the certified inverse runs even sizes only");
   return JDS_OK;
 }

@@ -51,6 +51,7 @@
 #include "jds_internal.hpp"
 #include "jds_inv_common.hpp"
 #include "jds_inv_exact.hpp"
+#include "jds_inv16_exact.hpp"
 
 // every fusion the compiler forms is covered by the bound (two roundings per
 // fused pair); reassociation stays off
@@ -63,6 +64,9 @@ namespace jds {
 // (tests/test_inv_bound_cpu.py asserts kernel >= model)
 constexpr double K_LIN = 1.103043e-12 * 1.01;
 constexpr double K_CONST = 1.081459e-12 * 1.01;
+// the same for 16x16 blocks (fidct16 vs dct3_line16, tools/inv_bound.py --b16)
+constexpr double K_LIN16 = 4.268828e-12 * 1.01;
+constexpr double K_CONST16 = 1.081459e-12 * 1.01;
 
 // AAN scale factors a_k = sqrt(2) cos(k pi / 16), a_0 = 1 (correctly rounded;
 // tools/inv_bound.py reads them from this list and prices their representation
@@ -76,6 +80,18 @@ constexpr double F_SQ2 = 0x1.6a09e667f3bcdp+0;   // sqrt(2)
 constexpr double F_A2C2 = 0x1.d906bcf328d46p+0;  // 2 cos(pi/8)
 constexpr double F_K10 = 0x1.1517a7bdb3895p+0;   // 2 (cos(pi/8) - cos(3pi/8))
 constexpr double F_K12 = 0x1.4e7ae9144f0fcp+1;   // 2 (cos(pi/8) + cos(3pi/8))
+
+// 16-point lines (fidct16, the 16x16 stretch path): odd-part pre-scales
+// cos(j pi / 16), j = 1..7, and post-scales sqrt(2) / (8 cos((2n+1) pi / 32)),
+// n = 0..7 (correctly rounded; tools/inv_bound.py --b16 reads both lists)
+#define JDS_F16_PRE_LIST                                                                                     \
+  0x1.f6297cff75cb0p-1, 0x1.d906bcf328d46p-1, 0x1.a9b66290ea1a3p-1, 0x1.6a09e667f3bcdp-1, 0x1.1c73b39ae68c8p-1, \
+      0x1.87de2a6aea963p-2, 0x1.8f8b83c69a60bp-3
+#define JDS_F16_POST_LIST                                                                                    \
+  0x1.6bca591d6776cp-3, 0x1.7a54542b3c092p-3, 0x1.9a82e694c86a2p-3, 0x1.d45957fdd6b90p-3, 0x1.1d57ab02f5b32p-2, \
+      0x1.80019f8d550e5p-2, 0x1.37cbd5ba8838cp-1, 0x1.cdb4095cb49fcp+0
+constexpr double F16_PRE[8] = {1.0, JDS_F16_PRE_LIST};  // [0]: W_0 = Z_0 unscaled
+constexpr double F16_POST[8] = {JDS_F16_POST_LIST};
 
 // The chain's multiply-adds go through a policy so that the host restatement
 // (jds_selftest_inv_fast, tests/test_inv_bound_cpu.py) runs the same source:
@@ -687,6 +703,344 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
 #endif
 }
 
+// ------------------------------------------------ 16 x 16 blocks (4:2:x) --
+//
+// fidct16: the orthonormal 16-point IDCT on scaled inputs.  Even outputs of
+// the split x_n = E_n + O_n, x_{15-n} = E_n - O_n (n < 8): E is the 8-point
+// IDCT of the even coefficients / sqrt(2), i.e. aan8 on inputs pre-scaled by
+// a_m / 4 (folded into the dequantisation table with the other axis's
+// scale); O_n = sqrt(2)/4 sum_m Z_m cos((2n+1)(2m+1) pi / 32) of the odd
+// coefficients Z_m comes from Lee's identity 2 cos(t) cos((2m+1) t) =
+// cos(2(m+1) t) + cos(2m t): 2 cos(t_n) sum_m Z_m cos((2m+1) t_n) is the
+// unnormalised 8-point DCT-III of W_0 = Z_0, W_j = Z_{j-1} + Z_j, i.e. aan8 on
+// W_j cos(j pi / 16) (W_0 unscaled), then scaled by
+// p_n = sqrt(2) / (8 cos((2n+1) pi / 32)).  92 operations per line against
+// dct3_line16's 144 (tools/inv_bound.py fast16_line models this sequence and
+// checks the linear forms against the orthonormal IDCT).
+template <class M = MadDev>
+__host__ __device__ __forceinline__ void fidct16(double (&c)[16]) {
+  double e[8], w[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) e[m] = c[2 * m];
+  aan8<M>(e);
+  w[0] = c[1];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) w[j] = (c[2 * j - 1] + c[2 * j + 1]) * F16_PRE[j];
+  aan8<M>(w);
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    c[n] = M::mad(w[n], F16_POST[n], e[n]);
+    c[15 - n] = M::mad(w[n], -F16_POST[n], e[n]);
+  }
+}
+
+// fidct16's per-axis input scale of coefficient index k: a_{k/2} / 4 (even),
+// 1 (odd); the table entry is (Q16 * s_u) * s_v
+__host__ __device__ __forceinline__ double s16_of(const double* aan, int k) {
+  return (k & 1) ? 1.0 : aan[k >> 1] * 0.25;
+}
+
+// Dequantise and 2-D fidct16 (axis 0, then axis 1) of one 16x16 block held by
+// its 16 lanes (line = 0..15) through the block's LDS slot (k_inv16s's
+// exchange, rows of RS16); returns row `line` clipped to [-128, 127] (no +128:
+// luma adds it on the magic grid, chroma stays shifted).  The dequantised
+// input is ((q * Q16) * s_u) * s_v: q * Q16 an exact integer (|q Q| < 2^23,
+// v_mul_i32_i24), then the two per-axis scales (s_u the lane's own, s_v a
+// constant per unrolled k): no table in LDS, which keeps the kernel at three
+// workgroups per CU.  qi: the frame's 8x8 table as integers; qhi / qlo track the
+// coefficients the lane read.
+__device__ __forceinline__ void fidct16_block(const Row16& rw, const int* __restrict__ qi, double* __restrict__ sb,
+                                              int line, double (&r)[16], int& qhi, int& qlo) {
+  {
+    const uint32_t w[8] = {rw.a.x, rw.a.y, rw.a.z, rw.a.w, rw.b.x, rw.b.y, rw.b.z, rw.b.w};
+    const double su = s16_of(c_aan, line);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int qv = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
+      qhi = max(qhi, qv);
+      qlo = min(qlo, qv);
+      sb[line * RS16 + k] = ((double)__mul24(qv, qi[(line >> 1) * 8 + (k >> 1)]) * su) * s16_of(c_aan, k);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  double c[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) c[i] = sb[i * RS16 + line];
+  fidct16(c);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sb[i * RS16 + line] = c[i];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) c[k] = sb[line * RS16 + k];
+  fidct16(c);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) r[k] = fmin(fmax(c[k], -128.0), 127.0);
+}
+
+// byte_cert_y for a value that may lie outside the image (ok false: the byte
+// is not stored and the value stays out of the certificate)
+__device__ __forceinline__ uint32_t byte_cert_m(double y, bool ok, uint32_t& lo_min, uint32_t& lo_max) {
+  const uint32_t lo = ok ? (uint32_t)__double2loint(y) : 0x80000000u, hi = (uint32_t)__double2hiint(y);
+  lo_min = lo_min < lo ? lo_min : lo;
+  lo_max = lo_max > lo ? lo_max : lo;
+  const uint32_t c = hi < MAGIC_HI ? MAGIC_HI : hi;
+  return c > MAGIC_HI + 255u ? MAGIC_HI + 255u : c;
+}
+
+// k_inv16_fast<MODE>: the certified fast inverse for 16x16 blocks at 4:2:x
+// (plan runs without SSE terms; BASELINE configs[4]).  k_inv16s's tile, window
+// and exchange layout (jds_inv16_exact.hpp: one chroma window at a time in
+// LDS, Cb then Cr), with k_inv_fast's arithmetic: the folded dequantisation
+// table, fidct16 lines, both planes clipped to [-128, 127], the difference
+// form upsample (fvblend / fhblend), the colour terms on the magic grid and
+// byte_cert_y's certificate, E = K_LIN16 * Dmax + K_CONST16 + 2^-31
+// (tools/inv_bound.py --b16; tests/test_inv_bound_cpu.py runs this chain on
+// the host against the oracle).  A tile with an uncertain value is recomputed
+// by k_inv16s's exact body (inv16s_tile) in the same LDS.
+template <int MODE>
+__global__ void __launch_bounds__(Inv16<MODE>::NT)
+k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+             uint8_t* __restrict__ rgb_out, unsigned* __restrict__ fixcount, unsigned* __restrict__ next_count,
+             unsigned* __restrict__ item_cnt, const int rot, const int fix_all) {
+  using I = Inv16<MODE>;
+  static_assert(I::NT == 256, "one table entry per thread");
+  __shared__ __attribute__((aligned(16))) double s_b[I::NG * BS16];
+  __shared__ double s_cw[I::CWR * I::CWC];
+  __shared__ int s_qi[64];  // (the exact fallback reads the 8x8 table from fq: 3 workgroups per CU at 4:2:2)
+  __shared__ double s_qmax;
+  __shared__ double s_dq[I::NT / 64];
+  __shared__ uint32_t s_lmin[I::NT / 64], s_lmax[I::NT / 64];
+  __shared__ int s_redo;
+  const int tid = threadIdx.x, grp = tid >> 4, line = tid & 15;
+  const int frame = blockIdx.y, tile = blockIdx.x;
+  const unsigned n_items = gridDim.y;
+  unsigned* cnt_now = item_cnt + rot * n_items;
+  if (tile == 0 && tid == 0) {
+    item_cnt[((rot + 1) % 3) * n_items + frame] = 0u;  // the next run's
+    if (frame == 0) *next_count = 0u;                  // the next run counts from zero
+  }
+  if (tid < 64) {
+    double m = fq[frame].q[tid];
+    s_qi[tid] = (int)m;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (tid == 0) s_qmax = m;
+  }
+  __syncthreads();
+
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int Y0 = ty * I::TH, X0 = tx * I::TW;
+  const int16_t* cf = coeffs + (size_t)frame * g.cpf;
+  const int cwy0 = Y0 / I::SY - I::RY, cwx0 = X0 / 2 - 1;
+  const int cby0 = (Y0 / I::SY) / 16 - I::RY, cbx0 = (X0 / 2) / 16 - 1;
+  double* const sb = s_b + grp * BS16;
+  constexpr int NCR = (I::NCB + I::NG - 1) / I::NG;  // chroma rounds per plane
+  Row16 crow[2][NCR];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll
+    for (int k = 0; k < NCR; ++k) {
+      const int bi = k * I::NG + grp;
+      const int by = cby0 + bi / I::CBC, bx = cbx0 + bi % I::CBC;
+      if (bi < I::NCB && by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx)
+        crow[p][k] = load_row16(cf + (p ? g.off_cr : g.off_cb) + ((long long)by * g.ncx + bx) * 256, line);
+    }
+  }
+  const int by = Y0 / 16 + grp / I::YBC, bx = X0 / 16 + grp % I::YBC;
+  Row16 lrow;
+  if (by < g.nby && bx < g.nbx) lrow = load_row16(cf + ((long long)by * g.nbx + bx) * 256, line);
+
+  int qhi = 0, qlo = 0;
+  auto build = [&](int p) {  // plane p's window: (C - 128) of the blocks the tile reaches (+ ring)
+#pragma unroll
+    for (int k = 0; k < NCR; ++k) {
+      const int bi = k * I::NG + grp;
+      if (bi < I::NCB) {
+        const int cy = cby0 + bi / I::CBC, cx = cbx0 + bi % I::CBC;
+        if (cy >= 0 && cx >= 0 && cy < g.ncy && cx < g.ncx) {  // uniform per 16-lane group
+          double r[16];
+          fidct16_block(crow[p][k], s_qi, sb, line, r, qhi, qlo);
+          const int wr = cy * 16 + line - cwy0;
+          if ((unsigned)wr < (unsigned)I::CWR) {
+            double* w = &s_cw[wr * I::CWC];
+            const int wc0 = cx * 16 - cwx0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+              if ((unsigned)(wc0 + j) < (unsigned)I::CWC) w[wc0 + j] = r[j];
+          }
+        }
+      }
+    }
+  };
+  // one plane's upsampled (C - 128) at pixels x0 .. x0 + 7 of row (wq, wt)
+  // (chroma8_fast's blends; cv2's clamped taps at the image's edge pixels
+  // take the edge sample, as in k_inv16s)
+  auto upsample = [&](int x0, int wq, int wt, double (&C)[8]) {
+    const int c0 = x0 / 2 - 1 - cwx0;
+    double vb[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      if constexpr (I::SY == 2)
+        vb[j] = fvblend(s_cw[wq * I::CWC + c0 + j], s_cw[wt * I::CWC + c0 + j]);
+      else
+        vb[j] = s_cw[wq * I::CWC + c0 + j];
+    }
+    double d[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) d[j] = vb[j] - vb[j + 1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      C[2 * i] = fhblend(d[i], 0.25, vb[i + 1]);
+      C[2 * i + 1] = fhblend(d[i + 1], -0.25, vb[i + 1]);
+    }
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int kl = side == 0 ? (x0 == 0 ? 0 : -1) : (g.W - 1 - x0 < 8 ? g.W - 1 - x0 : -1);
+      if (kl >= 0) {
+        const int e = (side == 0 ? 0 : g.wc - 1) - cwx0;
+        double v = s_cw[wq * I::CWC + e];
+        if constexpr (I::SY == 2) v = fvblend(v, s_cw[wt * I::CWC + e]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) C[k] = k == kl ? v : C[k];
+      }
+    }
+  };
+
+  // ---- 1. Cb window; luma row, B bytes and the G partial on the grid -------
+  build(0);
+  __syncthreads();
+  const int y = by * 16 + line;
+  const bool act = by < g.nby && bx < g.nbx;  // uniform per 16-lane group
+  const bool rowok = act && y < g.H;
+  uint32_t lo_min = 0xffffffffu, lo_max = 0u;
+  double Yv[16], Gt[16];
+  uint32_t bpk[4] = {0u, 0u, 0u, 0u};  // B bytes of the row, packed
+  int wq = 0, wt = 0;
+  if (act) fidct16_block(lrow, s_qi, sb, line, Yv, qhi, qlo);
+  if (rowok) {
+    if constexpr (I::SY == 2) {  // cv2 INTER_LINEAR rows (k_inv16s): wq weight 1/4, wt weight 3/4
+      float fy = (float)((y + 0.5) * g.up_sy - 0.5);
+      const int sy = (int)floorf(fy);
+      fy -= (float)sy;
+      const int r0 = clampi(clampi(sy, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+      const int r1 = clampi(clampi(sy + 1, 0, g.hc - 1) - cwy0, 0, I::CWR - 1);
+      const bool q0 = fy == 0.75f;
+      wq = q0 ? r0 : r1;
+      wt = q0 ? r1 : r0;
+    } else {
+      wq = y - cwy0;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int x0 = bx * 16 + 8 * h;
+      if (x0 < g.W) {
+        double C[8];
+        upsample(x0, wq, wt, C);
+        uint32_t cb[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const double yv = Yv[8 * h + k] + (MAGIC + 128.0);
+          Yv[8 * h + k] = yv;
+          cb[k] = byte_cert_m(col_b(yv, C[k]), x0 + k < g.W, lo_min, lo_max);
+          Gt[8 * h + k] = col_gt(yv, C[k]);
+        }
+        bpk[2 * h] = pack4(cb[0], cb[1], cb[2], cb[3]);
+        bpk[2 * h + 1] = pack4(cb[4], cb[5], cb[6], cb[7]);
+      }
+    }
+  }
+  __syncthreads();  // every Cb read done
+  // ---- 2. Cr window; R, G bytes and the stores --------------------------------
+  build(1);
+  __syncthreads();
+  uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
+  if (rowok) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int x0 = bx * 16 + 8 * h;
+      if (x0 < g.W) {
+        double C[8];
+        upsample(x0, wq, wt, C);
+        const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
+        uint32_t ch[24];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const bool ok = k < nx;
+          ch[3 * k] = byte_cert_m(col_r(Yv[8 * h + k], C[k]), ok, lo_min, lo_max);
+          ch[3 * k + 1] = byte_cert_m(col_g(Gt[8 * h + k], C[k]), ok, lo_min, lo_max);
+          ch[3 * k + 2] = (bpk[2 * h + (k >> 2)] >> (8 * (k & 3))) & 255u;
+        }
+        uint32_t pk[6];
+#pragma unroll
+        for (int w = 0; w < 6; ++w) pk[w] = pack4(ch[4 * w], ch[4 * w + 1], ch[4 * w + 2], ch[4 * w + 3]);
+        uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
+        if (nx == 8 && ((((uintptr_t)o) & 7u) == 0)) {
+          uint2* o2 = reinterpret_cast<uint2*>(o);
+          o2[0] = make_uint2(pk[0], pk[1]);
+          o2[1] = make_uint2(pk[2], pk[3]);
+          o2[2] = make_uint2(pk[4], pk[5]);
+        } else {
+#pragma unroll
+          for (int b = 0; b < 24; ++b)
+            if (b < 3 * nx) o[b] = (uint8_t)(pk[b >> 2] >> (8 * (b & 3)));
+        }
+      }
+    }
+  }
+
+  // ---- 3. certification: the tile's closest approach to an integer vs its bound
+  int qm = max(qhi, -qlo);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t a = __shfl_xor(lo_min, o, 64), b = __shfl_xor(lo_max, o, 64);
+    lo_min = lo_min < a ? lo_min : a;
+    lo_max = lo_max > b ? lo_max : b;
+    qm = max(qm, __shfl_xor(qm, o, 64));
+  }
+  if ((tid & 63) == 0) {
+    s_lmin[tid >> 6] = lo_min;
+    s_lmax[tid >> 6] = lo_max;
+    s_dq[tid >> 6] = (double)qm;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t mn = 0xffffffffu, mx = 0u;
+    double q = 0.0;
+    for (int i = 0; i < I::NT / 64; ++i) {
+      mn = mn < s_lmin[i] ? mn : s_lmin[i];
+      mx = mx > s_lmax[i] ? mx : s_lmax[i];
+      q = fmax(q, s_dq[i]);
+    }
+    const double E = K_LIN16 * (q * s_qmax) + K_CONST16 + 0x1p-31;
+    const double T = ceil(E * 0x1p+32) + 1.0;
+    const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
+    s_redo = uncertain || fix_all;
+    if (s_redo) {
+      atomicAdd(fixcount, 1u);  // tiles recomputed (jds_plan_fix_counts)
+      atomicAdd(cnt_now + frame, 1u);
+    }
+  }
+  __syncthreads();
+#ifndef JDS_PROBE_NOFALLBACK
+  if (s_redo)  // (uniform) the exact tile body overwrites the tile
+    inv16s_tile<MODE, 0>(s_b, s_cw, fq[frame].q, nullptr, nullptr, g, tiles_x, (int)gridDim.x, frame, tile, coeffs,
+                         nullptr, rgb_out, nullptr, nullptr, nullptr, nullptr);
+#endif
+}
+
+hipError_t launch_inv16_fast(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
+                             uint8_t* rgb_out, const InvFix& fx, hipStream_t s) {
+  auto go = [&](auto kern, int TH, int TW) {
+    const int tx = (g.W + TW - 1) / TW, ty = (g.H + TH - 1) / TH;
+    hipLaunchKernelGGL(kern, dim3(ty * tx, n), dim3(256), 0, s, g, tx, coeffs, fq, rgb_out, fx.count + fx.parity,
+                       fx.count + (fx.parity ^ 1), fx.item, fx.rot, fx.fix_all);
+    return hipGetLastError();
+  };
+  if (mode == M420) return go(k_inv16_fast<M420>, Inv16<M420>::TH, Inv16<M420>::TW);
+  if (mode == M422) return go(k_inv16_fast<M422>, Inv16<M422>::TH, Inv16<M422>::TW);
+  return hipErrorInvalidValue;  // 4:4:4 keeps k_chroma16 + k_inv16
+}
+
 // ------------------------------------------------------------ launchers --
 
 template <int MODE>
@@ -726,47 +1080,62 @@ hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs,
 
 // ------------------------------------------- host: the chain (tests only) --
 //
-// k_inv_fast's arithmetic evaluated on the host for a whole image, with the
-// kernel's own helpers (aan8, fvblend, fhblend, col_*): dequantisation with the
-// folded table, AAN along axis 0 then axis 1, clip to [-128, 127], the
-// vertical then difference-form horizontal chroma blends with cv2's clamped
-// taps (the kernel's replicated window ring gives the same operands), the
+// k_inv_fast's (BS = 8) and k_inv16_fast's (BS = 16) arithmetic evaluated on
+// the host for a whole image, with the kernels' own helpers (aan8 / fidct16,
+// fvblend, fhblend, col_*): dequantisation with the folded table, the IDCT
+// along axis 0 then axis 1, clip to [-128, 127], the vertical then
+// difference-form horizontal chroma blends with cv2's clamped taps (the
+// kernels' replicated window ring or edge selects give the same operands), the
 // colour terms on the magic grid and byte_cert_y's byte.  fuse = 0: every
 // multiply-add rounded twice (MadDev on x86-64); 1: every one fused (MadFma).
 // values[] = v' = y - MAGIC (exact), the value the certificate judges.
-template <class M>
+// Q: the 8x8 table (16x16: Q16[u][v] = Q[u/2][v/2]).
+template <class M, int BS>
 static void inv_fast_host_t(int mode, const int16_t* cf, const double* Q, int H, int W, double* vout,
                             uint8_t* bout) {
   const int sy = mode == M420 ? 2 : 1, sx = mode == M444 ? 1 : 2;
+  // dequantised input of coefficient (u, v): 8x8, q * qs with the folded table;
+  // 16x16, ((q * Q16) * s_u) * s_v (fidct16_block's order)
   double qs[64];
   for (int i = 0; i < 64; ++i) qs[i] = Q[i] * h_aan[i >> 3] * h_aan[i & 7] * 0.125;
+  auto deq = [&](int q, int u, int v) {
+    if constexpr (BS == 8) return (double)q * qs[u * 8 + v];
+    return ((double)(q * (int)Q[(u >> 1) * 8 + (v >> 1)]) * s16_of(h_aan, u)) * s16_of(h_aan, v);
+  };
+  auto line = [](double(&c)[BS]) {
+    if constexpr (BS == 8)
+      aan8<M>(c);
+    else
+      fidct16<M>(c);
+  };
   std::vector<double> pl[3];
   int ph[3], pw[3], st[3];
   size_t off = 0;
   for (int p = 0; p < 3; ++p) {
     ph[p] = p ? H / sy : H;
     pw[p] = p ? W / sx : W;
-    const int nby = (ph[p] + 7) / 8, nbx = (pw[p] + 7) / 8;
-    st[p] = nbx * 8;
-    pl[p].assign((size_t)nby * 8 * st[p], 0.0);
+    const int nby = (ph[p] + BS - 1) / BS, nbx = (pw[p] + BS - 1) / BS;
+    st[p] = nbx * BS;
+    pl[p].assign((size_t)nby * BS * st[p], 0.0);
     for (int by = 0; by < nby; ++by)
       for (int bx = 0; bx < nbx; ++bx) {
-        const int16_t* b = cf + off + ((size_t)by * nbx + bx) * 64;
-        double mid[8][8];
-        for (int v = 0; v < 8; ++v) {  // fast_col
-          double c[8];
-          for (int r = 0; r < 8; ++r) c[r] = (double)b[r * 8 + v] * qs[r * 8 + v];
-          aan8<M>(c);
-          for (int r = 0; r < 8; ++r) mid[r][v] = c[r];
+        const int16_t* b = cf + off + ((size_t)by * nbx + bx) * BS * BS;
+        double mid[BS][BS];
+        for (int v = 0; v < BS; ++v) {  // axis 0
+          double c[BS];
+          for (int r = 0; r < BS; ++r) c[r] = deq(b[r * BS + v], r, v);
+          line(c);
+          for (int r = 0; r < BS; ++r) mid[r][v] = c[r];
         }
-        for (int u = 0; u < 8; ++u) {  // fast_row<-128>
-          double c[8];
-          for (int k = 0; k < 8; ++k) c[k] = mid[u][k];
-          aan8<M>(c);
-          for (int k = 0; k < 8; ++k) pl[p][(size_t)(by * 8 + u) * st[p] + bx * 8 + k] = fmin(fmax(c[k], -128.0), 127.0);
+        for (int u = 0; u < BS; ++u) {  // axis 1, clip
+          double c[BS];
+          for (int k = 0; k < BS; ++k) c[k] = mid[u][k];
+          line(c);
+          for (int k = 0; k < BS; ++k)
+            pl[p][(size_t)(by * BS + u) * st[p] + bx * BS + k] = fmin(fmax(c[k], -128.0), 127.0);
         }
       }
-    off += (size_t)nby * nbx * 64;
+    off += (size_t)nby * nbx * BS * BS;
   }
   auto S = [&](int p, int r, int c) {  // clamped taps (cv2) = the kernel's ring / clampi rows
     r = r < 0 ? 0 : (r > ph[p] - 1 ? ph[p] - 1 : r);
@@ -807,13 +1176,20 @@ static void inv_fast_host_t(int mode, const int16_t* cf, const double* Q, int H,
     }
 }
 
-int inv_fast_host(int mode, const int16_t* cf, const double* Q, int H, int W, int fuse, double* vout, uint8_t* bout) {
+int inv_fast_host(int mode, const int16_t* cf, const double* Q, int H, int W, int fuse, int block, double* vout,
+                  uint8_t* bout) {
   const int sy = mode == M420 ? 2 : 1, sx = mode == M444 ? 1 : 2;
-  if (H % sy || W % sx) return -1;  // the tiled kernels' even geometries
-  if (fuse)
-    inv_fast_host_t<MadFma>(mode, cf, Q, H, W, vout, bout);
-  else
-    inv_fast_host_t<MadDev>(mode, cf, Q, H, W, vout, bout);
+  if (H % sy || W % sx || (block != 8 && block != 16)) return -1;  // the tiled kernels' even geometries
+  if (block == 16) {
+    if (fuse)
+      inv_fast_host_t<MadFma, 16>(mode, cf, Q, H, W, vout, bout);
+    else
+      inv_fast_host_t<MadDev, 16>(mode, cf, Q, H, W, vout, bout);
+  } else if (fuse) {
+    inv_fast_host_t<MadFma, 8>(mode, cf, Q, H, W, vout, bout);
+  } else {
+    inv_fast_host_t<MadDev, 8>(mode, cf, Q, H, W, vout, bout);
+  }
   return 0;
 }
 

@@ -105,6 +105,7 @@ _SIGS = {
     'jds_selftest_dct16x16': (C.c_int, [_P, _P, C.c_int64, C.c_int32]),
     'jds_selftest_area_tab': (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P]),
     'jds_selftest_inv_fast': (C.c_int, [C.c_int32, _P, _P, C.c_int64, C.c_int64, C.c_int32, _P, _P]),
+    'jds_selftest_inv_fast16': (C.c_int, [C.c_int32, _P, _P, C.c_int64, C.c_int64, C.c_int32, _P, _P]),
     'jds_selftest_fwd32': (C.c_int, [C.c_int32, C.c_int32, _P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P,
                                      _P]),
     'jds_selftest_fwd16': (C.c_int, [C.c_int32, C.c_int32, _P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P,

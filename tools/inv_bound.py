@@ -55,6 +55,7 @@ constants are at least these and checks the chain itself against the oracle
 import math
 import os
 import re
+import sys
 from decimal import Decimal, getcontext
 from fractions import Fraction
 
@@ -326,6 +327,178 @@ def colour_bound(ey, ec_, chain, mode):
     return max(((x.el, x.ec) for x in (R, G, B)), key=lambda t: t[0] * 2048 + t[1])
 
 
+# ---- 16x16 blocks (BASELINE configs[4] stretch): k_inv16_fast vs k_inv16s -----
+
+def kernel_constants16():
+    """The 16-point fast chain's doubles and K_LIN16 / K_CONST16, read from
+    jds_inv_fast.hip (odd-part pre- and post-scales of fidct16)."""
+    src = open(os.path.join(CSRC, 'jds_inv_fast.hip')).read()
+
+    def lst(name):
+        m = re.search(r'#define ' + name + r'((?:[^\n]*\\\n)*[^\n]*)\n', src)
+        return [float.fromhex(t) for t in (x.strip() for x in m.group(1).replace('\\\n', ' ').split(','))]
+    klin = re.search(r'constexpr double K_LIN16 = ([0-9.e+-]+) \* ([0-9.]+);', src)
+    kcon = re.search(r'constexpr double K_CONST16 = ([0-9.e+-]+) \* ([0-9.]+);', src)
+    out = {'pre': lst('JDS_F16_PRE_LIST'), 'post': lst('JDS_F16_POST_LIST'),
+           'K_LIN16': float(klin.group(1)) * float(klin.group(2)) if klin else None,
+           'K_CONST16': float(kcon.group(1)) * float(kcon.group(2)) if kcon else None}
+    assert len(out['pre']) == 7 and len(out['post']) == 8, out
+    return out
+
+
+def pocketfft16_constants():
+    """csrc/jds_dct16.hpp's doubles: DT16[15], WR[3], WI[3], SQRT2, HSQT2."""
+    src = open(os.path.join(CSRC, 'jds_dct16.hpp')).read()
+    out = {}
+    for m in re.finditer(r'constexpr double (\w+)\[(\d+)\] = \{([^}]*)\};', src):
+        out[m.group(1)] = [float.fromhex(t.strip()) for t in m.group(3).split(',')]
+        assert len(out[m.group(1)]) == int(m.group(2))
+    for m in re.finditer(r'constexpr double (\w+) = (0x[0-9a-fA-F.]+p[-+]?\d+);', src):
+        out[m.group(1)] = float.fromhex(m.group(2))
+    return out
+
+
+def fast16_line(v, K, K16):
+    """jds_inv_fast.hip fidct16: the even half through aan8 (inputs pre-scaled
+    a_m / 4 by the table), the odd half by Lee's identity: W_0 = Z_0,
+    W_j = (Z_{j-1} + Z_j) cos(j pi / 16), aan8, then x_n = E_n + W_n p_n and
+    x_{15-n} = E_n - W_n p_n with p_n = sqrt(2) / (8 cos((2n+1) pi / 32))."""
+    e = aan_line([v[2 * m] for m in range(8)], K)
+    w = [v[1]] + [mul(add(v[2 * j - 1], v[2 * j + 1]), cos_pi(j, 16), K16['pre'][j - 1]) for j in range(1, 8)]
+    w = aan_line(w, K)
+    out = [None] * 16
+    for n in range(8):
+        o = mul(w[n], SQRT2 / (8 * cos_pi(2 * n + 1, 32)), K16['post'][n])  # fused or not: two roundings
+        out[n] = add(e[n], o)
+        out[15 - n] = add(e[n], o, -1)
+    return out
+
+
+def _radf4(IDO, L1, cc, D):
+    """jds_dct16.hpp radf4<IDO, L1> on V values (pocketfft's rfftp forward radix 4)."""
+    ch = [None] * 16
+
+    def CC(a, b, c):
+        return cc[a + IDO * (b + L1 * c)]
+
+    def CH(a, b, c, val):
+        ch[a + IDO * (b + 4 * c)] = val
+    hs = SQRT2 / 2
+    wr = [cos_pi(j, 8) for j in (1, 2, 3)]
+    wi = [cos_pi(4 - j, 8) for j in (1, 2, 3)]  # sin(j pi / 8)
+    for k in range(L1):
+        tr1 = add(CC(0, k, 3), CC(0, k, 1))
+        CH(0, 2, k, add(CC(0, k, 3), CC(0, k, 1), -1))
+        tr2 = add(CC(0, k, 0), CC(0, k, 2))
+        CH(IDO - 1, 1, k, add(CC(0, k, 0), CC(0, k, 2), -1))
+        CH(0, 0, k, add(tr2, tr1))
+        CH(IDO - 1, 3, k, add(tr2, tr1, -1))
+    if IDO == 4:
+        for k in range(L1):
+            ti1 = mul(add(CC(3, k, 1), CC(3, k, 3)), -hs, -D['HSQT2'])
+            tr1 = mul(add(CC(3, k, 1), CC(3, k, 3), -1), hs, D['HSQT2'])
+            CH(3, 0, k, add(CC(3, k, 0), tr1))
+            CH(3, 2, k, add(CC(3, k, 0), tr1, -1))
+            CH(0, 3, k, add(ti1, CC(3, k, 2)))
+            CH(0, 1, k, add(ti1, CC(3, k, 2), -1))
+        for k in range(L1):
+            def rot(idx, j):  # (WR a + WI b, WR b - WI a) of (a, b) = (CC(1, k, idx), CC(2, k, idx))
+                a, b = CC(1, k, idx), CC(2, k, idx)
+                cr = add(mul(a, wr[j], D['WR'][j]), mul(b, wi[j], D['WI'][j]))
+                ci = add(mul(b, wr[j], D['WR'][j]), mul(a, wi[j], D['WI'][j]), -1)
+                return cr, ci
+            cr2, ci2 = rot(1, 0)
+            cr3, ci3 = rot(2, 1)
+            cr4, ci4 = rot(3, 2)
+            tr1 = add(cr4, cr2); tr4 = add(cr4, cr2, -1)
+            ti1 = add(ci2, ci4); ti4 = add(ci2, ci4, -1)
+            tr2 = add(CC(1, k, 0), cr3); tr3 = add(CC(1, k, 0), cr3, -1)
+            ti2 = add(CC(2, k, 0), ci3); ti3 = add(CC(2, k, 0), ci3, -1)
+            CH(1, 0, k, add(tr2, tr1)); CH(1, 3, k, add(tr2, tr1, -1))
+            CH(2, 0, k, add(ti1, ti2)); CH(2, 3, k, add(ti1, ti2, -1))
+            CH(1, 2, k, add(tr3, ti4)); CH(1, 1, k, add(tr3, ti4, -1))
+            CH(2, 2, k, add(tr4, ti3)); CH(2, 1, k, add(tr4, ti3, -1))
+    return ch
+
+
+def pocket_dct3_16(c, D):
+    """csrc/jds_dct16.hpp dct3_line16 (pocketfft T_dcst23 type 3, N = 16)."""
+    dt = [cos_pi(i + 1, 32) for i in range(15)]
+    c = list(c)
+    c[0] = mul(c[0], SQRT2, D['SQRT2'])
+    for k in range(1, 8):
+        kc = 16 - k
+        t1 = add(c[k], c[kc]); t2 = add(c[k], c[kc], -1)
+        c[k] = add(mul(t2, dt[k - 1], D['DT16'][k - 1]), mul(t1, dt[kc - 1], D['DT16'][kc - 1]))
+        c[kc] = add(mul(t1, dt[k - 1], D['DT16'][k - 1]), mul(t2, dt[kc - 1], D['DT16'][kc - 1]), -1)
+    c[8] = mul(c[8], 2 * dt[7], 2 * D['DT16'][7])
+    o = _radf4(4, 1, _radf4(1, 4, c, D), D)
+    out = [o[0]] + [None] * 14 + [o[15]]
+    for k in range(1, 15, 2):
+        out[k] = add(o[k], o[k + 1], -1)
+        out[k + 1] = add(o[k + 1], o[k])
+    return out
+
+
+def idct_matrix16():
+    C = np.zeros((16, 16))
+    for n in range(16):
+        for k in range(16):
+            C[n, k] = math.sqrt((1 if k == 0 else 2) / 16) * math.cos((2 * n + 1) * k * math.pi / 32)
+    return C
+
+
+def block_bound16(chain, K, K16, D):
+    """block_bound for 16 x 16 blocks: the fast chain (((q * Q16) * s_u) * s_v,
+    q * Q16 exact, s_2m = a_m / 4, s_2m+1 = 1; fidct16 on axis 0 then axis 1)
+    or the exact one (q * Q, dct3_line16 twice, * 1/32 (exact) + 128 in one
+    rounding)."""
+    N = 256
+    if chain == 'fast':
+        A = [F(1)] + [SQRT2 * cos_pi(k, 16) for k in range(1, 8)]
+        s = [A[k // 2] / 4 if k % 2 == 0 else F(1) for k in range(16)]
+        sd = [K['aan'][k // 2] * 0.25 if k % 2 == 0 else 1.0 for k in range(16)]
+        d = [[None] * 16 for _ in range(16)]
+        for u in range(16):
+            for v in range(16):
+                k = s[u] * s[v]
+                # both scales' representation errors and the rounding of the
+                # first product; the second product's rounding is .rnd()
+                rel = (rep_err(sd[u], s[u]) / float(s[u]) + rep_err(sd[v], s[v]) / float(s[v]) + U) * (1 + 1e-9)
+                d[u][v] = V(np.eye(N)[u * 16 + v] * float(k), 0.0, float(k) * rel, 0.0).rnd()
+        cols = [fast16_line([d[u][v] for u in range(16)], K, K16) for v in range(16)]
+        out = [fast16_line([cols[v][m] for v in range(16)], K, K16) for m in range(16)]
+    else:
+        basis = [[V(np.eye(N)[u * 16 + v].copy()) for v in range(16)] for u in range(16)]
+        cols = [pocket_dct3_16([basis[u][v] for u in range(16)], D) for v in range(16)]
+        rows = [pocket_dct3_16([cols[v][m] for v in range(16)], D) for m in range(16)]
+        out = [[const_add(mul(x, F(1, 32), exact_product=True), 128.0) for x in r] for r in rows]
+    Cm = idct_matrix16()
+    for m in range(16):
+        for n in range(16):
+            want = np.kron(Cm[m], Cm[n])
+            got = out[m][n].L
+            assert np.abs(got - want).max() < 1e-12, (chain, m, n, np.abs(got - want).max())
+    worst = (0.0, 0.0)
+    for r in out:
+        for x in r:
+            if x.el * 2048 + x.ec > worst[0] * 2048 + worst[1]:
+                worst = (x.el, x.ec)
+    return worst
+
+
+def bounds16():
+    K, K16, D = kernel_constants(), kernel_constants16(), pocketfft16_constants()
+    res = {}
+    for chain in ('fast', 'ref'):
+        eb = block_bound16(chain, K, K16, D)
+        res[chain] = {m: colour_bound(eb, eb, chain, m) for m in ('4:2:2', '4:2:0')}
+    worst = {c: max(res[c].values(), key=lambda t: t[0] * 2048 + t[1]) for c in res}
+    k_lin = 2 * (worst['fast'][0] + worst['ref'][0])
+    k_const = 2 * (worst['fast'][1] + worst['ref'][1])
+    return res, k_lin, k_const
+
+
 def bounds():
     K, P = kernel_constants(), pocketfft_constants()
     res = {}
@@ -338,7 +511,15 @@ def bounds():
     return res, k_lin, k_const
 
 
-if __name__ == '__main__':
+if __name__ == '__main__' and '--b16' in sys.argv:
+    res, k_lin, k_const = bounds16()
+    K16 = kernel_constants16()
+    for chain, per in res.items():
+        for m, (el, ec) in per.items():
+            print(f'{chain:5s} 16x16 {m}: e <= {el:.4e} * Dmax + {ec:.4e}')
+    print(f'model : K_LIN16 = {k_lin:.6e}  K_CONST16 = {k_const:.6e}  (x2 safety included)')
+    print(f'kernel: K_LIN16 = {K16["K_LIN16"]}  K_CONST16 = {K16["K_CONST16"]}')
+elif __name__ == '__main__':
     res, k_lin, k_const = bounds()
     K = kernel_constants()
     for chain, per in res.items():
