@@ -521,6 +521,10 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
            const int fin) {
   // the transpose buffer and chroma window are the exact fallback's own
   __shared__ __attribute__((aligned(16))) InvShared<MODE, XTRA> sh;
+#ifdef JDS_PROBE_LDS_PAD  // tools: extra LDS per workgroup (occupancy probe)
+  __shared__ unsigned s_pad[JDS_PROBE_LDS_PAD];
+  if (threadIdx.x == 0) s_pad[blockIdx.x % JDS_PROBE_LDS_PAD] = 0u;
+#endif
   const int tid = threadIdx.x;
   const int frame = blockIdx.y, tile = blockIdx.x;
   // k_finalize's work for runs without SSE terms (fin >= 0; fin = 1 adds the
