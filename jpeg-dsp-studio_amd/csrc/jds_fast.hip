@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "jds_dct8.hpp"
 #include "jds_device.hpp"
@@ -894,6 +895,188 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   }
 }
 
+// ---- 4:4:4, wave-local -----------------------------------------------------------
+//
+// k_fwd444w: k_fwd32i's certified arithmetic for 4:4:4 plans (no subsampling,
+// no prefilter: a block reads only its own 8 x 8 pixels) without the tile
+// staging.  A wave owns 8 blocks in raster order, each lane one 8-pixel row of
+// its block: 24-byte RGB load (np.pad reflect rows / columns at the padded
+// edge, engines/block_processor.py), fp32 colour (luma32m, cb32 - 128,
+// cr32 - 128: fwd_input_error's chains), then per plane the row DCT in
+// registers, the block's column pass through its own LDS slot (the 8 lanes of a
+// block are one wave's, whose LDS operations execute in order: no workgroup
+// barrier), certified quantisation, the in-place int16 transpose and 16-byte
+// row stores.  Both pass orders are covered by fast_fwd_thresholds.  A lane
+// quantises 24 coefficients, so its common-bin counts are kept in 16-bit
+// fields (quant8's nibbles are folded after each plane) and the workgroup's
+// statistics go to a per-workgroup partial once (last-wave ticket, as
+// stats_flush_ticket), summed per frame by k_fwd_reduce.  Measured (256 x
+// 512^2, same box): 190 us against k_fwd32i<4:4:4>'s 274 (JDS_FWD444_TILED=1
+// keeps the tiled kernel for A/B); 92 VGPRs, 5 waves per SIMD -- forcing 6
+// spills 10 registers and takes 255 us.
+constexpr int F444_WAVES = 4;
+#ifndef JDS_F444_WPE
+#define JDS_F444_WPE 5
+#endif
+
+__global__ void __launch_bounds__(64 * F444_WAVES) __attribute__((amdgpu_waves_per_eu(JDS_F444_WPE)))
+k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs, const FastQ* __restrict__ fq,
+          uint32_t* __restrict__ part, uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount,
+          jds_frame_stats* __restrict__ stz) {
+  __shared__ __attribute__((aligned(16))) float s_blk[8 * F444_WAVES * BS32];
+  __shared__ __attribute__((aligned(16))) float s_rqT[64];
+  __shared__ __attribute__((aligned(16))) float s_thT[2][64];
+  __shared__ unsigned s_st[NSTAT + 1];  // rare bins (quant8) + the waves' ticket
+  __shared__ unsigned s_rows[F444_WAVES][4][5];
+  __shared__ unsigned s_nvalid[F444_WAVES];
+  const int tid = threadIdx.x, lv = tid & 7, lb = tid >> 3;
+  const int frame = blockIdx.y;
+  if (blockIdx.x == 0) {  // this launch owns the frame statistics' reset (k_fwd_reduce adds after it)
+    uint64_t* z = reinterpret_cast<uint64_t*>(stz + frame);
+    for (int i = tid; i < (int)(sizeof(jds_frame_stats) / 8); i += blockDim.x) z[i] = 0ull;
+  }
+  if (tid < 64) {
+    const int t = (tid & 7) * 8 + (tid >> 3);  // [v][k] <- [k][v]
+    s_rqT[tid] = fq[frame].rq[t];
+    s_thT[0][tid] = fq[frame].thr[0][t];
+    s_thT[1][tid] = fq[frame].thr[1][t];
+  }
+  if (tid <= NSTAT) s_st[tid] = 0u;
+  __syncthreads();
+
+  const int nblk = g.nby * g.nbx;
+  const int blk = blockIdx.x * (8 * F444_WAVES) + lb;
+  const bool valid = blk < nblk;
+  const int bq = valid ? blk : 0;
+  const int by = bq / g.nbx, bx = bq - by * g.nbx;
+  const int y = by * 8 + lv, x0 = bx * 8;
+  const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
+  uint32_t w[6];
+  {
+    const int yr = reflect_pad(y, g.H);
+    const uint8_t* row = img + (size_t)yr * g.W * 3;
+    if (x0 + 8 <= g.W && (g.W & 7) == 0) {  // 8-byte aligned rows: three 8-byte loads
+      const uint2* p2 = reinterpret_cast<const uint2*>(row + (size_t)x0 * 3);
+      const uint2 a = p2[0], b = p2[1], c = p2[2];
+      w[0] = a.x; w[1] = a.y; w[2] = b.x; w[3] = b.y; w[4] = c.x; w[5] = c.y;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) w[i] = 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint8_t* px = row + (size_t)reflect_pad(x0 + k, g.W) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) w[(3 * k + c) >> 2] |= (uint32_t)px[c] << (8 * ((3 * k + c) & 3));
+      }
+    }
+  }
+
+  LaneStats ls;
+  unsigned acc[4] = {0u, 0u, 0u, 0u};  // common bins 22..29 in 16-bit fields: (22, 23), (24, 25), ...
+  float* slot = s_blk + lb * BS32;
+  int16_t* tq = reinterpret_cast<int16_t*>(slot);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    // the plane's samples from the packed bytes, per plane (fewer live registers
+    // than all three planes at once)
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float R = (float)byte_at(w, 3 * k), G = (float)byte_at(w, 3 * k + 1), B = (float)byte_at(w, 3 * k + 2);
+      v[k] = p == 0 ? luma32m(R, G, B) : (p == 1 ? cb32(R, G, B) - 128.0f : cr32(R, G, B) - 128.0f);
+    }
+    fdct8_f32(v);  // axis 1 of row lv
+    float4* d4 = reinterpret_cast<float4*>(slot + lv * 8);
+    d4[0] = make_float4(v[0], v[1], v[2], v[3]);
+    d4[1] = make_float4(v[4], v[5], v[6], v[7]);
+    __builtin_amdgcn_wave_barrier();
+    float c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = slot[i * 8 + lv];  // column lv
+    fdct8_f32(c);                                           // axis 0
+    const float4* rq4 = reinterpret_cast<const float4*>(s_rqT + lv * 8);
+    const float4* th4 = reinterpret_cast<const float4*>(s_thT[p ? 1 : 0] + lv * 8);
+    const float4 ra = rq4[0], rb = rq4[1], ta = th4[0], tb = th4[1];
+    const float rq[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+    const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+    int q[8];
+    ls.hn = 0u;
+    ls.nflag = 0u;
+    quant8(c, rq, thr, valid, q, ls, s_st);
+    __builtin_amdgcn_wave_barrier();  // every lane's column read precedes the int16 rows
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tq[k * 16 + lv] = (int16_t)q[k];
+    __builtin_amdgcn_wave_barrier();
+    const uint4 rowq = *reinterpret_cast<const uint4*>(tq + lv * 16);
+    if (valid)
+      *reinterpret_cast<uint4*>(coeffs + (long long)frame * g.cpf + (p == 0 ? 0 : (p == 1 ? g.off_cb : g.off_cr)) +
+                                (long long)bq * 64 + lv * 8) = rowq;
+    flag_block_list(ls, valid, lv, frame, p, bq, fixlist, fixcount, g.cpf / 64);
+    const unsigned h = ls.hn;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += ((h >> (8 * j)) & 15u) | (((h >> (8 * j + 4)) & 15u) << 16);
+    __builtin_amdgcn_wave_barrier();  // the rows are read before the next plane writes the slot
+  }
+
+  // ---- statistics: row sums, one record per 16-lane row, the last wave decodes
+  unsigned r5[4] = {acc[0], acc[1], acc[2], acc[3]};
+  unsigned nzmb = ls.nz | (ls.mb << 16);  // <= 24 and <= 24 * 16 per lane
+  if (!valid) {
+    r5[0] = r5[1] = r5[2] = r5[3] = 0u;
+    nzmb = 0u;
+  }
+  row_sums4(r5);
+  nzmb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)nzmb, 0x111, 0xf, 0xf, true);  // row_shr 1, 2, 4, 8
+  nzmb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)nzmb, 0x112, 0xf, 0xf, true);
+  nzmb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)nzmb, 0x114, 0xf, 0xf, true);
+  nzmb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)nzmb, 0x118, 0xf, 0xf, true);
+  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
+  const int wv = tid >> 6, lane = tid & 63;
+  if ((lane & 15) == 15) {
+    unsigned* rr = s_rows[wv][lane >> 4];
+    rr[0] = r5[0];
+    rr[1] = r5[1];
+    rr[2] = r5[2];
+    rr[3] = r5[3];
+    rr[4] = nzmb;
+    if (lane == 63) s_nvalid[wv] = nvalid;
+  }
+  __asm__ volatile("" ::: "memory");
+  unsigned ticket = 0u;
+  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
+  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
+  if (ticket != (unsigned)(F444_WAVES - 1)) return;
+  __asm__ volatile("" ::: "memory");
+  if (lane < NSTAT) {
+    unsigned tot = s_st[lane];  // rare bins (quant8's LDS atomics)
+    for (int i = 0; i < F444_WAVES; ++i) {
+      unsigned nz = 0u, mb = 0u, f[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const unsigned* rr = s_rows[i][r];
+        nz += rr[4] & 0xffffu;
+        mb += rr[4] >> 16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f[j] += rr[j];  // (per-field sums <= 4 * 384: no carry between fields)
+      }
+      if (lane == 0) {
+        tot += nz;
+      } else if (lane == 1) {
+        tot += mb + nz;  // magnitude bits = bit length + 1 per nonzero
+      } else if (lane >= 2 + 22 && lane < 2 + 30) {
+        const int b = lane - 2 - 22;
+        unsigned c = (f[b >> 1] >> (16 * (b & 1))) & 0xffffu;
+        if (b == 3) c -= 24u * s_nvalid[i] - nz;  // zeros fall in bin 25: k_finalize adds them
+        tot += c;
+      }
+    }
+    part[((size_t)frame * gridDim.x + blockIdx.x) * NSTAT + lane] = tot;
+  }
+}
+
+// workgroups per frame of k_fwd444w (its statistics partials per frame)
+int fwd444w_groups(const Geo& g) { return (g.nby * g.nbx + 8 * F444_WAVES - 1) / (8 * F444_WAVES); }
+
 // End of the certified forward's producer launches: the statistics partials
 // into the frame stats (reduce_partials), then (sweep plans) bitmap -> list:
 // each wave takes 64 bitmap words of the workgroup's share of item f's
@@ -1318,6 +1501,19 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   // Tiles lying wholly inside the image (no padding blocks, no phantom MCUs;
   // only the 1-px ring may reflect) form a rectangle of tile indices and take
   // k_fwd32i; the rest run in k_fwd32 beside it on the side stream.
+  // 4:4:4 single-quality plans: the wave-local kernel (k_fwd444w) for every block
+  if (MODE == M444 && !mq && !getenv("JDS_FWD444_TILED")) {
+    const int ng = fwd444w_groups(g);
+    hipLaunchKernelGGL(k_fwd444w, dim3(ng, n), dim3(64 * F444_WAVES), 0, s, g, rgb, coeffs, fq32, part, fixlist, fc, st);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if ((e = launch_fwd_reduce(n, st, part, ng, s)) != hipSuccess) return e;
+    const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
+                       fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
+  }
   int4 rect;
   rect.x = (g.ty_off * C::MH > 0) ? 1 : 0;                           // first tile row with y0 >= 0
   rect.y = (g.H / C::MH + g.ty_off) / C::MY - 1;                     // last tile row with y0 + TH <= H
