@@ -123,10 +123,53 @@ __device__ __forceinline__ unsigned rare_bin_total(const unsigned* s_rh, int b) 
 // s_st's histogram with per-coefficient branches (REPL false: rare values are
 // sparse at the headline qualities), or branch-free into replicated
 // histograms at s_rh (REPL true).
+// Round-half-even to an integer by the magic constant 1.5 * 2^23: for
+// |t| < 2^22 the sum f = t + M lies in [2^23, 2^24), where the float spacing is
+// 1, so the addition rounds t to the nearest integer, ties to even (rintf's
+// result); r = f - M is exact, and f's encoding is 0x4B400000 + r (its low 16
+// bits are r as int16).  |t| <= 1024 here (|c| <= 8 * 128, Q >= 1).
+constexpr float QMAGIC = 0x1.8p+23f;
+constexpr uint32_t QMAGIC_BITS = 0x4B400000u;
+
 template <bool REPL = false>
 __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8], const float (&thr)[8], bool valid,
                                        int (&q)[8], LaneStats& ls, unsigned* s_st) {
   unsigned nrare = 0u;
+#ifndef JDS_QUANT8_CLASSIC
+  // Written for gfx950's issue costs (tools/microbench/op_rates.hip): fp32
+  // add / sub / mul / fma and integer add / and / or / lshr issue in ~2.5
+  // cycles per wave, compares, selects, conversions, rndne and frexp in ~4.3,
+  // so the rounding is the magic add, the certificate a sign bit and the rare
+  // test an OR.
+  unsigned ok = 0xffffffffu, orr = 0u;
+  unsigned top;  // 2^31 in a VGPR, opaque (the shift below must not fold back into 1 << x)
+  asm("v_mov_b32 %0, 0x80000000" : "=v"(top));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float t = v[k] * rq[k];
+    const float f = t + QMAGIC;
+    const float r = f - QMAGIC;  // rintf(t)
+    const uint32_t fb = __float_as_uint(f);
+    // uncertain when |t - r| >= thr - |t| 2^-22 (|t - r| exact by Sterbenz;
+    // thr[k] holds 0.5 - E/Q - slack, rounded down): e = |t - r| - g is < 0
+    // exactly when the rounding is certain (the rounded difference keeps the
+    // exact one's sign, and g > 0, so e is never -0)
+    const float e = fabsf(t - r) - fmaf(fabsf(t), -0x1p-22f, thr[k]);
+    ok &= __float_as_uint(e);
+    q[k] = (int)(fb - QMAGIC_BITS);
+    const int x = __builtin_amdgcn_frexp_expf(r);  // bit length of |q| (0 for q = 0; <= 11)
+    ls.nz += (unsigned)(x + 15) >> 4;
+    ls.mb += (unsigned)x;
+    const unsigned o = fb - (QMAGIC_BITS - 12u);  // q + 12
+    // bins 22..29: += 1 << (o & 28) as 2^31 >> ((o & 28) ^ 31) (one bitop3 and a
+    // right shift instead of a left shift); a rare q lands in some nibble and is
+    // taken back below
+    ls.hn += top >> ((o & 28u) ^ 31u);
+    orr |= o;  // any o >= 32 (q outside [-12, 19]) sets a bit >= 5
+  }
+  ls.nflag += (~ok) >> 31;
+  nrare = REPL ? orr : (orr >= 32u ? 1u : 0u);
+#else
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const float t = v[k] * rq[k];
@@ -143,6 +186,7 @@ __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8]
     else
       nrare += o >= 32u ? 1u : 0u;
   }
+#endif
 #ifdef JDS_PROBE_NORARE  // tools/probe: drop the rare-bin atomics
   nrare = 0u;
 #endif
