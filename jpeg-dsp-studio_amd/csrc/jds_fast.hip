@@ -123,19 +123,12 @@ __device__ __forceinline__ unsigned rare_bin_total(const unsigned* s_rh, int b) 
 // s_st's histogram with per-coefficient branches (REPL false: rare values are
 // sparse at the headline qualities), or branch-free into replicated
 // histograms at s_rh (REPL true).
-// Round-half-even to an integer by the magic constant 1.5 * 2^23: for
-// |t| < 2^22 the sum f = t + M lies in [2^23, 2^24), where the float spacing is
-// 1, so the addition rounds t to the nearest integer, ties to even (rintf's
-// result); r = f - M is exact, and f's encoding is 0x4B400000 + r (its low 16
-// bits are r as int16).  |t| <= 1024 here (|c| <= 8 * 128, Q >= 1).
-constexpr float QMAGIC = 0x1.8p+23f;
-constexpr uint32_t QMAGIC_BITS = 0x4B400000u;
-
 template <bool REPL = false>
 __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8], const float (&thr)[8], bool valid,
                                        int (&q)[8], LaneStats& ls, unsigned* s_st) {
   unsigned nrare = 0u;
 #ifndef JDS_QUANT8_CLASSIC
+  // |t| <= 1024 (|c| <= 8 * 128, Q >= 1): QMAGIC rounds exactly.
   // Written for gfx950's issue costs (tools/microbench/op_rates.hip): fp32
   // add / sub / mul / fma and integer add / and / or / lshr issue in ~2.5
   // cycles per wave, compares, selects, conversions, rndne and frexp in ~4.3,
@@ -265,10 +258,10 @@ __device__ __forceinline__ void flag_block_bits(const LaneStats& ls, bool valid,
 
 // The workgroup's statistics into this tile's slot of the per-tile partials
 // (plain stores; k_fwd_reduce_fix reduces them per frame).  Each lane's eight
-// common-bin nibbles (<= 8 each) and nonzero count go into three words of
-// 10-bit fields (a wave sums to <= 512 per field), the magnitude bits into a
-// fourth; four-word row sums, one LDS record per row, and the last wave
-// decodes and adds the waves' rows to the rare bins the quantiser counted.
+// common-bin nibbles (<= 8 each) go into two words of 8-bit fields, the nonzero
+// count and magnitude bits into a third; three-word row sums (a 16-lane row
+// sums to <= 128 per bin), one LDS record per row, and the last wave decodes
+// and adds the waves' rows to the rare bins the quantiser counted.
 // s_st holds NSTAT + 1 words: the last is the waves' ticket counter.
 constexpr int NW_MAX = 8;  // waves per forward workgroup (TF <= 512)
 
@@ -309,11 +302,12 @@ __device__ __forceinline__ void stats_flush_ticket(LaneStats ls, bool valid, uns
   if (ls.hn == 0x12345u && ls.mb == 7u && ls.nz == 3u) slot[0] = 1u;
   return;
 #endif
+  // 8-bit fields: a 16-lane row sums to <= 16 * 8 = 128 per bin; even bins
+  // (22, 24, 26, 28) in v[0], odd in v[1], nonzero | magnitude bits << 16 in
+  // v[2] (<= 128 and <= 16 * 88); three row sums of fast and / shift ops
   const unsigned h = ls.hn;
-  unsigned v[4] = {(h & 15u) | ((h >> 4) & 15u) << 10 | ((h >> 8) & 15u) << 20,
-                   ((h >> 12) & 15u) | ((h >> 16) & 15u) << 10 | ((h >> 20) & 15u) << 20,
-                   ((h >> 24) & 15u) | (h >> 28) << 10 | ls.nz << 20, ls.mb};
-  row_sums4(v);
+  unsigned v[3] = {h & 0x0f0f0f0fu, (h >> 4) & 0x0f0f0f0fu, ls.nz | (ls.mb << 16)};
+  row_sums3(v);
   const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nw = (int)(blockDim.x >> 6);
@@ -322,7 +316,7 @@ __device__ __forceinline__ void stats_flush_ticket(LaneStats ls, bool valid, uns
   // wave's operations in order, so everyone's rows and rare-bin atomics
   // precede the last ticket) decodes and stores the tile's slot
   if ((lane & 15) == 15) {
-    *reinterpret_cast<uint4*>(&s_wave[w][lane >> 4][0]) = make_uint4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<uint4*>(&s_wave[w][lane >> 4][0]) = make_uint4(v[0], v[1], v[2], 0u);
     if (lane == 63) s_nvalid[w] = nvalid;
   }
   // (a compiler barrier only: a memory fence would also wait for the wave's
@@ -336,24 +330,23 @@ __device__ __forceinline__ void stats_flush_ticket(LaneStats ls, bool valid, uns
   const int t = lane;
   if (t < NSTAT) {
     unsigned tot = s_st[t];  // rare bins (quant8's LDS atomics)
+    const int b = t - 2 - 22;  // common bin 22 + b: word b & 1, byte b >> 1
+    const bool odd = (b & 1) != 0;
+    const int sh = 8 * ((b >> 1) & 3);
     for (int i = 0; i < nw; ++i) {
-      unsigned wv[4] = {0u, 0u, 0u, 0u};
+      unsigned nz = 0u, mb = 0u, c = 0u;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < 4; ++r) {  // (per-row fields, unpacked before the rows are added; no branches)
         const uint4 x = *reinterpret_cast<const uint4*>(&s_wave[i][r][0]);
-        wv[0] += x.x;
-        wv[1] += x.y;
-        wv[2] += x.z;
-        wv[3] += x.w;
+        nz += x.z & 0xffffu;
+        mb += x.z >> 16;
+        c += ((odd ? x.y : x.x) >> sh) & 255u;
       }
-      const unsigned nz = (wv[2] >> 20) & 1023u;
       if (t == 0) {
         tot += nz;
       } else if (t == 1) {
-        tot += wv[3] + nz;  // magnitude bits = bit length + 1 per nonzero
-      } else if (t >= 2 + 22 && t < 2 + 30) {
-        const int b = t - 2 - 22;  // common bin 22 + b: word b / 3, field b % 3
-        unsigned c = (wv[b / 3] >> (10 * (b % 3))) & 1023u;
+        tot += mb + nz;  // magnitude bits = bit length + 1 per nonzero
+      } else if (b >= 0 && b < 8) {
         if (b == 3) c -= 8u * s_nvalid[i] - nz;  // zeros fall in bin 25: k_finalize adds them
         tot += c;
       }

@@ -507,7 +507,11 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       }
     }
     int q[16];
-    unsigned nrare = 0u;
+    // quant8's form (jds_fast.hip): |t| <= 2048 (|c| <= 16 * 128, Q >= 1), so
+    // QMAGIC rounds exactly; the certificate is the sign bit of
+    // |t - r| - (thr - |t| 2^-22) (< 0 exactly when certain), the rare test an OR
+    unsigned ok = 0xffffffffu, orr = 0u, top;
+    asm("v_mov_b32 %0, 0x80000000" : "=v"(top));  // opaque 2^31 (keeps the right shift below)
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
 #ifdef JDS_P16_NOQ  // tools/probe: truncation instead of the certified quantiser (timing only)
@@ -515,17 +519,21 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       continue;
 #endif
       const float t = v[k] * rqv[k];
-      const float r = rintf(t);
+      const float f = t + QMAGIC;
+      const float r = f - QMAGIC;  // rintf(t)
+      const uint32_t fb = __float_as_uint(f);
       // |t - r| is exact (Sterbenz); thr holds 0.5 - E/Q - slack, rounded down
-      flag |= fabsf(t - r) >= fmaf(fabsf(t), -0x1p-22f, thv[k]) ? 1u : 0u;
-      q[k] = (int)r;
-      nz += r != 0.0f ? 1u : 0u;
-      mb += (unsigned)__builtin_amdgcn_frexp_expf(r);  // bit length of |q|
-      const unsigned o = (unsigned)(q[k] + 12);     // bin 22 + o / 4 for q in [-12, 19]
-      h[k >> 3] += 1u << (o & 28u);
-      nrare += o >= 32u ? 1u : 0u;
+      ok &= __float_as_uint(fabsf(t - r) - fmaf(fabsf(t), -0x1p-22f, thv[k]));
+      q[k] = (int)(fb - QMAGIC_BITS);
+      const int x = __builtin_amdgcn_frexp_expf(r);  // bit length of |q| (0 for q = 0; <= 12)
+      nz += (unsigned)(x + 15) >> 4;
+      mb += (unsigned)x;
+      const unsigned o = fb - (QMAGIC_BITS - 12u);  // q + 12: bin 22 + o / 4 for q in [-12, 19]
+      h[k >> 3] += top >> ((o & 28u) ^ 31u);       // 1 << (o & 28)
+      orr |= o;
     }
-    if (nrare) {  // rare values: taken back out of the nibbles, LDS atomics on the bin
+    flag |= (~ok) >> 31;
+    if (orr >= 32u) {  // rare values: taken back out of the nibbles, LDS atomics on the bin
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const unsigned o = (unsigned)(q[k] + 12);

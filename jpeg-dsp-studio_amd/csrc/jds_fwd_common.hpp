@@ -82,20 +82,33 @@ __device__ inline double sample64(const uint8_t* img, const Geo& g, int plane, i
 // Sums of four words over each 16-lane row of a wave: inclusive sums by four
 // DPP row shifts, the four words interleaved so that no DPP read waits on the
 // write before it.
-template <int SH>
-__device__ __forceinline__ void row_shr_add4(unsigned (&v)[4]) {
-  unsigned t[4];
+// Round-half-even to an integer by the magic constant 1.5 * 2^23: for
+// |t| < 2^22 the sum f = t + M lies in [2^23, 2^24), where the float spacing is
+// 1, so the addition rounds t to the nearest integer, ties to even (rintf's
+// result); r = f - M is exact, and f's encoding is 0x4B400000 + r (its low 16
+// bits are r as int16).  The certified quantisers (quant8, k_fwd16f) use it
+// in place of rndne + cvt: gfx950 issues fp32 add / sub in ~2.5 cycles per
+// wave, conversions in ~4.3 (tools/microbench/op_rates.hip).
+constexpr float QMAGIC = 0x1.8p+23f;
+constexpr uint32_t QMAGIC_BITS = 0x4B400000u;
+
+template <int SH, int N>
+__device__ __forceinline__ void row_shr_add(unsigned (&v)[N]) {
+  unsigned t[N];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) t[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v[k], 0x110 + SH, 0xf, 0xf, true);
+  for (int k = 0; k < N; ++k) t[k] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v[k], 0x110 + SH, 0xf, 0xf, true);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) v[k] += t[k];
+  for (int k = 0; k < N; ++k) v[k] += t[k];
 }
-__device__ __forceinline__ void row_sums4(unsigned (&v)[4]) {
-  row_shr_add4<1>(v);
-  row_shr_add4<2>(v);
-  row_shr_add4<4>(v);
-  row_shr_add4<8>(v);  // lane 15 of each 16-lane row now holds the row's sums
+template <int N>
+__device__ __forceinline__ void row_sums(unsigned (&v)[N]) {
+  row_shr_add<1>(v);
+  row_shr_add<2>(v);
+  row_shr_add<4>(v);
+  row_shr_add<8>(v);  // lane 15 of each 16-lane row now holds the row's sums
 }
+__device__ __forceinline__ void row_sums3(unsigned (&v)[3]) { row_sums(v); }
+__device__ __forceinline__ void row_sums4(unsigned (&v)[4]) { row_sums(v); }
 
 // ---- host: bound helpers (jds_fast.hip) ----
 // One pass of an FMA-chain transform over inputs (bound X, error e): output k's
