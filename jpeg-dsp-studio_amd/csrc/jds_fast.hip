@@ -31,6 +31,10 @@
 #ifndef JDS_FOLD_MODE
 #define JDS_FOLD_MODE 1
 #endif
+// k_fwd32i's staging pass: ring rows on the lanes after the tile's rows
+#ifndef JDS_RING_LAST
+#define JDS_RING_LAST 1
+#endif
 
 namespace jds {
 
@@ -354,10 +358,118 @@ __device__ __forceinline__ void stats_flush_ticket(LaneStats ls, bool valid, uns
     slot[t] = tot;
   }
 }
+// The ticket form with the per-row records summed by the LDS instead of by the
+// last wave: each 16-lane row total widens its 8-bit bin fields into four
+// words of 16-bit fields (a workgroup counts <= 384 lanes x 8 = 3072 per bin,
+// nonzero <= 3072, magnitude bits <= 384 x 88 = 33792) and adds them, with the
+// nonzero | magnitude-bits word, into s_st[NSTAT + 1 ..] by LDS atomics (no
+// return); lane 63 adds the wave's valid-lane count.  The last wave then
+// decodes five words once instead of 4 x waves records (the ticket form's
+// loop was ~24 dependent reads and ~200 VALU in one wave per workgroup).
+// s_st holds NST_LDS words (zeroed by the kernel): [0, NSTAT) the tile's
+// record with quant8's rare bins, [NSTAT] the ticket, then the packed sums.
+constexpr int NST_LDS = NSTAT + 8;
+__device__ __forceinline__ void stats_flush_atomic(LaneStats ls, bool valid, unsigned* s_st,
+                                                   uint32_t* __restrict__ slot) {
+  if (!valid) ls = LaneStats();
+  const unsigned h = ls.hn;
+  unsigned v[3] = {h & 0x0f0f0f0fu, (h >> 4) & 0x0f0f0f0fu, ls.nz | (ls.mb << 16)};
+  row_sums3(v);
+  const int lane = threadIdx.x & 63;
+  const int nw = (int)(blockDim.x >> 6);
+  unsigned* pk = s_st + NSTAT + 1;
+  if ((lane & 15) == 15) {
+    // even bins 22, 24, 26, 28 in v[0]'s bytes, odd in v[1]'s: words of
+    // 16-bit fields (22 | 26), (24 | 28), (23 | 27), (25 | 29)
+    atomicAdd(pk + 0, v[0] & 0x00ff00ffu);
+    atomicAdd(pk + 1, (v[0] >> 8) & 0x00ff00ffu);
+    atomicAdd(pk + 2, v[1] & 0x00ff00ffu);
+    atomicAdd(pk + 3, (v[1] >> 8) & 0x00ff00ffu);
+    atomicAdd(pk + 4, v[2]);
+  }
+  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
+  if (lane == 63) atomicAdd(pk + 5, nvalid);
+  // (a compiler barrier only: a memory fence would also wait for the wave's
+  // global coefficient stores; the LDS performs one wave's operations in order)
+  __asm__ volatile("" ::: "memory");
+  unsigned ticket = 0u;
+  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
+  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
+  if (ticket != (unsigned)(nw - 1)) return;
+  __asm__ volatile("" ::: "memory");
+  if (lane < NSTAT) {
+    const unsigned nzmb = pk[4];
+    const unsigned nz = nzmb & 0xffffu, mb = nzmb >> 16;
+    const int b = lane - 2 - 22;  // common bin 22 + b: word 2 (b & 1) + ((b >> 1) & 1), field b >> 2
+    const unsigned w = pk[((b & 1) << 1) | ((b >> 1) & 1)];
+    unsigned add = (b >> 2) ? (w >> 16) : (w & 0xffffu);
+    if (b == 3) add -= 8u * pk[5] - nz;  // zeros fall in bin 25: k_finalize adds them
+    add = lane == 0 ? nz : (lane == 1 ? mb + nz : ((unsigned)b < 8u ? add : 0u));
+    slot[lane] = s_st[lane] + add;
+  }
+}
+
+// The ticket form with the wave's rows summed in the wave: after the row sums
+// the 8-bit fields widen into four words of 16-bit fields plus the nonzero |
+// magnitude-bits word (a wave counts <= 64 x 8 = 512 per bin), two DPP row
+// broadcasts sum the rows into lane 63, which stores one 5-word record; the
+// last wave decodes one record per wave instead of four.
+__device__ __forceinline__ void stats_flush_wave(LaneStats ls, bool valid, unsigned* s_st,
+                                                 uint32_t* __restrict__ slot) {
+  __shared__ __attribute__((aligned(16))) unsigned s_wr[NW_MAX][8];  // [wave][word]: 5 sums, valid lanes
+  if (!valid) ls = LaneStats();
+  const unsigned h = ls.hn;
+  unsigned v[3] = {h & 0x0f0f0f0fu, (h >> 4) & 0x0f0f0f0fu, ls.nz | (ls.mb << 16)};
+  row_sums3(v);
+  // words of 16-bit fields: (22 | 26), (24 | 28), (23 | 27), (25 | 29), nz | mb
+  unsigned u[5] = {v[0] & 0x00ff00ffu, (v[0] >> 8) & 0x00ff00ffu, v[1] & 0x00ff00ffu, (v[1] >> 8) & 0x00ff00ffu, v[2]};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) u[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u[k], 0x142, 0xa, 0xf, false);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) u[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u[k], 0x143, 0xc, 0xf, false);
+  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nw = (int)(blockDim.x >> 6);
+  if (lane == 63) {
+    *reinterpret_cast<uint4*>(&s_wr[w][0]) = make_uint4(u[0], u[1], u[2], u[3]);
+    *reinterpret_cast<uint2*>(&s_wr[w][4]) = make_uint2(u[4], nvalid);
+  }
+  __asm__ volatile("" ::: "memory");
+  unsigned ticket = 0u;
+  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
+  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
+  if (ticket != (unsigned)(nw - 1)) return;
+  __asm__ volatile("" ::: "memory");
+  if (lane < NSTAT) {
+    // lane 0: nz; lane 1: mb + nz; lanes 24..31: bin 22 + b from word
+    // 2 (b & 1) + ((b >> 1) & 1), field b >> 2; bin 25 less the zeros
+    const int b = lane - 2 - 22;
+    const bool bin = (unsigned)b < 8u;
+    const int k = bin ? ((b & 1) << 1) | ((b >> 1) & 1) : 4;
+    const unsigned sh = bin ? 16u * (unsigned)(b >> 2) : 0u;
+    const unsigned m1 = (lane < 2 || bin) ? 0xffffu : 0u, m2 = lane == 1 ? 0xffffu : 0u;
+    unsigned tot = 0u, zeros = 0u;
+    for (int i = 0; i < nw; ++i) {
+      const unsigned x = s_wr[i][k];
+      tot += ((x >> sh) & m1) + ((x >> 16) & m2);
+      zeros += 8u * s_wr[i][5] - (s_wr[i][4] & 0xffffu);
+    }
+    if (b == 3) tot -= zeros;  // zeros fall in bin 25: k_finalize adds them
+    slot[lane] = s_st[lane] + tot;
+  }
+}
+
+#ifndef JDS_FLUSH_FORM
+#define JDS_FLUSH_FORM 3  // 3: stats_flush_wave; 2: stats_flush_atomic; 1: stats_flush_ticket (below the barrier TF)
+#endif
 template <int TF>
 __device__ __forceinline__ void stats_flush(LaneStats ls, bool valid, unsigned* s_st, uint32_t* __restrict__ slot) {
   if constexpr (TF >= JDS_FLUSH_BARRIER_TF)
     stats_flush_barrier(ls, valid, s_st, slot);
+  else if constexpr (JDS_FLUSH_FORM == 3)
+    stats_flush_wave(ls, valid, s_st, slot);
+  else if constexpr (JDS_FLUSH_FORM == 2)
+    stats_flush_atomic(ls, valid, s_st, slot);
   else
     stats_flush_ticket(ls, valid, s_st, slot);
 }
@@ -390,7 +502,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   __shared__ __attribute__((aligned(16))) float s_u[U_F];
   __shared__ __attribute__((aligned(16))) float s_rq[64];
   __shared__ __attribute__((aligned(16))) float s_thr[2][64];
-  __shared__ unsigned s_st[NSTAT + 1];  // + stats_flush's ticket
+  __shared__ unsigned s_st[NST_LDS];  // + stats_flush's ticket and packed sums
 
   const int tid = threadIdx.x;
   const int frame = blockIdx.y;
@@ -433,7 +545,7 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
     s_thr[0][tid] = fq[frame].thr[0][tid];
     s_thr[1][tid] = fq[frame].thr[1][tid];
   }
-  if (tid <= NSTAT) s_st[tid] = 0u;
+  if (tid < NST_LDS) s_st[tid] = 0u;
 
   const int blk = tid >> 3, line = tid & 7;
   int plane, by_t, bx_t;
@@ -658,7 +770,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   __shared__ __attribute__((aligned(16))) float s_cd[NCD * BS32];   // chroma blocks after the row DCT
   __shared__ __attribute__((aligned(16))) float s_rqT[64];          // 1/Q transposed: [v][k]
   __shared__ __attribute__((aligned(16))) float s_thT[2][64];
-  __shared__ unsigned s_st[NSTAT + 1];  // + stats_flush's ticket
+  __shared__ unsigned s_st[NST_LDS];  // + stats_flush's ticket and packed sums
 
   const int tid = threadIdx.x, frame = blockIdx.y;
   const int ncol = rect.w - rect.z + 1;
@@ -679,14 +791,21 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     s_thT[0][tid] = fq[frame].thr[0][t];
     s_thT[1][tid] = fq[frame].thr[1][t];
   }
-  if (tid <= NSTAT) s_st[tid] = 0u;
+  if (tid < NST_LDS) s_st[tid] = 0u;
   const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
   float* s_cb = s_c;
   float* s_cr = s_c + CR * CW;
 
   // ---- 1. row segments --------------------------------------------------------
   if (tid < WR * SEG) {
+#if JDS_RING_LAST
+    // the tile's rows 1..TH on the first TH * SEG lanes (whole waves), the
+    // prefilter's ring rows 0 and TH + 1 (chroma only) after them: the wave
+    // holding the ring rows skips the luma row DCT as a whole
+    const int r = tid < TH * SEG ? 1 + tid / SEG : (tid < (TH + 1) * SEG ? 0 : TH + 1), c = tid % SEG;
+#else
     const int r = tid / SEG, c = tid % SEG;
+#endif
     if (CPLANE || (r >= 1 && r <= TH)) {  // uniform per row (lane groups of SEG)
       // the tile lies inside the image; only the 1-px ring may leave it:
       // BORDER_REFLECT_101 maps row -1 to 1 and row H to H-2 (columns below)

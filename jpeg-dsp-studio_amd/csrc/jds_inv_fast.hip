@@ -255,6 +255,38 @@ __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, ui
   return ab | cd;
 }
 
+// The tile certificate's reduction (JDS_INV_CERT_DPP): per 16-lane row by four
+// DPP row shifts (lanes without a source keep the identity), then the row
+// totals into three LDS words by LDS min / max atomics (no return): thread 0
+// reads three words instead of looping over every wave's record, and the
+// waves skip six cross-lane permutes per value.
+#ifndef JDS_INV_CERT_DPP
+#define JDS_INV_CERT_DPP 1
+#endif
+#ifndef JDS_INV_WIN_SEL
+#define JDS_INV_WIN_SEL 1
+#endif
+template <int SH>
+__device__ __forceinline__ void cert_row_step(uint32_t& mn, uint32_t& mx, uint32_t& qm) {
+  const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)mn, 0x110 + SH, 0xf, 0xf, false);
+  const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x110 + SH, 0xf, 0xf, false);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)qm, 0x110 + SH, 0xf, 0xf, false);
+  mn = mn < a ? mn : a;
+  mx = mx > b ? mx : b;
+  qm = qm > c ? qm : c;
+}
+__device__ __forceinline__ void cert_to_lds(uint32_t mn, uint32_t mx, uint32_t qm, uint32_t* s_cert) {
+  cert_row_step<1>(mn, mx, qm);
+  cert_row_step<2>(mn, mx, qm);
+  cert_row_step<4>(mn, mx, qm);
+  cert_row_step<8>(mn, mx, qm);  // lane 15 of each row: the row's min / max
+  if ((threadIdx.x & 15) == 15) {
+    atomicMin(&s_cert[0], mn);
+    atomicMax(&s_cert[1], mx);
+    atomicMax(&s_cert[2], qm);
+  }
+}
+
 // The fast pass over one tile (sets sh.redo when the tile must be recomputed).
 template <int MODE, int XTRA>
 __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const Geo& g, const int tiles_x,
@@ -271,6 +303,10 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   __shared__ double s_qmax;
   __shared__ double s_red[I::NT / 64], s_dq[I::NT / 64];
   __shared__ uint32_t s_lmin[I::NT / 64], s_lmax[I::NT / 64];
+  __shared__ uint32_t s_cert[3];  // JDS_INV_CERT_DPP: min / max fraction word, max |q|
+#if JDS_INV_WIN_SEL
+  __shared__ double s_dummy[64];  // the window stores' sink for ring columns outside it
+#endif
   __shared__ unsigned long long s_sse;
   const int tid = threadIdx.x, lv = tid & 7, lb = tid >> 3;
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
@@ -282,7 +318,12 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     double m = q;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-    if (tid == 0) s_qmax = m;
+    if (tid == 0) {
+      s_qmax = m;
+      s_cert[0] = 0xffffffffu;
+      s_cert[1] = 0u;
+      s_cert[2] = 0u;
+    }
   }
   if (XTRA && tid == 0) s_sse = 0ull;
   __syncthreads();
@@ -323,9 +364,17 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
           fast_row<-128>(s_mid + lb * MS, lv, c);
           double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWC];
           const int wc0 = bx * 8 - cwx0;
+#if JDS_INV_WIN_SEL
+          // the ring blocks' columns outside the window go to a per-lane dummy
+          // slot: a select per store instead of a branch per store
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            *((unsigned)(wc0 + k) < (unsigned)I::CWC ? w + wc0 + k : s_dummy + (tid & 63)) = c[k];
+#else
 #pragma unroll
           for (int k = 0; k < 8; ++k)
             if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k];
+#endif
           if constexpr (I::SX == 2) {
             // cv2's clamped taps at the image's left / right edge pixels read the
             // edge column alone: replicate it into the ring (and past the
@@ -458,6 +507,9 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
 
   // ---- 3. certification: the tile's closest approach to an integer vs its bound
   int qm = max(qhi, -qlo);  // max |q| this lane read
+#if JDS_INV_CERT_DPP
+  cert_to_lds(lo_min, lo_max, (uint32_t)qm, s_cert);
+#else
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t a = __shfl_xor(lo_min, o, 64), b = __shfl_xor(lo_max, o, 64);
@@ -465,6 +517,7 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     lo_max = lo_max > b ? lo_max : b;
     qm = max(qm, __shfl_xor(qm, o, 64));
   }
+#endif
   if constexpr (XTRA > 0) {
     unsigned long long s = sse;
 #pragma unroll
@@ -475,13 +528,19 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     for (int o = 32; o > 0; o >>= 1) d = d + __shfl_xor(d, o, 64);  // (no products: nothing to fuse)
     if ((tid & 63) == 0) s_red[tid >> 6] = d;
   }
+#if !JDS_INV_CERT_DPP
   if ((tid & 63) == 0) {
     s_lmin[tid >> 6] = lo_min;
     s_lmax[tid >> 6] = lo_max;
     s_dq[tid >> 6] = (double)qm;
   }
+#endif
   __syncthreads();
   if (tid == 0) {
+#if JDS_INV_CERT_DPP
+    const uint32_t mn = s_cert[0], mx = s_cert[1];
+    const double q = (double)s_cert[2];
+#else
     uint32_t mn = 0xffffffffu, mx = 0u;
     double q = 0.0;
     for (int i = 0; i < I::NT / 64; ++i) {
@@ -489,6 +548,7 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       mx = mx > s_lmax[i] ? mx : s_lmax[i];
       q = fmax(q, s_dq[i]);
     }
+#endif
     // |v_fast - v_ref| <= E, plus <= 3 roundings on the magic grid (2^-33 each:
     // byte_cert); T in units of 2^-32
     const double E = K_LIN * (q * s_qmax) + K_CONST + 0x1p-31;
