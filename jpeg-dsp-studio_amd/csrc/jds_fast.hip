@@ -35,6 +35,14 @@
 #ifndef JDS_RING_LAST
 #define JDS_RING_LAST 1
 #endif
+// k_fwd444w's statistics: one record per wave (rows summed by DPP broadcasts)
+#ifndef JDS_F444_WAVE_REC
+#define JDS_F444_WAVE_REC 1
+#endif
+// k_fwd32i's staging pass: neighbour samples by DPP instead of ds_bpermute
+#ifndef JDS_STAGE_DPP
+#define JDS_STAGE_DPP 1
+#endif
 
 namespace jds {
 
@@ -274,7 +282,7 @@ constexpr int NW_MAX = 8;  // waves per forward workgroup (TF <= 512)
 // with 8 waves per workgroup (4:2:2: k_fwd32i 379 vs 418 us per 16 x 4K),
 // the ticket form below with 6 (4:2:0: 325 vs 333 us per 64 x 1080p).
 #ifndef JDS_FLUSH_BARRIER_TF
-#define JDS_FLUSH_BARRIER_TF 512  // workgroups of at least this many threads take the barrier form
+#define JDS_FLUSH_BARRIER_TF 1024  // workgroups of at least this many threads take the barrier form (512: see DESIGN)
 #endif
 __device__ __forceinline__ void stats_flush_barrier(LaneStats ls, bool valid, unsigned* s_st,
                                                     uint32_t* __restrict__ slot) {
@@ -758,6 +766,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
          jds_frame_stats* __restrict__ stz, const int nzq) {
   using C = Cfg<MODE>;
   constexpr int TH = C::TH, TW = C::TW, WR = TH + 2, SEG = TW / 8;
+  static_assert(16 % SEG == 0, "staging segment groups tile the 16-lane DPP rows");
   constexpr bool SUB = MODE != M444;
   constexpr bool CPLANE = SUB && PF;
   constexpr int CR = SUB ? (CPLANE ? WR : TH) : TH;  // chroma plane rows
@@ -855,8 +864,16 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
           dr[1] = make_float4(cr[4], cr[5], cr[6], cr[7]);
         }
       } else if constexpr (CPLANE) {
+#if JDS_STAGE_DPP
+        // neighbours' edge samples by DPP row shifts (a 16-lane row holds two
+        // segment groups; the lanes whose source lies outside their group,
+        // c == 0 and c == SEG - 1, take the ring values below)
+        float lb = dpp_f32<0x111>(cb[7]), lr = dpp_f32<0x111>(cr[7]);  // row_shr:1
+        float rb = dpp_f32<0x101>(cb[0]), rr = dpp_f32<0x101>(cr[0]);  // row_shl:1
+#else
         float lb = __shfl_up(cb[7], 1, SEG), lr = __shfl_up(cr[7], 1, SEG);
         float rb = __shfl_down(cb[0], 1, SEG), rr = __shfl_down(cr[0], 1, SEG);
+#endif
         if (c == 0) {  // bytes 5..7 of the 8 before the segment; pixel 1 at the image edge
           const float R = (float)((ring.y >> 8) & 255u), G = (float)((ring.y >> 16) & 255u), B = (float)(ring.y >> 24);
           lb = left_edge ? cb[1] : cb32(R, G, B);
@@ -1188,6 +1205,22 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
   nzmb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)nzmb, 0x118, 0xf, 0xf, true);
   const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
   const int wv = tid >> 6, lane = tid & 63;
+#if JDS_F444_WAVE_REC
+  // the four rows into lane 63 by two DPP row broadcasts (a wave counts <= 64 x
+  // 24 = 1536 per field, magnitude bits <= 64 x 384): one record per wave
+  unsigned u5[5] = {r5[0], r5[1], r5[2], r5[3], nzmb};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) u5[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u5[k], 0x142, 0xa, 0xf, false);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) u5[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u5[k], 0x143, 0xc, 0xf, false);
+  if (lane == 63) {
+    unsigned* rr = s_rows[wv][0];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) rr[k] = u5[k];
+    s_nvalid[wv] = nvalid;
+  }
+  constexpr int NREC = 1;
+#else
   if ((lane & 15) == 15) {
     unsigned* rr = s_rows[wv][lane >> 4];
     rr[0] = r5[0];
@@ -1197,6 +1230,8 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     rr[4] = nzmb;
     if (lane == 63) s_nvalid[wv] = nvalid;
   }
+  constexpr int NREC = 4;
+#endif
   __asm__ volatile("" ::: "memory");
   unsigned ticket = 0u;
   if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
@@ -1208,7 +1243,7 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     for (int i = 0; i < F444_WAVES; ++i) {
       unsigned nz = 0u, mb = 0u, f[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < NREC; ++r) {
         const unsigned* rr = s_rows[i][r];
         nz += rr[4] & 0xffffu;
         mb += rr[4] >> 16;

@@ -92,6 +92,13 @@ __device__ inline double sample64(const uint8_t* img, const Geo& g, int plane, i
 constexpr float QMAGIC = 0x1.8p+23f;
 constexpr uint32_t QMAGIC_BITS = 0x4B400000u;
 
+// A float from another lane of the same 16-lane row by a DPP move (lanes
+// whose source lies outside the row read 0).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, true));
+}
+
 template <int SH, int N>
 __device__ __forceinline__ void row_shr_add(unsigned (&v)[N]) {
   unsigned t[N];

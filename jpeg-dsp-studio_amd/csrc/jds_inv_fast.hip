@@ -723,8 +723,16 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
   }
   // the block's Dmax over its three planes (its 8 lanes), then this lane's margin
   int qm = max(qhi, -qlo);
+#if JDS_INV_CERT_DPP
+  // over the block's 8 lanes by DPP: quad_perm xor 1, xor 2, then row_half_mirror
+  // (lane i of 8 with lane 7 - i, in the other quad)
+  qm = max(qm, __builtin_amdgcn_update_dpp(0, qm, 0xb1, 0xf, 0xf, true));
+  qm = max(qm, __builtin_amdgcn_update_dpp(0, qm, 0x4e, 0xf, 0xf, true));
+  qm = max(qm, __builtin_amdgcn_update_dpp(0, qm, 0x141, 0xf, 0xf, true));
+#else
 #pragma unroll
   for (int m = 1; m < 8; m <<= 1) qm = max(qm, __shfl_xor(qm, m, 64));
+#endif
   const double E = K_LIN * ((double)qm * s_qmax) + K_CONST + 0x1p-31;
   const double T = ceil(E * 0x1p+32) + 1.0;
   const bool unc = row_ok && ((double)lo_min <= T || (double)lo_max >= 0x1p+32 - 1.0 - T);
@@ -874,6 +882,7 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
   __shared__ double s_qmax;
   __shared__ double s_dq[I::NT / 64];
   __shared__ uint32_t s_lmin[I::NT / 64], s_lmax[I::NT / 64];
+  __shared__ uint32_t s_cert[3];  // JDS_INV_CERT_DPP: min / max fraction word, max |q|
   __shared__ int s_redo;
   const int tid = threadIdx.x, grp = tid >> 4, line = tid & 15;
   const int frame = blockIdx.y, tile = blockIdx.x;
@@ -888,7 +897,12 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
     s_qi[tid] = (int)m;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-    if (tid == 0) s_qmax = m;
+    if (tid == 0) {
+      s_qmax = m;
+      s_cert[0] = 0xffffffffu;
+      s_cert[1] = 0u;
+      s_cert[2] = 0u;
+    }
   }
   __syncthreads();
 
@@ -1054,6 +1068,9 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
 
   // ---- 3. certification: the tile's closest approach to an integer vs its bound
   int qm = max(qhi, -qlo);
+#if JDS_INV_CERT_DPP
+  cert_to_lds(lo_min, lo_max, (uint32_t)qm, s_cert);
+#else
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t a = __shfl_xor(lo_min, o, 64), b = __shfl_xor(lo_max, o, 64);
@@ -1066,8 +1083,13 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
     s_lmax[tid >> 6] = lo_max;
     s_dq[tid >> 6] = (double)qm;
   }
+#endif
   __syncthreads();
   if (tid == 0) {
+#if JDS_INV_CERT_DPP
+    const uint32_t mn = s_cert[0], mx = s_cert[1];
+    const double q = (double)s_cert[2];
+#else
     uint32_t mn = 0xffffffffu, mx = 0u;
     double q = 0.0;
     for (int i = 0; i < I::NT / 64; ++i) {
@@ -1075,6 +1097,7 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
       mx = mx > s_lmax[i] ? mx : s_lmax[i];
       q = fmax(q, s_dq[i]);
     }
+#endif
     const double E = K_LIN16 * (q * s_qmax) + K_CONST16 + 0x1p-31;
     const double T = ceil(E * 0x1p+32) + 1.0;
     const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
