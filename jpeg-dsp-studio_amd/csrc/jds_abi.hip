@@ -284,9 +284,12 @@ static void fill_geometry(const Geo& G, int mode, jds_geometry* o) {
 }
 
 static void make_fq(const jds_params* p, FrameQ* q) {
+  q->qmax = 0.0;
+  q->pad_ = 0.0;
   for (int i = 0; i < 64; ++i) {
     q->q[i] = p->qtable[i];
     q->q16[i] = 16.0 * p->qtable[i];  // exact
+    q->qmax = q->qmax > p->qtable[i] ? q->qmax : p->qtable[i];
   }
 }
 

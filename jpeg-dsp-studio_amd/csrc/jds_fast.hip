@@ -39,6 +39,10 @@
 #ifndef JDS_F444_WAVE_REC
 #define JDS_F444_WAVE_REC 1
 #endif
+// k_fwd32i: the quantiser tables loaded by the wave without staging work
+#ifndef JDS_TABLES_IDLE_WAVE
+#define JDS_TABLES_IDLE_WAVE 1
+#endif
 // k_fwd32i's staging pass: neighbour samples by DPP instead of ds_bpermute
 #ifndef JDS_STAGE_DPP
 #define JDS_STAGE_DPP 1
@@ -794,12 +798,25 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
   const int y0 = m0y * C::MH, x0 = m0x * C::MW;
   const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
+#if JDS_TABLES_IDLE_WAVE
+  // the quantiser tables by the last wave, which has no staging work: the
+  // staging waves do not wait for these loads before their own
+  static_assert((TH + 2) * (TW / 8) <= Cfg<MODE>::TF - 64, "the last wave is idle in the staging pass");
+  if (!MQ && tid >= Cfg<MODE>::TF - 64) {
+    const int l = tid - (Cfg<MODE>::TF - 64);
+    const int t = (l & 7) * 8 + (l >> 3);  // [v][k] <- [k][v]
+    s_rqT[l] = fq[frame].rq[t];
+    s_thT[0][l] = fq[frame].thr[0][t];
+    s_thT[1][l] = fq[frame].thr[1][t];
+  }
+#else
   if (!MQ && tid < 64) {
     const int t = (tid & 7) * 8 + (tid >> 3);  // [v][k] <- [k][v]
     s_rqT[tid] = fq[frame].rq[t];
     s_thT[0][tid] = fq[frame].thr[0][t];
     s_thT[1][tid] = fq[frame].thr[1][t];
   }
+#endif
   if (tid < NST_LDS) s_st[tid] = 0u;
   const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
   float* s_cb = s_c;

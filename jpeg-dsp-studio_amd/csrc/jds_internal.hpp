@@ -114,6 +114,8 @@ struct InvFix {
 struct FrameQ {
   double q16[64];
   double q[64];
+  double qmax;  // max q (the certified inverses' Dmax scale: a scalar load, no reduction)
+  double pad_;
 };
 
 // Tile configuration per subsampling mode.

@@ -266,6 +266,12 @@ __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, ui
 #ifndef JDS_INV_WIN_SEL
 #define JDS_INV_WIN_SEL 1
 #endif
+#ifndef JDS_INV_EARLY_LOADS
+#define JDS_INV_EARLY_LOADS 1
+#endif
+#ifndef JDS_INV_QMAX_FQ
+#define JDS_INV_QMAX_FQ 1
+#endif
 template <int SH>
 __device__ __forceinline__ void cert_row_step(uint32_t& mn, uint32_t& mx, uint32_t& qm) {
   const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)mn, 0x110 + SH, 0xf, 0xf, false);
@@ -312,22 +318,8 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int Y0 = ty * I::TH, X0 = tx * I::TW;
   const int16_t* cf = coeffs + (size_t)frame * g.cpf;
-  if (tid < 64) {
-    const double q = fq[frame].q[tid];
-    s_qs[tid] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
-    double m = q;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-    if (tid == 0) {
-      s_qmax = m;
-      s_cert[0] = 0xffffffffu;
-      s_cert[1] = 0u;
-      s_cert[2] = 0u;
-    }
-  }
-  if (XTRA && tid == 0) s_sse = 0ull;
-  __syncthreads();
-
+  // the tile's first coefficient loads are issued before the table set-up and
+  // its barrier (JDS_INV_EARLY_LOADS), so their latency overlaps it
   int qhi = 0, qlo = 0;  // max / min q this lane read (max |q| = max(qhi, -qlo))
 
   // ---- 1. chroma window: (clip(IDCT) - 128) of the blocks the tile reaches --
@@ -340,19 +332,60 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     bx = X0 / 8 + bj;
     return by < g.nby && bx < g.nbx;
   };
+  auto table_setup = [&]() {
+    if (tid < 64) {
+      const double q = fq[frame].q[tid];
+      s_qs[tid] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
+#if JDS_INV_QMAX_FQ
+      // max Q from the host's FrameQ::qmax (a scalar load at the end): no
+      // cross-lane reduction before the barrier
+      if (tid == 0) {
+        s_cert[0] = 0xffffffffu;
+        s_cert[1] = 0u;
+        s_cert[2] = 0u;
+      }
+#else
+      double m = q;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+      if (tid == 0) {
+        s_qmax = m;
+        s_cert[0] = 0xffffffffu;
+        s_cert[1] = 0u;
+        s_cert[2] = 0u;
+      }
+#endif
+    }
+    if (XTRA && tid == 0) s_sse = 0ull;
+    __syncthreads();
+  };
+#if !JDS_INV_EARLY_LOADS
+  table_setup();
+#endif
   Col16 lq;
   {
     int by, bx;
     const bool ok = luma_blk(0, by, bx);
     lq = load_col(cf, ((long long)by * g.nbx + bx) * 64, lv, ok);
   }
-  if (tid < I::NCB * 8) {
-    const int i = lb / I::CBC, j = lb - i * I::CBC;
-    const int by = cby0 + i, bx = cbx0 + j;
-    const bool bvalid = by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx;
+  const bool ctask = tid < I::NCB * 8;
+  const int ci = lb / I::CBC, cj = lb - ci * I::CBC;
+  const int cby = cby0 + ci, cbx = cbx0 + cj;
+  const bool cvalid = ctask && cby >= 0 && cbx >= 0 && cby < g.ncy && cbx < g.ncx;
+  const long long cboff = ((long long)cby * g.ncx + cbx) * 64;
+  Col16 cq = load_col(cf + g.off_cb, cboff, lv, cvalid);
+#if JDS_INV_EARLY_LOADS
+  table_setup();
+#endif
+#if JDS_INV_QMAX_FQ
+  if (tid == 0) s_qmax = fq[frame].qmax;  // (used by this thread after the next barrier)
+#endif
+  if (ctask) {
+    const int i = ci;
+    const int by = cby, bx = cbx;
+    const bool bvalid = cvalid;
     const bool need = !I::RY || (i == 0 ? lv == 7 : (i == I::CBR - 1 ? lv == 0 : true));
-    const long long boff = ((long long)by * g.ncx + bx) * 64;
-    Col16 cq = load_col(cf + g.off_cb, boff, lv, bvalid);
+    const long long boff = cboff;
 #pragma unroll 1
     for (int p = 0; p < 2; ++p) {
       const Col16 cur = cq;
@@ -651,16 +684,6 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
     item_cnt[((rot + 1) % 3) * n_items + frame] = 0u;  // the next run's
     if (frame == 0) *next_count = 0u;                  // the next run counts from zero
   }
-  if (tid < 64) {
-    const double q = fq[frame].q[tid];
-    s_qs[tid] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
-    s_qi[tid] = (int)q;
-    double m = q;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-    if (tid == 0) s_qmax = m;
-  }
-  __syncthreads();
   const long long nblk = (long long)g.nby * g.nbx;
   const long long blk = (long long)blockIdx.x * (8 * I444_WAVES) + lb;
   const bool bvalid = blk < nblk;
@@ -668,9 +691,28 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
   const int by = (int)(bq / g.nbx), bx = (int)(bq - (long long)by * g.nbx);
   const int16_t* cf = coeffs + (size_t)frame * g.cpf;
   double* slot = s_mid + lb * MS;
+  // the coefficient loads are issued before the table set-up and its barrier
   const Col16 qy = load_col(cf, bq * 64, lv, bvalid);
   const Col16 qb = load_col(cf + g.off_cb, bq * 64, lv, bvalid);
   const Col16 qr = load_col(cf + g.off_cr, bq * 64, lv, bvalid);
+  if (tid < 64) {
+    const double q = fq[frame].q[tid];
+    s_qs[tid] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
+    s_qi[tid] = (int)q;
+#if JDS_INV_QMAX_FQ
+#else
+    double m = q;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if (tid == 0) s_qmax = m;
+#endif
+  }
+  __syncthreads();
+#if JDS_INV_QMAX_FQ
+  const double qmax = fq[frame].qmax;
+#else
+  const double qmax = s_qmax;
+#endif
   const int y = by * 8 + lv, x0 = bx * 8;
   const bool row_ok = bvalid && y < g.H;
   const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
@@ -733,7 +775,7 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
 #pragma unroll
   for (int m = 1; m < 8; m <<= 1) qm = max(qm, __shfl_xor(qm, m, 64));
 #endif
-  const double E = K_LIN * ((double)qm * s_qmax) + K_CONST + 0x1p-31;
+  const double E = K_LIN * ((double)qm * qmax) + K_CONST + 0x1p-31;
   const double T = ceil(E * 0x1p+32) + 1.0;
   const bool unc = row_ok && ((double)lo_min <= T || (double)lo_max >= 0x1p+32 - 1.0 - T);
 #ifndef JDS_PROBE_NOFALLBACK
@@ -895,8 +937,12 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
   if (tid < 64) {
     double m = fq[frame].q[tid];
     s_qi[tid] = (int)m;
+#if JDS_INV_QMAX_FQ
+    m = fq[frame].qmax;
+#else
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+#endif
     if (tid == 0) {
       s_qmax = m;
       s_cert[0] = 0xffffffffu;
