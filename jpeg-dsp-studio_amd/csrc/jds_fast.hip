@@ -39,6 +39,10 @@
 #ifndef JDS_F444_WAVE_REC
 #define JDS_F444_WAVE_REC 1
 #endif
+// single-quality forwards: the statistics partials summed inside k_fix_fwd's launch
+#ifndef JDS_FIX_REDUCE
+#define JDS_FIX_REDUCE 1
+#endif
 // k_fwd32i: the quantiser tables loaded by the wave without staging work
 #ifndef JDS_TABLES_IDLE_WAVE
 #define JDS_TABLES_IDLE_WAVE 1
@@ -1352,7 +1356,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(JDS_FIX
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
           const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq, const int n_flat,
-          unsigned* __restrict__ rearm) {
+          unsigned* __restrict__ rearm, const uint32_t* __restrict__ part = nullptr, const int ptiles = 0,
+          const int fix_gx = 0) {
+  // single-quality plans (JDS_FIX_REDUCE): the workgroups past the fix-up's
+  // grid (blockIdx.x >= fix_gx) sum the statistics partials of 8 tiles of
+  // frame blockIdx.y into the frame stats -- k_fwd_reduce's work in the same
+  // launch (both only add to the stats, so the two orders agree)
+  if (ptiles > 0 && (int)blockIdx.x >= fix_gx) {
+    const int f = blockIdx.y, t0 = ((int)blockIdx.x - fix_gx) * 8, j = threadIdx.x;
+    if (j < NSTAT) {
+      unsigned v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = t0 + i < ptiles ? part[((size_t)f * ptiles + t0 + i) * NSTAT + j] : 0u;
+      unsigned long long a = 0ull;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a += v[i];
+      jds_frame_stats* sf = st + f;
+      unsigned long long* dst = j == 0 ? (unsigned long long*)&sf->nonzero
+                                : j == 1 ? (unsigned long long*)&sf->magnitude_bits
+                                         : (unsigned long long*)&sf->hist[j - 2];
+      if (a) atomicAdd(dst, a);
+    }
+    return;
+  }
   constexpr bool CPLANE = (MODE != M444) && PF;
   constexpr int SY = Cfg<MODE>::SY;
   constexpr int WRR = 8 * SY + 2, WCC = 18;  // prefilter source window of one chroma block
@@ -1399,7 +1425,8 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     if (rearm != nullptr && blockIdx.x == 0 && t == 0) rearm[blockIdx.y] = 0u;
   }
   const double k[3] = {gk[0], gk[1], gk[2]};
-  for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
+  const unsigned gstride = fix_gx > 0 ? (unsigned)fix_gx : gridDim.x;
+  for (unsigned e = blockIdx.x; e < count; e += gstride) {
     uint2 ent;
     if (n_flat) {  // entry e of the concatenated lists: item = last start <= e
       int lo = 0, hi = n_flat - 1;
@@ -1410,7 +1437,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
       ent = list[(size_t)lo * cap + (e - s_off[lo])];
     } else {
       ent = next;
-      if (e + gridDim.x < count) next = list[e + gridDim.x];
+      if (e + gstride < count) next = list[e + gstride];
     }
     const int frame = (int)ent.x;
     const int plane = (int)(ent.y >> 24);
@@ -1715,10 +1742,15 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     hipLaunchKernelGGL(k_fwd444w, dim3(ng, n), dim3(64 * F444_WAVES), 0, s, g, rgb, coeffs, fq32, part, fixlist, fc, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if ((e = launch_fwd_reduce(n, st, part, ng, s)) != hipSuccess) return e;
     const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
+#if JDS_FIX_REDUCE
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ng + 7) / 8, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st,
+                       fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ng, gx);
+#else
+    if ((e = launch_fwd_reduce(n, st, part, ng, s)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
+#endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
   }
@@ -1777,9 +1809,14 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     // the front end appended to and re-arms the other bank.  (Reducing the
     // partials inside k_fix_fwd instead of this launch measured slower: 49.4
     // vs 29.1 + 5.4 us per 64 x 1080p.)
+#if JDS_FIX_REDUCE
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ptiles + 7) / 8, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk,
+                       st, fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ptiles, gx);
+#else
     if ((e = launch_fwd_reduce(n, st, part, ptiles, s)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
+#endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
   }

@@ -272,6 +272,9 @@ __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, ui
 #ifndef JDS_INV_QMAX_FQ
 #define JDS_INV_QMAX_FQ 1
 #endif
+#ifndef JDS_INV_ONE_BARRIER
+#define JDS_INV_ONE_BARRIER 0  // every thread deciding without the second barrier measured slower (312 vs 309 us)
+#endif
 template <int SH>
 __device__ __forceinline__ void cert_row_step(uint32_t& mn, uint32_t& mx, uint32_t& qm) {
   const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)mn, 0x110 + SH, 0xf, 0xf, false);
@@ -295,7 +298,7 @@ __device__ __forceinline__ void cert_to_lds(uint32_t mn, uint32_t mx, uint32_t q
 
 // The fast pass over one tile (sets sh.redo when the tile must be recomputed).
 template <int MODE, int XTRA>
-__device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const Geo& g, const int tiles_x,
+__device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const Geo& g, const int tiles_x,
                                               const int frame, const int tile, const int16_t* __restrict__ coeffs,
                                               const FrameQ* __restrict__ fq, const uint8_t* __restrict__ rgb_in,
                                               uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
@@ -569,6 +572,33 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   }
 #endif
   __syncthreads();
+#if JDS_INV_CERT_DPP && JDS_INV_ONE_BARRIER
+  {
+    // every thread decides from the three words (the same values for all: a
+    // uniform decision without thread 0's serial section and a second
+    // barrier; the exact fallback may overwrite the window at once, since
+    // every wave has passed the barrier above)
+    const uint32_t mn = s_cert[0], mx = s_cert[1];
+    const double q = (double)s_cert[2];
+    const double E = K_LIN * (q * s_qmax) + K_CONST + 0x1p-31;
+    const double T = ceil(E * 0x1p+32) + 1.0;
+    const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
+    const bool redo = uncertain || fix_all;
+    if (tid == 0) {
+      if (redo) {
+        atomicAdd(fixcount, 1u);  // tiles recomputed (jds_plan_fix_counts)
+        atomicAdd(cnt_now + frame, 1u);
+      } else if constexpr (XTRA > 0) {
+        double a = 0.0;
+        for (int i = 0; i < I::NT / 64; ++i) a = a + s_red[i];
+        sse_y_part[(size_t)frame * gridDim.x + tile] = a;
+        atomicAdd((unsigned long long*)&st[frame].sse_rgb, s_sse);
+      }
+      if (frame == 0 && tile == 0) *next_count = 0u;  // the next run counts from zero
+    }
+    return redo;
+  }
+#else
   if (tid == 0) {
 #if JDS_INV_CERT_DPP
     const uint32_t mn = s_cert[0], mx = s_cert[1];
@@ -600,6 +630,8 @@ __device__ __forceinline__ void inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     if (frame == 0 && tile == 0) *next_count = 0u;  // the next run counts from zero
   }
   __syncthreads();  // sh.redo is visible to the caller's uniform branch
+  return sh.redo != 0;
+#endif
 }
 
 // XTRA: 0 = RGB only; 1 = + exact integer SSE and luma SSE partials (sweeps),
@@ -630,6 +662,7 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
   const unsigned prev = cnt_prev[frame];
   if (tile == 0 && tid == 0) item_cnt[((rot + 1) % 3) * n_items + frame] = 0u;  // the next run's
   const bool item_exact = !probe && !fix_all && prev * 8u > ntile;
+  bool redo = false;
   if (item_exact) {
     // (uniform) this item runs the exact tile code directly and keeps its count
     if (tile == 0 && tid == 0) {
@@ -639,12 +672,12 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
     }
   } else {
     sh.redo = 0;
-    inv_fast_tile<MODE, XTRA>(sh, g, tiles_x, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part, fixcount,
-                              next_count, cnt_now, in_div, fix_all);
+    redo = inv_fast_tile<MODE, XTRA>(sh, g, tiles_x, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part,
+                                     fixcount, next_count, cnt_now, in_div, fix_all);
   }
   // one call site of the exact tile code: items in exact mode, uncertain tiles
 #ifndef JDS_PROBE_NOFALLBACK  // tools/stage_budget.py: the fast path's code alone
-  if (item_exact || sh.redo)  // (uniform)
+  if (item_exact || redo)  // (uniform)
     inv2_tile<MODE, XTRA>(sh, g, tiles_x, ntile, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part, nullptr,
                           nullptr, in_div);
 #endif
