@@ -114,8 +114,64 @@ constexpr int BS16F = 272;  // floats per 16x16 block in LDS (256 + 16 pad: colu
 // k_fwd_finish / k_finalize add bin 25's zeros from the nonzero count.
 constexpr int NW16 = 6;  // waves per k_fwd16f workgroup (TF <= 384)
 
+// The wave-record form (JDS_FLUSH16_WAVE): the bin bytes widen into four words
+// of 16-bit fields (a wave counts <= 64 x 16 = 1024 per bin) plus nonzero |
+// magnitude bits << 16 (<= 1024, <= 64 x 240), summed over the whole wave by
+// DPP (row shifts, then two row broadcasts) into lane 63, one record per
+// wave; the last wave decodes one record per wave instead of four.
+#ifndef JDS_FLUSH16_WAVE
+#define JDS_FLUSH16_WAVE 1
+#endif
+__device__ __forceinline__ void stats_flush16_wave(unsigned h0, unsigned h1, unsigned nz, unsigned mb, bool valid,
+                                                   unsigned* s_st, uint32_t* __restrict__ slot) {
+  __shared__ __attribute__((aligned(16))) unsigned s_wr[NW16][8];  // [wave][word]: 5 sums, valid lanes
+  const unsigned e = (h0 & 0x0f0f0f0fu) + (h1 & 0x0f0f0f0fu);                 // bins 0, 2, 4, 6 (bytes)
+  const unsigned o = ((h0 >> 4) & 0x0f0f0f0fu) + ((h1 >> 4) & 0x0f0f0f0fu);   // bins 1, 3, 5, 7
+  // (0 | 4), (2 | 6), (1 | 5), (3 | 7), nz | mb
+  unsigned u[5] = {e & 0x00ff00ffu, (e >> 8) & 0x00ff00ffu, o & 0x00ff00ffu, (o >> 8) & 0x00ff00ffu, nz | (mb << 16)};
+  row_sums(u);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) u[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u[k], 0x142, 0xa, 0xf, false);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) u[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u[k], 0x143, 0xc, 0xf, false);
+  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nw = (int)(blockDim.x >> 6);
+  if (lane == 63) {
+    *reinterpret_cast<uint4*>(&s_wr[w][0]) = make_uint4(u[0], u[1], u[2], u[3]);
+    *reinterpret_cast<uint2*>(&s_wr[w][4]) = make_uint2(u[4], nvalid);
+  }
+  __asm__ volatile("" ::: "memory");  // a compiler barrier (a fence would wait on the coefficient stores)
+  unsigned ticket = 0u;
+  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
+  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
+  if (ticket != (unsigned)(nw - 1)) return;
+  __asm__ volatile("" ::: "memory");
+  if (lane < NSTAT) {
+    // lane 0: nz; lane 1: mb + nz; lanes 24..31: bin 22 + b from word
+    // 2 (b & 1) + ((b >> 1) & 1), field b >> 2; bin 25 less the zeros
+    const int b = lane - 2 - 22;
+    const bool bin = (unsigned)b < 8u;
+    const int k = bin ? ((b & 1) << 1) | ((b >> 1) & 1) : 4;
+    const unsigned sh = bin ? 16u * (unsigned)(b >> 2) : 0u;
+    const unsigned m1 = (lane < 2 || bin) ? 0xffffu : 0u, m2 = lane == 1 ? 0xffffu : 0u;
+    unsigned tot = 0u, zeros = 0u;
+    for (int i = 0; i < nw; ++i) {
+      const unsigned x = s_wr[i][k];
+      tot += ((x >> sh) & m1) + ((x >> 16) & m2);
+      zeros += 16u * s_wr[i][5] - (s_wr[i][4] & 0xffffu);
+    }
+    if (b == 3) tot -= zeros;  // the zeros counted in bin 25
+    slot[lane] = s_st[lane] + tot;
+  }
+}
+
 __device__ __forceinline__ void stats_flush16(unsigned h0, unsigned h1, unsigned nz, unsigned mb, bool valid,
                                               unsigned* s_st, uint32_t* __restrict__ slot) {
+#if JDS_FLUSH16_WAVE
+  stats_flush16_wave(h0, h1, nz, mb, valid, s_st, slot);
+  return;
+#endif
   __shared__ __attribute__((aligned(16))) unsigned s_row[NW16][4][4];  // [wave][row][word]
   __shared__ unsigned s_nvalid[NW16];
   const unsigned e = (h0 & 0x0f0f0f0fu) + (h1 & 0x0f0f0f0fu);                 // bins 0, 2, 4, 6 (bytes)

@@ -23,6 +23,7 @@ for p in $PAIRS; do
     q422) a="--height 2160 --width 3840 --frames 16 --mode 4:2:2" ;;
     s444) a="--height 512 --width 512 --frames 256 --mode 4:4:4 --prefilter 0" ;;
     b16) a="--height 2160 --width 3840 --frames 16 --mode 4:2:2 --block 16" ;;
+    b16f) a="--height 2160 --width 3840 --frames 16 --mode 4:2:2 --block 16 --inv-fast" ;;
     q10) a="--height 2160 --width 3840 --frames 16 --quality 10" ;;
   esac
   echo "== $w"; BENCH_ARGS="$a" bash tools/var_prof.sh base $(echo ${p#*:} | tr , ' ') || exit 1
