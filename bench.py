@@ -478,8 +478,9 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
         if dom == 'k_fwd':
             kname = f'k_fwd16<{mcode},{pfs}>' if args.exact else f'k_fwd16f<{mcode},{pfs}> + k_fix_fwd16<{mcode},{pfs}>'
         else:
-            # the plan's 16x16 inverse: exact k_inv16s; the certified k_inv16_fast with --inv-fast
-            kname = ((f'k_inv16_fast<{mcode}>' if args.inv_fast and not (args.exact or args.exact_inv)
+            # the plan's 16x16 inverse: the certified k_inv16_fast (4:2:x); the
+            # exact k_inv16s with --exact-inv
+            kname = ((f'k_inv16_fast<{mcode}>' if not (args.exact or args.exact_inv)
                       else f'k_inv16s<{mcode},0>') if mcode
                      else f'k_chroma16<{mcode}> + k_inv16<{mcode}>')
     else:

@@ -634,13 +634,13 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
                        (unsigned*)p->counters.p,
                        (flags & JDS_RUN_FWD_FIXALL) ? 1 : 0, (int)(p->fwd16_runs & 1u)};
     if (phases & 1) HIP_TRY(hipMemsetAsync(stats, 0, sizeof(jds_frame_stats) * p->n, s));
-    // the certified fast inverse (k_inv16_fast) on request (JDS_RUN_INV_FAST)
-    // for 4:2:x runs without SSE terms: measured level with the exact k_inv16s
-    // (configs[4]: 524-526 vs 520-522 us, same box), both held by their LDS
-    // footprint to 3 workgroups per CU, so the plan keeps the exact kernel
+    // the certified fast inverse (k_inv16_fast) for 4:2:x runs without SSE
+    // terms unless JDS_RUN_EXACT_INV: level with the exact k_inv16s in round 3
+    // (524-526 vs 520-522 us at configs[4]), 511 vs 522 us once its certificate
+    // reduction went to DPP and its max Q to the host (profiles/r03_v29_ab.txt)
     InvFix fx16 = p->inv_fix();
     fx16.fix_all = (flags & JDS_RUN_INV_FIXALL) ? 1 : 0;
-    const bool fast_inv16 = (phases & 2) && (flags & JDS_RUN_INV_FAST) && !exact && !(flags & JDS_RUN_EXACT_INV) &&
+    const bool fast_inv16 = (phases & 2) && !exact && !(flags & JDS_RUN_EXACT_INV) &&
                             !(flags & JDS_RUN_SSE) && p->mode != JDS_SS_444 && p->invfix.p;
     HIP_TRY(launch_codec16(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                            (const double*)p->gk.p, stats, (double*)p->part.p, (double*)p->planes.p,

@@ -41,7 +41,7 @@
 #endif
 // single-quality forwards: the statistics partials summed inside k_fix_fwd's launch
 #ifndef JDS_FIX_REDUCE
-#define JDS_FIX_REDUCE 1
+#define JDS_FIX_REDUCE 0  // 1 measured level or slower once the 4:2:2 and 4K points were timed (profiles/r03_v29_ab.txt, ab9)
 #endif
 // k_fwd32i: the quantiser tables loaded by the wave without staging work
 #ifndef JDS_TABLES_IDLE_WAVE
@@ -1348,6 +1348,10 @@ k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ 
 //   many workgroups as it has entries.  Each workgroup prefix-sums the n list
 //   lengths in LDS (dynamic, 4 (n + 1) bytes) and maps its entry index to
 //   (item, slot) by binary search.
+#ifndef JDS_FIX_RED_TILES
+#define JDS_FIX_RED_TILES 32
+#endif
+constexpr int FIX_RED_TILES = JDS_FIX_RED_TILES;  // statistics partials per reducing workgroup of k_fix_fwd
 template <int MODE, bool PF>
 #ifndef JDS_FIX_WPE
 #define JDS_FIX_WPE 5
@@ -1363,14 +1367,22 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
   // frame blockIdx.y into the frame stats -- k_fwd_reduce's work in the same
   // launch (both only add to the stats, so the two orders agree)
   if (ptiles > 0 && (int)blockIdx.x >= fix_gx) {
-    const int f = blockIdx.y, t0 = ((int)blockIdx.x - fix_gx) * 8, j = threadIdx.x;
+    const int f = blockIdx.y, t0 = ((int)blockIdx.x - fix_gx) * FIX_RED_TILES, j = threadIdx.x;
     if (j < NSTAT) {
-      unsigned v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = t0 + i < ptiles ? part[((size_t)f * ptiles + t0 + i) * NSTAT + j] : 0u;
+      // FIX_RED_TILES tiles per workgroup: few enough device atomics per stats
+      // word (8 tiles per workgroup measured 41.7 vs 31.8 us at 16 x 4K 4:2:2)
       unsigned long long a = 0ull;
+#pragma unroll 1
+      for (int i0 = 0; i0 < FIX_RED_TILES; i0 += 8) {
+        unsigned v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a += v[i];
+        for (int i = 0; i < 8; ++i) {
+          const int tt = t0 + i0 + i;
+          v[i] = tt < ptiles ? part[((size_t)f * ptiles + tt) * NSTAT + j] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a += v[i];
+      }
       jds_frame_stats* sf = st + f;
       unsigned long long* dst = j == 0 ? (unsigned long long*)&sf->nonzero
                                 : j == 1 ? (unsigned long long*)&sf->magnitude_bits
@@ -1744,7 +1756,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     if (e != hipSuccess) return e;
     const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
 #if JDS_FIX_REDUCE
-    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ng + 7) / 8, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st,
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ng + FIX_RED_TILES - 1) / FIX_RED_TILES, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st,
                        fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ng, gx);
 #else
     if ((e = launch_fwd_reduce(n, st, part, ng, s)) != hipSuccess) return e;
@@ -1810,7 +1822,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     // partials inside k_fix_fwd instead of this launch measured slower: 49.4
     // vs 29.1 + 5.4 us per 64 x 1080p.)
 #if JDS_FIX_REDUCE
-    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ptiles + 7) / 8, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk,
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ptiles + FIX_RED_TILES - 1) / FIX_RED_TILES, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk,
                        st, fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ptiles, gx);
 #else
     if ((e = launch_fwd_reduce(n, st, part, ptiles, s)) != hipSuccess) return e;

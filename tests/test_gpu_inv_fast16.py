@@ -5,10 +5,11 @@ k_inv16_fast reconstructs 4:2:x frames of 16x16 blocks with fidct16 lines, the
 difference-form upsample and the colour terms on the magic grid, and certifies
 every truncation against E = K_LIN16 * Dmax + K_CONST16 + 2^-31
 (tools/inv_bound.py --b16, pinned on the CPU by tests/test_inv_bound_cpu.py);
-a tile with an uncertain value is recomputed by k_inv16s's exact body.  It
-measured level with k_inv16s, so plans run it on request (JDS_RUN_INV_FAST)
-and keep the exact kernel by default.  Bar: the fast inverse gives
-bit-identical bytes to the default (k_inv16s), to JDS_RUN_INV_FIXALL (every
+a tile with an uncertain value is recomputed by k_inv16s's exact body.  Plans
+run it by default for 4:2:x without SSE terms (it measured 511 vs 522 us
+against k_inv16s at configs[4]); JDS_RUN_EXACT_INV keeps the exact kernel.
+Bar: the fast inverse gives
+bit-identical bytes to the exact k_inv16s, to JDS_RUN_INV_FIXALL (every
 tile recomputed) and to the CPU oracle with Q16 = kron(Q8, ones(2, 2)):
 random and structured frames, ragged sizes, arbitrary int16 coefficients, and
 configs[4] at full size.  Runs with SSE terms and 4:4:4 keep the exact
@@ -75,12 +76,13 @@ def test_inv16_fast_matches_exact_fixall_and_oracle(shape, mode, pf, qs):
     h, w = shape
     frames = np.stack([cpu_ref.random_image(h, w, 3 * h + w + i) for i in range(len(qs))])
     F = _abi.RUN_INV_FAST
-    fast, exact, fixall = _run(frames, qs, mode, pf, [F, 0, F | _abi.RUN_INV_FIXALL])
+    fast, exact, fixall, default = _run(frames, qs, mode, pf, [F, _abi.RUN_EXACT_INV, F | _abi.RUN_INV_FIXALL, 0])
     assert np.array_equal(fast[1], exact[1])
     assert np.array_equal(fast[0], exact[0]), int(np.sum(fast[0] != exact[0]))
     assert np.array_equal(fixall[0], exact[0])
     assert fixall[2] == len(qs) * _tiles(mode, h, w)  # every tile recomputed
     assert exact[2] == 0 and fast[2] <= fixall[2]
+    assert np.array_equal(default[0], fast[0]) and default[2] == fast[2]  # the plan's default is the fast kernel
     for i, q in enumerate(qs):
         ref = cpu_ref.compress_reconstruct(frames[i], q, 16, mode, pf, metrics=False, stretch=True)
         assert np.array_equal(fast[0][i], ref['reconstructed']), q
@@ -94,7 +96,7 @@ def test_inv16_fast_structured_inputs(kind, mode, pf):
     from jds import _abi
     qs = [1, 10, 50, 90, 100]
     frames = np.stack([_structured(96, 160, kind, seed=i) for i in range(len(qs))])
-    fast, exact = _run(frames, qs, mode, pf, [_abi.RUN_INV_FAST, 0])
+    fast, exact = _run(frames, qs, mode, pf, [_abi.RUN_INV_FAST, _abi.RUN_EXACT_INV])
     assert np.array_equal(fast[0], exact[0]), (kind, int(np.sum(fast[0] != exact[0])))
     for i, q in enumerate(qs):
         ref = cpu_ref.compress_reconstruct(frames[i], q, 16, mode, pf, metrics=False, stretch=True)
@@ -113,7 +115,7 @@ def test_inv16_fast_arbitrary_int16_coefficients(scale, mode):
                                          codec.gaussian_kernel3(), block_size=16), h, w).coeffs_per_frame
     rng = np.random.default_rng(scale)
     cf = np.clip(rng.normal(0, scale, (3, cpf)), -32768, 32767).astype(np.int16)
-    fast, exact = _run(frames, [5, 50, 100], mode, False, [_abi.RUN_INV_FAST, 0], coeffs=cf)
+    fast, exact = _run(frames, [5, 50, 100], mode, False, [_abi.RUN_INV_FAST, _abi.RUN_EXACT_INV], coeffs=cf)
     assert np.array_equal(fast[0], exact[0]), int(np.sum(fast[0] != exact[0]))
 
 
@@ -122,7 +124,7 @@ def test_inv16_fast_configs4_full_size():
     inverse == the default exact inverse == oracle, and few tiles fall back."""
     from jds import _abi
     img = cpu_ref.random_image(2160, 3840, 46)[None]
-    fast, exact = _run(img, [50], '4:2:2', True, [_abi.RUN_INV_FAST, 0])
+    fast, exact = _run(img, [50], '4:2:2', True, [_abi.RUN_INV_FAST, _abi.RUN_EXACT_INV])
     assert np.array_equal(fast[0], exact[0])
     ref = cpu_ref.compress_reconstruct(img[0], 50, 16, '4:2:2', True, metrics=False, stretch=True)
     assert np.array_equal(fast[0][0], ref['reconstructed'])
@@ -131,10 +133,11 @@ def test_inv16_fast_configs4_full_size():
     assert fast[2] <= 0.05 * tiles
 
 
-@pytest.mark.parametrize('mode,flags', [('4:2:2', 0), ('4:4:4', 0), ('4:4:4', 128)])
-def test_inv16_default_and_444_keep_exact_kernels(mode, flags):
-    """Plans keep k_inv16s by default and 4:4:4 16x16 plans keep k_chroma16 +
-    k_inv16 even when the fast inverse is requested (no fix-up count)."""
+@pytest.mark.parametrize('mode,flags', [('4:2:2', 16), ('4:4:4', 0), ('4:4:4', 128)])
+def test_inv16_exact_and_444_keep_exact_kernels(mode, flags):
+    """JDS_RUN_EXACT_INV (16) keeps k_inv16s, and 4:4:4 16x16 plans keep
+    k_chroma16 + k_inv16 even when the fast inverse is requested (no fix-up
+    count)."""
     img = cpu_ref.random_image(64, 96, 5)[None]
     (out, cf, fixed), = _run(img, [50], mode, False, [flags])
     assert fixed == 0
