@@ -155,15 +155,38 @@ __host__ __device__ __forceinline__ double col_g(double gt, double cr) { return 
 // the luma's +128 rides on the magic constant, see byte_cert_y).
 // qhi / qlo track the largest and smallest q the lane read (integer max3 /
 // min3 chains: cheaper than an fp64 max of |q| per coefficient).
+// The folded table is held transposed in LDS (JDS_INV_QS_T: column v's eight
+// entries contiguous, rows padded to QS_STRIDE doubles so the 8 columns' 16-B
+// slots fall on disjoint banks): four ds_read_b128 per column instead of four
+// ds_read2_b64 (8 LDS cycles each at 32-bank granularity, MI355X_MICROARCH.md).
+#ifndef JDS_INV_QS_T
+#define JDS_INV_QS_T 1
+#endif
+constexpr int QS_STRIDE = 10;
+constexpr int QS_WORDS = JDS_INV_QS_T ? 8 * QS_STRIDE : 64;
+__device__ __forceinline__ int qs_index(int r, int v) { return JDS_INV_QS_T ? v * QS_STRIDE + r : r * 8 + v; }
 __device__ __forceinline__ void fast_col(const Col16& in, const double* __restrict__ qs, int v,
                                          double* __restrict__ dst, int& qhi, int& qlo) {
   double c[8];
+#if JDS_INV_QS_T
+  double t[8];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const double2 d = *reinterpret_cast<const double2*>(qs + v * QS_STRIDE + 2 * p);
+    t[2 * p] = d.x;
+    t[2 * p + 1] = d.y;
+  }
+#endif
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const double qd = (double)in.q[r];
     qhi = max(qhi, (int)in.q[r]);
     qlo = min(qlo, (int)in.q[r]);
+#if JDS_INV_QS_T
+    c[r] = qd * t[r];
+#else
     c[r] = qd * qs[r * 8 + v];
+#endif
   }
   aan8(c);
 #pragma unroll
@@ -308,7 +331,7 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   using I = Inv<MODE>;
   double* s_mid = sh.mid;
   double (*s_cw)[I::CWR * I::CWC] = sh.cw;
-  __shared__ double s_qs[64];  // Q[u][v] * a_u * a_v / 8
+  __shared__ __attribute__((aligned(16))) double s_qs[QS_WORDS];  // Q[u][v] * a_u * a_v / 8 at qs_index(u, v)
   __shared__ double s_qmax;
   __shared__ double s_red[I::NT / 64], s_dq[I::NT / 64];
   __shared__ uint32_t s_lmin[I::NT / 64], s_lmax[I::NT / 64];
@@ -338,7 +361,7 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   auto table_setup = [&]() {
     if (tid < 64) {
       const double q = fq[frame].q[tid];
-      s_qs[tid] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
+      s_qs[qs_index(tid >> 3, tid & 7)] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
 #if JDS_INV_QMAX_FQ
       // max Q from the host's FrameQ::qmax (a scalar load at the end): no
       // cross-lane reduction before the barrier
@@ -705,7 +728,7 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
               unsigned* __restrict__ next_count, unsigned* __restrict__ item_cnt, const int rot, const int fix_all,
               const int fin) {
   __shared__ __attribute__((aligned(16))) double s_mid[8 * I444_WAVES * MS];
-  __shared__ double s_qs[64];
+  __shared__ __attribute__((aligned(16))) double s_qs[QS_WORDS];
   __shared__ int s_qi[64];
   __shared__ double s_qmax;
   const int tid = threadIdx.x, lv = tid & 7, lb = tid >> 3;
@@ -730,7 +753,7 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
   const Col16 qr = load_col(cf + g.off_cr, bq * 64, lv, bvalid);
   if (tid < 64) {
     const double q = fq[frame].q[tid];
-    s_qs[tid] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
+    s_qs[qs_index(tid >> 3, tid & 7)] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
     s_qi[tid] = (int)q;
 #if JDS_INV_QMAX_FQ
 #else
