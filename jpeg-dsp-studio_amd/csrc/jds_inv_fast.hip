@@ -295,6 +295,9 @@ __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, ui
 #ifndef JDS_INV_QMAX_FQ
 #define JDS_INV_QMAX_FQ 1
 #endif
+#ifndef JDS_INV_MIX_PLANES
+#define JDS_INV_MIX_PLANES 1
+#endif
 #ifndef JDS_INV_ONE_BARRIER
 #define JDS_INV_ONE_BARRIER 0  // every thread deciding without the second barrier measured slower (312 vs 309 us)
 #endif
@@ -394,59 +397,98 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     const bool ok = luma_blk(0, by, bx);
     lq = load_col(cf, ((long long)by * g.nbx + bx) * 64, lv, ok);
   }
-  const bool ctask = tid < I::NCB * 8;
-  const int ci = lb / I::CBC, cj = lb - ci * I::CBC;
-  const int cby = cby0 + ci, cbx = cbx0 + cj;
-  const bool cvalid = ctask && cby >= 0 && cbx >= 0 && cby < g.ncy && cbx < g.ncx;
-  const long long cboff = ((long long)cby * g.ncx + cbx) * 64;
-  Col16 cq = load_col(cf + g.off_cb, cboff, lv, cvalid);
-#if JDS_INV_EARLY_LOADS
-  table_setup();
-#endif
-#if JDS_INV_QMAX_FQ
-  if (tid == 0) s_qmax = fq[frame].qmax;  // (used by this thread after the next barrier)
-#endif
-  if (ctask) {
-    const int i = ci;
-    const int by = cby, bx = cbx;
-    const bool bvalid = cvalid;
+  // one chroma block task: column pass, and for the rows the tile needs the row
+  // pass, clip and window stores (plane p, block row i of the window)
+  auto chroma_task = [&](const int p, const int i, const int by, const int bx, const Col16& cur) {
     const bool need = !I::RY || (i == 0 ? lv == 7 : (i == I::CBR - 1 ? lv == 0 : true));
-    const long long boff = cboff;
-#pragma unroll 1
-    for (int p = 0; p < 2; ++p) {
-      const Col16 cur = cq;
-      if (p == 0) cq = load_col(cf + g.off_cr, boff, lv, bvalid);
-      if (bvalid) {
-        fast_col(cur, s_qs, lv, s_mid + lb * MS, qhi, qlo);
-        if (need) {
-          double c[8];
-          fast_row<-128>(s_mid + lb * MS, lv, c);
-          double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWC];
-          const int wc0 = bx * 8 - cwx0;
+    fast_col(cur, s_qs, lv, s_mid + lb * MS, qhi, qlo);
+    if (need) {
+      double c[8];
+      fast_row<-128>(s_mid + lb * MS, lv, c);
+      double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWC];
+      const int wc0 = bx * 8 - cwx0;
 #if JDS_INV_WIN_SEL
-          // the ring blocks' columns outside the window go to a per-lane dummy
-          // slot: a select per store instead of a branch per store
+      // the ring blocks' columns outside the window go to a per-lane dummy
+      // slot: a select per store instead of a branch per store
 #pragma unroll
-          for (int k = 0; k < 8; ++k)
-            *((unsigned)(wc0 + k) < (unsigned)I::CWC ? w + wc0 + k : s_dummy + (tid & 63)) = c[k];
+      for (int k = 0; k < 8; ++k)
+        *((unsigned)(wc0 + k) < (unsigned)I::CWC ? w + wc0 + k : s_dummy + (tid & 63)) = c[k];
 #else
 #pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k];
+      for (int k = 0; k < 8; ++k)
+        if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k];
 #endif
-          if constexpr (I::SX == 2) {
-            // cv2's clamped taps at the image's left / right edge pixels read the
-            // edge column alone: replicate it into the ring (and past the
-            // plane's right end, where pixels beyond the image read too)
-            if (bx == 0 && wc0 >= 1) w[wc0 - 1] = c[0];
-            const int ke = g.wc - 1 - bx * 8;
-            if ((unsigned)ke < 8u) {
-              const double e = (ke == 0 ? c[0] : ke == 1 ? c[1] : ke == 2 ? c[2] : ke == 3 ? c[3]
-                                : ke == 4 ? c[4] : ke == 5 ? c[5] : ke == 6 ? c[6] : c[7]);
-              for (int col = wc0 + ke + 1; col < I::CWC; ++col) w[col] = e;
-            }
-          }
+      if constexpr (I::SX == 2) {
+        // cv2's clamped taps at the image's left / right edge pixels read the
+        // edge column alone: replicate it into the ring (and past the
+        // plane's right end, where pixels beyond the image read too)
+        if (bx == 0 && wc0 >= 1) w[wc0 - 1] = c[0];
+        const int ke = g.wc - 1 - bx * 8;
+        if ((unsigned)ke < 8u) {
+          const double e = (ke == 0 ? c[0] : ke == 1 ? c[1] : ke == 2 ? c[2] : ke == 3 ? c[3]
+                            : ke == 4 ? c[4] : ke == 5 ? c[5] : ke == 6 ? c[6] : c[7]);
+          for (int col = wc0 + ke + 1; col < I::CWC; ++col) w[col] = e;
         }
+      }
+    }
+  };
+  // JDS_INV_MIX_PLANES (4:2:2): the two planes' 2 x NCB block tasks dealt over
+  // the workgroup's RB lane groups (one pass each, a second pass for the first
+  // 2 NCB - RB groups) instead of NCB groups taking Cb then Cr while the other
+  // waves wait at the barrier: the busiest SIMD runs 3 passes instead of 4
+  constexpr bool MIXP = JDS_INV_MIX_PLANES && MODE == M422 && 2 * I::NCB > I::RB && 2 * I::NCB <= 2 * I::RB;
+  if constexpr (MIXP) {
+    constexpr int NTASK = 2 * I::NCB;
+    auto tinfo = [&](int tt, int& pp, int& ii, int& by, int& bx, bool& ok) -> long long {
+      pp = tt >= I::NCB ? 1 : 0;
+      const int b = tt - pp * I::NCB;
+      ii = b / I::CBC;
+      const int jj = b - ii * I::CBC;
+      by = cby0 + ii;
+      bx = cbx0 + jj;
+      ok = tt < NTASK && by >= 0 && bx >= 0 && by < g.ncy && bx < g.ncx;
+      return ((long long)by * g.ncx + bx) * 64;
+    };
+    int pp, ii, by, bx;
+    bool ok;
+    long long off = tinfo(lb, pp, ii, by, bx, ok);
+    Col16 cq = load_col(cf + (pp ? g.off_cr : g.off_cb), off, lv, ok);
+#if JDS_INV_EARLY_LOADS
+    table_setup();
+#endif
+#if JDS_INV_QMAX_FQ
+    if (tid == 0) s_qmax = fq[frame].qmax;  // (used by this thread after the next barrier)
+#endif
+#pragma unroll 1
+    for (int tt = lb; tt < NTASK; tt += I::RB) {  // (uniform per wave: RB lane groups, 8 per wave)
+      const Col16 cur = cq;
+      const int pc = pp, ic = ii, byc = by, bxc = bx;
+      const bool okc = ok;
+      if (tt + I::RB < NTASK) {
+        off = tinfo(tt + I::RB, pp, ii, by, bx, ok);
+        cq = load_col(cf + (pp ? g.off_cr : g.off_cb), off, lv, ok);
+      }
+      if (okc) chroma_task(pc, ic, byc, bxc, cur);
+    }
+  } else {
+    const bool ctask = tid < I::NCB * 8;
+    const int ci = lb / I::CBC, cj = lb - ci * I::CBC;
+    const int cby = cby0 + ci, cbx = cbx0 + cj;
+    const bool cvalid = ctask && cby >= 0 && cbx >= 0 && cby < g.ncy && cbx < g.ncx;
+    const long long cboff = ((long long)cby * g.ncx + cbx) * 64;
+    Col16 cq = load_col(cf + g.off_cb, cboff, lv, cvalid);
+#if JDS_INV_EARLY_LOADS
+    table_setup();
+#endif
+#if JDS_INV_QMAX_FQ
+    if (tid == 0) s_qmax = fq[frame].qmax;  // (used by this thread after the next barrier)
+#endif
+    if (ctask) {
+#pragma unroll 1
+      for (int p = 0; p < 2; ++p) {
+        const Col16 cur = cq;
+        if (p == 0) cq = load_col(cf + g.off_cr, cboff, lv, cvalid);
+        if (cvalid) chroma_task(p, ci, cby, cbx, cur);
       }
     }
   }
