@@ -307,7 +307,8 @@ def sweep_main(args):
     torch.cuda.synchronize(dev)
 
     def step():
-        plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), _abi.RUN_SSE, s.cuda_stream)
+        plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(),
+                 _abi.RUN_SSE | (_abi.RUN_INV_FAST if args.inv_fast else 0), s.cuda_stream)
 
     nwarm = prewarm(lambda k: step(), args.warmup, dev)
     if world > 1:
