@@ -170,6 +170,7 @@ __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8]
     const float e = fabsf(t - r) - fmaf(fabsf(t), -0x1p-22f, thr[k]);
     ok &= __float_as_uint(e);
     q[k] = (int)(fb - QMAGIC_BITS);
+#ifndef JDS_PROBE_NOQSTATS  // tools/probe: the per-coefficient statistics removed (timing only)
     const int x = __builtin_amdgcn_frexp_expf(r);  // bit length of |q| (0 for q = 0; <= 11)
     ls.nz += (unsigned)(x + 15) >> 4;
     ls.mb += (unsigned)x;
@@ -179,6 +180,7 @@ __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8]
     // taken back below
     ls.hn += top >> ((o & 28u) ^ 31u);
     orr |= o;  // any o >= 32 (q outside [-12, 19]) sets a bit >= 5
+#endif
   }
   ls.nflag += (~ok) >> 31;
   nrare = REPL ? orr : (orr >= 32u ? 1u : 0u);
@@ -434,6 +436,10 @@ __device__ __forceinline__ void stats_flush_wave(LaneStats ls, bool valid, unsig
                                                  uint32_t* __restrict__ slot) {
   __shared__ __attribute__((aligned(16))) unsigned s_wr[NW_MAX][8];  // [wave][word]: 5 sums, valid lanes
   if (!valid) ls = LaneStats();
+#ifdef JDS_PROBE_NOSTATS  // tools/probe: stop before the statistics
+  if (ls.hn == 0x12345u && ls.mb == 7u && ls.nz == 3u) slot[0] = 1u;
+  return;
+#endif
   const unsigned h = ls.hn;
   unsigned v[3] = {h & 0x0f0f0f0fu, (h >> 4) & 0x0f0f0f0fu, ls.nz | (ls.mb << 16)};
   row_sums3(v);
@@ -446,6 +452,13 @@ __device__ __forceinline__ void stats_flush_wave(LaneStats ls, bool valid, unsig
   const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nw = (int)(blockDim.x >> 6);
+#ifdef JDS_PROBE_FLUSH_NOTICKET  // tools/probe: the wave's record straight to the slot, no ticket / decode (timing only)
+  if (lane == 63) {
+    *reinterpret_cast<uint4*>(slot + 8 * w) = make_uint4(u[0], u[1], u[2], u[3]);
+    *reinterpret_cast<uint2*>(slot + 8 * w + 4) = make_uint2(u[4], nvalid);
+  }
+  return;
+#endif
   if (lane == 63) {
     *reinterpret_cast<uint4*>(&s_wr[w][0]) = make_uint4(u[0], u[1], u[2], u[3]);
     *reinterpret_cast<uint2*>(&s_wr[w][4]) = make_uint2(u[4], nvalid);
