@@ -39,6 +39,7 @@ size_t mag_scratch_bytes(long long nblocks, int max_chunks);
 hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* chunk_sum, int max_chunks,
                           double* out, hipStream_t s);
 void combined_taps32(const double* gk, float* out5);
+size_t fast_part_words(const Geo& g, int n);
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
                            jds_frame_stats* st, uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount,
@@ -538,7 +539,10 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
         (e = p->fixbits.ensure(4 * (size_t)n * (size_t)fix_wpi(g))) != hipSuccess ||
         (e = p->fixlist.ensure(8 * nblk)) != hipSuccess ||
         (e = p->counters.ensure(8 * (size_t)n + 64)) != hipSuccess ||
-        (e = p->part32.ensure(sizeof(uint32_t) * 52 * (size_t)n * ptiles)) != hipSuccess ||
+        (e = p->part32.ensure(sizeof(uint32_t) * (n_q > 1 ? 52 * (size_t)n * ptiles
+                                                          : std::max((size_t)52 * n * ptiles, fast_part_words(g, n))))) !=
+            hipSuccess ||
+        (e = hipMemset(p->part32.p, 0, p->part32.n)) != hipSuccess ||
         (e = p->invfix.ensure(64 + 12 * (size_t)n)) != hipSuccess ||
         (e = hipMemset(p->invfix.p, 0, 64 + 12 * (size_t)n)) != hipSuccess ||
         (n_q > 1 && (e = p->dct32.ensure(sizeof(float) * (size_t)n_frames * g.cpf)) != hipSuccess) ||

@@ -488,13 +488,41 @@ __device__ __forceinline__ void stats_flush_wave(LaneStats ls, bool valid, unsig
   }
 }
 
+// FORM 5: no workgroup-level step at all.  After the 16-lane row sums of the
+// packed counters (8-bit fields; the row's valid-lane count rides in bits
+// 8..15 of the nonzero | magnitude-bits word), lanes 15 / 31 / 47 / 63 store
+// their row's three words straight into the tile's slot of the partials
+// (PSLOT words: [wave][row][4]); quant8's rare bins go to the frame's rare row
+// (global atomics; rare values are sparse) behind the tiles' slots, and
+// k_fwd_reduce_rows decodes the records, adds the rare row and re-zeroes it.
+// Saves the two row-broadcast passes, the widening, the ticket and the last
+// wave's decode of the wave-record form.
+__device__ __forceinline__ void stats_flush_rows(LaneStats ls, bool valid, uint32_t* __restrict__ slot) {
+  if (!valid) ls = LaneStats();
+  const unsigned h = ls.hn;
+  unsigned v[3] = {h & 0x0f0f0f0fu, (h >> 4) & 0x0f0f0f0fu, ls.nz | ((valid ? 1u : 0u) << 8) | (ls.mb << 16)};
+  row_sums3(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if ((lane & 15) == 15)
+    *reinterpret_cast<uint4*>(slot + 4 * (4 * w + (lane >> 4))) = make_uint4(v[0], v[1], v[2], 0u);
+}
+
 #ifndef JDS_FLUSH_FORM
-#define JDS_FLUSH_FORM 3  // 3: stats_flush_wave; 2: stats_flush_atomic; 1: stats_flush_ticket (below the barrier TF)
+#define JDS_FLUSH_FORM 5  // 5: stats_flush_rows; 3: stats_flush_wave; 2: stats_flush_atomic; 1: stats_flush_ticket (below the barrier TF)
 #endif
+// words per tile slot of the per-tile partials (FORM 5: 8 waves x 4 rows x 4 words)
+constexpr int PSLOT = JDS_FLUSH_FORM == 5 ? 128 : NSTAT;
+constexpr bool FLUSH_ROWS = JDS_FLUSH_FORM == 5;
+// FORM 5: the frame's rare-bin row (64 words: [2 + bin]) behind every tile slot
+__device__ __forceinline__ unsigned* rare_row(uint32_t* part, const Geo& g, int nframes, int frame) {
+  return part + (size_t)nframes * g.tiles_y * g.tiles_x * PSLOT + (size_t)frame * 64;
+}
 template <int TF>
 __device__ __forceinline__ void stats_flush(LaneStats ls, bool valid, unsigned* s_st, uint32_t* __restrict__ slot) {
   if constexpr (TF >= JDS_FLUSH_BARRIER_TF)
     stats_flush_barrier(ls, valid, s_st, slot);
+  else if constexpr (JDS_FLUSH_FORM == 5)
+    stats_flush_rows(ls, valid, slot);
   else if constexpr (JDS_FLUSH_FORM == 3)
     stats_flush_wave(ls, valid, s_st, slot);
   else if constexpr (JDS_FLUSH_FORM == 2)
@@ -752,12 +780,12 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
   int q[8];
   LaneStats ls;
-  quant8(v, rq, thr, valid, q, ls, s_st);
+  quant8(v, rq, thr, valid, q, ls, FLUSH_ROWS && !MQ ? rare_row(part, g, gridDim.y, frame) : s_st);
   if (valid)
     *reinterpret_cast<uint4*>(coeffs + (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
                               (long long)bidx * 64 + u * 8) = pack_q(q);
   flag_block_list(ls, valid, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
-  stats_flush<C::TF>(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
+  stats_flush<C::TF>(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * PSLOT);
 }
 
 // ---- interior tiles ------------------------------------------------------------
@@ -998,7 +1026,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     const float rq[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
     const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
     int q[8];
-    quant8(v, rq, thr, valid, q, ls, s_st);
+    quant8(v, rq, thr, valid, q, ls, FLUSH_ROWS && !MQ ? rare_row(part, g, gridDim.y, frame) : s_st);
     // int16 transpose in place (row k at byte offset k * rs * 4).  Rotating
     // full-width rows across the wave's 8 blocks (so a block's 8 lanes read 8
     // bank groups instead of one) measured 6 us slower: the address math
@@ -1098,7 +1126,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   }
   if constexpr (!MQ) {
     flag_block_list(ls, valid, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
-    stats_flush<C::TF>(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * NSTAT);
+    stats_flush<C::TF>(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * PSLOT);
   }
 }
 
@@ -1297,6 +1325,87 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     }
     part[((size_t)frame * gridDim.x + blockIdx.x) * NSTAT + lane] = tot;
   }
+}
+
+// FORM 5's reduction: the row records of 64 tiles of frame blockIdx.y per
+// workgroup (nrec = 4 x waves per tile), decoded into the 8 common bins, the
+// nonzero count, the magnitude bits and the zeros (8 coefficients per valid
+// lane, all in bin 25 by the nibble counters: taken back), summed per thread,
+// then per wave (DPP-based __reduce_add_sync) and per workgroup (LDS), and
+// added to the frame stats; workgroup 0 of the frame also adds and re-zeroes
+// the frame's rare-bin row for the next run.
+#ifndef JDS_RROWS_TILES
+#define JDS_RROWS_TILES 64
+#endif
+constexpr int RROWS_TILES = JDS_RROWS_TILES;  // tiles per k_fwd_reduce_rows workgroup
+template <int NREC>
+__global__ void __launch_bounds__(256)
+k_fwd_reduce_rows(const Geo g, jds_frame_stats* __restrict__ st, uint32_t* __restrict__ part, const int ptiles) {
+  constexpr int RT = RROWS_TILES;
+  __shared__ unsigned s_acc[4][11];
+  const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t0 = blockIdx.x * RT, t1 = min(ptiles, t0 + RT);
+  unsigned acc[11] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // bins 22..29, nz, mb, zeros
+  const int nr = (t1 - t0) * NREC;
+  // a fixed trip count with compile-time record arithmetic: every load issued before the first use
+  static_assert((RT * NREC) % 256 == 0, "whole record passes");
+  uint4 xs[RT * NREC / 256];
+#pragma unroll
+  for (int it = 0; it < RT * NREC / 256; ++it) {
+    const int i = t + 256 * it;
+    const int tile = t0 + i / NREC, r = i % NREC;
+    xs[it] = i < nr ? *reinterpret_cast<const uint4*>(part + ((size_t)f * ptiles + tile) * PSLOT + 4 * r)
+                    : make_uint4(0u, 0u, 0u, 0u);
+  }
+#pragma unroll
+  for (int it = 0; it < RT * NREC / 256; ++it) {
+    const uint4 x = xs[it];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[2 * j] += (x.x >> (8 * j)) & 255u;
+      acc[2 * j + 1] += (x.y >> (8 * j)) & 255u;
+    }
+    const unsigned nz = x.z & 255u, nv = (x.z >> 8) & 255u;
+    acc[8] += nz;
+    acc[9] += x.z >> 16;
+    acc[10] += 8u * nv - nz;
+  }
+#pragma unroll
+  for (int k = 0; k < 11; ++k) {
+    const unsigned v = __reduce_add_sync(~0ull, acc[k]);
+    if (lane == 0) s_acc[w][k] = v;
+  }
+  __syncthreads();
+  jds_frame_stats* sf = st + f;
+  if (t < 11) {
+    const unsigned long long v = (unsigned long long)s_acc[0][t] + s_acc[1][t] + s_acc[2][t] + s_acc[3][t];
+    if (t < 8) {
+      // bin 22 + t; zeros fall in bin 25 (k_finalize adds them back)
+      const unsigned long long z = t == 3 ? (unsigned long long)s_acc[0][10] + s_acc[1][10] + s_acc[2][10] + s_acc[3][10]
+                                          : 0ull;
+      if (v - z) atomicAdd((unsigned long long*)&sf->hist[22 + t], v - z);
+    } else if (t == 8) {
+      if (v) atomicAdd((unsigned long long*)&sf->nonzero, v);
+    } else if (t == 9) {
+      const unsigned long long nz = (unsigned long long)s_acc[0][8] + s_acc[1][8] + s_acc[2][8] + s_acc[3][8];
+      if (v + nz) atomicAdd((unsigned long long*)&sf->magnitude_bits, v + nz);  // bit length + 1 per nonzero
+    }
+  }
+  if (blockIdx.x == 0 && t >= 64 && t < 64 + 50) {
+    unsigned* rr = rare_row(part, g, gridDim.y, f);
+    const int b = t - 64;
+    const unsigned v = rr[2 + b];
+    if (v) {
+      atomicAdd((unsigned long long*)&sf->hist[b], (unsigned long long)v);
+      rr[2 + b] = 0u;
+    }
+  }
+}
+
+// words of the statistics partials a single-quality 8x8 plan needs (tile slots
+// of either flush form, plus FORM 5's rare rows); the buffer starts zeroed
+size_t fast_part_words(const Geo& g, int n) {
+  return ((size_t)PSLOT * g.tiles_y * g.tiles_x + 64) * (size_t)n;
 }
 
 // workgroups per frame of k_fwd444w (its statistics partials per frame)
@@ -1838,7 +1947,13 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ptiles + FIX_RED_TILES - 1) / FIX_RED_TILES, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk,
                        st, fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ptiles, gx);
 #else
-    if ((e = launch_fwd_reduce(n, st, part, ptiles, s)) != hipSuccess) return e;
+    if constexpr (FLUSH_ROWS && C::TF < JDS_FLUSH_BARRIER_TF) {
+      hipLaunchKernelGGL(k_fwd_reduce_rows<4 * (C::TF / 64)>, dim3((ptiles + RROWS_TILES - 1) / RROWS_TILES, n),
+                         dim3(256), 0, s, g, st, part, ptiles);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if ((e = launch_fwd_reduce(n, st, part, ptiles, s)) != hipSuccess) {
+      return e;
+    }
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
 #endif
