@@ -491,7 +491,7 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
         inv_fast = (mcode == 0 or float(qt[0][0]) <= 60.0 or args.inv_fast) and not (args.exact or args.exact_inv)
         # (k_fwd32 runs only for border tiles k_fwd32i cannot take: fold_rows in jds_fast.hip)
         fwd_name = ('k_fwd444w + k_fwd_reduce + k_fix_fwd' if mcode == 0 and not args.exact else
-                    f'k_fwd32i<{mcode},{pfs}> (+ k_fwd32 border tiles if any) + k_fwd_reduce + k_fix_fwd')
+                    f'k_fwd32i<{mcode},{pfs}> (+ k_fwd32 border tiles if any) + k_fwd_reduce_rows + k_fix_fwd')
         kname = (fwd_name
                  if dom == 'k_fwd' else ((('k_inv_fast444' if mcode == 0 else f'k_inv_fast<{mcode},0>') if inv_fast
                                           else f'k_inv2<{mcode},0>')))
