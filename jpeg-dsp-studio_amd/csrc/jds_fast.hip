@@ -1237,7 +1237,9 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     int q[8];
     ls.hn = 0u;
     ls.nflag = 0u;
-    quant8(c, rq, thr, valid, q, ls, s_st);
+    // (FORM 5: rare bins to the frame's rare row behind the workgroups' slots)
+    quant8(c, rq, thr, valid, q, ls,
+           FLUSH_ROWS ? part + (size_t)gridDim.y * gridDim.x * PSLOT + (size_t)frame * 64 : s_st);
     __builtin_amdgcn_wave_barrier();  // every lane's column read precedes the int16 rows
 #pragma unroll
     for (int k = 0; k < 8; ++k) tq[k * 16 + lv] = (int16_t)q[k];
@@ -1267,6 +1269,18 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
   nzmb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)nzmb, 0x118, 0xf, 0xf, true);
   const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
   const int wv = tid >> 6, lane = tid & 63;
+  if constexpr (FLUSH_ROWS) {
+    // FORM 5: each 16-lane row's sums (and its valid lanes) straight into the
+    // workgroup's slot, decoded by k_fwd_reduce_rows<16, 1>
+    const unsigned long long vb = __ballot(valid);  // (the whole wave's: a ballot inside the branch sees 4 lanes)
+    if ((lane & 15) == 15) {
+      const unsigned rv = (unsigned)__popcll(vb & (0xffffull << (lane & 48)));
+      uint32_t* rec = part + ((size_t)frame * gridDim.x + blockIdx.x) * PSLOT + 8 * (4 * wv + (lane >> 4));
+      *reinterpret_cast<uint4*>(rec) = make_uint4(r5[0], r5[1], r5[2], r5[3]);
+      *reinterpret_cast<uint2*>(rec + 4) = make_uint2(nzmb, rv);
+    }
+    return;
+  }
 #if JDS_F444_WAVE_REC
   // the four rows into lane 63 by two DPP row broadcasts (a wave counts <= 64 x
   // 24 = 1536 per field, magnitude bits <= 64 x 384): one record per wave
@@ -1338,10 +1352,13 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
 #define JDS_RROWS_TILES 64
 #endif
 constexpr int RROWS_TILES = JDS_RROWS_TILES;  // tiles per k_fwd_reduce_rows workgroup
-template <int NREC>
+// FMT 0: k_fwd32i's 4-word records (8-bit fields); FMT 1: k_fwd444w's 8-word
+// records (16-bit fields, 24 coefficients per valid lane).  ptiles = slots per frame.
+template <int NREC, int FMT = 0>
 __global__ void __launch_bounds__(256)
 k_fwd_reduce_rows(const Geo g, jds_frame_stats* __restrict__ st, uint32_t* __restrict__ part, const int ptiles) {
   constexpr int RT = RROWS_TILES;
+  constexpr int RW = FMT ? 8 : 4;  // words per record
   __shared__ unsigned s_acc[4][11];
   const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int t0 = blockIdx.x * RT, t1 = min(ptiles, t0 + RT);
@@ -1349,26 +1366,43 @@ k_fwd_reduce_rows(const Geo g, jds_frame_stats* __restrict__ st, uint32_t* __res
   const int nr = (t1 - t0) * NREC;
   // a fixed trip count with compile-time record arithmetic: every load issued before the first use
   static_assert((RT * NREC) % 256 == 0, "whole record passes");
-  uint4 xs[RT * NREC / 256];
+  static_assert(RW * NREC <= PSLOT, "records fit the slot");
+  uint4 xs[RT * NREC / 256], ys[FMT ? RT * NREC / 256 : 1];
 #pragma unroll
   for (int it = 0; it < RT * NREC / 256; ++it) {
     const int i = t + 256 * it;
     const int tile = t0 + i / NREC, r = i % NREC;
-    xs[it] = i < nr ? *reinterpret_cast<const uint4*>(part + ((size_t)f * ptiles + tile) * PSLOT + 4 * r)
-                    : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t* rec = part + ((size_t)f * ptiles + tile) * PSLOT + RW * r;
+    xs[it] = i < nr ? *reinterpret_cast<const uint4*>(rec) : make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (FMT) ys[it] = i < nr ? *reinterpret_cast<const uint4*>(rec + 4) : make_uint4(0u, 0u, 0u, 0u);
   }
 #pragma unroll
   for (int it = 0; it < RT * NREC / 256; ++it) {
     const uint4 x = xs[it];
+    if constexpr (FMT == 0) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc[2 * j] += (x.x >> (8 * j)) & 255u;
-      acc[2 * j + 1] += (x.y >> (8 * j)) & 255u;
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += (x.x >> (8 * j)) & 255u;
+        acc[2 * j + 1] += (x.y >> (8 * j)) & 255u;
+      }
+      const unsigned nz = x.z & 255u, nv = (x.z >> 8) & 255u;
+      acc[8] += nz;
+      acc[9] += x.z >> 16;
+      acc[10] += 8u * nv - nz;
+    } else {
+      // word j: bins 2j (low 16 bits) and 2j + 1 (high); then nz | mb << 16, valid lanes
+      const uint4 y = ys[it];
+      const unsigned wd[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += wd[j] & 0xffffu;
+        acc[2 * j + 1] += wd[j] >> 16;
+      }
+      const unsigned nz = y.x & 0xffffu;
+      acc[8] += nz;
+      acc[9] += y.x >> 16;
+      acc[10] += 24u * y.y - nz;
     }
-    const unsigned nz = x.z & 255u, nv = (x.z >> 8) & 255u;
-    acc[8] += nz;
-    acc[9] += x.z >> 16;
-    acc[10] += 8u * nv - nz;
   }
 #pragma unroll
   for (int k = 0; k < 11; ++k) {
@@ -1392,7 +1426,7 @@ k_fwd_reduce_rows(const Geo g, jds_frame_stats* __restrict__ st, uint32_t* __res
     }
   }
   if (blockIdx.x == 0 && t >= 64 && t < 64 + 50) {
-    unsigned* rr = rare_row(part, g, gridDim.y, f);
+    unsigned* rr = part + (size_t)gridDim.y * ptiles * PSLOT + (size_t)f * 64;  // the frame's rare row
     const int b = t - 64;
     const unsigned v = rr[2 + b];
     if (v) {
@@ -1881,7 +1915,14 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ng + FIX_RED_TILES - 1) / FIX_RED_TILES, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st,
                        fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ng, gx);
 #else
-    if ((e = launch_fwd_reduce(n, st, part, ng, s)) != hipSuccess) return e;
+    if constexpr (FLUSH_ROWS) {
+      static_assert(F444_WAVES * 4 == 16, "16 row records per k_fwd444w workgroup");
+      hipLaunchKernelGGL((k_fwd_reduce_rows<16, 1>), dim3((ng + RROWS_TILES - 1) / RROWS_TILES, n), dim3(256), 0, s, g,
+                         st, part, ng);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if ((e = launch_fwd_reduce(n, st, part, ng, s)) != hipSuccess) {
+      return e;
+    }
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
 #endif
