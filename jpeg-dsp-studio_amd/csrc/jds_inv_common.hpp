@@ -8,6 +8,10 @@
 
 #include "jds_internal.hpp"
 
+#ifndef JDS_CW_PAD
+#define JDS_CW_PAD 1
+#endif
+
 namespace jds {
 
 template <int MODE>
@@ -22,6 +26,11 @@ struct Inv {
   static constexpr int CBR = TH / (8 * SY) + 2 * RY, CBC = TW / (8 * SX) + 2 * RX;  // chroma blocks incl. ring
   static constexpr int NCB = CBR * CBC;                                    // per plane
   static constexpr int CWR = TH / SY + 2 * RY, CWC = TW / SX + 2 * RX;     // chroma sample window
+  // row stride of the window in LDS: 4 doubles of padding for subsampled planes
+  // (66 -> 70) put the 16-lane groups' ds_read_b128 of chroma8_fast on fewer
+  // shared banks (a bank model of the two luma rounds: 576 -> 192 extra LDS
+  // cycles per tile; JDS_CW_PAD=0 keeps the unpadded stride)
+  static constexpr int CWS = (JDS_CW_PAD && SX == 2) ? CWC + 4 : CWC;
   static constexpr int NROW = (CBR - 2 * RY) * CBC * 8 + 2 * RY * CBC;     // chroma row tasks per plane
   static constexpr int MB = NCB > RB ? NCB : RB;                           // transpose-buffer blocks
   static constexpr int WPE = (MODE == M444) ? 3 : 4;                       // 2 or 3 workgroups per CU

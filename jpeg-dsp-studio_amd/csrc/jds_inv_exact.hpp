@@ -83,13 +83,13 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
   using I = Inv<MODE>;
   if constexpr (I::SX == 1) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) C[k] = cw[wq * I::CWC + x0 + k - cwx0];
+    for (int k = 0; k < 8; ++k) C[k] = cw[wq * I::CWS + x0 + k - cwx0];
   } else {
     const int c0 = x0 / 2 - 1 - cwx0;
     double h0[8];
 #pragma unroll
     for (int rr = 0; rr < (I::SY == 2 ? 2 : 1); ++rr) {
-      const double* s = &cw[(rr ? wt : wq) * I::CWC + c0];
+      const double* s = &cw[(rr ? wt : wq) * I::CWS + c0];
       // s*0.25 is exact, so fl(s0*0.25 + fl(s1*0.75)) == fma(s0, 0.25, fl(s1*0.75))
       double q75[6];
 #pragma unroll
@@ -118,9 +118,9 @@ __device__ __forceinline__ void chroma8(const double* __restrict__ cw, const Geo
       const int kl = side == 0 ? (x0 == 0 ? 0 : -1) : (g.W - 1 - x0 < 8 ? g.W - 1 - x0 : -1);
       if (kl >= 0) {
         const int e = (side == 0 ? 0 : g.wc - 1) - cwx0;
-        const double v0 = cw[wq * I::CWC + e];
+        const double v0 = cw[wq * I::CWS + e];
         double v = v0;
-        if constexpr (I::SY == 2) v = vblend(v0, cw[wt * I::CWC + e]);
+        if constexpr (I::SY == 2) v = vblend(v0, cw[wt * I::CWS + e]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) C[k] = k == kl ? v : C[k];  // selects, not branches
       }
@@ -169,7 +169,7 @@ __device__ __forceinline__ void colour8_exact_cr(const double (&Yv)[8], const do
 template <int MODE, int XTRA>
 struct InvShared {
   double mid[Inv<MODE>::MB * MS];
-  double cw[2][Inv<MODE>::CWR * Inv<MODE>::CWC];
+  double cw[2][Inv<MODE>::CWR * Inv<MODE>::CWS];
   int q[64];  // integer quantiser table Q
   double red[Inv<MODE>::NT / 64];
   unsigned long long sse;
@@ -193,7 +193,7 @@ __device__ __forceinline__ void inv2_tile(InvShared<MODE, XTRA>& sh, const Geo& 
   using I = Inv<MODE>;
   static_assert(I::NYB / I::RB <= 2, "at most two luma rounds per lane");
   double* s_mid = sh.mid;
-  double (*s_cw)[I::CWR * I::CWC] = sh.cw;
+  double (*s_cw)[I::CWR * I::CWS] = sh.cw;
   int* s_q = sh.q;
   double* s_red = sh.red;
   unsigned long long& s_sse = sh.sse;
@@ -244,7 +244,7 @@ __device__ __forceinline__ void inv2_tile(InvShared<MODE, XTRA>& sh, const Geo& 
         if (need) {
           double c[8];
           idct_row(s_mid + lb * MS, lv, c);
-          double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWC];
+          double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWS];
           const int wc0 = bx * 8 - cwx0;
 #pragma unroll
           for (int k = 0; k < 8; ++k)

@@ -225,16 +225,16 @@ __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int 
   using I = Inv<MODE>;
   if constexpr (I::SX == 1) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) C[k] = cw[wq * I::CWC + x0 + k - cwx0];
+    for (int k = 0; k < 8; ++k) C[k] = cw[wq * I::CWS + x0 + k - cwx0];
   } else {
     const int c0 = x0 / 2 - 1 - cwx0;
     double vb[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       if constexpr (I::SY == 2)
-        vb[j] = fvblend(cw[wq * I::CWC + c0 + j], cw[wt * I::CWC + c0 + j]);
+        vb[j] = fvblend(cw[wq * I::CWS + c0 + j], cw[wt * I::CWS + c0 + j]);
       else
-        vb[j] = cw[wq * I::CWC + c0 + j];
+        vb[j] = cw[wq * I::CWS + c0 + j];
     }
     double d[5];
 #pragma unroll
@@ -333,7 +333,7 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
                                               const int in_div, const int fix_all) {
   using I = Inv<MODE>;
   double* s_mid = sh.mid;
-  double (*s_cw)[I::CWR * I::CWC] = sh.cw;
+  double (*s_cw)[I::CWR * I::CWS] = sh.cw;
   __shared__ __attribute__((aligned(16))) double s_qs[QS_WORDS];  // Q[u][v] * a_u * a_v / 8 at qs_index(u, v)
   __shared__ double s_qmax;
   __shared__ double s_red[I::NT / 64], s_dq[I::NT / 64];
@@ -405,7 +405,7 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     if (need) {
       double c[8];
       fast_row<-128>(s_mid + lb * MS, lv, c);
-      double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWC];
+      double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWS];
       const int wc0 = bx * 8 - cwx0;
 #if JDS_INV_WIN_SEL
       // the ring blocks' columns outside the window go to a per-lane dummy
