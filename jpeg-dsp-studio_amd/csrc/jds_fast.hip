@@ -1889,7 +1889,10 @@ static void fold_rows(const Geo& g, int4& rect) {
 hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s);
 // k_fix_fwd workgroups in all (x items, grid-stride over each item's list):
 // typical lists (0.4 % of 3M blocks at Q50) need one block per workgroup
-constexpr int FIX_GRID = 16384;
+#ifndef JDS_FIX_GRID
+#define JDS_FIX_GRID 16384
+#endif
+constexpr int FIX_GRID = JDS_FIX_GRID;
 
 template <int MODE, bool PF>
 static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
