@@ -11,6 +11,9 @@
 #ifndef JDS_CW_PAD
 #define JDS_CW_PAD 1
 #endif
+#ifndef JDS_CW_PAD422
+#define JDS_CW_PAD422 4  // 4:2:2's padding (the model: 6 halves its read conflicts again; A/B in DESIGN)
+#endif
 
 namespace jds {
 
@@ -30,7 +33,7 @@ struct Inv {
   // (66 -> 70) put the 16-lane groups' ds_read_b128 of chroma8_fast on fewer
   // shared banks (a bank model of the two luma rounds: 576 -> 192 extra LDS
   // cycles per tile; JDS_CW_PAD=0 keeps the unpadded stride)
-  static constexpr int CWS = (JDS_CW_PAD && SX == 2) ? CWC + 4 : CWC;
+  static constexpr int CWS = (JDS_CW_PAD && SX == 2) ? CWC + (SY == 2 ? 4 : JDS_CW_PAD422) : CWC;
   static constexpr int NROW = (CBR - 2 * RY) * CBC * 8 + 2 * RY * CBC;     // chroma row tasks per plane
   static constexpr int MB = NCB > RB ? NCB : RB;                           // transpose-buffer blocks
   static constexpr int WPE = (MODE == M444) ? 3 : 4;                       // 2 or 3 workgroups per CU
