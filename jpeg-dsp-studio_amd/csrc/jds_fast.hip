@@ -43,6 +43,10 @@
 #ifndef JDS_FIX_REDUCE
 #define JDS_FIX_REDUCE 0  // 1 measured level or slower once the 4:2:2 and 4K points were timed (profiles/r03_v29_ab.txt, ab9)
 #endif
+// k_fwd32i (4:2:x): padding of the luma plane's rows in LDS (floats)
+#ifndef JDS_SY_PAD
+#define JDS_SY_PAD 0
+#endif
 // k_fwd32i: the quantiser tables loaded by the wave without staging work
 #ifndef JDS_TABLES_IDLE_WAVE
 #define JDS_TABLES_IDLE_WAVE 1
@@ -820,7 +824,10 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   constexpr bool CPLANE = SUB && PF;
   constexpr int CR = SUB ? (CPLANE ? WR : TH) : TH;  // chroma plane rows
   constexpr int NCD = SUB ? 2 * C::NCB : 1;          // chroma row-DCT blocks (SUB)
-  __shared__ __attribute__((aligned(16))) float s_y[TH * TW];       // luma after the row DCT
+  // luma row stride: JDS_SY_PAD floats of padding (4:2:x) put the 8 rows of a
+  // block's in-place int16 transpose on different banks for the row reads
+  constexpr int YS = SUB ? TW + JDS_SY_PAD : TW;
+  __shared__ __attribute__((aligned(16))) float s_y[TH * YS];       // luma after the row DCT
   // chroma planes (4:4:4: after the row DCT; prefiltered 4:2:x: the horizontal
   // pair sums, TW / 2 per row)
   constexpr int CW = CPLANE ? TW / 2 : TW;
@@ -905,7 +912,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       const int o = (r - 1) * TW + 8 * c;
       if (r >= 1 && r <= TH) {
         fdct8_f32(yy);
-        float4* dy = reinterpret_cast<float4*>(s_y + o);
+        float4* dy = reinterpret_cast<float4*>(s_y + (r - 1) * YS + 8 * c);
         dy[0] = make_float4(yy[0], yy[1], yy[2], yy[3]);
         dy[1] = make_float4(yy[4], yy[5], yy[6], yy[7]);
       }
@@ -1045,7 +1052,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 
   if constexpr (SUB) {
     if (plane == 0) {
-      column(s_y + by_t * 8 * TW + bx_t * 8, TW, 0);
+      column(s_y + by_t * 8 * YS + bx_t * 8, YS, 0);
     } else {
       // chroma sample row `line` of the block: vertical filter + area average of
       // the row-filtered (or raw) planes, then the row DCT
