@@ -2,16 +2,18 @@
 """bench.py — Mpixels/s of the forward+inverse block-DCT pipeline @ Q=50 4:2:0 (+PSNR vs reference).
 
 Workload (BASELINE.json configs[1]): 1920x1080 uniform-random RGB frames, Q=50,
-4:2:0, prefilter ON, through the fused HIP kernels (forward phase: k_fwd32i /
-k_fwd32 / k_fix_fwd, RGB -> int16 coefficients + statistics; inverse phase:
-k_inv2, coefficients -> RGB).  One step = one pass over a batch of
+4:2:0, prefilter ON, through the fused HIP kernels (forward phase: k_fwd32i +
+k_fwd_reduce_rows + k_fix_fwd, RGB -> int16 coefficients + statistics; inverse
+phase: the certified k_inv_fast, coefficients -> RGB, with its in-launch exact
+tile fix-up; k_inv2 where the plan's certificate does not pay).  One step = one pass over a batch of
 `--frames` device-resident 1080p frames per GPU (default 64, the size of the
 reference's cfg4 batch sweep); inputs are generated on the device before the
 timed region.  A step is one jds_plan_run (forward then inverse) on one stream;
 `--pipeline 1` instead overlaps the forward of batch k+1 with the inverse of
 batch k on a second stream (two buffer sets).  Multi-GPU: one process per GPU (torchrun), frames shard across
-ranks with no data-path collective (weak scaling); RCCL is used only for the
-barrier and the max-over-ranks time.
+ranks with no data-path collective (weak scaling); RCCL carries the quant-table
+broadcast from rank 0, the barrier, the max-over-ranks time and the per-rank
+frame-0 parity gather (`parity_ranks`).
 
 Prints ONE JSON line (rank 0).  The roofline object describes the dominant
 kernel (longer average launch) with ALGORITHMIC bytes: k_fwd reads 3 B/px RGB and
@@ -272,6 +274,23 @@ def dist_info(world, backend):
     return {'world_size': 1, 'backend': None}
 
 
+def gather_parity(local, world, backend):
+    """Every rank's own frame-0 parity record on rank 0 (one all_gather_object
+    outside the timed region), so the line shows every rank's shard checked."""
+    import torch.distributed as dist
+    rec = dict(local)
+    if world > 1 and dist.is_initialized():
+        rec['rank'] = dist.get_rank()
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, rec)
+    else:
+        rec['rank'] = 0
+        parts = [rec]
+    return {'world_size': len(parts), 'backend': backend if world > 1 else None, 'ranks': parts,
+            'all_exact': all(p.get('mismatches', 0) == 0 and p.get('coeff_mismatch', 0) == 0 and
+                             p.get('recon_mismatch_bytes', 0) == 0 for p in parts)}
+
+
 SWEEP_QS = [5, 10, 20, 50, 80, 95]  # BASELINE configs[3]
 
 
@@ -351,16 +370,46 @@ def sweep_main(args):
                         else 'none (one rank)', 'items_gathered': len(gathered), 'items_expected': F * nq * world,
                         'frames_covered': sorted({it['frame'] for it in gathered}) == list(range(F * world)),
                         'seconds': round(time.perf_counter() - tg, 4), **dist_info(world, backend)}
-    if rank == 0 and not args.no_parity:
+    # the per-item SSIM of the reference's CompressionResult (gui/worker.py:62-68 ->
+    # utils/metrics.py:9-28) for every item of the step, batched on the device
+    # (jds_psnr_ssim_batch_dev), timed on its own after the headline region
+    if not rep:
+        from jds import codec as _codec
+        pa = [rgb[f].data_ptr() for f in range(F) for _ in SWEEP_QS]
+        pb = [out[k].data_ptr() for k in range(F * nq)]
+        torch.cuda.synchronize(dev)
+        _codec.psnr_ssim_batch_dev(pa, pb, H, W, local, None)  # warm: scratch, code objects
+        reps = 3
+        t0s = time.perf_counter()
+        for _ in range(reps):
+            ss = _codec.psnr_ssim_batch_dev(pa, pb, H, W, local, None)
+        dt = (time.perf_counter() - t0s) / reps
+        result['ssim'] = {'entry': 'jds_psnr_ssim_batch_dev (csrc/jds_ssim_band.hip)', 'items': F * nq,
+                          'ms_per_item': round(dt * 1e3 / (F * nq), 4), 'ms_per_step': round(dt * 1e3, 3),
+                          'items_per_s': round(F * nq / dt, 1), 'includes': 'SSIM R/G/B/Y + luma MSE + RGB SSE '
+                          'per item, host wall time of the call (launches + one copy back)',
+                          'ssim_rgb_item0': float(np.mean(ss[0][:3])), 'ssim_y_item0': float(ss[0][3])}
+    if not args.no_parity:
+        # every rank checks its own frame 0 at every quality against the oracle
         from oracle import cpu_ref
         stats = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(-1)
         f0 = rgb[0].cpu().numpy()
         bad = 0
+        ssim_bad = None
         for qi, q in enumerate(SWEEP_QS):
             ref = cpu_ref.compress_reconstruct(f0, q, 8, args.mode, bool(args.prefilter), metrics=False)
             bad += int(np.sum(cf[qi].cpu().numpy() != ref['coeffs']))
             bad += int(stats[qi]['sse_rgb'] != int(((f0.astype(np.int64) - ref['reconstructed']) ** 2).sum()))
-        result['parity'] = {'frame': 0, 'qualities': SWEEP_QS, 'mismatches': bad}
+            if qi == 3 and 'ssim' in result:  # Q50: the batched SSIM of item (0, Q50) vs the oracle's skimage restatement
+                m = cpu_ref.compute_psnr_ssim(f0, out[qi].cpu().numpy())
+                ssim_bad = int(m['ssim_y'] != ss[qi][3]) + int(m['ssim_rgb'] != float(np.mean(ss[qi][:3])))
+        rec = {'frame': 0, 'qualities': SWEEP_QS, 'mismatches': bad}
+        if ssim_bad is not None:
+            rec['ssim_mismatches_q50'] = ssim_bad
+        pr = gather_parity(rec, world, backend)
+        if rank == 0:
+            result['parity'] = rec
+            result['parity_ranks'] = pr
     plan.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -629,9 +678,14 @@ def main():
             int(st0['nonzero']), float(st0['magnitude_bits']), int(st0['total_coeffs']), (H, W), 8)['bpp'], 4)
         del files
 
-    if rank == 0 and not args.no_parity:
-        # PSNR / bytes vs the reference restatement on frame 0 (outside the timed region)
-        result['parity'] = frame0_parity(state, args.quality, args.mode, args.prefilter, args.block)
+    if not args.no_parity:
+        # PSNR / bytes vs the reference restatement on frame 0 (outside the timed
+        # region) -- on every rank, its own frames; rank 0 reports all of them
+        par = frame0_parity(state, args.quality, args.mode, args.prefilter, args.block)
+        pr = gather_parity(par, world, backend)
+        if rank == 0:
+            result['parity'] = par
+            result['parity_ranks'] = pr
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         n = max(1, min(B, 64))
         host = rgb[:n].cpu().numpy()
@@ -658,8 +712,12 @@ def main():
         result['north_star']['config'] = {'workload': r_ns['config']['workload'],
                                           'frames_per_gpu_per_step': ns['B'], 'steps': args.steps}
         result['north_star']['target_pipeline_roofline_frac'] = 0.60
-        if rank == 0 and not args.no_parity:
-            result['north_star']['parity'] = frame0_parity(st_ns, ns['quality'], ns['mode'], ns['pf'], 8)
+        if not args.no_parity:
+            par = frame0_parity(st_ns, ns['quality'], ns['mode'], ns['pf'], 8)
+            pr = gather_parity(par, world, backend)
+            if rank == 0:
+                result['north_star']['parity'] = par
+                result['north_star']['parity_ranks'] = {k: pr[k] for k in ('world_size', 'backend', 'all_exact')}
         for p_ in st_ns['plans']:
             p_.close()
         del st_ns

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define JDS_ABI_VERSION 2
+#define JDS_ABI_VERSION 3
 
 #define JDS_OK       0
 #define JDS_EINVAL  (-1)  /* bad argument                    -> ValueError   */
@@ -47,6 +47,10 @@ extern "C" {
                                 (4:4:4, coarse tables: DESIGN.md section 3) */
 #define JDS_RUN_FWD_FIXALL 64u /* test, 16x16 plans: the certified fp32 forward lists every block, so
                                   k_fix_fwd16 recomputes the whole frame (exercises the fix-up path) */
+
+/* `after` argument of the *_dev functions below: no wait, the caller has
+ * synchronised the inputs.  (NULL is the HIP null stream, which is waited for.) */
+#define JDS_AFTER_NONE ((void*)(intptr_t)-1)
 
 typedef struct jds_ctx jds_ctx;    /* one per (thread, device): owns a HIP stream + scratch */
 typedef struct jds_plan jds_plan;  /* fixed geometry + per-frame quant tables, device-resident */
@@ -170,10 +174,18 @@ int jds_psnr_ssim_dev(jds_ctx* ctx, const uint8_t* a_dev, const uint8_t* b_dev, 
 
 /* jds_psnr_ssim_dev without the device-wide wait: the context's stream waits
  * only for the work queued so far on `after` (a hipStream_t, e.g. the plan
- * run's stream; NULL = the caller has already synchronised the images), so
- * leased contexts of other threads keep running.  out on the host. */
+ * run's stream; NULL = the HIP null stream; JDS_AFTER_NONE = the caller has
+ * already synchronised the images), so leased contexts of other threads keep
+ * running.  out on the host. */
 int jds_psnr_ssim_dev_after(jds_ctx* ctx, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W,
                             double* out, void* after);
+
+/* The same for n device-resident image pairs of one size (the batch sweep's
+ * items, gui/worker.py:62-68): pair i = (a_dev[i], b_dev[i]) (host arrays of
+ * device pointers); out[6 i + 0..5] as above.  The pairs run together
+ * (up to 32 per launch), so a sweep's SSIM fills the chip.  `after` as above. */
+int jds_psnr_ssim_batch_dev(jds_ctx* ctx, int32_t n, const uint8_t* const* a_dev, const uint8_t* const* b_dev,
+                            int64_t H, int64_t W, double* out, void* after);
 
 /* NumPy's float32 sum of magnitude_bits over device-resident int16
  * coefficients (utils/metrics.py:77-78: np.sum(np.ceil(np.log2(|q| + 1)) + 1)
@@ -183,6 +195,10 @@ int jds_psnr_ssim_dev_after(jds_ctx* ctx, const uint8_t* a_dev, const uint8_t* b
  * n_coeffs: a multiple of 64 (one frame's IntermediateData layout); `after` as
  * above.  *out on the host. */
 int jds_magnitude_bits_f32_dev(jds_ctx* ctx, const int16_t* coeffs_dev, int64_t n_coeffs, double* out, void* after);
+/* The same for n_items coefficient arrays at coeffs_dev + i * item_stride
+ * (int16 elements), one wait: out[i] on the host. */
+int jds_magnitude_bits_f32_batch_dev(jds_ctx* ctx, const int16_t* coeffs_dev, int32_t n_items, int64_t n_coeffs,
+                                     int64_t item_stride, double* out, void* after);
 
 /* Per-stage functions of the engines.* API (engines/__init__.py:10-27), on host
  * fp64 arrays staged through the context's device memory.  Synchronous.
@@ -233,6 +249,12 @@ int jds_plan_entropy(jds_plan* plan, const int16_t* coeffs, uint8_t* out, int64_
                      uint64_t* scan_bits, void* stream);
 int jds_encode_jfif(jds_ctx* ctx, const jds_params* p, int64_t H, int64_t W, const int16_t* coeffs, uint8_t* out,
                     int64_t out_cap, int64_t* out_len, uint64_t* scan_bits);
+
+/* Test-only: jds_psnr_ssim_dev through the round-1..3 SSIM kernels
+ * (jds_ssim.hip: IEEE divisions, one line per lane), the reference the
+ * batched pipeline is compared with bit for bit.  out[0..5] as above. */
+int jds_selftest_psnr_ssim_legacy_dev(jds_ctx* ctx, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W,
+                                      double* out);
 
 /* Test-only: evaluate the device DCT expressions (jds_dct8.hpp) on the host so
  * the CPU test suite can pin them against SciPy without a GPU.  Not used by

@@ -34,6 +34,11 @@ hipError_t stage_area_gen(const double* in, int H, int W, const AreaTap* ytab, c
 hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, double c1, double c2,
                             double* scratch_planes, double* scratch_smap, double* scratch_chunks, double* out,
                             hipStream_t s);
+hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const* b, int items, int H, int W,
+                                  double c1, double c2, double* scratch, double* out, int out_stride,
+                                  unsigned long long* sse, hipStream_t s);
+size_t ssim_batch_scratch_doubles(int H, int W);
+int ssim_batch_max_items();
 hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
 size_t mag_scratch_bytes(long long nblocks, int max_chunks);
 hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* chunk_sum, int max_chunks,
@@ -136,7 +141,7 @@ struct jds_ctx {
   hipEvent_t xfer_ev = nullptr;
   // host-path scratch
   DevBuf rgb, out, coeffs, stats, part, fq, gk, erry, errrgb, sel;
-  DevBuf ss_planes, ss_map, ss_chunks, ss_out, img_a, img_b;
+  DevBuf ss_planes, ss_map, ss_chunks, ss_out, img_a, img_b;  // ss_planes: k_ss_* scratch; map/chunks: legacy
   DevBuf st[5];  // per-stage API staging
   DevBuf chunks;
   DevBuf planes;  // 16x16 path: reconstructed chroma planes
@@ -144,8 +149,36 @@ struct jds_ctx {
   DevBuf gen_tab, gen_sub, gen_rec;  // general-geometry path (jds_gen.hip)
 };
 
-// SSIM scratch in the context; returns the device pointer of 5 result doubles
+// SSIM of `items` image pairs (K4, jds_ssim_band.hip) on the context's stream:
+// out[i * out_stride + 0..4] = SSIM R, G, B, Y, MSE of Y (device doubles);
+// sse[i] (nullable, zeroed here) = the pair's integer RGB squared-error sum.
+// Batches beyond the kernel's per-launch limit run as consecutive launches.
+static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const uint8_t* const* b, int H, int W,
+                          double* out, int out_stride, unsigned long long* sse) {
+  const int per = ssim_batch_max_items();
+  const size_t each = ssim_batch_scratch_doubles(H, W) * sizeof(double);
+  // scratch for up to `per` items, at most ~2 GB (1080p: ~110 MB per item)
+  int group = (int)std::max<size_t>(1, std::min<size_t>((size_t)per, ((size_t)2 << 30) / each));
+  group = std::min(group, items);
+  HIP_TRY(c->ss_planes.ensure(each * group));
+  if (sse) HIP_TRY(hipMemsetAsync(sse, 0, sizeof(unsigned long long) * items, c->stream));
+  for (int i0 = 0; i0 < items; i0 += group) {
+    const int k = std::min(group, items - i0);
+    HIP_TRY(launch_psnr_ssim_batch(a + i0, b + i0, k, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_planes.p,
+                                   out + (size_t)i0 * out_stride, out_stride, sse ? sse + i0 : nullptr,
+                                   c->stream));
+  }
+  return JDS_OK;
+}
+
+// one pair; returns the device pointer of 5 result doubles in dres
 static int run_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int H, int W, double* dres) {
+  return run_ssim_batch(c, 1, &a, &b, H, W, dres, 5, nullptr);
+}
+
+// the round-1..3 kernels (k_uf_axis0 / k_uf_axis1_ssim / k_chunks_*): kept as
+// the A/B and test reference of the batched pipeline (jds_selftest_psnr_ssim_legacy_dev)
+static int run_ssim_legacy(jds_ctx* c, const uint8_t* a, const uint8_t* b, int H, int W, double* dres) {
   const size_t n = (size_t)H * W;
   HIP_TRY(c->ss_planes.ensure(4 * 5 * n * sizeof(double)));  // the four channels at once
   HIP_TRY(c->ss_map.ensure(4 * (size_t)(H - 6) * (W - 6) * sizeof(double)));
@@ -811,6 +844,12 @@ int jds_compress_reconstruct(jds_ctx* c, const jds_params* prm, const uint8_t* r
       return rc;
   }
   hipStream_t x = c->xfer;
+  // every exit from here on waits for the copies queued on x: an error return
+  // must not leave copies into the caller's arrays in flight
+  struct XferWait {
+    hipStream_t x;
+    ~XferWait() { (void)hipStreamSynchronize(x); }
+  } xfer_wait{x};
   HIP_TRY(hipMemcpyAsync(rgb_out, c->out.p, nimg, hipMemcpyDeviceToHost, x));
   if (coeffs) HIP_TRY(hipMemcpyAsync(coeffs, c->coeffs.p, ncf * sizeof(int16_t), hipMemcpyDeviceToHost, x));
   if (maps) {
@@ -846,25 +885,37 @@ static int psnr_ssim_args(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_
   return JDS_OK;
 }
 
-// SSIM / MSE of two device-resident images (the context's stream)
-static int psnr_ssim_device(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out) {
+// SSIM / MSE of `items` device-resident image pairs (the context's stream):
+// out[6 i + 0..5] = SSIM R, G, B, Y, MSE Y, MSE RGB on the host
+static int psnr_ssim_device_batch(jds_ctx* c, int items, const uint8_t* const* a, const uint8_t* const* b,
+                                  int64_t H, int64_t W, double* out) {
   const size_t nb = (size_t)H * W * 3;
-  HIP_TRY(c->ss_out.ensure(5 * sizeof(double) + sizeof(unsigned long long)));
+  const size_t bytes = (size_t)items * (5 * sizeof(double) + sizeof(unsigned long long));
+  HIP_TRY(c->ss_out.ensure(bytes));
   hipStream_t s = c->stream;
-  HIP_TRY(hipMemsetAsync(c->ss_out.p, 0, 5 * sizeof(double) + sizeof(unsigned long long), s));
   double* dres = (double*)c->ss_out.p;
-  unsigned long long* dsse = (unsigned long long*)(dres + 5);
-  int rc = run_ssim(c, a, b, (int)H, (int)W, dres);
+  unsigned long long* dsse = (unsigned long long*)(dres + (size_t)5 * items);
+  int rc = run_ssim_batch(c, items, a, b, (int)H, (int)W, dres, 5, dsse);
   if (rc) return rc;
-  HIP_TRY(launch_sse_u8(a, b, (long long)nb, dsse, s));
-  double res[5];
-  unsigned long long sse = 0;
-  HIP_TRY(hipMemcpyAsync(res, dres, sizeof res, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(&sse, dsse, sizeof sse, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  for (int i = 0; i < 5; ++i) out[i] = res[i];
-  out[5] = (double)sse / (double)nb;  // exact: integer sum, one division (np.mean)
+  double* res = (double*)malloc(bytes);
+  if (!res) return fail(JDS_ENOMEM, "host allocation failed");
+  hipError_t e = hipMemcpyAsync(res, dres, bytes, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    free(res);
+    return fail(JDS_EHIP, "HIP error: %s", hipGetErrorString(e));
+  }
+  const unsigned long long* sse = (const unsigned long long*)(res + (size_t)5 * items);
+  for (int i = 0; i < items; ++i) {
+    for (int k = 0; k < 5; ++k) out[6 * i + k] = res[5 * i + k];
+    out[6 * i + 5] = (double)sse[i] / (double)nb;  // exact: integer sum, one division (np.mean)
+  }
+  free(res);
   return JDS_OK;
+}
+
+static int psnr_ssim_device(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out) {
+  return psnr_ssim_device_batch(c, 1, &a, &b, H, W, out);
 }
 
 int jds_psnr_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int64_t H, int64_t W, double* out) {
@@ -887,9 +938,10 @@ int jds_psnr_ssim_dev(jds_ctx* c, const uint8_t* a_dev, const uint8_t* b_dev, in
   return psnr_ssim_device(c, a_dev, b_dev, H, W, out);
 }
 
-// the context's stream waits for what `after` has queued so far (one event)
+// the context's stream waits for what `after` has queued so far (one event);
+// JDS_AFTER_NONE: no wait (the caller has synchronised); NULL: the HIP null stream
 static int wait_after(jds_ctx* c, void* after) {
-  if (!after) return JDS_OK;
+  if (after == JDS_AFTER_NONE) return JDS_OK;
   hipEvent_t e;
   HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   hipError_t err = hipEventRecord(e, (hipStream_t)after);
@@ -907,6 +959,68 @@ int jds_psnr_ssim_dev_after(jds_ctx* c, const uint8_t* a_dev, const uint8_t* b_d
   HIP_TRY(hipSetDevice(c->device));
   if ((rc = wait_after(c, after))) return rc;
   return psnr_ssim_device(c, a_dev, b_dev, H, W, out);
+}
+
+int jds_psnr_ssim_batch_dev(jds_ctx* c, int32_t n, const uint8_t* const* a_dev, const uint8_t* const* b_dev, int64_t H,
+                            int64_t W, double* out, void* after) {
+  if (!c || n < 0 || (n > 0 && (!a_dev || !b_dev || !out))) return fail(JDS_EINVAL, "null argument");
+  if (n == 0) return JDS_OK;
+  for (int i = 0; i < n; ++i) {
+    int rc = psnr_ssim_args(c, a_dev[i], b_dev[i], H, W, out);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = wait_after(c, after);
+  if (rc) return rc;
+  return psnr_ssim_device_batch(c, n, a_dev, b_dev, H, W, out);
+}
+
+int jds_selftest_psnr_ssim_legacy_dev(jds_ctx* c, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W,
+                                      double* out) {
+  int rc = psnr_ssim_args(c, a_dev, b_dev, H, W, out);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(c->ss_out.ensure(5 * sizeof(double) + sizeof(unsigned long long)));
+  hipStream_t s = c->stream;
+  HIP_TRY(hipMemsetAsync(c->ss_out.p, 0, 5 * sizeof(double) + sizeof(unsigned long long), s));
+  double* dres = (double*)c->ss_out.p;
+  unsigned long long* dsse = (unsigned long long*)(dres + 5);
+  if ((rc = run_ssim_legacy(c, a_dev, b_dev, (int)H, (int)W, dres))) return rc;
+  const size_t nb = (size_t)H * W * 3;
+  HIP_TRY(launch_sse_u8(a_dev, b_dev, (long long)nb, dsse, s));
+  double res[5];
+  unsigned long long sse = 0;
+  HIP_TRY(hipMemcpyAsync(res, dres, sizeof res, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&sse, dsse, sizeof sse, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int i = 0; i < 5; ++i) out[i] = res[i];
+  out[5] = (double)sse / (double)nb;
+  return JDS_OK;
+}
+
+int jds_magnitude_bits_f32_batch_dev(jds_ctx* c, const int16_t* coeffs_dev, int32_t n_items, int64_t n_coeffs,
+                                     int64_t item_stride, double* out, void* after) {
+  if (!c || n_items < 0 || (n_items > 0 && (!coeffs_dev || !out)) || n_coeffs < 0 || n_coeffs % 64 ||
+      item_stride < n_coeffs)
+    return fail(JDS_EINVAL, "bad argument");
+  if (n_coeffs > ((int64_t)1 << 31)) return fail(JDS_EINVAL, "too many coefficients");
+  if (n_items == 0) return JDS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = wait_after(c, after);
+  if (rc) return rc;
+  hipStream_t s = c->stream;
+  const long long nblk = n_coeffs / 64;
+  const int max_chunks = (int)((n_coeffs + 8191) / 8192) + 1;
+  HIP_TRY(c->chunks.ensure(mag_scratch_bytes(nblk, max_chunks)));
+  HIP_TRY(c->ss_out.ensure(sizeof(double) * (size_t)n_items));
+  double* d = (double*)c->ss_out.p;
+  // one launch chain per item on the stream (the scratch is reused in order), one copy, one wait
+  for (int i = 0; i < n_items; ++i)
+    HIP_TRY(launch_mag_f32(coeffs_dev + (size_t)i * item_stride, nblk, (unsigned*)c->chunks.p, max_chunks, d + i, s));
+  HIP_TRY(hipMemcpyAsync(out, d, sizeof(double) * (size_t)n_items, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return JDS_OK;
 }
 
 int jds_magnitude_bits_f32_dev(jds_ctx* c, const int16_t* coeffs_dev, int64_t n_coeffs, double* out, void* after) {

@@ -287,6 +287,19 @@ __device__ __forceinline__ void code_block(const BlockRegs& r, int pred, const u
   o.finish();
 }
 
+template <int K>
+__device__ __forceinline__ void ac_bits(const BlockRegs& r, int& last, int& amax, uint32_t& nb, const uint16_t* tb) {
+  if constexpr (K < 64) {
+    const int v = coef_at<ZZC[K]>(r);
+    const int a = v < 0 ? -v : v;
+    amax = a > amax ? a : amax;
+    const int sz = a ? 32 - __clz(a) : 0;
+    nb += tb[((K - 1 - last) << 5) | sz];
+    last = a ? K : last;
+    ac_bits<K + 1>(r, last, amax, nb, tb);
+  }
+}
+
 __global__ void __launch_bounds__(256) k_ent_bits(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
                                                   const EntTab* __restrict__ gt, unsigned long long* __restrict__ bits,
                                                   unsigned long long* __restrict__ bad) {
@@ -301,6 +314,57 @@ __global__ void __launch_bounds__(256) k_ent_bits(const EntGeo e, long long nblk
     bool bd;
     code_block<SINK_COUNT>(r, pred, t.dc[s ? 1 : 0], t.ac[s ? 1 : 0], o, bd);
     bits[gb] = (unsigned long long)o.total;
+    if (bd) bad[frame] = 1ull;  // not baseline-codable: the frame is reported
+  }
+}
+
+// k_ent_bits2: the same bit counts without the walk's branches.  Per table
+// class, bl[run * 32 + s] = the bits a nonzero coefficient of size s after
+// `run` zeros costs: (run >> 4) ZRL codes + the (run & 15, min(s, 10)) code +
+// min(s, 10) magnitude bits (the clamp of code_ac); bl[run * 32 + 0] = 0, so a
+// zero coefficient adds nothing and every zigzag position runs the same
+// branch-free ops: size, one LDS lookup, an add, a select for the last
+// nonzero.  The AC error flag comes from the largest magnitude.
+#ifndef JDS_ENT_BITS_TABLE
+#define JDS_ENT_BITS_TABLE 1
+#endif
+constexpr int ENT_BL = 64 * 32;  // entries per table class
+
+__global__ void __launch_bounds__(256) k_ent_bits2(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
+                                                   const EntTab* __restrict__ gt, unsigned long long* __restrict__ bits,
+                                                   unsigned long long* __restrict__ bad) {
+  __shared__ EntTab t;
+  __shared__ uint16_t bl[2][ENT_BL];
+  load_tab(gt, &t);
+  for (int i = threadIdx.x; i < 2 * ENT_BL; i += blockDim.x) {
+    const int c = i / ENT_BL, run = (i % ENT_BL) >> 5, sz = i & 31;
+    uint32_t v = 0;
+    if (sz) {
+      const int sc = sz > 10 ? 10 : sz;
+      const uint32_t code = t.ac[c][((run & 15) << 4) | sc], zrl = t.ac[c][0xF0];
+      v = (uint32_t)(run >> 4) * (zrl >> 16) + (code >> 16) + (uint32_t)sc;
+    }
+    bl[c][i % ENT_BL] = (uint16_t)v;
+  }
+  __syncthreads();
+  for (long long gb = (long long)blockIdx.x * blockDim.x + threadIdx.x; gb < nblk; gb += (long long)gridDim.x * blockDim.x) {
+    const int frame = (int)(gb / e.nb), b = (int)(gb - (long long)frame * e.nb);
+    const int s = scan_of(e, b);
+    const BlockRegs r = load_block(coeffs + gb * 64);
+    const int pred = b == e.first[s] ? 0 : (int)coeffs[(gb - 1) * 64];
+    const uint16_t* tb = bl[s ? 1 : 0];
+    const uint32_t* dct = t.dc[s ? 1 : 0];
+    const int diff = coef_at<0>(r) - pred;
+    const int da = diff < 0 ? -diff : diff;
+    int ds = da ? 32 - __clz(da) : 0;
+    bool bd = ds > 11;
+    ds = ds > 11 ? 11 : ds;
+    uint32_t nb = (dct[ds] >> 16) + (uint32_t)ds;
+    int last = 0, amax = 0;
+    ac_bits<1>(r, last, amax, nb, tb);
+    if (last < 63) nb += t.ac[s ? 1 : 0][0x00] >> 16;  // EOB
+    bd |= amax > 1023;                                  // size > 10
+    bits[gb] = (unsigned long long)nb;
     if (bd) bad[frame] = 1ull;  // not baseline-codable: the frame is reported
   }
 }
@@ -584,7 +648,10 @@ hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* cons
   unsigned long long* bad = info + 6 * n;
   if ((err = hipMemsetAsync(bits + nblk, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
   if ((err = hipMemsetAsync(bad, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) return err;
-  hipLaunchKernelGGL(k_ent_bits, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, bad);
+  if (JDS_ENT_BITS_TABLE)
+    hipLaunchKernelGGL(k_ent_bits2, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, bad);
+  else
+    hipLaunchKernelGGL(k_ent_bits, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, bad);
   if ((err = hipGetLastError()) != hipSuccess) return err;
   size_t tb = sz[7];
   if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, bits, excl, (int)(nblk + 1), s)) != hipSuccess) return err;

@@ -517,6 +517,9 @@ __device__ __forceinline__ void stats_flush_rows(LaneStats ls, bool valid, uint3
 // words per tile slot of the per-tile partials (FORM 5: 8 waves x 4 rows x 4 words)
 constexpr int PSLOT = JDS_FLUSH_FORM == 5 ? 128 : NSTAT;
 constexpr bool FLUSH_ROWS = JDS_FLUSH_FORM == 5;
+// k_fix_fwd's in-launch reduction (JDS_FIX_REDUCE) reads NSTAT-stride slots and
+// never drains the rare-bin row: it does not know FORM 5's row records
+static_assert(!(JDS_FIX_REDUCE && JDS_FLUSH_FORM == 5), "JDS_FIX_REDUCE needs a slot-record flush form (not 5)");
 // FORM 5: the frame's rare-bin row (64 words: [2 + bin]) behind every tile slot
 __device__ __forceinline__ unsigned* rare_row(uint32_t* part, const Geo& g, int nframes, int frame) {
   return part + (size_t)nframes * g.tiles_y * g.tiles_x * PSLOT + (size_t)frame * 64;
@@ -1915,7 +1918,10 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   // only the 1-px ring may reflect) form a rectangle of tile indices and take
   // k_fwd32i; the rest run in k_fwd32 beside it on the side stream.
   // 4:4:4 single-quality plans: the wave-local kernel (k_fwd444w) for every block
-  if (MODE == M444 && !mq && !getenv("JDS_FWD444_TILED")) {
+  // (A/B knob read once per process: every plan of the process leaves its
+  // rare-bin row where its own forward kind put it)
+  static const bool fwd444_tiled = getenv("JDS_FWD444_TILED") != nullptr;
+  if (MODE == M444 && !mq && !fwd444_tiled) {
     const int ng = fwd444w_groups(g);
     hipLaunchKernelGGL(k_fwd444w, dim3(ng, n), dim3(64 * F444_WAVES), 0, s, g, rgb, coeffs, fq32, part, fixlist, fc, st);
     hipError_t e = hipGetLastError();

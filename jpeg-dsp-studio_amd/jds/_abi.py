@@ -68,6 +68,9 @@ class JDSError(RuntimeError):
 
 
 _P = C.c_void_p
+ABI_VERSION = 3
+# `after` of the *_dev calls: no wait (the caller has synchronised); include/jds.h JDS_AFTER_NONE
+AFTER_NONE = C.c_void_p(-1 & ((1 << (8 * C.sizeof(C.c_void_p))) - 1))
 _SIGS = {
     'jds_abi_version': (C.c_int, []),
     'jds_last_error': (C.c_char_p, []),
@@ -89,6 +92,9 @@ _SIGS = {
     'jds_psnr_ssim_dev': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, _P]),
     'jds_psnr_ssim_dev_after': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, _P, _P]),
     'jds_magnitude_bits_f32_dev': (C.c_int, [_P, _P, C.c_int64, _P, _P]),
+    'jds_magnitude_bits_f32_batch_dev': (C.c_int, [_P, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P]),
+    'jds_psnr_ssim_batch_dev': (C.c_int, [_P, C.c_int32, _P, _P, C.c_int64, C.c_int64, _P, _P]),
+    'jds_selftest_psnr_ssim_legacy_dev': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, _P]),
     'jds_stage_rgb_to_ycbcr': (C.c_int, [_P, _P, _P, C.c_int64]),
     'jds_stage_ycbcr_to_rgb': (C.c_int, [_P, _P, _P, C.c_int64]),
     'jds_stage_subsample': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P]),
@@ -147,7 +153,7 @@ def lib():
             f = getattr(h, name, None)
             if f is not None:
                 f.restype, f.argtypes = res, args
-        if h.jds_abi_version() != 2:
+        if h.jds_abi_version() != ABI_VERSION:
             raise ImportError('libjds.so ABI version mismatch')
         _lib = h
         return h

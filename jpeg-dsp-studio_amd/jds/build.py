@@ -20,12 +20,17 @@ LIB = os.path.join(HERE, 'libjds.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('JDS_OFFLOAD_ARCH', 'gfx950')
 
-SOURCES = ['jds_codec.hip', 'jds_gen.hip', 'jds_b16.hip', 'jds_inv.hip', 'jds_inv_fast.hip', 'jds_fast.hip', 'jds_fast16.hip', 'jds_stages.hip', 'jds_ssim.hip', 'jds_entropy.hip', 'jds_abi.hip']
-HEADERS = ['jds_dct8.hpp', 'jds_dct16.hpp', 'jds_internal.hpp', 'jds_device.hpp', 'jds_inv_common.hpp', 'jds_inv_exact.hpp', 'jds_fwd_common.hpp']
+SOURCES = ['jds_codec.hip', 'jds_gen.hip', 'jds_b16.hip', 'jds_inv.hip', 'jds_inv_fast.hip', 'jds_fast.hip', 'jds_fast16.hip', 'jds_stages.hip', 'jds_ssim.hip', 'jds_ssim_band.hip', 'jds_entropy.hip', 'jds_abi.hip']
+
+
+def headers():
+    """Every header under csrc/ is a build input (tests/test_abi_cpu.py checks
+    that each #include "..." of the sources resolves to one of them)."""
+    return sorted(f for f in os.listdir(CSRC) if f.endswith('.hpp'))
 
 
 def _inputs():
-    files = [os.path.join(CSRC, s) for s in SOURCES + HEADERS if os.path.exists(os.path.join(CSRC, s))]
+    files = [os.path.join(CSRC, s) for s in SOURCES + headers() if os.path.exists(os.path.join(CSRC, s))]
     return files + [os.path.join(INCLUDE, 'jds.h')]
 
 

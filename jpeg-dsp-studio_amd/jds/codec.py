@@ -83,6 +83,12 @@ def psnr_ssim_raw(a: np.ndarray, b: np.ndarray, device: int = 0) -> np.ndarray:
     return out
 
 
+def _after(after):
+    """`after` of the *_dev calls: None = the caller has synchronised (JDS_AFTER_NONE);
+    otherwise a hipStream_t handle, passed unchanged (0 = the HIP null stream, waited for)."""
+    return _abi.AFTER_NONE if after is None else C.c_void_p(int(after))
+
+
 def psnr_ssim_dev(a_ptr: int, b_ptr: int, H: int, W: int, device: int = 0, after=-1) -> np.ndarray:
     """jds_psnr_ssim_dev: psnr_ssim_raw's six values for two HxWx3 uint8 images
     already in device memory (raw device pointers, e.g. torch tensors' data_ptr()).
@@ -95,7 +101,34 @@ def psnr_ssim_dev(a_ptr: int, b_ptr: int, H: int, W: int, device: int = 0, after
             check(lib().jds_psnr_ssim_dev(ctx.handle, int(a_ptr), int(b_ptr), int(H), int(W), out.ctypes.data))
         else:
             check(lib().jds_psnr_ssim_dev_after(ctx.handle, int(a_ptr), int(b_ptr), int(H), int(W), out.ctypes.data,
-                                                after or None))
+                                                _after(after)))
+    return out
+
+
+def psnr_ssim_batch_dev(a_ptrs, b_ptrs, H: int, W: int, device: int = 0, after=None) -> np.ndarray:
+    """jds_psnr_ssim_batch_dev: [n, 6] (psnr_ssim_raw's six values) for n
+    device-resident image pairs (a_ptrs[i], b_ptrs[i]) of one size, run together
+    on the GPU (the batch sweep's per-item SSIM).  after as in psnr_ssim_dev
+    (None: the caller has synchronised)."""
+    n = len(a_ptrs)
+    if len(b_ptrs) != n:
+        raise ValueError('a_ptrs and b_ptrs differ in length')
+    out = np.empty((n, 6), np.float64)
+    if n == 0:
+        return out
+    pa = (C.c_void_p * n)(*[int(p) for p in a_ptrs])
+    pb = (C.c_void_p * n)(*[int(p) for p in b_ptrs])
+    with lease(device) as ctx:
+        check(lib().jds_psnr_ssim_batch_dev(ctx.handle, n, pa, pb, int(H), int(W), out.ctypes.data, _after(after)))
+    return out
+
+
+def psnr_ssim_legacy_dev(a_ptr: int, b_ptr: int, H: int, W: int, device: int = 0) -> np.ndarray:
+    """Test-only: psnr_ssim_dev through the round-1..3 kernels (jds_selftest_psnr_ssim_legacy_dev)."""
+    out = np.empty(6, np.float64)
+    with lease(device) as ctx:
+        check(lib().jds_selftest_psnr_ssim_legacy_dev(ctx.handle, int(a_ptr), int(b_ptr), int(H), int(W),
+                                                      out.ctypes.data))
     return out
 
 
@@ -105,8 +138,21 @@ def magnitude_bits_f32_dev(coeffs_ptr: int, n_coeffs: int, device: int = 0, afte
     out = C.c_double()
     with lease(device) as ctx:
         check(lib().jds_magnitude_bits_f32_dev(ctx.handle, int(coeffs_ptr), int(n_coeffs), C.byref(out),
-                                               after or None))
+                                               _after(after)))
     return float(out.value)
+
+
+def magnitude_bits_f32_batch_dev(coeffs_ptr: int, n_items: int, n_coeffs: int, item_stride: int,
+                                 device: int = 0, after=None) -> np.ndarray:
+    """jds_magnitude_bits_f32_batch_dev: magnitude_bits_f32_dev for n_items
+    coefficient arrays at coeffs_ptr + 2 * i * item_stride bytes, one host wait."""
+    out = np.empty(n_items, np.float64)
+    if n_items == 0:
+        return out
+    with lease(device) as ctx:
+        check(lib().jds_magnitude_bits_f32_batch_dev(ctx.handle, int(coeffs_ptr), int(n_items), int(n_coeffs),
+                                                     int(item_stride), out.ctypes.data, _after(after)))
+    return out
 
 
 # ----------------------------------------------------------- per-stage ops

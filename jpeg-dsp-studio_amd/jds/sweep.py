@@ -59,8 +59,8 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
     them (utils/metrics.py:77-78).  ssim=True adds the SSIM fields of the
     reference's per-item CompressionResult (ssim_rgb, ssim_y; gui/worker.py:62-68
     -> utils/metrics.py:9-28) from the device-resident reconstructions
-    (jds_psnr_ssim_dev_after: bit-identical to skimage, the heaviest per-item
-    tail) and takes mse_y / psnr_y from the same bit-exact reduction."""
+    (jds_psnr_ssim_batch_dev: bit-identical to skimage, every item of a chunk
+    in one batched launch sequence) and takes mse_y / psnr_y from the same bit-exact reduction."""
     import torch
     from jds import _abi, codec
     from engines.quantizer import scale_quant_matrix
@@ -90,13 +90,19 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
             torch.cuda.synchronize(dev)
             stats[:, c0:c0 + len(qc)] = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(F, len(qc))
             cpf = plan.geometry.coeffs_per_frame
-            for f in range(F):
-                for i in range(len(qc)):
-                    # the images and coefficients are complete (synchronised above)
-                    magf[f, c0 + i] = codec.magnitude_bits_f32_dev(cf[f * len(qc) + i].data_ptr(), cpf, device, None)
-                    if ssim:
-                        r = codec.psnr_ssim_dev(fr[f].data_ptr(), out[f * len(qc) + i].data_ptr(), H, W, device, None)
-                        ssims[f, c0 + i] = (float(np.mean(r[:3])), r[3], r[4])  # channel_axis=2: mean of R, G, B
+            nit = F * len(qc)
+            # the images and coefficients are complete (synchronised above): one
+            # batched call each for every item of the chunk
+            magf[:, c0:c0 + len(qc)] = codec.magnitude_bits_f32_batch_dev(
+                cf.data_ptr(), nit, cpf, cpf, device, None).reshape(F, len(qc))
+            if ssim:
+                a = [fr[f].data_ptr() for f in range(F) for _ in qc]
+                b = [out[k].data_ptr() for k in range(nit)]
+                r = codec.psnr_ssim_batch_dev(a, b, H, W, device, None)
+                for f in range(F):
+                    for i in range(len(qc)):
+                        rk = r[f * len(qc) + i]
+                        ssims[f, c0 + i] = (float(np.mean(rk[:3])), rk[3], rk[4])  # channel_axis=2: mean of R, G, B
         finally:
             plan.close()
     items = []

@@ -38,7 +38,24 @@ def test_library_exports_every_declared_symbol(L):
     assert not missing, missing
     for n in names:
         assert hasattr(L, n)
-    assert L.jds_abi_version() == 2
+    assert L.jds_abi_version() == _abi.ABI_VERSION == 3
+
+
+def test_every_csrc_include_is_a_build_input():
+    """jds/build.py's up_to_date() must see every header a source includes, or a
+    non-forced build can reuse a stale libjds.so."""
+    from jds import build
+    csrc = build.CSRC
+    inputs = {os.path.basename(f) for f in build._inputs()}
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith(('.hip', '.hpp')):
+            continue
+        for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', open(os.path.join(csrc, f)).read(), re.M):
+            assert os.path.basename(inc) in inputs, (f, inc)
+    for s in build.SOURCES:
+        assert s in inputs
+    hips = {f for f in os.listdir(csrc) if f.endswith('.hip')}
+    assert hips == set(build.SOURCES), hips ^ set(build.SOURCES)
 
 
 def test_library_has_gfx950_code_object(L):

@@ -1,0 +1,92 @@
+"""K4 v2 (csrc/jds_ssim_band.hip): the batched, band-swept SSIM pipeline against
+(a) the round-1..3 kernels (jds_selftest_psnr_ssim_legacy_dev: one scipy line
+per lane, IEEE divisions), bit for bit on all six values, over sizes that
+exercise every edge of the sweep (7-px images, partial bands, partial column
+chunks, partial NumPy buffers, odd map sizes), and (b) the oracle's NumPy /
+scipy restatement of utils/metrics.py:9-28."""
+import numpy as np
+import pytest
+
+from oracle import cpu_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module', autouse=True)
+def gpu():
+    from jds import build, _abi
+    build.build()
+    assert _abi.device_count() >= 1, 'no HIP device: the MI355X path has no CPU fallback'
+
+
+def _pair(h, w, seed, kind):
+    a = cpu_ref.random_image(h, w, seed)
+    if kind == 'noise':    # a reconstruction-like neighbour of a
+        d = cpu_ref.random_image(h, w, seed + 101).astype(np.int16) // 16 - 8
+        b = np.clip(a.astype(np.int16) + d, 0, 255).astype(np.uint8)
+    elif kind == 'flat':   # constant images: zero variances, exact-integer corner cases
+        a = np.full((h, w, 3), 30, np.uint8)
+        b = np.full((h, w, 3), 29, np.uint8)
+    elif kind == 'smooth':  # gradients: large sums, small differences
+        yy, xx = np.mgrid[0:h, 0:w]
+        a = np.stack([(xx * 255 // max(w - 1, 1)), (yy * 255 // max(h - 1, 1)), (xx + yy) % 256], -1).astype(np.uint8)
+        b = np.clip(a.astype(np.int16) + (xx % 3 - 1)[..., None], 0, 255).astype(np.uint8)
+    else:                  # independent images
+        b = cpu_ref.random_image(h, w, seed + 202)
+    return np.ascontiguousarray(a), np.ascontiguousarray(b)
+
+
+SIZES = [(7, 7), (7, 40), (40, 7), (8, 9), (13, 8), (14, 14), (15, 39), (23, 70), (31, 37), (64, 64),
+         (100, 37), (129, 131), (255, 257), (518, 931), (1080, 1920)]
+
+
+@pytest.mark.parametrize('h,w', SIZES)
+def test_batched_pipeline_equals_legacy_kernels_bitwise(h, w):
+    import torch
+    from jds import codec
+    kinds = ['noise', 'indep', 'flat', 'smooth'] if h * w <= 300000 else ['noise']
+    pairs = [_pair(h, w, 17 + i, k) for i, k in enumerate(kinds)]
+    dev = torch.device('cuda', 0)
+    ta = [torch.from_numpy(a).to(dev) for a, _ in pairs]
+    tb = [torch.from_numpy(b).to(dev) for _, b in pairs]
+    torch.cuda.synchronize()
+    batch = codec.psnr_ssim_batch_dev([t.data_ptr() for t in ta], [t.data_ptr() for t in tb], h, w, 0, None)
+    for k in range(len(pairs)):
+        leg = codec.psnr_ssim_legacy_dev(ta[k].data_ptr(), tb[k].data_ptr(), h, w, 0)
+        one = codec.psnr_ssim_dev(ta[k].data_ptr(), tb[k].data_ptr(), h, w, 0)
+        assert np.array_equal(batch[k].view(np.uint64), leg.view(np.uint64)), (kinds[k], batch[k], leg)
+        assert np.array_equal(one.view(np.uint64), leg.view(np.uint64)), (kinds[k], one, leg)
+
+
+@pytest.mark.parametrize('h,w', [(7, 7), (31, 37), (100, 37), (257, 130)])
+def test_batched_pipeline_equals_oracle(h, w):
+    """Against the NumPy / scipy restatement (the golden fixtures pin that one to skimage)."""
+    from utils.metrics import compute_psnr_ssim
+    for i, k in enumerate(['noise', 'indep', 'smooth']):
+        a, b = _pair(h, w, 5 + i, k)
+        assert compute_psnr_ssim(a, b) == cpu_ref.compute_psnr_ssim(a, b)
+
+
+def test_batch_larger_than_one_launch():
+    """More pairs than one launch carries (32): consecutive launches, same values."""
+    import torch
+    from jds import codec
+    h, w = 21, 29
+    pairs = [_pair(h, w, 300 + i, 'noise' if i % 2 else 'indep') for i in range(37)]
+    dev = torch.device('cuda', 0)
+    ta = [torch.from_numpy(a).to(dev) for a, _ in pairs]
+    tb = [torch.from_numpy(b).to(dev) for _, b in pairs]
+    torch.cuda.synchronize()
+    r = codec.psnr_ssim_batch_dev([t.data_ptr() for t in ta], [t.data_ptr() for t in tb], h, w, 0, None)
+    for k, (a, b) in enumerate(pairs):
+        ref = codec.psnr_ssim_raw(a, b)
+        assert np.array_equal(r[k], ref)
+
+
+def test_batch_rejects_small_images():
+    import torch
+    from jds import codec
+    t = torch.zeros((6, 9, 3), dtype=torch.uint8, device='cuda')
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError, match='win_size exceeds image extent'):
+        codec.psnr_ssim_batch_dev([t.data_ptr()], [t.data_ptr()], 6, 9, 0, None)
