@@ -561,6 +561,28 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
         except Exception:
             traffic = None
 
+    # VALU issue roofline of the same phase (profiles/pmc_valu.json, tools/r4_pmc.sh):
+    # PMC-counted VALU instructions per launch by class x their measured issue
+    # cost, over what 1024 SIMDs at 2.4 GHz issue in this run's launch time
+    valu = None
+    vf = os.path.join(ROOT, 'profiles', 'pmc_valu.json')
+    if os.path.exists(vf):
+        try:
+            vrec = json.load(open(vf))
+            vkey = (f'{W}x{H}_q{quality}_{mode}_pf{int(bool(pf))}' + ('_B16' if block == 16 else '') + f'_b{B}')
+            ph = vrec.get(vkey, {}).get(dom)
+            if ph and not (args.exact or args.exact_inv or args.inv_fast):
+                cap = 1024 * 2.4e9 * t_dom * 1e-3
+                lo, hi = ph['issue_cycles_lo'] / cap, ph['issue_cycles_hi'] / cap
+                valu = {'frac_lo': round(lo, 4), 'frac_hi': round(hi, 4), 'frac': round((lo + hi) / 2, 4),
+                        'peak': '1024 SIMDs x 2.4 GHz, one VALU wave instruction at its measured issue cost',
+                        'valu_insts_per_launch': sum(k['valu_insts'] for k in ph['kernels']),
+                        'kernels': [k['kernel'] for k in ph['kernels']],
+                        'source': f'profiles/pmc_valu.json[{vkey}] ({vrec[vkey].get("source", "")})'}
+        except Exception:
+            valu = None
+    bound = 'valu' if valu and valu['frac'] > achieved / HBM_PEAK_GBS else 'hbm'
+
     result = {
         'metric': metric_name(quality, mode),
         'value': round(value, 2),
@@ -581,14 +603,16 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
                    'pipeline': ('image stream: forward of batch k+1 beside the inverse of batch k (two streams, '
                                 'two buffer sets)' if NS > 1 else 'serial forward then inverse per step'),
                    'parallelism': f'frame-shard x{world}', **dist_info(world, backend)},
-        'roofline': {'bound': 'hbm', 'kernel': kname, 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
+        'roofline': {'bound': bound, 'kernel': kname, 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'frac_vs_measured_copy_bw': round(achieved / HBM_COPY_GBS, 4),
                      'algorithmic_bytes_per_launch': bytes_fwd if dom == 'k_fwd' else bytes_inv,
                      'avg_launch_ms': round(t_dom, 4),
                      'timing': 'HIP events on the launch stream, serial calibration pass after the timed region',
-                     'limiter': 'VALU issue, not HBM: the forward computes in certified fp32, the bit-exact '
-                                'inverse in fp64 (DESIGN.md section 4, profiles/*_pmc_summary.json)'},
+                     'valu': valu,
+                     'note': ('achieved / peak / frac: the HBM roofline by algorithmic bytes; bound: the resource '
+                              'with the larger fraction (valu.frac: issue cycles / SIMD cycles, DESIGN.md section 4 '
+                              'floor table)')},
         'kernels_ms': {'k_fwd': round(t_fwd, 4), 'k_inv': round(t_inv, 4)},
         'fixups_last_step': {'fwd_blocks': int(plans[0].fix_counts()[0]), 'inv_tiles': int(plans[0].fix_counts()[1])},
         'pipeline_roofline_frac': round(value / world * 1e6 * (6 + 2 * S) / (HBM_PEAK_GBS * 1e9), 4),

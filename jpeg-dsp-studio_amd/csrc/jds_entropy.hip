@@ -464,6 +464,129 @@ __global__ void __launch_bounds__(256) k_ent_pack(const EntGeo e, long long nblk
   }
 }
 
+// k_ent_pack2: k_ent_pack's wave windows with the walk made branch-free for
+// the common symbols.  Per table class, pk[run * 32 + s] = (length << 16) |
+// code of the (run, s) symbol for run < 16 (s clamped to 10 as code_ac does),
+// 0 for s = 0: a zero coefficient appends nothing.  Every zigzag position
+// appends code << s | magnitude (<= 26 bits) to a 64-bit accumulator and
+// ORs one window word (0 when fewer than 32 bits are pending: no branch); only
+// ZRL codes (a nonzero after >= 16 zeros) take a branch.
+#ifndef JDS_ENT_PACK_TABLE
+#define JDS_ENT_PACK_TABLE 1
+#endif
+struct PackAcc {
+  uint64_t acc;
+  int n;
+  uint32_t* dst;
+  __device__ __forceinline__ void put(uint32_t v, int len) {  // len <= 32
+    acc = (acc << len) | v;
+    n += len;
+    const bool f = n >= 32;
+    const uint32_t w = (uint32_t)(acc >> (f ? n - 32 : 0));
+    atomicOr(dst, f ? w : 0u);  // ds_or_b32
+    dst += f ? 1 : 0;
+    n -= f ? 32 : 0;
+  }
+};
+
+template <int K>
+__device__ __forceinline__ void ac_pack(const BlockRegs& r, int& last, PackAcc& o, const uint32_t* pk, uint32_t zrl) {
+  if constexpr (K < 64) {
+    const int v = coef_at<ZZC[K]>(r);
+    const int a = v < 0 ? -v : v;
+    int sz = a ? 32 - __clz(a) : 0;
+    sz = sz > 10 ? 10 : sz;
+    int run = K - 1 - last;
+    if (a && run >= 16) {  // rare: one ZRL code per 16 zeros first
+      for (; run >= 16; run -= 16) o.put(zrl & 0xFFFFu, (int)(zrl >> 16));
+    }
+    const uint32_t e = pk[((run & 15) << 5) | sz];
+    const uint32_t mag = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << sz) - 1u);
+    o.put(((e & 0xFFFFu) << sz) | mag, (int)(e >> 16) + sz);
+    last = a ? K : last;
+    ac_pack<K + 1>(r, last, o, pk, zrl);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_ent_pack2(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
+                                                   const EntTab* __restrict__ gt,
+                                                   const unsigned long long* __restrict__ bits,
+                                                   const unsigned long long* __restrict__ excl,
+                                                   const unsigned long long* __restrict__ info,
+                                                   uint32_t* __restrict__ raw) {
+  __shared__ EntTab t;
+  __shared__ uint32_t pkt[2][16 * 32];
+  __shared__ uint32_t s_win[4][ENT_WIN];
+  load_tab(gt, &t);
+  for (int i = threadIdx.x; i < 2 * 16 * 32; i += blockDim.x) {
+    const int c = i >> 9, run = (i >> 5) & 15, sz = i & 31;
+    pkt[c][i & 511] = sz ? t.ac[c][(run << 4) | (sz > 10 ? 10 : sz)] : 0u;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* win = s_win[wv];
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long g0 = ((long long)blockIdx.x * 4 + wv) * 64; g0 < nblk; g0 += stride) {
+    const long long gb = g0 + lane;
+    const bool valid = gb < nblk;
+    const long long gl = (nblk - g0 < 64 ? nblk : g0 + 64) - 1;  // last block of the wave
+    const int frame = (int)((valid ? gb : gl) / e.nb), b = (int)((valid ? gb : gl) - (long long)frame * e.nb);
+    const int s = scan_of(e, b);
+    const unsigned long long base = info[2 * (frame * 3 + s)];
+    const unsigned long long rel = (valid ? excl[gb] : excl[gl]) - base;
+    const int f0 = (int)(g0 / e.nb), fl = (int)(gl / e.nb);
+    const int s0 = scan_of(e, (int)(g0 - (long long)f0 * e.nb)), sl = scan_of(e, (int)(gl - (long long)fl * e.nb));
+    const unsigned long long rel0 = __shfl(rel, 0, 64);
+    const unsigned long long end = excl[gl] + bits[gl] - base;
+    const long long w0 = (long long)(rel0 >> 5), nw = (long long)((end + 31) >> 5) - w0;
+    const bool fast = f0 == fl && s0 == sl && nw <= ENT_WIN;
+    BlockRegs r;
+    int pred = 0;
+    if (valid) {
+      r = load_block(coeffs + gb * 64);
+      pred = b == e.first[s] ? 0 : (int)coeffs[(gb - 1) * 64];
+    }
+    bool bd;
+    if (fast) {
+      for (int i = lane; i < nw; i += 64) win[i] = 0u;
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (valid) {
+        const int cls = s ? 1 : 0;
+        PackAcc o{0ull, (int)(rel & 31), win + ((long long)(rel >> 5) - w0)};
+        const int diff = coef_at<0>(r) - pred;
+        const int da = diff < 0 ? -diff : diff;
+        int ds = da ? 32 - __clz(da) : 0;
+        ds = ds > 11 ? 11 : ds;
+        const uint32_t dc = t.dc[cls][ds];
+        o.put(((dc & 0xFFFFu) << ds) | ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << ds) - 1u)),
+              (int)(dc >> 16) + ds);
+        int last = 0;
+        ac_pack<1>(r, last, o, pkt[cls], t.ac[cls][0xF0]);
+        if (last < 63) {
+          const uint32_t eob = t.ac[cls][0x00];
+          o.put(eob & 0xFFFFu, (int)(eob >> 16));
+        }
+        if (o.n > 0) atomicOr(o.dst, (uint32_t)(o.acc << (32 - o.n)));
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      uint32_t* dst = raw + raw_base(e, f0, s0) + w0;
+      for (int i = lane; i < nw; i += 64) {
+        const uint32_t w = __builtin_bswap32(win[i]);
+        if (i == 0 || i == nw - 1) atomicOr(dst + i, w); else dst[i] = w;
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    } else if (valid) {
+      BitSink<SINK_GLOBAL> o;
+      o.dst = raw + raw_base(e, frame, s) + (rel >> 5);
+      o.n = (int)(rel & 31);
+      code_block<SINK_GLOBAL>(r, pred, t.dc[s ? 1 : 0], t.ac[s ? 1 : 0], o, bd);
+    }
+  }
+}
+
 constexpr int ENT_CH = 1024;  // bytes per stuffing chunk (256 threads x 4)
 
 // byte i of scan (f, s) with the 1-bit pad applied (T.81 F.1.2.3)
@@ -657,7 +780,10 @@ hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* cons
   if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, bits, excl, (int)(nblk + 1), s)) != hipSuccess) return err;
   hipLaunchKernelGGL(k_ent_info, dim3((3 * n + 63) / 64), dim3(64), 0, s, e, n, excl, info, scan_bits);
   hipLaunchKernelGGL(k_ent_zero, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, e, nblk, bits, excl, info, raw);
-  hipLaunchKernelGGL(k_ent_pack, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, excl, info, raw);
+  if (JDS_ENT_PACK_TABLE)
+    hipLaunchKernelGGL(k_ent_pack2, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, excl, info, raw);
+  else
+    hipLaunchKernelGGL(k_ent_pack, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, excl, info, raw);
   const dim3 cg(e.chunks < 64 ? e.chunks : 64, 3, n);
   if ((err = hipMemsetAsync(ffc, 0, sizeof(unsigned long long) * (nch + 1), s)) != hipSuccess) return err;
   hipLaunchKernelGGL(k_ent_ff, cg, dim3(256), 0, s, e, info, raw, ffc);

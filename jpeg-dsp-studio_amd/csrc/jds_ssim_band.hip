@@ -59,6 +59,7 @@ namespace jds {
 constexpr int SB_NP_BUF = 8192;  // NumPy ufunc buffer (elements)
 constexpr int SB_CW = 32;        // output columns per chunk
 constexpr int SB_RING = 64;      // ring slots per row (power of two >= CW + 7)
+static_assert(SB_RING == 2 * SB_CW, "chain_chunk's ring phase is 0 or CW");
 constexpr int SB_RP = 65;        // ring row pitch in doubles (odd: lane = row reads hit distinct banks)
 constexpr int SB_SP = SB_CW + 1; // chain output tile pitch
 constexpr int SB_THREADS = 256;
@@ -247,34 +248,34 @@ struct BandLds {
   double st[5][BH][SB_SP];    // axis-1 running sums of the current chunk
 };
 
-// Raw inputs of one fill lane: the terms of rows i0 - 3 .. i0 + nr + 2 (RGB,
-// exact integers) or of the luma planes (fp64), loaded before the lane's map
-// work so the loads are in flight meanwhile.
+// Raw inputs of one fill lane: the bytes of rows i0 - 3 .. i0 + nr + 2 (RGB)
+// or the luma planes' values and the chain's checkpoint (Y), loaded before the
+// lane's map work so the loads are in flight meanwhile (nothing consumes them
+// before fill_store).
 template <int BH>
 struct FillRegs {
-  int ti[BH + 6];
+  int bx[BH + 6], by[BH + 6];
   double tx[BH + 6], ty[BH + 6];
+  double s0;
 };
 
 template <int BH>
 __device__ __forceinline__ void fill_load(const SsimBatch& B, int c, const uint8_t* a, const uint8_t* b,
-                                          const double* X, const double* Y, int i0, int q, int col,
-                                          FillRegs<BH>& R) {
+                                          const double* X, const double* Y, const double* ck, int band, int i0,
+                                          int q, int col, FillRegs<BH>& R) {
   const int W = B.W;
-  // rows i0 - 3 .. i0 + nr + 2; in a partial last band the rows past H - 1 are
-  // clamped (loaded, never used): unpredicated loads stay in flight together
+  // in a partial last band the rows past H - 1 are clamped (loaded, never
+  // used): unpredicated loads stay in flight together
   if (c < 3) {
-    int x[BH + 6], y[BH + 6];
 #pragma unroll
     for (int r = 0; r < BH + 6; ++r) {
       const size_t px = ((size_t)min(i0 - 3 + r, B.H - 1) * W + col) * 3 + c;
-      x[r] = a[px];
-      y[r] = b[px];
+      R.bx[r] = a[px];
+      R.by[r] = b[px];
     }
-#pragma unroll
-    for (int r = 0; r < BH + 6; ++r) R.ti[r] = qterm<int>(q, x[r], y[r]);
   } else {
     // the chain resumes at i0 from its checkpoint (old rows from i0 - 3, new rows from i0 + 4)
+    R.s0 = ck[((size_t)q * B.NB + band) * W + col];
 #pragma unroll
     for (int r = 0; r < BH + 6; ++r) {
       const size_t p = (size_t)min(i0 - 3 + r, B.H - 1) * W + col;
@@ -285,23 +286,25 @@ __device__ __forceinline__ void fill_load(const SsimBatch& B, int c, const uint8
 }
 
 template <int BH>
-__device__ __forceinline__ void fill_store(const SsimBatch& B, int c, const double* ck, int band, int nr, int q,
-                                           int col, const FillRegs<BH>& R, BandLds<BH>& L) {
+__device__ __forceinline__ void fill_store(int c, int nr, int q, int col, const FillRegs<BH>& R, BandLds<BH>& L) {
   const int slot = col & (SB_RING - 1);
   if (c < 3) {
+    int t[BH + 6];
+#pragma unroll
+    for (int r = 0; r < BH + 6; ++r) t[r] = qterm<int>(q, R.bx[r], R.by[r]);
     int S = 0;
 #pragma unroll
-    for (int r = 0; r < 7; ++r) S += R.ti[r];  // exact
+    for (int r = 0; r < 7; ++r) S += t[r];  // exact
     L.ring[q][0][slot] = div7((double)S);
 #pragma unroll
     for (int rr = 1; rr < BH; ++rr) {
       if (rr < nr) {
-        S += R.ti[rr + 6] - R.ti[rr - 1];
+        S += t[rr + 6] - t[rr - 1];
         L.ring[q][rr][slot] = div7((double)S);
       }
     }
   } else {
-    double s = ck[((size_t)q * B.NB + band) * B.W + col];
+    double s = R.s0;
     L.ring[q][0][slot] = div7(s);
 #pragma unroll
     for (int rr = 1; rr < BH; ++rr) {
@@ -314,6 +317,58 @@ __device__ __forceinline__ void fill_store(const SsimBatch& B, int c, const doub
       }
     }
   }
+}
+
+// One chunk of a chain lane's axis-1 running sum, steps j = jc + jj: every ring
+// read first (static LDS offsets: jc is a multiple of CW, so the ring phase
+// BASE = jc & (RING - 1) is 0 or CW), then the dependent adds.  FIRST: j = 0
+// starts scipy's reflected window; NJ: steps in this chunk (all CW but the last).
+template <int BASE, bool FIRST>
+__device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double* __restrict__ o, double& s, int nj) {
+  constexpr int M = SB_RING - 1;
+  double nv[SB_CW], ov[SB_CW];
+#pragma unroll
+  for (int jj = 0; jj < SB_CW; ++jj) {
+    nv[jj] = R[(BASE + jj + 3) & M];
+    ov[jj] = R[(BASE + jj - 4) & M];
+  }
+  int jj0 = 0;
+  if constexpr (FIRST) {
+    // scipy's first window: reflect(-3 .. 3) = 2, 1, 0, 0, 1, 2, 3; then j = 1..3
+    // take their old column from reflect(j - 4) = 2, 1, 0
+    const double r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3];
+    s = s + r2;
+    s = s + r1;
+    s = s + r0;
+    s = s + r0;
+    s = s + r1;
+    s = s + r2;
+    s = s + r3;
+    o[0] = s;
+    s = s + (nv[1] - r2);
+    o[1] = s;
+    s = s + (nv[2] - r1);
+    o[2] = s;
+    s = s + (nv[3] - r0);
+    o[3] = s;
+    jj0 = 4;
+  }
+  if (nj == SB_CW) {
+#pragma unroll
+    for (int jj = FIRST ? 4 : 0; jj < SB_CW; ++jj) {
+      s = s + (nv[jj] - ov[jj]);
+      o[jj] = s;
+    }
+  } else {
+#pragma unroll
+    for (int jj = FIRST ? 4 : 0; jj < SB_CW; ++jj) {
+      if (jj < nj) {
+        s = s + (nv[jj] - ov[jj]);
+        o[jj] = s;
+      }
+    }
+  }
+  (void)jj0;
 }
 
 template <int BH>
@@ -346,8 +401,8 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_band(SsimBatch B) {
     if (t < 5 * nc) {
       FillRegs<BH> R;
       const int q = t / nc, col = lo + t % nc;
-      fill_load<BH>(B, c, pr.a, pr.b, X, Y, i0, q, col, R);
-      fill_store<BH>(B, c, ck, band, nr, q, col, R, L);
+      fill_load<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, q, col, R);
+      fill_store<BH>(c, nr, q, col, R, L);
     }
   }
   __syncthreads();
@@ -361,39 +416,13 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_band(SsimBatch B) {
     if (chain_lane) {
       const double* R = L.ring[cq][crow];
       double* o = L.st[cq][crow];
-      if (k == 0) {
-        // scipy's first window: reflect(-3 .. 3) = 2, 1, 0, 0, 1, 2, 3
-        s = s + R[2];
-        s = s + R[1];
-        s = s + R[0];
-        s = s + R[0];
-        s = s + R[1];
-        s = s + R[2];
-        s = s + R[3];
-        o[0] = s;
-        s = s + (R[4] - R[2]);  // j = 1..3: old column reflect(j - 4) = 2, 1, 0
-        o[1] = s;
-        s = s + (R[5] - R[1]);
-        o[2] = s;
-        s = s + (R[6] - R[0]);
-        o[3] = s;
-#pragma unroll
-        for (int jj = 4; jj < SB_CW; ++jj) {
-          if (jj < jend) {
-            s = s + (R[(jj + 3) & (SB_RING - 1)] - R[(jj - 4) & (SB_RING - 1)]);
-            o[jj] = s;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int jj = 0; jj < SB_CW; ++jj) {
-          const int j = jc + jj;
-          if (j < jend) {
-            s = s + (R[(j + 3) & (SB_RING - 1)] - R[(j - 4) & (SB_RING - 1)]);
-            o[jj] = s;
-          }
-        }
-      }
+      const int nj = min(SB_CW, jend - jc);
+      if (k == 0)
+        chain_chunk<0, true>(R, o, s, nj);
+      else if (jc & SB_CW)
+        chain_chunk<SB_CW, false>(R, o, s, nj);
+      else
+        chain_chunk<0, false>(R, o, s, nj);
     }
     __syncthreads();
 
@@ -407,7 +436,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_band(SsimBatch B) {
     if (fl) {
       fq = t / nc;
       fcol = lo + t % nc;
-      fill_load<BH>(B, c, pr.a, pr.b, X, Y, i0, fq, fcol, R);
+      fill_load<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, fq, fcol, R);
     }
     for (int p = t; p < BH * SB_CW; p += SB_THREADS) {
       const int row = p / SB_CW, jj = p % SB_CW, j = jc + jj;
@@ -425,7 +454,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_band(SsimBatch B) {
         smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = (a1 * a2) / d;
       }
     }
-    if (fl) fill_store<BH>(B, c, ck, band, nr, fq, fcol, R, L);
+    if (fl) fill_store<BH>(c, nr, fq, fcol, R, L);
     __syncthreads();
   }
 }
@@ -651,7 +680,10 @@ __global__ void __launch_bounds__(256) k_ss_final(SsimBatch B) {
 
 // ------------------------------------------------------------------ host --
 
-constexpr int SB_BH = 8;  // band height (rows per workgroup)
+#ifndef JDS_SSIM_BH
+#define JDS_SSIM_BH 8
+#endif
+constexpr int SB_BH = JDS_SSIM_BH;  // band height (rows per workgroup; 8 or 16)
 
 int ssim_bands(int H) { return (H - 6 + SB_BH - 1) / SB_BH; }
 
