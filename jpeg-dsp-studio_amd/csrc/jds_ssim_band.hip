@@ -48,6 +48,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string.h>
+
 #include <algorithm>
 
 #include "jds_internal.hpp"
@@ -70,6 +72,19 @@ struct SsimPair {
   const uint8_t* b;
 };
 
+// NumPy's pairwise_sum recursion over the last, partial 8192-element buffer
+// of a stream (m < 8192 elements), built on the host (pw_tree): its leaves in
+// order (<= 65, each <= 128 elements) and its internal nodes sorted by height
+// (children: index < nl a leaf, else nl + internal index), so the device sums
+// the leaves in parallel and combines one height per barrier interval.
+constexpr int PW_MAXN = 72;
+struct PwTree {
+  uint16_t off[PW_MAXN], n[PW_MAXN];
+  uint8_t l[PW_MAXN], r[PW_MAXN];
+  uint8_t hs[10];  // internal nodes of height h + 1: [hs[h], hs[h + 1])
+  uint8_t nl, ni, nh;
+};
+
 struct SsimBatch {
   SsimPair pairs[SB_MAX_ITEMS];  // by value: nothing to stage or keep alive on the host
   int H, W;
@@ -86,6 +101,7 @@ struct SsimBatch {
   double* out;            // [item][out_stride]: ssim R, G, B, Y, mse_Y
   int out_stride;
   unsigned long long* sse;  // [item]: sum of (a - b)^2 over the H*W*3 bytes (zeroed by the caller)
+  PwTree tree_s, tree_y;    // the partial buffers of the map stream and of the luma MSE stream
 };
 
 // x / 7 correctly rounded: q0 = RN(x * RN(1/7)) is within an ulp of x/7, the
@@ -242,76 +258,133 @@ __global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
 
 // ------------------------------------------------------------ band sweep --
 
+constexpr int SB_SC = SB_CW + 4;  // staged columns per chunk (chunk 0 fills CW + 3)
+
 template <int BH>
 struct BandLds {
   double ring[5][BH][SB_RP];  // axis-0 outputs, column c at slot c & (SB_RING - 1)
   double st[5][BH][SB_SP];    // axis-1 running sums of the current chunk
+  // inputs of the fill of one chunk, double-buffered (staged two chunks ahead):
+  // per staged column, rows i0 - 3 .. i0 + BH + 2 of both images
+  union {
+    uint8_t b[SB_SC][2][16];           // RGB: the channel's bytes (a, b)
+    double y[SB_SC][2][BH + 6];        // luma: the planes' values (a, b)
+  } in[2];
+  double ck[2][5][SB_SC];              // luma: the axis-0 chains' states at row i0
 };
 
-// Raw inputs of one fill lane: the bytes of rows i0 - 3 .. i0 + nr + 2 (RGB)
-// or the luma planes' values and the chain's checkpoint (Y), loaded before the
-// lane's map work so the loads are in flight meanwhile (nothing consumes them
-// before fill_store).
+// fill columns of chunk k: chunk 0 fills [0, CW + 3), chunk k > 0 the new
+// columns [k CW + 3, (k + 1) CW + 3), clipped to W
+__device__ __forceinline__ void fill_cols(int k, int W, int& lo, int& hi) {
+  lo = k == 0 ? 0 : k * SB_CW + 3;
+  hi = min((k + 1) * SB_CW + 3, W);
+}
+
+// Staging of one chunk's fill inputs: every thread loads up to SE elements
+// (coalesced: consecutive threads take consecutive columns of a row) into
+// registers; stage_commit writes them into the chunk's LDS buffer once the
+// loads have landed, a barrier interval later in program order.
+constexpr int SB_SE = (2 * 16 * SB_SC + SB_THREADS - 1) / SB_THREADS;  // >= 2 * (BH + 6) * SC / THREADS
 template <int BH>
-struct FillRegs {
-  int bx[BH + 6], by[BH + 6];
-  double tx[BH + 6], ty[BH + 6];
-  double s0;
+struct StageRegs {
+  uint32_t b[SB_SE];
+  double y[SB_SE];
+  double ck;
 };
 
 template <int BH>
-__device__ __forceinline__ void fill_load(const SsimBatch& B, int c, const uint8_t* a, const uint8_t* b,
-                                          const double* X, const double* Y, const double* ck, int band, int i0,
-                                          int q, int col, FillRegs<BH>& R) {
-  const int W = B.W;
-  // in a partial last band the rows past H - 1 are clamped (loaded, never
-  // used): unpredicated loads stay in flight together
-  if (c < 3) {
+__device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uint8_t* a, const uint8_t* b,
+                                            const double* X, const double* Y, const double* ck, int band, int i0,
+                                            int k, int nchunks, StageRegs<BH>& R) {
+  constexpr int NR = BH + 6;
+  static_assert(2 * NR * SB_SC <= SB_SE * SB_THREADS, "staging slots");
+  if (k >= nchunks) return;
+  int lo, hi;
+  fill_cols(k, B.W, lo, hi);
+  const int t = threadIdx.x;
 #pragma unroll
-    for (int r = 0; r < BH + 6; ++r) {
-      const size_t px = ((size_t)min(i0 - 3 + r, B.H - 1) * W + col) * 3 + c;
-      R.bx[r] = a[px];
-      R.by[r] = b[px];
+  for (int i = 0; i < SB_SE; ++i) {
+    const int e = t + i * SB_THREADS;
+    const int cc = e % SB_SC, r = (e / SB_SC) % NR, im = e / (SB_SC * NR);
+    // columns past hi and rows past H - 1 (partial last band) load a valid
+    // clamped element that is never used: no predicated loads
+    const int col = min(lo + cc, hi - 1), row = min(i0 - 3 + r, B.H - 1);
+    const size_t px = (size_t)row * B.W + col;
+    if (c < 3) {
+      const uint8_t* img = im ? b : a;
+      R.b[i] = e < 2 * NR * SB_SC ? img[px * 3 + c] : 0u;
+    } else {
+      const double* P = im ? Y : X;
+      R.y[i] = e < 2 * NR * SB_SC ? P[px] : 0.0;
     }
-  } else {
-    // the chain resumes at i0 from its checkpoint (old rows from i0 - 3, new rows from i0 + 4)
-    R.s0 = ck[((size_t)q * B.NB + band) * W + col];
-#pragma unroll
-    for (int r = 0; r < BH + 6; ++r) {
-      const size_t p = (size_t)min(i0 - 3 + r, B.H - 1) * W + col;
-      R.tx[r] = X[p];
-      R.ty[r] = Y[p];
-    }
+  }
+  if (c == 3 && t < 5 * SB_SC) {
+    const int q = t / SB_SC, col = min(lo + t % SB_SC, hi - 1);
+    R.ck = ck[((size_t)q * B.NB + band) * B.W + col];
   }
 }
 
 template <int BH>
-__device__ __forceinline__ void fill_store(int c, int nr, int q, int col, const FillRegs<BH>& R, BandLds<BH>& L) {
-  const int slot = col & (SB_RING - 1);
-  if (c < 3) {
-    int t[BH + 6];
+__device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const StageRegs<BH>& R, BandLds<BH>& L) {
+  constexpr int NR = BH + 6;
+  if (k >= nchunks) return;
+  const int t = threadIdx.x, buf = k & 1;
 #pragma unroll
-    for (int r = 0; r < BH + 6; ++r) t[r] = qterm<int>(q, R.bx[r], R.by[r]);
+  for (int i = 0; i < SB_SE; ++i) {
+    const int e = t + i * SB_THREADS;
+    if (e < 2 * NR * SB_SC) {
+      const int cc = e % SB_SC, r = (e / SB_SC) % NR, im = e / (SB_SC * NR);
+      if (c < 3)
+        L.in[buf].b[cc][im][r] = (uint8_t)R.b[i];
+      else
+        L.in[buf].y[cc][im][r] = R.y[i];
+    }
+  }
+  if (c == 3 && t < 5 * SB_SC) L.ck[buf][t / SB_SC][t % SB_SC] = R.ck;
+}
+
+// the fill of chunk k from its staged inputs: lanes (q, column), the axis-0
+// outputs of the band's rows into the ring (RGB: exact window sums; luma: the
+// chain resumed from its checkpoint)
+template <int BH>
+__device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<BH>& L) {
+  constexpr int NR = BH + 6;
+  int lo, hi;
+  fill_cols(k, W, lo, hi);
+  const int nc = hi - lo, t = threadIdx.x;
+  if (t >= 5 * nc) return;
+  const int q = t / nc, cc = t % nc, buf = k & 1;
+  const int slot = (lo + cc) & (SB_RING - 1);
+  if (c < 3) {
+    const uint4 xa = *reinterpret_cast<const uint4*>(L.in[buf].b[cc][0]);
+    const uint4 ya = *reinterpret_cast<const uint4*>(L.in[buf].b[cc][1]);
+    const uint32_t xw[4] = {xa.x, xa.y, xa.z, xa.w}, yw[4] = {ya.x, ya.y, ya.z, ya.w};
+    int tt[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      tt[r] = qterm<int>(q, (int)((xw[r >> 2] >> (8 * (r & 3))) & 255u), (int)((yw[r >> 2] >> (8 * (r & 3))) & 255u));
     int S = 0;
 #pragma unroll
-    for (int r = 0; r < 7; ++r) S += t[r];  // exact
+    for (int r = 0; r < 7; ++r) S += tt[r];  // exact
     L.ring[q][0][slot] = div7((double)S);
 #pragma unroll
     for (int rr = 1; rr < BH; ++rr) {
       if (rr < nr) {
-        S += t[rr + 6] - t[rr - 1];
+        S += tt[rr + 6] - tt[rr - 1];
         L.ring[q][rr][slot] = div7((double)S);
       }
     }
   } else {
-    double s = R.s0;
+    const double* tx = L.in[buf].y[cc][0];
+    const double* ty = L.in[buf].y[cc][1];
+    double s = L.ck[buf][q][cc];
     L.ring[q][0][slot] = div7(s);
 #pragma unroll
     for (int rr = 1; rr < BH; ++rr) {
       if (rr < nr) {
         // row i = i0 + rr: new row i + 3 (index rr + 6), old row i - 4 (rr - 1)
-        const double tn = qterm<double>(q, R.tx[rr + 6], R.ty[rr + 6]);
-        const double to = qterm<double>(q, R.tx[rr - 1], R.ty[rr - 1]);
+        const double tn = qterm<double>(q, tx[rr + 6], ty[rr + 6]);
+        const double to = qterm<double>(q, tx[rr - 1], ty[rr - 1]);
         s = s + (tn - to);
         L.ring[q][rr][slot] = div7(s);
       }
@@ -372,7 +445,7 @@ __device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double
 }
 
 template <int BH>
-__global__ void __launch_bounds__(SB_THREADS) k_ss_band(SsimBatch B) {
+__global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(3))) k_ss_band(SsimBatch B) {
   __shared__ BandLds<BH> L;
   const int band = blockIdx.x, c = blockIdx.y, item = blockIdx.z;
   const int H = B.H, W = B.W;
@@ -388,56 +461,52 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_band(SsimBatch B) {
   const int nchunks = (jend + SB_CW - 1) / SB_CW;
   const int cw = W - 6;
 
-  // fill lanes: (q, column) over [lo, hi); chunk 0 fills [0, CW + 3), chunk k
-  // > 0 the new columns [k CW + 3, (k + 1) CW + 3), clipped to W
-  auto fill_cols = [&](int k, int& lo, int& hi) {
-    lo = k == 0 ? 0 : k * SB_CW + 3;
-    hi = min((k + 1) * SB_CW + 3, W);
-  };
-  {
-    int lo, hi;
-    fill_cols(0, lo, hi);
-    const int nc = hi - lo;
-    if (t < 5 * nc) {
-      FillRegs<BH> R;
-      const int q = t / nc, col = lo + t % nc;
-      fill_load<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, q, col, R);
-      fill_store<BH>(c, nr, q, col, R, L);
-    }
-  }
+  // chunk k's fill inputs are loaded three chunks ahead (two register sets),
+  // stored into LDS two chunks ahead (two buffers): each load has a whole
+  // chunk period -- the barrier interval that issued it and the next one --
+  // before its value is needed
+  StageRegs<BH> RA, RB;
+  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, 0, nchunks, RA);
+  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, 1, nchunks, RB);
+  stage_commit<BH>(c, 0, nchunks, RA, L);
+  stage_commit<BH>(c, 1, nchunks, RB, L);
+  __syncthreads();
+  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, 2, nchunks, RA);
+  fill_chunk<BH>(c, nr, 0, W, L);
   __syncthreads();
 
   // chain lanes: (q, row)
   const int cq = t / BH, crow = t % BH;
   const bool chain_lane = t < 5 * BH && crow < nr;
   double s = 0.0;
-  for (int k = 0; k < nchunks; ++k) {
+  // one chunk: cur holds chunk k + 2's loaded inputs (committed here), nxt
+  // receives chunk k + 3's
+  auto step = [&](int k, StageRegs<BH>& cur, StageRegs<BH>& nxt) {
     const int jc = k * SB_CW;
+#ifndef JDS_SSIM_PROBE_NOCHAIN  // tools: timing probes only (wrong values)
     if (chain_lane) {
-      const double* R = L.ring[cq][crow];
+#else
+    if (false) {
+#endif
+      const double* Rg = L.ring[cq][crow];
       double* o = L.st[cq][crow];
       const int nj = min(SB_CW, jend - jc);
       if (k == 0)
-        chain_chunk<0, true>(R, o, s, nj);
+        chain_chunk<0, true>(Rg, o, s, nj);
       else if (jc & SB_CW)
-        chain_chunk<SB_CW, false>(R, o, s, nj);
+        chain_chunk<SB_CW, false>(Rg, o, s, nj);
       else
-        chain_chunk<0, false>(R, o, s, nj);
+        chain_chunk<0, false>(Rg, o, s, nj);
     }
     __syncthreads();
-
-    // next chunk's fill (loads first) beside this chunk's map
-    int lo = 0, hi = 0;
-    if (k + 1 < nchunks) fill_cols(k + 1, lo, hi);
-    const int nc = hi - lo;
-    const bool fl = t < 5 * nc;
-    FillRegs<BH> R;
-    int fq = 0, fcol = 0;
-    if (fl) {
-      fq = t / nc;
-      fcol = lo + t % nc;
-      fill_load<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, fq, fcol, R);
-    }
+    // chunk k + 1's fill (LDS buffer (k + 1) & 1), chunk k's map, chunk k + 2's
+    // inputs into the buffer chunk k's fill has released, chunk k + 3's loads
+#ifndef JDS_SSIM_PROBE_NOFILL
+    if (k + 1 < nchunks) fill_chunk<BH>(c, nr, k + 1, W, L);
+#endif
+#ifdef JDS_SSIM_PROBE_NOMAP
+    if (false)
+#endif
     for (int p = t; p < BH * SB_CW; p += SB_THREADS) {
       const int row = p / SB_CW, jj = p % SB_CW, j = jc + jj;
       if (row < nr && j >= 3 && j < jend) {
@@ -454,104 +523,17 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_band(SsimBatch B) {
         smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = (a1 * a2) / d;
       }
     }
-    if (fl) fill_store<BH>(c, nr, fq, fcol, R, L);
+    stage_commit<BH>(c, k + 2, nchunks, cur, L);
+    stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, k + 3, nchunks, nxt);
     __syncthreads();
+  };
+  for (int k = 0; k < nchunks; k += 2) {
+    step(k, RA, RB);
+    if (k + 1 < nchunks) step(k + 1, RB, RA);
   }
 }
 
 // ---------------------------------------------------------- NumPy means --
-
-// general NumPy pairwise_sum of one buffer (any m <= 8192): the in-order
-// leaves of the recursion, their 8-accumulator sums, then the recursion's
-// combine order (the last, partial buffer only)
-struct SbLeaf {
-  int off, n;
-};
-
-__device__ int sb_leaves(int n, SbLeaf* out) {
-  int so[24], sn[24], sp = 1, cnt = 0;
-  so[0] = 0;
-  sn[0] = n;
-  while (sp > 0) {
-    --sp;
-    const int off = so[sp], m = sn[sp];
-    if (m <= 128) {
-      out[cnt++] = {off, m};
-    } else {
-      int m2 = m / 2;
-      m2 -= m2 % 8;
-      so[sp] = off + m2;
-      sn[sp] = m - m2;
-      ++sp;
-      so[sp] = off;
-      sn[sp] = m2;
-      ++sp;
-    }
-  }
-  return cnt;
-}
-
-__device__ double sb_leaf_sum(const double* v, int off, int n) {
-  if (n < 8) {
-    double r = 0.0;
-    for (int i = 0; i < n; ++i) r = r + v[off + i];
-    return r;
-  }
-  double r[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) r[k] = v[off + k];
-  int i = 8;
-  for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r[k] = r[k] + v[off + i + k];
-  }
-  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; ++i) res = res + v[off + i];
-  return res;
-}
-
-__device__ double sb_combine(int n, const double* ls) {
-  int fn[24], fph[24];
-  double fl[24];
-  int sp = 1, li = 0;
-  double res = 0.0;
-  bool ret = false;
-  fn[0] = n;
-  fph[0] = 0;
-  while (sp > 0) {
-    const int t = sp - 1;
-    if (ret) {
-      ret = false;
-      if (fph[t] == 1) {
-        fl[t] = res;
-        fph[t] = 2;
-        int m2 = fn[t] / 2;
-        m2 -= m2 % 8;
-        fn[sp] = fn[t] - m2;
-        fph[sp] = 0;
-        ++sp;
-      } else {
-        res = fl[t] + res;
-        --sp;
-        ret = true;
-      }
-      continue;
-    }
-    if (fn[t] <= 128) {
-      res = ls[li++];
-      --sp;
-      ret = true;
-      continue;
-    }
-    int m2 = fn[t] / 2;
-    m2 -= m2 % 8;
-    fph[t] = 1;
-    fn[sp] = m2;
-    fph[sp] = 0;
-    ++sp;
-  }
-  return res;
-}
 
 // LDS image of one buffer: element e at e + 8 * (e >> 7) (8-double pad per
 // leaf: the per-leaf 16-B reads of a wave land on distinct banks)
@@ -563,9 +545,7 @@ __device__ __forceinline__ int sb_pad(int e) { return e + 8 * (e >> 7); }
 __global__ void __launch_bounds__(SB_THREADS) k_ss_chunks(SsimBatch B) {
   __shared__ double v[SB_NP_BUF + 8 * (SB_NP_BUF / 128)];
   __shared__ double wsum[4];
-  __shared__ SbLeaf leaf[SB_NP_BUF / 64 + 2];
-  __shared__ double lsum[SB_NP_BUF / 64 + 2];
-  __shared__ int nleaf;
+  __shared__ double lsum[2 * PW_MAXN];
   const int ch = blockIdx.y, item = blockIdx.z, t = threadIdx.x;
   const long long n = ch < 4 ? B.ns : (long long)B.H * B.W;
   const long long c0 = (long long)blockIdx.x * SB_NP_BUF;
@@ -630,28 +610,32 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_chunks(SsimBatch B) {
     __syncthreads();
     if (t == 0) *out = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
   } else {
-    if (t == 0) nleaf = sb_leaves(m, leaf);
-    __syncthreads();
-    // the leaf sums read the unpadded order: copy-free via sb_pad in the getter
-    for (int l = t; l < nleaf; l += SB_THREADS) {
-      const SbLeaf lr = leaf[l];
+    // the partial buffer: host-built tree (pw_tree), leaves in parallel, then
+    // one height of internal nodes per barrier interval
+    const PwTree& T = ch < 4 ? B.tree_s : B.tree_y;
+    for (int l = t; l < T.nl; l += SB_THREADS) {
+      const int off = T.off[l], ln = T.n[l];
       double acc;
-      if (lr.n < 8) {
+      if (ln < 8) {
         acc = 0.0;
-        for (int i = 0; i < lr.n; ++i) acc = acc + v[sb_pad(lr.off + i)];
+        for (int i = 0; i < ln; ++i) acc = acc + v[sb_pad(off + i)];
       } else {
-        double r[8];
-        for (int k = 0; k < 8; ++k) r[k] = v[sb_pad(lr.off + k)];
+        double r8[8];
+        for (int k = 0; k < 8; ++k) r8[k] = v[sb_pad(off + k)];
         int i = 8;
-        for (; i < lr.n - (lr.n % 8); i += 8)
-          for (int k = 0; k < 8; ++k) r[k] = r[k] + v[sb_pad(lr.off + i + k)];
-        acc = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-        for (; i < lr.n; ++i) acc = acc + v[sb_pad(lr.off + i)];
+        for (; i < ln - (ln % 8); i += 8)
+          for (int k = 0; k < 8; ++k) r8[k] = r8[k] + v[sb_pad(off + i + k)];
+        acc = ((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7]));
+        for (; i < ln; ++i) acc = acc + v[sb_pad(off + i)];
       }
       lsum[l] = acc;
     }
     __syncthreads();
-    if (t == 0) *out = sb_combine(m, lsum);
+    for (int h = 0; h < T.nh; ++h) {
+      for (int i = T.hs[h] + t; i < T.hs[h + 1]; i += SB_THREADS) lsum[T.nl + i] = lsum[T.l[i]] + lsum[T.r[i]];
+      __syncthreads();
+    }
+    if (t == 0) *out = lsum[T.ni ? T.nl + T.ni - 1 : 0];
   }
 }
 
@@ -688,6 +672,60 @@ constexpr int SB_BH = JDS_SSIM_BH;  // band height (rows per workgroup; 8 or 16)
 int ssim_bands(int H) { return (H - 6 + SB_BH - 1) / SB_BH; }
 
 // scratch doubles per item for H x W (H, W >= 7)
+// NumPy pairwise_sum (numpy/core/src/umath/loops_utils.h.src): n <= 128 is a
+// leaf (8 accumulators); above, n2 = n / 2 rounded down to a multiple of 8 and
+// pw(n2) + pw(n - n2).  The tree of a partial buffer of m elements.
+static void pw_tree(int m, PwTree* T) {
+  memset(T, 0, sizeof *T);
+  if (m <= 0) return;
+  struct Node {
+    int l, r, h;  // children as signed ids: >= 0 leaf index, < 0 -(internal index + 1)
+  };
+  Node nodes[PW_MAXN];
+  int nl = 0, ni = 0;
+  struct Rec {
+    static int build(int off, int n, PwTree* T, Node* nodes, int& nl, int& ni, int& h) {
+      if (n <= 128) {
+        T->off[nl] = (uint16_t)off;
+        T->n[nl] = (uint16_t)n;
+        h = 0;
+        return nl++;
+      }
+      int n2 = n / 2;
+      n2 -= n2 % 8;
+      int ha, hb;
+      const int a = build(off, n2, T, nodes, nl, ni, ha);
+      const int b = build(off + n2, n - n2, T, nodes, nl, ni, hb);
+      nodes[ni] = {a, b, (ha > hb ? ha : hb) + 1};
+      h = nodes[ni].h;
+      return -(ni++) - 1;
+    }
+  };
+  int h;
+  Rec::build(0, m, T, nodes, nl, ni, h);
+  // internal nodes by height (a child's height is below its parent's)
+  int order[PW_MAXN], rank[PW_MAXN], k = 0, nh = 0;
+  for (int hh = 1; hh <= 16; ++hh) {
+    T->hs[hh - 1] = (uint8_t)k;
+    for (int i = 0; i < ni; ++i)
+      if (nodes[i].h == hh) order[k++] = i;
+    if (k == ni) {
+      nh = hh;
+      T->hs[hh] = (uint8_t)k;
+      break;
+    }
+  }
+  for (int i = 0; i < ni; ++i) rank[order[i]] = i;
+  auto id = [&](int c) { return c >= 0 ? c : nl + rank[-c - 1]; };
+  for (int i = 0; i < ni; ++i) {
+    T->l[i] = (uint8_t)id(nodes[order[i]].l);
+    T->r[i] = (uint8_t)id(nodes[order[i]].r);
+  }
+  T->nl = (uint8_t)nl;
+  T->ni = (uint8_t)ni;
+  T->nh = (uint8_t)nh;
+}
+
 static long long ns_pitch_of(int H, int W) { return (((long long)(H - 6) * (W - 6)) + 63) & ~63LL; }
 static long long n_pitch_of(int H, int W) { return ((long long)H * W + 63) & ~63LL; }
 
@@ -716,6 +754,8 @@ hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const*
   B.ns = (long long)(H - 6) * (W - 6);
   B.ns_pitch = ns_pitch_of(H, W);
   B.n_pitch = n_pitch_of(H, W);
+  pw_tree((int)(B.ns % SB_NP_BUF), &B.tree_s);
+  pw_tree((int)(((long long)H * W) % SB_NP_BUF), &B.tree_y);
   const long long n = (long long)H * W;
   B.nch_s = (int)((B.ns + SB_NP_BUF - 1) / SB_NP_BUF);
   B.nch_y = (int)((n + SB_NP_BUF - 1) / SB_NP_BUF);
