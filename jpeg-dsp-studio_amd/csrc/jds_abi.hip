@@ -1215,7 +1215,8 @@ static int ent_prepare(const Geo& g, int mode, int n, const double* qt, DevBuf* 
   free(h);
   HIP_TRY(e);
   if (!tab.p) {
-    char t[4096];
+    alignas(16) static thread_local char t[16384];
+    if (ent_tab_size() > sizeof t) return fail(JDS_EINVAL, "entropy tables exceed the staging buffer");
     ent_build_tables((EntTab*)t);
     HIP_TRY(tab.ensure(ent_tab_size()));
     HIP_TRY(hipMemcpy(tab.p, t, ent_tab_size(), hipMemcpyHostToDevice));

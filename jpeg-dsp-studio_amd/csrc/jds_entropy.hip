@@ -79,6 +79,18 @@ struct EntTab {
   uint8_t zz[64];
 };
 
+// left-aligned symbols: code << (32 - len) | len (len <= 16 sits below the code)
+struct EsTab {
+  uint32_t ac[2][16 * 32];  // (run & 15, size) -> AC symbol, size clamped to 10 (code_ac's clamp); 0 for size 0
+  uint32_t dc[2][16];
+  uint32_t zrl[2], eob[2];
+};
+
+__host__ __device__ __forceinline__ uint32_t es_left(uint32_t e) {  // (len << 16 | code) -> left-aligned | len
+  const uint32_t len = e >> 16;
+  return len ? (((e & 0xFFFFu) << (32u - len)) | len) : 0u;
+}
+
 // T.81 Annex C: code lengths and codes in order of increasing length
 static void huff_codes(const uint8_t* bits, const uint8_t* vals, uint32_t* out, int nsym) {
   for (int i = 0; i < nsym; ++i) out[i] = 0;
@@ -97,9 +109,20 @@ void ent_build_tables(EntTab* t) {
   huff_codes(K5_BITS, K5_VALS, t->ac[0], 256);
   huff_codes(K6_BITS, K6_VALS, t->ac[1], 256);
   memcpy(t->zz, ZZ, 64);
+  // the single-pass coder's left-aligned symbols follow the table (ent_tab_size)
+  EsTab* es = reinterpret_cast<EsTab*>(t + 1);
+  for (int c = 0; c < 2; ++c) {
+    for (int i = 0; i < 16 * 32; ++i) {
+      const int run = i >> 5, sz = i & 31;
+      es->ac[c][i] = sz ? es_left(t->ac[c][(run << 4) | (sz > 10 ? 10 : sz)]) : 0u;
+    }
+    for (int i = 0; i < 16; ++i) es->dc[c][i] = es_left(t->dc[c][i]);
+    es->zrl[c] = es_left(t->ac[c][0xF0]);
+    es->eob[c] = es_left(t->ac[c][0x00]);
+  }
 }
 
-size_t ent_tab_size() { return sizeof(EntTab); }
+size_t ent_tab_size() { return sizeof(EntTab) + sizeof(EsTab); }
 
 // JFIF header template (oracle/jpeg_entropy.py::jfif_headers): returns its length
 // (ENT_HDR bytes) or -1 if the table is not baseline (integers in [1, 255]).
@@ -138,6 +161,7 @@ int ent_header(const double* q, int mode, int H, int W, uint8_t* o) {
 struct EntGeo {
   int nb;          // blocks per frame (Y + Cb + Cr)
   int first[4];    // first block of each scan within the frame, first[3] = nb
+  int sfirst[4];   // single-pass coder: first 64-block segment of each scan within the frame, sfirst[3] = per frame
   int cap_w[3];    // packed-scan capacity in 32-bit words (worst case 1660 bits per block)
   long long raw_w; // packed words per frame
   int chunks;      // 1 KiB chunks per scan (worst-case Y scan)
@@ -587,6 +611,492 @@ __global__ void __launch_bounds__(256) k_ent_pack2(const EntGeo e, long long nbl
   }
 }
 
+// ------------------------------------------------ single pass (round 4) --
+//
+// k_ent_seg replaces k_ent_bits, the block scan, k_ent_info, k_ent_zero and
+// k_ent_pack (JDS_ENT_FUSED): one wave per segment of 64 consecutive blocks of
+// one scan, segments in launch order.
+//  * walk: each lane packs its block MSB-first into lane-private staging
+//    words (LDS, word-major across the wave's lanes so every store hits its
+//    own bank; words past ES_SW spill to a per-block global area), so the
+//    block's bit count comes out of the same walk that packs it.  Appending a
+//    symbol is two funnel shifts (v_alignbit) on a 32-bit pending word.
+//  * offset: a wave-wide prefix of the lanes' bit counts, then a decoupled
+//    look-back over the scan's earlier segments (each publishes its
+//    aggregate, then its inclusive prefix; the single-pass scan of Merrill and
+//    Garland), 64 descriptors per probe.
+//  * placement: each lane writes its words shifted into place.  Words it
+//    alone covers: plain stores.  A word shared by several lanes is written
+//    once, by the lane holding its first bit, with the others' bits gathered
+//    by a segmented OR across the wave.  The segment's first word, when the
+//    previous segment holds its first bit, goes to headw[g]; k_ent_fix ORs it
+//    in afterwards (no zeroed memory, no global atomics on the stream).
+//  * the 0xFF bytes of every word the segment finalises are counted here
+//    (k_ent_fix counts the shared words), and each scan's last byte is padded
+//    with 1-bits (T.81 F.1.2.3), so the stuffing pass reads final words.
+// A segment that is not the last of its scan holds >= 256 bits (every block
+// costs >= 4), so only consecutive segments share a word.
+#ifndef JDS_ENT_FUSED
+#define JDS_ENT_FUSED 1
+#endif
+#ifndef JDS_ENT_WPE
+#define JDS_ENT_WPE 4  // waves per SIMD the walk's registers are held to (the scheduler hoists lookups freely)
+#endif
+#ifndef JDS_ENT_SCHED
+#define JDS_ENT_SCHED 0  // zigzag positions between scheduling barriers in the fast walk (0: none)
+#endif
+#ifndef ES_LB
+#define ES_LB 8  // look-back descriptors per lane and probe
+#endif
+constexpr int ES_SW = 32;                // LDS staging words per lane (1024 bits)
+constexpr int ES_MAXW = 53;              // words per block at most (1660 bits + the partial word): the spill area
+constexpr int ES_WAVES = 4;
+constexpr unsigned long long ES_FA = 1ull << 62, ES_FP = 2ull << 62, ES_VAL = ES_FA - 1ull;
+
+// Append the L (<= 32) bits of symL (left-aligned; bits below the symbol are
+// ignored) to the pending word acc (n bits, right-aligned; bits above n are
+// ignored).  Two sinks for the completed words:
+//  * EsFast: the lane's LDS staging, branch-free: the pending word is stored
+//    into slot k at every symbol and k advances when it completes, so a
+//    slot's last store is its finished word; k is clamped to the last slot
+//    (a block needing more than ES_SW words is redone by EsSafe);
+//  * EsSafe: every word to the block's global spill area.
+struct EsFast {
+  uint32_t* st;     // this lane's slot 0 (slots 64 words apart)
+  uint32_t ka = 0;  // slot k * 64
+  __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
+    const int t = n + L;
+    st[ka] = __builtin_amdgcn_alignbit(acc, symL, (uint32_t)n);  // the top 32 bits of acc . sym
+    const uint32_t nx = ka + ((uint32_t)(t & 32) << 1);
+    ka = nx < (uint32_t)((ES_SW - 1) * 64) ? nx : (uint32_t)((ES_SW - 1) * 64);
+    // (acc << L) | sym, also for L = 0 (a 64-bit shift by 32 - L: no select)
+    acc = (uint32_t)(((((uint64_t)acc) << 32) | symL) >> (32 - L));
+    n = t & 31;
+  }
+  __device__ __forceinline__ void store(uint32_t w) { st[ka] = w; }
+};
+struct EsSafe {
+  uint32_t* ov;
+  int k = 0;
+  __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
+    const int t = n + L;
+    if (t >= 32) ov[k++] = __builtin_amdgcn_alignbit(acc, symL, (uint32_t)n);
+    acc = L ? __builtin_amdgcn_alignbit(acc, symL, (uint32_t)(32 - L)) : acc;
+    n = t & 31;
+  }
+  __device__ __forceinline__ void store(uint32_t w) { ov[k] = w; }
+};
+
+// EsStage (JDS_ENT_WALK = 1): the LDS staging with a branch per completed
+// word (slots >= ES_SW to the global spill area) and ZRL codes inline: one
+// walk, no redo.
+struct EsStage {
+  uint32_t* st;
+  uint32_t* ov;
+  int k = 0;
+  __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
+    const int t = n + L;
+    if (t >= 32) {
+      const uint32_t w = __builtin_amdgcn_alignbit(acc, symL, (uint32_t)n);
+      if (k < ES_SW) st[k * 64] = w; else ov[k] = w;
+      ++k;
+    }
+    acc = L ? __builtin_amdgcn_alignbit(acc, symL, (uint32_t)(32 - L)) : acc;
+    n = t & 31;
+  }
+  __device__ __forceinline__ void store(uint32_t w) {
+    if (k < ES_SW) st[k * 64] = w; else ov[k] = w;
+  }
+};
+#ifndef JDS_ENT_WALK
+#define JDS_ENT_WALK 1  // 0: EsFast + EsSafe redo; 1: EsStage
+#endif
+
+// The AC walk.  SAFE = false: no ZRL codes -- zr records the longest zero run
+// before a nonzero, and a lane with zr >= 16 is redone with SAFE = true.
+template <int K, bool SAFE, class S>
+__device__ __forceinline__ void es_ac(const BlockRegs& r, int& last, int& aor, int& zr, const uint32_t* ac,
+                                      uint32_t zrl, uint32_t& acc, int& n, uint32_t& nb, S& o) {
+  if constexpr (K < 64) {
+    // bound how far the scheduler hoists the table lookups (registers)
+    if constexpr (!SAFE && JDS_ENT_SCHED > 0 && K % JDS_ENT_SCHED == 0) __builtin_amdgcn_sched_barrier(0);
+    const int v = coef_at<ZZC[K]>(r);
+    const int a = v < 0 ? -v : v;
+    aor |= a;
+    int sz = a ? 32 - __clz(a) : 0;
+    sz = sz > 10 ? 10 : sz;
+    const int run = K - 1 - last;
+    if constexpr (SAFE) {
+      if (a && run >= 16) {  // one ZRL code per 16 zeros first
+        const int zl = (int)(zrl & 31u);
+        for (int i = 0; i < (run >> 4); ++i) {
+          o.put(zrl, zl, acc, n);
+          nb += (uint32_t)zl;
+        }
+      }
+    } else {
+      const int nz = a < 1 ? a : 1;  // (a != 0) without a lane mask
+      const int rz = run * nz;
+      zr = rz > zr ? rz : zr;
+    }
+    const uint32_t e = ac[((run & 15) << 5) | sz];
+    const int L = (int)(e & 31u) + sz;
+    const uint32_t mag = (uint32_t)(v + (v >> 31)) & ((1u << sz) - 1u);  // v, or v - 1 for v < 0, in sz bits
+    o.put(e | (mag << ((32 - L) & 31)), L, acc, n);
+    nb += (uint32_t)L;
+    if constexpr (SAFE) {
+      last = a ? K : last;
+    } else {
+      const int kk = K * (a < 1 ? a : 1);
+      last = kk > last ? kk : last;
+    }
+    es_ac<K + 1, SAFE>(r, last, aor, zr, ac, zrl, acc, n, nb, o);
+  }
+}
+
+// One block: DC difference, AC walk, EOB, the partial word (left-aligned).
+// Returns the bit count; bd = not baseline-codable, zr as es_ac.
+template <bool SAFE, class S>
+__device__ __forceinline__ uint32_t es_block(const BlockRegs& r, int diff, const EsTab& es, int cls, S& o, bool& bd,
+                                             int& zr) {
+  uint32_t acc = 0u;
+  int n = 0;
+  const int da = diff < 0 ? -diff : diff;
+  int ds = da ? 32 - __clz(da) : 0;
+  bd = ds > 11;
+  ds = ds > 11 ? 11 : ds;
+  const uint32_t ed = es.dc[cls][ds];
+  const int Ld = (int)(ed & 31u) + ds;
+  const uint32_t md = (uint32_t)(diff + (diff >> 31)) & ((1u << ds) - 1u);
+  o.put(ed | (md << ((32 - Ld) & 31)), Ld, acc, n);
+  uint32_t nb = (uint32_t)Ld;
+  int last = 0, aor = 0;
+  zr = 0;
+  es_ac<1, SAFE>(r, last, aor, zr, es.ac[cls], es.zrl[cls], acc, n, nb, o);
+  const uint32_t eb = es.eob[cls];
+  const int Le = last < 63 ? (int)(eb & 31u) : 0;  // EOB unless coefficient 63 is set
+  o.put(eb, Le, acc, n);
+  nb += (uint32_t)Le;
+  bd |= aor > 1023;  // AC size > 10
+  o.store(n ? acc << (32 - n) : 0u);
+  return nb;
+}
+
+struct EsSeg {
+  int f, s, seg, nseg_s, nbs;
+};
+__device__ __forceinline__ EsSeg es_seg(const EntGeo& e, int g) {
+  EsSeg q;
+  q.f = g / e.sfirst[3];
+  const int r = g - q.f * e.sfirst[3];
+  q.s = r < e.sfirst[1] ? 0 : (r < e.sfirst[2] ? 1 : 2);
+  q.seg = r - e.sfirst[q.s];
+  q.nseg_s = e.sfirst[q.s + 1] - e.sfirst[q.s];
+  q.nbs = e.first[q.s + 1] - e.first[q.s];
+  return q;
+}
+
+// the scan's final word: 1-bits from the scan's end to its byte boundary;
+// returns the number of the word's bytes that belong to the scan
+__device__ __forceinline__ int es_pad(uint32_t& v, unsigned long long W1, unsigned long long widx) {
+  const int used = (int)(W1 - 32ull * widx);  // 1..32
+  const int pb = (8 - (used & 7)) & 7;
+  if (pb) v |= ((1u << pb) - 1u) << (32 - used - pb);
+  return (used + 7) >> 3;
+}
+
+__device__ __forceinline__ int es_ff(uint32_t v, int nbytes) {  // 0xFF bytes among the first nbytes (stream order)
+  int c = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) c += (b < nbytes && ((v >> (24 - 8 * b)) & 255u) == 255u) ? 1 : 0;
+  return c;
+}
+
+__global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per_eu(JDS_ENT_WPE))) k_ent_seg(const EntGeo e, const int nseg, const int16_t* __restrict__ coeffs,
+                                                            const EsTab* __restrict__ gt,
+                                                            unsigned long long* __restrict__ desc,
+                                                            uint32_t* __restrict__ ovf, uint32_t* __restrict__ raw,
+                                                            uint32_t* __restrict__ headw,
+                                                            unsigned long long* __restrict__ ffs,
+                                                            unsigned long long* __restrict__ info,
+                                                            unsigned long long* __restrict__ scan_bits,
+                                                            unsigned long long* __restrict__ bad) {
+  __shared__ EsTab es;
+  __shared__ uint32_t stage[ES_WAVES][ES_SW][64];
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(gt);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&es);
+    for (int i = threadIdx.x; i < (int)(sizeof(EsTab) / 4); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // Segments in launch order: a workgroup waits only for segments of lower
+  // index, and each XCD dispatches its workgroups in index order, so the
+  // lowest unfinished segment is always resident (no ticket: one
+  // device-scope counter for every wave serialised the launch).
+  const int g = blockIdx.x * ES_WAVES + wv;
+  if (g >= nseg) return;  // (whole wave; no barrier follows)
+  const EsSeg q = es_seg(e, g);
+  const int bi = q.seg * 64 + lane;  // block within the scan
+  const bool valid = bi < q.nbs;
+  const int nvalid = q.nbs - q.seg * 64 < 64 ? q.nbs - q.seg * 64 : 64;
+  const bool last_seg = q.seg == q.nseg_s - 1;
+  const long long gb = (long long)q.f * e.nb + e.first[q.s] + (valid ? bi : q.nbs - 1);
+  const BlockRegs rg = load_block(coeffs + gb * 64);
+  const int dc = coef_at<0>(rg);
+  int pred = __shfl_up(dc, 1, 64);
+  if (lane == 0) pred = q.seg ? (int)coeffs[(gb - 1) * 64] : 0;
+  const int cls = q.s ? 1 : 0;
+  uint32_t* st = &stage[wv][0][lane];
+  uint32_t* ov = ovf + gb * ES_MAXW;
+  uint32_t nb = 0u;
+  int k = 0, zr = 0;
+  bool bd = false, safe = false;
+  if (JDS_ENT_WALK == 1) {
+    if (valid) {
+      EsStage o{st, ov};
+      nb = es_block<true>(rg, dc - pred, es, cls, o, bd, zr);
+      k = (int)((nb + 31u) >> 5);
+    }
+  } else {
+    if (valid) {
+      EsFast o{st};
+      nb = es_block<false>(rg, dc - pred, es, cls, o, bd, zr);
+      k = (int)((nb + 31u) >> 5);
+      safe = zr >= 16 || k > ES_SW;  // ZRL codes, or more words than the staging holds
+    }
+  }
+  if (JDS_ENT_WALK == 0 && __any(safe)) {  // rare: redo those blocks with ZRL codes, words to the spill area
+    if (safe) {
+      EsSafe o{ov};
+      nb = es_block<true>(rg, dc - pred, es, cls, o, bd, zr);
+      k = (int)((nb + 31u) >> 5);
+    }
+  }
+  if (bd) bad[q.f] = 1ull;  // not baseline-codable: the frame is reported
+
+  // ---- offset: the wave's prefix, then the look-back over the scan's segments
+  uint32_t inc = nb;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  const uint32_t excl = inc - nb;
+  const unsigned long long A = __shfl(inc, 63, 64);
+  unsigned long long pre = 0ull;
+#ifdef JDS_ENT_PROBE_NOLB  // timing probe (wrong output): no look-back
+  if (true) {
+    if (lane == 0) __hip_atomic_store(&desc[g], ES_FP | A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else
+#endif
+  if (q.seg == 0) {
+    if (lane == 0) __hip_atomic_store(&desc[g], ES_FP | A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (lane == 0) __hip_atomic_store(&desc[g], ES_FA | A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int lo = g - q.seg;  // the scan's first segment (publishes its prefix at once)
+    // each probe reads ES_LB descriptors per lane: segments base - ES_LB * lane - r, r = 0 .. ES_LB - 1,
+    // i.e. 64 * ES_LB predecessors per round trip
+    int base = g - 1, spins = 0;
+    while (true) {
+      int rp = ES_LB;        // the lane's first inclusive prefix (index r), ES_LB if none
+      bool zb = false;       // a not-yet-published descriptor before it
+      unsigned long long v = 0ull;
+#pragma unroll
+      for (int r = 0; r < ES_LB; ++r) {
+        const int j = base - ES_LB * lane - r;
+        const unsigned long long d =
+            j >= lo ? __hip_atomic_load(&desc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ES_FP;
+        const unsigned long long fl = d >> 62;
+        if (rp == ES_LB) {
+          zb |= fl == 0ull;
+          v += d & ES_VAL;
+          if (fl == 2ull) rp = r;
+        }
+      }
+      const unsigned long long pm = __ballot(rp < ES_LB);
+      const int p = pm ? (int)__builtin_ctzll(pm) : 64;
+      const unsigned long long upto = p >= 63 ? ~0ull : ((2ull << p) - 1ull);
+      if (__ballot(zb) & upto) {  // a predecessor has not published yet
+        if (++spins > (1 << 22)) {  // never expected: give up rather than hang (the frame reports failure)
+          bad[q.f] = 1ull;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
+      v = lane <= p ? v : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      pre += v;
+      if (p < 64) break;
+      base -= 64 * ES_LB;
+    }
+    if (lane == 0) __hip_atomic_store(&desc[g], ES_FP | (pre + A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const unsigned long long W1 = pre + A;
+
+  // ---- placement
+  auto stw = [&](int j) -> uint32_t { return j >= k ? 0u : ((safe || j >= ES_SW) ? ov[j] : st[j * 64]); };
+  const unsigned long long o = pre + excl;  // the lane's first bit in the scan
+  const int sh = (int)(o & 31ull);
+  const unsigned long long hw = o >> 5, tw = (o + nb - 1ull) >> 5;
+  const bool single = hw == tw;
+  const uint32_t s0 = stw(0);
+  const uint32_t hv = s0 >> sh;
+  // the next lane starts inside this lane's tail word
+  const bool c = valid && ((o + nb) & 31ull) != 0ull && lane + 1 < nvalid;
+  // X = this lane's head word bits | those of the following lanes that share it
+  uint32_t X = valid ? hv : 0u;
+  int F = (valid && single && c) ? 1 : 0;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t Xn = __shfl_down(X, d, 64);
+    const int Fn = __shfl_down(F, d, 64);
+    if (F && lane + d < 64) {
+      X |= Xn;
+      F = Fn;
+    }
+  }
+  const uint32_t X1 = __shfl_down(X, 1, 64);
+  const uint32_t in_tail = c ? X1 : 0u;
+  uint32_t* rs = raw + raw_base(e, q.f, q.s);
+  const unsigned long long wlast = (W1 - 1ull) >> 5;
+  const bool open_end = !last_seg && (W1 & 31ull);
+  int ffc = 0;
+  auto put_word = [&](unsigned long long widx, uint32_t v) {
+    int nb4 = 4;
+    if (last_seg && widx == wlast) nb4 = es_pad(v, W1, widx);
+    rs[widx] = __builtin_bswap32(v);  // byte 0 of the stream first
+    if (!(open_end && widx == wlast)) ffc += es_ff(v, nb4);
+  };
+  if (valid) {
+    const bool own_head = sh == 0;
+    const int nout = (int)(tw - hw);
+    if (own_head && !single) put_word(hw, hv);
+    uint32_t prev = s0;
+    for (int j = 1; j < nout; ++j) {
+      const uint32_t cur = stw(j);
+      put_word(hw + j, __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh));
+      prev = cur;
+    }
+    const uint32_t tv = single ? hv : __builtin_amdgcn_alignbit(prev, stw(nout), (uint32_t)sh);
+    if (!single || own_head) put_word(tw, tv | in_tail);
+    if (lane == 0 && !own_head) headw[g] = X;  // the previous segment holds this word's first bit
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) ffc += __shfl_xor(ffc, d, 64);
+  if (lane == 0) {
+    ffs[g] = (unsigned long long)ffc;
+    if (last_seg) {
+      info[2 * (q.f * 3 + q.s)] = 0ull;
+      info[2 * (q.f * 3 + q.s) + 1] = W1;
+      if (scan_bits) scan_bits[q.f * 3 + q.s] = W1;
+    }
+  }
+}
+
+// the first word of segment g when segment g - 1 holds its first bit: OR in
+// g's bits, pad if it is its scan's final word, count its 0xFF bytes for g - 1
+__global__ void k_ent_fix(const EntGeo e, const int nseg, const unsigned long long* __restrict__ desc,
+                          const uint32_t* __restrict__ headw, uint32_t* __restrict__ raw,
+                          unsigned long long* __restrict__ ffs) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nseg) return;
+  const EsSeg q = es_seg(e, g);
+  if (q.seg == 0) return;
+  const unsigned long long W0 = desc[g - 1] & ES_VAL, W1 = desc[g] & ES_VAL;
+  if (!(W0 & 31ull)) return;
+  const unsigned long long w = W0 >> 5;
+  uint32_t* rs = raw + raw_base(e, q.f, q.s);
+  uint32_t v = __builtin_bswap32(rs[w]) | headw[g];
+  int nb4 = 4;
+  if (q.seg == q.nseg_s - 1 && ((W1 - 1ull) >> 5) == w) nb4 = es_pad(v, W1, w);
+  rs[w] = __builtin_bswap32(v);
+  ffs[g - 1] += (unsigned long long)es_ff(v, nb4);
+}
+
+// output offset of scan s of frame f (after its SOS marker); ffx = exclusive
+// prefix of the segments' 0xFF counts
+__device__ __forceinline__ long long es_scan_out(const EntGeo& e, int f, int s, const unsigned long long* info,
+                                                 const unsigned long long* ffx) {
+  long long p = e.hdr + ENT_SOS;
+  const long long g0 = (long long)f * e.sfirst[3];
+  for (int j = 0; j < s; ++j) {
+    const unsigned long long nb = (info[2 * (f * 3 + j) + 1] + 7) >> 3;
+    const unsigned long long ff = ffx[g0 + e.sfirst[j + 1]] - ffx[g0 + e.sfirst[j]];
+    p += (long long)(nb + ff) + ENT_SOS;
+  }
+  return p;
+}
+
+// one wave per segment: the bytes of the words it finalised, stuffed (0x00
+// after every 0xFF) at their place in the file
+__global__ void __launch_bounds__(256) k_ent_emit2(const EntGeo e, const int nseg,
+                                                   const unsigned long long* __restrict__ desc,
+                                                   const unsigned long long* __restrict__ info,
+                                                   const uint32_t* __restrict__ raw,
+                                                   const unsigned long long* __restrict__ ffx,
+                                                   uint8_t* __restrict__ out, long long stride) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= nseg) return;
+  const EsSeg q = es_seg(e, g);
+  const unsigned long long W0 = q.seg ? (desc[g - 1] & ES_VAL) : 0ull, W1 = desc[g] & ES_VAL;
+  const unsigned long long nbytes = (info[2 * (q.f * 3 + q.s) + 1] + 7) >> 3;
+  const unsigned long long fw = (W0 + 31) >> 5, lw = (W1 - 1) >> 5;
+  if (fw > lw) return;
+  const unsigned long long b0 = 4 * fw, b1 = (4 * lw + 4 < nbytes) ? 4 * lw + 4 : nbytes;
+  long long o = es_scan_out(e, q.f, q.s, info, ffx) + (long long)b0 +
+                (long long)(ffx[g] - ffx[(long long)q.f * e.sfirst[3] + e.sfirst[q.s]]);
+  uint8_t* dst = out + (long long)q.f * stride;
+  const uint32_t* w = raw + raw_base(e, q.f, q.s);
+  for (unsigned long long i0 = b0; i0 < b1; i0 += 256) {
+    const unsigned long long i = i0 + 4 * lane;
+    uint32_t x = 0u;
+    int nv = 0, ff = 0;
+    if (i < b1) {
+      x = w[i >> 2];  // stream order in memory: byte k of the word is bits 8k..8k+7
+      nv = b1 - i < 4 ? (int)(b1 - i) : 4;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) ff += (kk < nv && ((x >> (8 * kk)) & 255u) == 255u) ? 1 : 0;
+    }
+    const int ex = wave_excl_sum(ff, lane);
+    const int tot = __shfl(ex + ff, 63, 64);
+    long long p = o + (long long)(i - i0) + ex;
+    for (int kk = 0; kk < nv; ++kk) {
+      const uint8_t b = (uint8_t)(x >> (8 * kk));
+      dst[p++] = b;
+      if (b == 0xFF) dst[p++] = 0x00;
+    }
+    o += (long long)((b1 - i0 < 256 ? b1 - i0 : 256)) + tot;
+  }
+}
+
+__global__ void k_ent_frame2(const EntGeo e, const uint8_t* __restrict__ hdr, const unsigned long long* __restrict__ info,
+                             const unsigned long long* __restrict__ ffx, uint8_t* __restrict__ out, long long stride,
+                             unsigned long long* __restrict__ lengths, const unsigned long long* __restrict__ bad) {
+  const int f = blockIdx.x;
+  uint8_t* dst = out + (long long)f * stride;
+  for (int i = threadIdx.x; i < e.hdr; i += blockDim.x) dst[i] = hdr[(long long)f * e.hdr + i];
+  if (threadIdx.x < 3) {
+    const int s = threadIdx.x;
+    uint8_t* m = dst + es_scan_out(e, f, s, info, ffx) - ENT_SOS;
+    const uint8_t sos[ENT_SOS] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(s + 1), (uint8_t)(s == 0 ? 0x00 : 0x11),
+                                  0x00, 0x3F, 0x00};
+    for (int i = 0; i < ENT_SOS; ++i) m[i] = sos[i];
+  }
+  if (threadIdx.x == 0) {
+    const long long g0 = (long long)f * e.sfirst[3];
+    const unsigned long long nb = (info[2 * (f * 3 + 2) + 1] + 7) >> 3;
+    const unsigned long long ff = ffx[g0 + e.sfirst[3]] - ffx[g0 + e.sfirst[2]];
+    const long long end = es_scan_out(e, f, 2, info, ffx) + (long long)(nb + ff);
+    dst[end] = 0xFF;
+    dst[end + 1] = 0xD9;
+    if (lengths) lengths[f] = bad[f] ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
+  }
+}
+
 constexpr int ENT_CH = 1024;  // bytes per stuffing chunk (256 threads x 4)
 
 // byte i of scan (f, s) with the 1-bit pad applied (T.81 F.1.2.3)
@@ -715,6 +1225,8 @@ EntGeo ent_geo(const Geo& g) {
   e.first[1] = ny;
   e.first[2] = ny + nc;
   e.first[3] = e.nb;
+  e.sfirst[0] = 0;
+  for (int s = 0; s < 3; ++s) e.sfirst[s + 1] = e.sfirst[s] + (e.first[s + 1] - e.first[s] + 63) / 64;
   e.cap_w[0] = (int)(((long long)ny * 1660 + 31) / 32) + 2;
   e.cap_w[1] = e.cap_w[2] = (int)(((long long)nc * 1660 + 31) / 32) + 2;
   e.raw_w = (long long)e.cap_w[0] + 2LL * e.cap_w[1];
@@ -729,18 +1241,33 @@ long long ent_capacity(const Geo& g) {
   return e.hdr + 3 * ENT_SOS + 2 * 4 * e.raw_w + 2;
 }
 
-// scratch sizes (bytes): [0] bits, [1] excl, [2] info, [3] raw, [4] ffc, [5] ffx, [6] hdr, [7] cub temp
+// scratch sizes (bytes).  Multi-pass coder: [0] bits, [1] excl, [2] info, [3] raw,
+// [4] ffc, [5] ffx, [6] hdr, [7] cub temp.  Single pass (JDS_ENT_FUSED): [0]
+// segment descriptors (from the second word) + head words, [1] spill words, [2] info, [3]
+// raw, [4] 0xFF counts per segment, [5] their prefix, [6] hdr, [7] cub temp.
 void ent_sizes(const Geo& g, int n, size_t* sz) {
   const EntGeo e = ent_geo(g);
   const long long nblk = (long long)n * e.nb;
+  sz[2] = sizeof(unsigned long long) * 7 * n;  // 6 per frame (scan start / bits) + the frame's error flag
+  sz[3] = sizeof(uint32_t) * e.raw_w * n;
+  sz[6] = (size_t)e.hdr * n;
+  if (JDS_ENT_FUSED) {
+    const long long nseg = (long long)n * e.sfirst[3];
+    sz[0] = sizeof(unsigned long long) * (nseg + 2) + sizeof(uint32_t) * (nseg + 1);
+    sz[1] = sizeof(uint32_t) * ES_MAXW * nblk;
+    sz[4] = sizeof(unsigned long long) * (nseg + 1);
+    sz[5] = sizeof(unsigned long long) * (nseg + 1);
+    size_t t1 = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                           (int)(nseg + 1));
+    sz[7] = t1 + 256;
+    return;
+  }
   const long long nch = (long long)n * 3 * e.chunks;
   sz[0] = sizeof(unsigned long long) * (nblk + 1);
   sz[1] = sizeof(unsigned long long) * (nblk + 1);
-  sz[2] = sizeof(unsigned long long) * 7 * n;  // 6 per frame (scan start / bits) + the frame's error flag
-  sz[3] = sizeof(uint32_t) * e.raw_w * n;
   sz[4] = sizeof(unsigned long long) * (nch + 1);
   sz[5] = sizeof(unsigned long long) * (nch + 1);
-  sz[6] = (size_t)e.hdr * n;
   size_t t1 = 0, t2 = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                          (int)(nblk + 1));
@@ -749,9 +1276,47 @@ void ent_sizes(const Geo& g, int n, size_t* sz) {
   sz[7] = (t1 > t2 ? t1 : t2) + 256;
 }
 
+// single pass: segments, fix-up of the shared words, stuffing
+static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeffs, void* const* buf,
+                                       const uint8_t* hdr_dev, const void* tab_dev, uint8_t* out, long long stride,
+                                       unsigned long long* lengths, unsigned long long* scan_bits, hipStream_t s) {
+  const EntGeo e = ent_geo(g);
+  const long long nseg_l = (long long)n * e.sfirst[3];
+  if (nseg_l >= (1ll << 31)) return hipErrorInvalidValue;
+  const int nseg = (int)nseg_l;
+  auto* desc = (unsigned long long*)buf[0] + 1;
+  auto* headw = (uint32_t*)(desc + nseg + 1);
+  auto* ovf = (uint32_t*)buf[1];
+  auto* info = (unsigned long long*)buf[2];
+  auto* raw = (uint32_t*)buf[3];
+  auto* ffs = (unsigned long long*)buf[4];
+  auto* ffx = (unsigned long long*)buf[5];
+  void* temp = buf[7];
+  size_t sz[8];
+  ent_sizes(g, n, sz);
+  unsigned long long* bad = info + 6 * n;
+  hipError_t err;
+  // every descriptor's flag starts at zero; ffs[nseg] closes the scan
+  if ((err = hipMemsetAsync(buf[0], 0, sizeof(unsigned long long) * (nseg + 1), s)) != hipSuccess) return err;
+  if ((err = hipMemsetAsync(ffs + nseg, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
+  if ((err = hipMemsetAsync(bad, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) return err;
+  const unsigned wg = (unsigned)((nseg + ES_WAVES - 1) / ES_WAVES);
+  const EsTab* est = reinterpret_cast<const EsTab*>((const char*)tab_dev + sizeof(EntTab));
+  hipLaunchKernelGGL(k_ent_seg, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, desc, ovf, raw, headw, ffs, info, scan_bits, bad);
+  if ((err = hipGetLastError()) != hipSuccess) return err;
+  hipLaunchKernelGGL(k_ent_fix, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, headw, raw, ffs);
+  size_t tb = sz[7];
+  if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, ffs, ffx, nseg + 1, s)) != hipSuccess) return err;
+  hipLaunchKernelGGL(k_ent_emit2, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, ffx, out, stride);
+  hipLaunchKernelGGL(k_ent_frame2, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, bad);
+  return hipGetLastError();
+}
+
 hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* const* buf, const uint8_t* hdr_dev,
                           const void* tab_dev, uint8_t* out, long long stride, unsigned long long* lengths,
                           unsigned long long* scan_bits, hipStream_t s) {
+  if (JDS_ENT_FUSED)
+    return launch_entropy_fused(g, n, coeffs, buf, hdr_dev, tab_dev, out, stride, lengths, scan_bits, s);
   const EntGeo e = ent_geo(g);
   const long long nblk = (long long)n * e.nb;
   const long long nch = (long long)n * 3 * e.chunks;

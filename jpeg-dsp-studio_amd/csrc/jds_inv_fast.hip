@@ -298,6 +298,15 @@ __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, ui
 #ifndef JDS_INV_MIX_PLANES
 #define JDS_INV_MIX_PLANES 1
 #endif
+// loop unrolling of the chroma plane loop (4:2:0 / 4:4:0) and the luma
+// rounds: 1 keeps the loops (the software-prefetched column is copied per
+// iteration), 2 unrolls them (A/B knobs)
+#ifndef JDS_INV_UNROLL_C
+#define JDS_INV_UNROLL_C 1
+#endif
+#ifndef JDS_INV_UNROLL_Y
+#define JDS_INV_UNROLL_Y 1
+#endif
 #ifndef JDS_INV_ONE_BARRIER
 #define JDS_INV_ONE_BARRIER 0  // every thread deciding without the second barrier measured slower (312 vs 309 us)
 #endif
@@ -484,7 +493,7 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     if (tid == 0) s_qmax = fq[frame].qmax;  // (used by this thread after the next barrier)
 #endif
     if (ctask) {
-#pragma unroll 1
+#pragma unroll JDS_INV_UNROLL_C
       for (int p = 0; p < 2; ++p) {
         const Col16 cur = cq;
         if (p == 0) cq = load_col(cf + g.off_cr, cboff, lv, cvalid);
@@ -501,7 +510,7 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   double ssy = 0.0;
   const uint8_t* in_f = XTRA ? rgb_in + (size_t)(frame / in_div) * g.H * g.W * 3 : nullptr;
   uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
-#pragma unroll 1
+#pragma unroll JDS_INV_UNROLL_Y
   for (int r = 0; r < I::NYB / I::RB; ++r) {
     int by, bx;
     const bool bvalid = luma_blk(r, by, bx);

@@ -3,6 +3,7 @@
 set -e
 cd "$(dirname "$0")/.."
 rm -f tools/bin/ab/*.so tools/bin/ab/*.o
-for v in NOCHAIN NOFILL NOMAP; do
-  python3 tools/build_variant.py ssim_$v "-DJDS_SSIM_PROBE_$v" jds_ssim_band.hip
-done
+python3 tools/build_variant.py A "" jds_entropy.hip
+python3 tools/build_variant.py LB1 "-DES_LB=1" jds_entropy.hip
+python3 tools/build_variant.py LB4 "-DES_LB=4" jds_entropy.hip
+python3 tools/build_variant.py NOLB "-DJDS_ENT_PROBE_NOLB" jds_entropy.hip
