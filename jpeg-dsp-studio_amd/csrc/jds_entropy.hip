@@ -642,11 +642,8 @@ __global__ void __launch_bounds__(256) k_ent_pack2(const EntGeo e, long long nbl
 #ifndef JDS_ENT_WPE
 #define JDS_ENT_WPE 4  // waves per SIMD the walk's registers are held to (the scheduler hoists lookups freely)
 #endif
-#ifndef JDS_ENT_SCHED
-#define JDS_ENT_SCHED 0  // zigzag positions between scheduling barriers in the fast walk (0: none)
-#endif
 #ifndef ES_LB
-#define ES_LB 8  // look-back descriptors per lane and probe
+#define ES_LB 1  // look-back descriptors per lane and probe (4: 0.473, 8: 0.545 vs 1: 0.386 ms per 64 x 1080p; device-coherent loads)
 #endif
 constexpr int ES_SW = 32;                // LDS staging words per lane (1024 bits)
 constexpr int ES_MAXW = 53;              // words per block at most (1660 bits + the partial word): the spill area
@@ -655,41 +652,9 @@ constexpr unsigned long long ES_FA = 1ull << 62, ES_FP = 2ull << 62, ES_VAL = ES
 
 // Append the L (<= 32) bits of symL (left-aligned; bits below the symbol are
 // ignored) to the pending word acc (n bits, right-aligned; bits above n are
-// ignored).  Two sinks for the completed words:
-//  * EsFast: the lane's LDS staging, branch-free: the pending word is stored
-//    into slot k at every symbol and k advances when it completes, so a
-//    slot's last store is its finished word; k is clamped to the last slot
-//    (a block needing more than ES_SW words is redone by EsSafe);
-//  * EsSafe: every word to the block's global spill area.
-struct EsFast {
-  uint32_t* st;     // this lane's slot 0 (slots 64 words apart)
-  uint32_t ka = 0;  // slot k * 64
-  __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
-    const int t = n + L;
-    st[ka] = __builtin_amdgcn_alignbit(acc, symL, (uint32_t)n);  // the top 32 bits of acc . sym
-    const uint32_t nx = ka + ((uint32_t)(t & 32) << 1);
-    ka = nx < (uint32_t)((ES_SW - 1) * 64) ? nx : (uint32_t)((ES_SW - 1) * 64);
-    // (acc << L) | sym, also for L = 0 (a 64-bit shift by 32 - L: no select)
-    acc = (uint32_t)(((((uint64_t)acc) << 32) | symL) >> (32 - L));
-    n = t & 31;
-  }
-  __device__ __forceinline__ void store(uint32_t w) { st[ka] = w; }
-};
-struct EsSafe {
-  uint32_t* ov;
-  int k = 0;
-  __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
-    const int t = n + L;
-    if (t >= 32) ov[k++] = __builtin_amdgcn_alignbit(acc, symL, (uint32_t)n);
-    acc = L ? __builtin_amdgcn_alignbit(acc, symL, (uint32_t)(32 - L)) : acc;
-    n = t & 31;
-  }
-  __device__ __forceinline__ void store(uint32_t w) { ov[k] = w; }
-};
-
-// EsStage (JDS_ENT_WALK = 1): the LDS staging with a branch per completed
-// word (slots >= ES_SW to the global spill area) and ZRL codes inline: one
-// walk, no redo.
+// ignored); a completed word goes to the lane's LDS staging slot k (slots 64
+// words apart, so a wave's stores hit 64 banks), slots >= ES_SW to the
+// block's global spill area.
 struct EsStage {
   uint32_t* st;
   uint32_t* ov;
@@ -697,70 +662,65 @@ struct EsStage {
   __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
     const int t = n + L;
     if (t >= 32) {
-      const uint32_t w = __builtin_amdgcn_alignbit(acc, symL, (uint32_t)n);
+      const uint32_t w = __builtin_amdgcn_alignbit(acc, symL, (uint32_t)n);  // the top 32 bits of acc . sym
       if (k < ES_SW) st[k * 64] = w; else ov[k] = w;
       ++k;
     }
-    acc = L ? __builtin_amdgcn_alignbit(acc, symL, (uint32_t)(32 - L)) : acc;
+    acc = L ? __builtin_amdgcn_alignbit(acc, symL, (uint32_t)(32 - L)) : acc;  // (acc << L) | sym
     n = t & 31;
   }
   __device__ __forceinline__ void store(uint32_t w) {
     if (k < ES_SW) st[k * 64] = w; else ov[k] = w;
   }
 };
-#ifndef JDS_ENT_WALK
-#define JDS_ENT_WALK 1  // 0: EsFast + EsSafe redo; 1: EsStage
-#endif
 
-// The AC walk.  SAFE = false: no ZRL codes -- zr records the longest zero run
-// before a nonzero, and a lane with zr >= 16 is redone with SAFE = true.
-template <int K, bool SAFE, class S>
-__device__ __forceinline__ void es_ac(const BlockRegs& r, int& last, int& aor, int& zr, const uint32_t* ac,
-                                      uint32_t zrl, uint32_t& acc, int& n, uint32_t& nb, S& o) {
+// size category of |v| (clamped to 10, code_ac's clamp)
+__device__ __forceinline__ int es_size(int a) {
+  const int sz = a ? 32 - __clz(a) : 0;
+  return sz > 10 ? 10 : sz;
+}
+
+// The AC walk, software-pipelined: e is position K's table entry, loaded
+// while position K - 1 was appended; position K + 1's lookup (its run needs
+// only whether K is nonzero) is issued before K's symbol is appended.
+template <int K>
+__device__ __forceinline__ void es_ac(const BlockRegs& r, int last, int& aor, const uint32_t* ac, uint32_t zrl,
+                                      uint32_t& acc, int& n, EsStage& o, uint32_t e, int v, int sz, int& lastK) {
   if constexpr (K < 64) {
-    // bound how far the scheduler hoists the table lookups (registers)
-    if constexpr (!SAFE && JDS_ENT_SCHED > 0 && K % JDS_ENT_SCHED == 0) __builtin_amdgcn_sched_barrier(0);
-    const int v = coef_at<ZZC[K]>(r);
     const int a = v < 0 ? -v : v;
     aor |= a;
-    int sz = a ? 32 - __clz(a) : 0;
-    sz = sz > 10 ? 10 : sz;
     const int run = K - 1 - last;
-    if constexpr (SAFE) {
-      if (a && run >= 16) {  // one ZRL code per 16 zeros first
-        const int zl = (int)(zrl & 31u);
-        for (int i = 0; i < (run >> 4); ++i) {
-          o.put(zrl, zl, acc, n);
-          nb += (uint32_t)zl;
-        }
-      }
-    } else {
-      const int nz = a < 1 ? a : 1;  // (a != 0) without a lane mask
-      const int rz = run * nz;
-      zr = rz > zr ? rz : zr;
+    const int nlast = a ? K : last;
+    uint32_t e1 = 0u;
+    int v1 = 0, sz1 = 0;
+    if constexpr (K + 1 < 64) {
+      v1 = coef_at<ZZC[K + 1]>(r);
+      sz1 = es_size(v1 < 0 ? -v1 : v1);
+      e1 = ac[((K - nlast) & 15) << 5 | sz1];
     }
-    const uint32_t e = ac[((run & 15) << 5) | sz];
+    if (a && run >= 16) {  // rare: one ZRL code per 16 zeros first
+      const int zl = (int)(zrl & 31u);
+      for (int i = 0; i < (run >> 4); ++i) o.put(zrl, zl, acc, n);
+    }
     const int L = (int)(e & 31u) + sz;
     const uint32_t mag = (uint32_t)(v + (v >> 31)) & ((1u << sz) - 1u);  // v, or v - 1 for v < 0, in sz bits
     o.put(e | (mag << ((32 - L) & 31)), L, acc, n);
-    nb += (uint32_t)L;
-    if constexpr (SAFE) {
-      last = a ? K : last;
-    } else {
-      const int kk = K * (a < 1 ? a : 1);
-      last = kk > last ? kk : last;
-    }
-    es_ac<K + 1, SAFE>(r, last, aor, zr, ac, zrl, acc, n, nb, o);
+    es_ac<K + 1>(r, nlast, aor, ac, zrl, acc, n, o, e1, v1, sz1, lastK);
+  } else {
+    lastK = last;
   }
 }
 
 // One block: DC difference, AC walk, EOB, the partial word (left-aligned).
-// Returns the bit count; bd = not baseline-codable, zr as es_ac.
-template <bool SAFE, class S>
-__device__ __forceinline__ uint32_t es_block(const BlockRegs& r, int diff, const EsTab& es, int cls, S& o, bool& bd,
-                                             int& zr) {
+// Returns the bit count (32 per completed word + the pending bits); bd = not
+// baseline-codable.
+__device__ __forceinline__ uint32_t es_block(const BlockRegs& r, int diff, const EsTab& es, int cls, EsStage& o,
+                                             bool& bd) {
   uint32_t acc = 0u;
   int n = 0;
+  const int v1 = coef_at<ZZC[1]>(r);
+  const int sz1 = es_size(v1 < 0 ? -v1 : v1);
+  const uint32_t e1 = es.ac[cls][sz1];  // run 0
   const int da = diff < 0 ? -diff : diff;
   int ds = da ? 32 - __clz(da) : 0;
   bd = ds > 11;
@@ -769,15 +729,13 @@ __device__ __forceinline__ uint32_t es_block(const BlockRegs& r, int diff, const
   const int Ld = (int)(ed & 31u) + ds;
   const uint32_t md = (uint32_t)(diff + (diff >> 31)) & ((1u << ds) - 1u);
   o.put(ed | (md << ((32 - Ld) & 31)), Ld, acc, n);
-  uint32_t nb = (uint32_t)Ld;
-  int last = 0, aor = 0;
-  zr = 0;
-  es_ac<1, SAFE>(r, last, aor, zr, es.ac[cls], es.zrl[cls], acc, n, nb, o);
+  int aor = 0, last = 0;
+  es_ac<1>(r, 0, aor, es.ac[cls], es.zrl[cls], acc, n, o, e1, v1, sz1, last);
   const uint32_t eb = es.eob[cls];
   const int Le = last < 63 ? (int)(eb & 31u) : 0;  // EOB unless coefficient 63 is set
   o.put(eb, Le, acc, n);
-  nb += (uint32_t)Le;
   bd |= aor > 1023;  // AC size > 10
+  const uint32_t nb = 32u * (uint32_t)o.k + (uint32_t)n;
   o.store(n ? acc << (32 - n) : 0u);
   return nb;
 }
@@ -850,28 +808,12 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   uint32_t* st = &stage[wv][0][lane];
   uint32_t* ov = ovf + gb * ES_MAXW;
   uint32_t nb = 0u;
-  int k = 0, zr = 0;
-  bool bd = false, safe = false;
-  if (JDS_ENT_WALK == 1) {
-    if (valid) {
-      EsStage o{st, ov};
-      nb = es_block<true>(rg, dc - pred, es, cls, o, bd, zr);
-      k = (int)((nb + 31u) >> 5);
-    }
-  } else {
-    if (valid) {
-      EsFast o{st};
-      nb = es_block<false>(rg, dc - pred, es, cls, o, bd, zr);
-      k = (int)((nb + 31u) >> 5);
-      safe = zr >= 16 || k > ES_SW;  // ZRL codes, or more words than the staging holds
-    }
-  }
-  if (JDS_ENT_WALK == 0 && __any(safe)) {  // rare: redo those blocks with ZRL codes, words to the spill area
-    if (safe) {
-      EsSafe o{ov};
-      nb = es_block<true>(rg, dc - pred, es, cls, o, bd, zr);
-      k = (int)((nb + 31u) >> 5);
-    }
+  int k = 0;
+  bool bd = false;
+  if (valid) {
+    EsStage o{st, ov};
+    nb = es_block(rg, dc - pred, es, cls, o, bd);
+    k = (int)((nb + 31u) >> 5);
   }
   if (bd) bad[q.f] = 1ull;  // not baseline-codable: the frame is reported
 
@@ -937,7 +879,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   const unsigned long long W1 = pre + A;
 
   // ---- placement
-  auto stw = [&](int j) -> uint32_t { return j >= k ? 0u : ((safe || j >= ES_SW) ? ov[j] : st[j * 64]); };
+  auto stw = [&](int j) -> uint32_t { return j >= k ? 0u : (j >= ES_SW ? ov[j] : st[j * 64]); };
   const unsigned long long o = pre + excl;  // the lane's first bit in the scan
   const int sh = (int)(o & 31ull);
   const unsigned long long hw = o >> 5, tw = (o + nb - 1ull) >> 5;
@@ -1030,16 +972,29 @@ __device__ __forceinline__ long long es_scan_out(const EntGeo& e, int f, int s, 
   return p;
 }
 
-// one wave per segment: the bytes of the words it finalised, stuffed (0x00
-// after every 0xFF) at their place in the file
-__global__ void __launch_bounds__(256) k_ent_emit2(const EntGeo e, const int nseg,
+// 0xFF bytes of a word as loaded from memory (byte j = bits 8j..8j+7), among its first nvb bytes
+__device__ __forceinline__ int es_ff_mem(uint32_t x, int nvb) {
+  const uint32_t y = ~x;
+  const uint32_t hi = ~((((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) | 0x7F7F7F7Fu);  // bit 8j+7: byte j == 0xFF
+  const uint32_t vm = nvb >= 4 ? 0x80808080u : (((1u << (8 * (nvb < 0 ? 0 : nvb))) - 1u) & 0x80808080u);
+  return __popc(hi & vm);
+}
+
+// One wave per segment: the bytes of the words it finalised, stuffed (0x00
+// after every 0xFF) at their place in the file.  Per 1 KiB of input (16 B per
+// lane): the lanes' stuffed lengths by a wave prefix, the stuffed bytes
+// assembled in the wave's LDS buffer at the output's alignment, then written
+// out as aligned dwords (bytes at the two partial ends).
+constexpr int EM_CHUNK = 1024;
+__global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nseg,
                                                    const unsigned long long* __restrict__ desc,
                                                    const unsigned long long* __restrict__ info,
                                                    const uint32_t* __restrict__ raw,
                                                    const unsigned long long* __restrict__ ffx,
                                                    uint8_t* __restrict__ out, long long stride) {
-  const int lane = threadIdx.x & 63;
-  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ uint32_t sbuf[4][(2 * EM_CHUNK + 8) / 4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = blockIdx.x * 4 + wv;
   if (g >= nseg) return;
   const EsSeg q = es_seg(e, g);
   const unsigned long long W0 = q.seg ? (desc[g - 1] & ES_VAL) : 0ull, W1 = desc[g] & ES_VAL;
@@ -1047,29 +1002,52 @@ __global__ void __launch_bounds__(256) k_ent_emit2(const EntGeo e, const int nse
   const unsigned long long fw = (W0 + 31) >> 5, lw = (W1 - 1) >> 5;
   if (fw > lw) return;
   const unsigned long long b0 = 4 * fw, b1 = (4 * lw + 4 < nbytes) ? 4 * lw + 4 : nbytes;
-  long long o = es_scan_out(e, q.f, q.s, info, ffx) + (long long)b0 +
-                (long long)(ffx[g] - ffx[(long long)q.f * e.sfirst[3] + e.sfirst[q.s]]);
-  uint8_t* dst = out + (long long)q.f * stride;
+  uint8_t* dst = out + (long long)q.f * stride + es_scan_out(e, q.f, q.s, info, ffx) + (long long)b0 +
+                 (long long)(ffx[g] - ffx[(long long)q.f * e.sfirst[3] + e.sfirst[q.s]]);
   const uint32_t* w = raw + raw_base(e, q.f, q.s);
-  for (unsigned long long i0 = b0; i0 < b1; i0 += 256) {
-    const unsigned long long i = i0 + 4 * lane;
-    uint32_t x = 0u;
+  uint8_t* lb = reinterpret_cast<uint8_t*>(sbuf[wv]);
+  for (unsigned long long i0 = b0; i0 < b1; i0 += EM_CHUNK) {
+    const unsigned long long i = i0 + 16 * lane;
+    uint32_t x[4] = {0u, 0u, 0u, 0u};
     int nv = 0, ff = 0;
     if (i < b1) {
-      x = w[i >> 2];  // stream order in memory: byte k of the word is bits 8k..8k+7
-      nv = b1 - i < 4 ? (int)(b1 - i) : 4;
+      nv = b1 - i < 16 ? (int)(b1 - i) : 16;
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) ff += (kk < nv && ((x >> (8 * kk)) & 255u) == 255u) ? 1 : 0;
+      for (int j = 0; j < 4; ++j) {
+        x[j] = 4 * j < nv ? w[(i >> 2) + j] : 0u;
+        ff += es_ff_mem(x[j], nv - 4 * j);
+      }
     }
-    const int ex = wave_excl_sum(ff, lane);
-    const int tot = __shfl(ex + ff, 63, 64);
-    long long p = o + (long long)(i - i0) + ex;
-    for (int kk = 0; kk < nv; ++kk) {
-      const uint8_t b = (uint8_t)(x >> (8 * kk));
-      dst[p++] = b;
-      if (b == 0xFF) dst[p++] = 0x00;
+    const int len = nv + ff;
+    const int ex = wave_excl_sum(len, lane);
+    const int tot = __shfl(ex + len, 63, 64);
+    const int sh0 = (int)((uintptr_t)dst & 3u);  // LDS byte sh0 <-> dst[0]
+    int p = sh0 + ex;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < nv) {
+        const uint8_t b = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
+        lb[p++] = b;
+        if (b == 0xFF) lb[p++] = 0x00;
+      }
     }
-    o += (long long)((b1 - i0 < 256 ? b1 - i0 : 256)) + tot;
+    __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations execute in order
+    asm volatile("" ::: "memory");
+    // out: global bytes dst[0 .. tot) <- LDS bytes [sh0, sh0 + tot); dword d covers LDS [4d, 4d + 4)
+    uint8_t* a0 = dst - sh0;  // 4-byte aligned
+    const int nd = (sh0 + tot + 3) >> 2;
+    for (int d = lane; d < nd; d += 64) {
+      const int lo = 4 * d, hi = 4 * d + 4;
+      if (lo >= sh0 && hi <= sh0 + tot) {
+        *reinterpret_cast<uint32_t*>(a0 + lo) = sbuf[wv][d];
+      } else {
+        for (int c = lo; c < hi; ++c)
+          if (c >= sh0 && c < sh0 + tot) a0[c] = lb[c];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the buffer is reused by the next iteration
+    asm volatile("" ::: "memory");
+    dst += tot;
   }
 }
 
@@ -1307,7 +1285,7 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
   hipLaunchKernelGGL(k_ent_fix, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, headw, raw, ffs);
   size_t tb = sz[7];
   if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, ffs, ffx, nseg + 1, s)) != hipSuccess) return err;
-  hipLaunchKernelGGL(k_ent_emit2, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, ffx, out, stride);
+  hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, ffx, out, stride);
   hipLaunchKernelGGL(k_ent_frame2, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, bad);
   return hipGetLastError();
 }

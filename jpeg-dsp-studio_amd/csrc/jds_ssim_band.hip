@@ -265,10 +265,13 @@ struct BandLds {
   double ring[5][BH][SB_RP];  // axis-0 outputs, column c at slot c & (SB_RING - 1)
   double st[5][BH][SB_SP];    // axis-1 running sums of the current chunk
   // inputs of the fill of one chunk, double-buffered (staged two chunks ahead):
-  // per staged column, rows i0 - 3 .. i0 + BH + 2 of both images
+  // per staged column, rows i0 - 3 .. i0 + BH + 2 of both images.  RGB: four
+  // rows per word, consecutive columns in consecutive words (the fill's and
+  // the staging's accesses of a wave hit distinct banks); luma: a column's
+  // 2 (BH + 6) values at an odd stride in doubles (likewise)
   union {
-    uint8_t b[SB_SC][2][16];           // RGB: the channel's bytes (a, b)
-    double y[SB_SC][2][BH + 6];        // luma: the planes' values (a, b)
+    uint32_t b4[2][4][SB_SC];           // RGB: byte r & 3 of word [image][r >> 2][column]
+    double y[SB_SC][2 * (BH + 6) + 1];  // luma: [column][image * (BH + 6) + r]
   } in[2];
   double ck[2][5][SB_SC];              // luma: the axis-0 chains' states at row i0
 };
@@ -283,40 +286,65 @@ __device__ __forceinline__ void fill_cols(int k, int W, int& lo, int& hi) {
 // Staging of one chunk's fill inputs: every thread loads up to SE elements
 // (coalesced: consecutive threads take consecutive columns of a row) into
 // registers; stage_commit writes them into the chunk's LDS buffer once the
-// loads have landed, a barrier interval later in program order.
-constexpr int SB_SE = (2 * 16 * SB_SC + SB_THREADS - 1) / SB_THREADS;  // >= 2 * (BH + 6) * SC / THREADS
+// loads have landed, a barrier interval later in program order.  The
+// per-thread element geometry does not change along the band: StagePlan holds
+// it (the row's first pixel, and column | image << 8 | committed << 9 | LDS
+// byte offset << 12), so a chunk costs a min, two adds and the load per element.
+template <int BH>
+struct StageCfg {
+  static constexpr int NR = BH + 6, SE = (2 * NR * SB_SC + SB_THREADS - 1) / SB_THREADS;
+};
+template <int BH>
+struct StagePlan {
+  uint32_t row[StageCfg<BH>::SE];
+  uint32_t ccv[StageCfg<BH>::SE];
+};
 template <int BH>
 struct StageRegs {
-  uint32_t b[SB_SE];
-  double y[SB_SE];
+  uint32_t b[StageCfg<BH>::SE];
+  double y[StageCfg<BH>::SE];
   double ck;
 };
 
 template <int BH>
+__device__ __forceinline__ StagePlan<BH> stage_plan(int c, int H, int W, int i0) {
+  constexpr int NR = StageCfg<BH>::NR, SE = StageCfg<BH>::SE;
+  static_assert(2 * NR * SB_SC <= SE * SB_THREADS, "staging slots");
+  StagePlan<BH> P;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < SE; ++i) {
+    const int e = t + i * SB_THREADS;
+    const bool ok = e < 2 * NR * SB_SC;
+    const int cc = e % SB_SC, r = ok ? (e / SB_SC) % NR : 0, im = ok ? e / (SB_SC * NR) : 0;
+    // rows past H - 1 (partial last band) load a valid clamped element that is never used
+    P.row[i] = (uint32_t)min(i0 - 3 + r, H - 1) * (uint32_t)W;
+    const uint32_t off = c < 3 ? (uint32_t)(((im * 4 + (r >> 2)) * SB_SC + cc) * 4 + (r & 3))
+                               : (uint32_t)((cc * (2 * NR + 1) + im * NR + r) * 8);
+    P.ccv[i] = (uint32_t)cc | ((uint32_t)im << 8) | ((ok ? 1u : 0u) << 9) | (off << 12);
+  }
+  return P;
+}
+
+template <int BH>
 __device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uint8_t* a, const uint8_t* b,
-                                            const double* X, const double* Y, const double* ck, int band, int i0,
-                                            int k, int nchunks, StageRegs<BH>& R) {
-  constexpr int NR = BH + 6;
-  static_assert(2 * NR * SB_SC <= SB_SE * SB_THREADS, "staging slots");
+                                            const double* X, const double* Y, const double* ck, int band, int k,
+                                            int nchunks, const StagePlan<BH>& P, StageRegs<BH>& R) {
+  constexpr int SE = StageCfg<BH>::SE;
   if (k >= nchunks) return;
   int lo, hi;
   fill_cols(k, B.W, lo, hi);
   const int t = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < SB_SE; ++i) {
-    const int e = t + i * SB_THREADS;
-    const int cc = e % SB_SC, r = (e / SB_SC) % NR, im = e / (SB_SC * NR);
-    // columns past hi and rows past H - 1 (partial last band) load a valid
-    // clamped element that is never used: no predicated loads
-    const int col = min(lo + cc, hi - 1), row = min(i0 - 3 + r, B.H - 1);
-    const size_t px = (size_t)row * B.W + col;
-    if (c < 3) {
-      const uint8_t* img = im ? b : a;
-      R.b[i] = e < 2 * NR * SB_SC ? img[px * 3 + c] : 0u;
-    } else {
-      const double* P = im ? Y : X;
-      R.y[i] = e < 2 * NR * SB_SC ? P[px] : 0.0;
-    }
+  for (int i = 0; i < SE; ++i) {
+    // columns past hi load a valid clamped element that is never used: no predicated loads
+    const uint32_t cc = P.ccv[i] & 255u, col = min((uint32_t)lo + cc, (uint32_t)hi - 1u);
+    const uint32_t px = P.row[i] + col;
+    const bool im = (P.ccv[i] >> 8) & 1u;
+    if (c < 3)
+      R.b[i] = (im ? b : a)[px * 3u + (uint32_t)c];
+    else
+      R.y[i] = (im ? Y : X)[px];
   }
   if (c == 3 && t < 5 * SB_SC) {
     const int q = t / SB_SC, col = min(lo + t % SB_SC, hi - 1);
@@ -325,19 +353,20 @@ __device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uin
 }
 
 template <int BH>
-__device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const StageRegs<BH>& R, BandLds<BH>& L) {
-  constexpr int NR = BH + 6;
+__device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const StagePlan<BH>& P,
+                                             const StageRegs<BH>& R, BandLds<BH>& L) {
+  constexpr int SE = StageCfg<BH>::SE;
   if (k >= nchunks) return;
   const int t = threadIdx.x, buf = k & 1;
+  uint8_t* base = reinterpret_cast<uint8_t*>(&L.in[buf]);
 #pragma unroll
-  for (int i = 0; i < SB_SE; ++i) {
-    const int e = t + i * SB_THREADS;
-    if (e < 2 * NR * SB_SC) {
-      const int cc = e % SB_SC, r = (e / SB_SC) % NR, im = e / (SB_SC * NR);
+  for (int i = 0; i < SE; ++i) {
+    if ((P.ccv[i] >> 9) & 1u) {
+      uint8_t* d = base + (P.ccv[i] >> 12);
       if (c < 3)
-        L.in[buf].b[cc][im][r] = (uint8_t)R.b[i];
+        *d = (uint8_t)R.b[i];
       else
-        L.in[buf].y[cc][im][r] = R.y[i];
+        *reinterpret_cast<double*>(d) = R.y[i];
     }
   }
   if (c == 3 && t < 5 * SB_SC) L.ck[buf][t / SB_SC][t % SB_SC] = R.ck;
@@ -356,9 +385,12 @@ __device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<
   const int q = t / nc, cc = t % nc, buf = k & 1;
   const int slot = (lo + cc) & (SB_RING - 1);
   if (c < 3) {
-    const uint4 xa = *reinterpret_cast<const uint4*>(L.in[buf].b[cc][0]);
-    const uint4 ya = *reinterpret_cast<const uint4*>(L.in[buf].b[cc][1]);
-    const uint32_t xw[4] = {xa.x, xa.y, xa.z, xa.w}, yw[4] = {ya.x, ya.y, ya.z, ya.w};
+    uint32_t xw[4], yw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xw[j] = L.in[buf].b4[0][j][cc];
+      yw[j] = L.in[buf].b4[1][j][cc];
+    }
     int tt[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r)
@@ -375,8 +407,8 @@ __device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<
       }
     }
   } else {
-    const double* tx = L.in[buf].y[cc][0];
-    const double* ty = L.in[buf].y[cc][1];
+    const double* tx = &L.in[buf].y[cc][0];
+    const double* ty = &L.in[buf].y[cc][NR];
     double s = L.ck[buf][q][cc];
     L.ring[q][0][slot] = div7(s);
 #pragma unroll
@@ -465,13 +497,14 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   // stored into LDS two chunks ahead (two buffers): each load has a whole
   // chunk period -- the barrier interval that issued it and the next one --
   // before its value is needed
+  const StagePlan<BH> P = stage_plan<BH>(c, H, W, i0);
   StageRegs<BH> RA, RB;
-  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, 0, nchunks, RA);
-  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, 1, nchunks, RB);
-  stage_commit<BH>(c, 0, nchunks, RA, L);
-  stage_commit<BH>(c, 1, nchunks, RB, L);
+  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, 0, nchunks, P, RA);
+  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, 1, nchunks, P, RB);
+  stage_commit<BH>(c, 0, nchunks, P, RA, L);
+  stage_commit<BH>(c, 1, nchunks, P, RB, L);
   __syncthreads();
-  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, 2, nchunks, RA);
+  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, 2, nchunks, P, RA);
   fill_chunk<BH>(c, nr, 0, W, L);
   __syncthreads();
 
@@ -523,8 +556,8 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
         smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = (a1 * a2) / d;
       }
     }
-    stage_commit<BH>(c, k + 2, nchunks, cur, L);
-    stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, i0, k + 3, nchunks, nxt);
+    stage_commit<BH>(c, k + 2, nchunks, P, cur, L);
+    stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, k + 3, nchunks, P, nxt);
     __syncthreads();
   };
   for (int k = 0; k < nchunks; k += 2) {
@@ -746,6 +779,7 @@ hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const*
                                   double c1, double c2, double* scratch, double* out, int out_stride,
                                   unsigned long long* sse, hipStream_t s) {
   if (items < 1 || items > SB_MAX_ITEMS || H < 7 || W < 7) return hipErrorInvalidValue;
+  if ((unsigned long long)H * (unsigned long long)W * 3ull >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit staging offsets
   SsimBatch B{};
   for (int i = 0; i < items; ++i) B.pairs[i] = {a[i], b[i]};
   B.H = H;
