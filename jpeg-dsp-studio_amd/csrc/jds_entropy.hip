@@ -654,7 +654,8 @@ constexpr unsigned long long ES_FA = 1ull << 62, ES_FP = 2ull << 62, ES_VAL = ES
 // ignored) to the pending word acc (n bits, right-aligned; bits above n are
 // ignored); a completed word goes to the lane's LDS staging slot k (slots 64
 // words apart, so a wave's stores hit 64 banks), slots >= ES_SW to the
-// block's global spill area.
+// segment's global area (same word-major layout: word k of lane l at
+// (g * ES_MAXW + k) * 64 + l).
 struct EsStage {
   uint32_t* st;
   uint32_t* ov;
@@ -663,14 +664,14 @@ struct EsStage {
     const int t = n + L;
     if (t >= 32) {
       const uint32_t w = __builtin_amdgcn_alignbit(acc, symL, (uint32_t)n);  // the top 32 bits of acc . sym
-      if (k < ES_SW) st[k * 64] = w; else ov[k] = w;
+      if (k < ES_SW) st[k * 64] = w; else ov[k * 64] = w;
       ++k;
     }
     acc = L ? __builtin_amdgcn_alignbit(acc, symL, (uint32_t)(32 - L)) : acc;  // (acc << L) | sym
     n = t & 31;
   }
   __device__ __forceinline__ void store(uint32_t w) {
-    if (k < ES_SW) st[k * 64] = w; else ov[k] = w;
+    if (k < ES_SW) st[k * 64] = w; else ov[k * 64] = w;
   }
 };
 
@@ -770,6 +771,75 @@ __device__ __forceinline__ int es_ff(uint32_t v, int nbytes) {  // 0xFF bytes am
   return c;
 }
 
+// Placement of a segment's staged words at scan bit offset pre (lane bits at
+// pre + excl): see k_ent_seg.  st: the lane's LDS staging (slots < ES_SW),
+// ov: its global words (slots >= ES_SW, or all slots when st is null).
+__device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g, int lane, bool valid, int nvalid,
+                                         bool last_seg, uint32_t nb, uint32_t excl, unsigned long long pre,
+                                         unsigned long long A, const uint32_t* st, const uint32_t* ov, int k,
+                                         uint32_t* __restrict__ raw, uint32_t* __restrict__ headw,
+                                         unsigned long long* __restrict__ ffs, unsigned long long* __restrict__ info,
+                                         unsigned long long* __restrict__ scan_bits) {
+  const unsigned long long W1 = pre + A;
+  auto stw = [&](int j) -> uint32_t { return j >= k ? 0u : ((st == nullptr || j >= ES_SW) ? ov[j * 64] : st[j * 64]); };
+  const unsigned long long o = pre + excl;  // the lane's first bit in the scan
+  const int sh = (int)(o & 31ull);
+  const unsigned long long hw = o >> 5, tw = (o + nb - 1ull) >> 5;
+  const bool single = hw == tw;
+  const uint32_t s0 = stw(0);
+  const uint32_t hv = s0 >> sh;
+  // the next lane starts inside this lane's tail word
+  const bool c = valid && ((o + nb) & 31ull) != 0ull && lane + 1 < nvalid;
+  // X = this lane's head word bits | those of the following lanes that share it
+  uint32_t X = valid ? hv : 0u;
+  int F = (valid && single && c) ? 1 : 0;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t Xn = __shfl_down(X, d, 64);
+    const int Fn = __shfl_down(F, d, 64);
+    if (F && lane + d < 64) {
+      X |= Xn;
+      F = Fn;
+    }
+  }
+  const uint32_t X1 = __shfl_down(X, 1, 64);
+  const uint32_t in_tail = c ? X1 : 0u;
+  uint32_t* rs = raw + raw_base(e, q.f, q.s);
+  const unsigned long long wlast = (W1 - 1ull) >> 5;
+  const bool open_end = !last_seg && (W1 & 31ull);
+  int ffc = 0;
+  auto put_word = [&](unsigned long long widx, uint32_t v) {
+    int nb4 = 4;
+    if (last_seg && widx == wlast) nb4 = es_pad(v, W1, widx);
+    rs[widx] = __builtin_bswap32(v);  // byte 0 of the stream first
+    if (!(open_end && widx == wlast)) ffc += es_ff(v, nb4);
+  };
+  if (valid) {
+    const bool own_head = sh == 0;
+    const int nout = (int)(tw - hw);
+    if (own_head && !single) put_word(hw, hv);
+    uint32_t prev = s0;
+    for (int j = 1; j < nout; ++j) {
+      const uint32_t cur = stw(j);
+      put_word(hw + j, __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh));
+      prev = cur;
+    }
+    const uint32_t tv = single ? hv : __builtin_amdgcn_alignbit(prev, stw(nout), (uint32_t)sh);
+    if (!single || own_head) put_word(tw, tv | in_tail);
+    if (lane == 0 && !own_head) headw[g] = X;  // the previous segment holds this word's first bit
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) ffc += __shfl_xor(ffc, d, 64);
+  if (lane == 0) {
+    ffs[g] = (unsigned long long)ffc;
+    if (last_seg) {
+      info[2 * (q.f * 3 + q.s)] = 0ull;
+      info[2 * (q.f * 3 + q.s) + 1] = W1;
+      if (scan_bits) scan_bits[q.f * 3 + q.s] = W1;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per_eu(JDS_ENT_WPE))) k_ent_seg(const EntGeo e, const int nseg, const int16_t* __restrict__ coeffs,
                                                             const EsTab* __restrict__ gt,
                                                             unsigned long long* __restrict__ desc,
@@ -806,7 +876,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   if (lane == 0) pred = q.seg ? (int)coeffs[(gb - 1) * 64] : 0;
   const int cls = q.s ? 1 : 0;
   uint32_t* st = &stage[wv][0][lane];
-  uint32_t* ov = ovf + gb * ES_MAXW;
+  uint32_t* ov = ovf + (size_t)g * ES_MAXW * 64 + lane;
   uint32_t nb = 0u;
   int k = 0;
   bool bd = false;
@@ -876,66 +946,94 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
     }
     if (lane == 0) __hip_atomic_store(&desc[g], ES_FP | (pre + A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  const unsigned long long W1 = pre + A;
+  es_place(e, q, g, lane, valid, nvalid, last_seg, nb, excl, pre, A, st, ov, k, raw, headw, ffs, info, scan_bits);
+}
 
-  // ---- placement
-  auto stw = [&](int j) -> uint32_t { return j >= k ? 0u : (j >= ES_SW ? ov[j] : st[j * 64]); };
-  const unsigned long long o = pre + excl;  // the lane's first bit in the scan
-  const int sh = (int)(o & 31ull);
-  const unsigned long long hw = o >> 5, tw = (o + nb - 1ull) >> 5;
-  const bool single = hw == tw;
-  const uint32_t s0 = stw(0);
-  const uint32_t hv = s0 >> sh;
-  // the next lane starts inside this lane's tail word
-  const bool c = valid && ((o + nb) & 31ull) != 0ull && lane + 1 < nvalid;
-  // X = this lane's head word bits | those of the following lanes that share it
-  uint32_t X = valid ? hv : 0u;
-  int F = (valid && single && c) ? 1 : 0;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t Xn = __shfl_down(X, d, 64);
-    const int Fn = __shfl_down(F, d, 64);
-    if (F && lane + d < 64) {
-      X |= Xn;
-      F = Fn;
-    }
+// JDS_ENT_SPLIT: the same work without the look-back.  k_ent_walk packs
+// each segment's blocks and stores the staged words (word-major per segment),
+// the lanes' bit counts and the segment's total; a hipCUB scan over the
+// totals gives every segment's offset; k_ent_place places the words.
+#ifndef JDS_ENT_SPLIT
+#define JDS_ENT_SPLIT 1
+#endif
+__global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per_eu(JDS_ENT_WPE))) k_ent_walk(
+    const EntGeo e, const int nseg, const int16_t* __restrict__ coeffs, const EsTab* __restrict__ gt,
+    uint32_t* __restrict__ gst, uint32_t* __restrict__ nbits, unsigned long long* __restrict__ agg,
+    unsigned long long* __restrict__ bad) {
+  __shared__ EsTab es;
+  __shared__ uint32_t stage[ES_WAVES][ES_SW][64];
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(gt);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&es);
+    for (int i = threadIdx.x; i < (int)(sizeof(EsTab) / 4); i += blockDim.x) dst[i] = src[i];
   }
-  const uint32_t X1 = __shfl_down(X, 1, 64);
-  const uint32_t in_tail = c ? X1 : 0u;
-  uint32_t* rs = raw + raw_base(e, q.f, q.s);
-  const unsigned long long wlast = (W1 - 1ull) >> 5;
-  const bool open_end = !last_seg && (W1 & 31ull);
-  int ffc = 0;
-  auto put_word = [&](unsigned long long widx, uint32_t v) {
-    int nb4 = 4;
-    if (last_seg && widx == wlast) nb4 = es_pad(v, W1, widx);
-    rs[widx] = __builtin_bswap32(v);  // byte 0 of the stream first
-    if (!(open_end && widx == wlast)) ffc += es_ff(v, nb4);
-  };
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = blockIdx.x * ES_WAVES + wv;
+  if (g >= nseg) return;  // (whole wave; no barrier follows)
+  const EsSeg q = es_seg(e, g);
+  const int bi = q.seg * 64 + lane;
+  const bool valid = bi < q.nbs;
+  const long long gb = (long long)q.f * e.nb + e.first[q.s] + (valid ? bi : q.nbs - 1);
+  const BlockRegs rg = load_block(coeffs + gb * 64);
+  const int dc = coef_at<0>(rg);
+  int pred = __shfl_up(dc, 1, 64);
+  if (lane == 0) pred = q.seg ? (int)coeffs[(gb - 1) * 64] : 0;
+  uint32_t* st = &stage[wv][0][lane];
+  uint32_t* ov = gst + (size_t)g * ES_MAXW * 64 + lane;
+  uint32_t nb = 0u;
+  int k = 0;
+  bool bd = false;
   if (valid) {
-    const bool own_head = sh == 0;
-    const int nout = (int)(tw - hw);
-    if (own_head && !single) put_word(hw, hv);
-    uint32_t prev = s0;
-    for (int j = 1; j < nout; ++j) {
-      const uint32_t cur = stw(j);
-      put_word(hw + j, __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh));
-      prev = cur;
-    }
-    const uint32_t tv = single ? hv : __builtin_amdgcn_alignbit(prev, stw(nout), (uint32_t)sh);
-    if (!single || own_head) put_word(tw, tv | in_tail);
-    if (lane == 0 && !own_head) headw[g] = X;  // the previous segment holds this word's first bit
+    EsStage o{st, ov};
+    nb = es_block(rg, dc - pred, es, q.s ? 1 : 0, o, bd);
+    k = (int)((nb + 31u) >> 5);
   }
+  if (bd) bad[q.f] = 1ull;
+  // the LDS slots to the segment's global area (one 256-B row per slot)
+  int kmax = k < ES_SW ? k : ES_SW;
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) ffc += __shfl_xor(ffc, d, 64);
-  if (lane == 0) {
-    ffs[g] = (unsigned long long)ffc;
-    if (last_seg) {
-      info[2 * (q.f * 3 + q.s)] = 0ull;
-      info[2 * (q.f * 3 + q.s) + 1] = W1;
-      if (scan_bits) scan_bits[q.f * 3 + q.s] = W1;
-    }
+  for (int d = 32; d > 0; d >>= 1) {
+    const int y = __shfl_xor(kmax, d, 64);
+    kmax = y > kmax ? y : kmax;
   }
+  for (int j = 0; j < kmax; ++j)
+    if (j < k) ov[j * 64] = st[j * 64];
+  nbits[(size_t)g * 64 + lane] = nb;
+  unsigned long long a = nb;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) a += __shfl_xor(a, d, 64);
+  if (lane == 0) agg[g] = a;
+}
+
+// segoff = exclusive prefix of agg over all segments; incl[g] = the segment's
+// end bit within its scan (k_ent_fix / k_ent_emit3 read it as desc)
+__global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nseg, const uint32_t* __restrict__ gst,
+                                                   const uint32_t* __restrict__ nbits,
+                                                   const unsigned long long* __restrict__ segoff,
+                                                   unsigned long long* __restrict__ incl, uint32_t* __restrict__ raw,
+                                                   uint32_t* __restrict__ headw, unsigned long long* __restrict__ ffs,
+                                                   unsigned long long* __restrict__ info,
+                                                   unsigned long long* __restrict__ scan_bits) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= nseg) return;
+  const EsSeg q = es_seg(e, g);
+  const bool valid = q.seg * 64 + lane < q.nbs;
+  const int nvalid = q.nbs - q.seg * 64 < 64 ? q.nbs - q.seg * 64 : 64;
+  const bool last_seg = q.seg == q.nseg_s - 1;
+  const uint32_t nb = nbits[(size_t)g * 64 + lane];
+  uint32_t inc = nb;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  const unsigned long long A = __shfl(inc, 63, 64);
+  const unsigned long long pre = segoff[g] - segoff[g - q.seg];
+  if (lane == 0) incl[g] = pre + A;
+  es_place(e, q, g, lane, valid, nvalid, last_seg, nb, inc - nb, pre, A, nullptr,
+           gst + (size_t)g * ES_MAXW * 64 + lane, (int)((nb + 31u) >> 5), raw, headw, ffs, info, scan_bits);
 }
 
 // the first word of segment g when segment g - 1 holds its first bit: OR in
@@ -1232,7 +1330,8 @@ void ent_sizes(const Geo& g, int n, size_t* sz) {
   if (JDS_ENT_FUSED) {
     const long long nseg = (long long)n * e.sfirst[3];
     sz[0] = sizeof(unsigned long long) * (nseg + 2) + sizeof(uint32_t) * (nseg + 1);
-    sz[1] = sizeof(uint32_t) * ES_MAXW * nblk;
+    sz[0] += sizeof(uint32_t) + sizeof(unsigned long long) * 2 * (nseg + 1) + sizeof(uint32_t) * 64 * nseg;  // JDS_ENT_SPLIT: agg, segoff, nbits
+    sz[1] = sizeof(uint32_t) * ES_MAXW * 64 * nseg;
     sz[4] = sizeof(unsigned long long) * (nseg + 1);
     sz[5] = sizeof(unsigned long long) * (nseg + 1);
     size_t t1 = 0;
@@ -1280,7 +1379,21 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
   if ((err = hipMemsetAsync(bad, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) return err;
   const unsigned wg = (unsigned)((nseg + ES_WAVES - 1) / ES_WAVES);
   const EsTab* est = reinterpret_cast<const EsTab*>((const char*)tab_dev + sizeof(EntTab));
-  hipLaunchKernelGGL(k_ent_seg, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, desc, ovf, raw, headw, ffs, info, scan_bits, bad);
+  if (JDS_ENT_SPLIT) {
+    auto* agg = (unsigned long long*)(headw + ((nseg + 2) & ~1));  // 8-B aligned
+    auto* segoff = agg + nseg + 1;
+    auto* nbits = (uint32_t*)(segoff + nseg + 1);
+    if ((err = hipMemsetAsync(agg + nseg, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
+    hipLaunchKernelGGL(k_ent_walk, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, ovf, nbits, agg, bad);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+    size_t tb0 = sz[7];
+    if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb0, agg, segoff, nseg + 1, s)) != hipSuccess) return err;
+    hipLaunchKernelGGL(k_ent_place, dim3(wg), dim3(256), 0, s, e, nseg, ovf, nbits, segoff, desc, raw, headw, ffs,
+                       info, scan_bits);
+  } else {
+    hipLaunchKernelGGL(k_ent_seg, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, desc, ovf, raw, headw,
+                       ffs, info, scan_bits, bad);
+  }
   if ((err = hipGetLastError()) != hipSuccess) return err;
   hipLaunchKernelGGL(k_ent_fix, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, headw, raw, ffs);
   size_t tb = sz[7];

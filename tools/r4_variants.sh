@@ -4,6 +4,4 @@ set -e
 cd "$(dirname "$0")/.."
 rm -f tools/bin/ab/*.so tools/bin/ab/*.o
 python3 tools/build_variant.py A "" jds_entropy.hip
-python3 tools/build_variant.py LB1 "-DES_LB=1" jds_entropy.hip
-python3 tools/build_variant.py LB4 "-DES_LB=4" jds_entropy.hip
-python3 tools/build_variant.py NOLB "-DJDS_ENT_PROBE_NOLB" jds_entropy.hip
+python3 tools/build_variant.py LB "-DJDS_ENT_SPLIT=0" jds_entropy.hip
