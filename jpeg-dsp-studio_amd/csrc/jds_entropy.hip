@@ -645,7 +645,15 @@ __global__ void __launch_bounds__(256) k_ent_pack2(const EntGeo e, long long nbl
 #ifndef ES_LB
 #define ES_LB 1  // look-back descriptors per lane and probe (4: 0.473, 8: 0.545 vs 1: 0.386 ms per 64 x 1080p; device-coherent loads)
 #endif
-constexpr int ES_SW = 32;                // LDS staging words per lane (1024 bits)
+#ifndef ES_DENSE
+#define ES_DENSE 32  // zigzag positions coded by the unrolled walk; the rest by the nonzero loop (64: none)
+#endif
+static_assert(ES_DENSE >= 32 && ES_DENSE <= 64, "the nonzero loop's mask is 32 bits");
+#ifndef ES_SW_DEF
+#define ES_SW_DEF (ES_DENSE < 64 ? 16 : 32)
+#endif
+constexpr int ES_SW = ES_SW_DEF;         // LDS staging words per lane (more spill to global)
+constexpr int ES_HI = 64 - ES_DENSE;     // positions of the nonzero loop
 constexpr int ES_MAXW = 53;              // words per block at most (1660 bits + the partial word): the spill area
 constexpr int ES_WAVES = 4;
 constexpr unsigned long long ES_FA = 1ull << 62, ES_FP = 2ull << 62, ES_VAL = ES_FA - 1ull;
@@ -687,14 +695,14 @@ __device__ __forceinline__ int es_size(int a) {
 template <int K>
 __device__ __forceinline__ void es_ac(const BlockRegs& r, int last, int& aor, const uint32_t* ac, uint32_t zrl,
                                       uint32_t& acc, int& n, EsStage& o, uint32_t e, int v, int sz, int& lastK) {
-  if constexpr (K < 64) {
+  if constexpr (K < ES_DENSE) {
     const int a = v < 0 ? -v : v;
     aor |= a;
     const int run = K - 1 - last;
     const int nlast = a ? K : last;
     uint32_t e1 = 0u;
     int v1 = 0, sz1 = 0;
-    if constexpr (K + 1 < 64) {
+    if constexpr (K + 1 < ES_DENSE) {
       v1 = coef_at<ZZC[K + 1]>(r);
       sz1 = es_size(v1 < 0 ? -v1 : v1);
       e1 = ac[((K - nlast) & 15) << 5 | sz1];
@@ -712,13 +720,52 @@ __device__ __forceinline__ void es_ac(const BlockRegs& r, int last, int& aor, co
   }
 }
 
+// Zigzag positions ES_DENSE .. 63 (mostly zero at every quality but the
+// finest): their coefficients go to the lane's LDS column (int16, word-major
+// across the wave) with a nonzero mask, and only the nonzero ones are coded,
+// in order, by a per-lane loop (run lengths from the mask).
+template <int K>
+__device__ __forceinline__ void es_hi_stash(const BlockRegs& r, int16_t* cz, uint32_t& m) {
+  if constexpr (K < 64) {
+    const int v = coef_at<ZZC[K]>(r);
+    cz[(K - ES_DENSE) * 64] = (int16_t)v;
+    m |= (v != 0 ? 1u : 0u) << (K - ES_DENSE);
+    es_hi_stash<K + 1>(r, cz, m);
+  }
+}
+
+__device__ __forceinline__ void es_hi_code(const int16_t* cz, uint32_t m, int& last, int& aor, const uint32_t* ac,
+                                           uint32_t zrl, uint32_t& acc, int& n, EsStage& o) {
+  while (m) {
+    const int b = __builtin_ctz(m);
+    m &= m - 1u;
+    const int K = ES_DENSE + b;
+    const int v = cz[b * 64];
+    const int a = v < 0 ? -v : v;
+    aor |= a;
+    const int sz = es_size(a);
+    const int run = K - 1 - last;
+    if (run >= 16) {  // one ZRL code per 16 zeros first
+      const int zl = (int)(zrl & 31u);
+      for (int i = 0; i < (run >> 4); ++i) o.put(zrl, zl, acc, n);
+    }
+    const uint32_t e = ac[((run & 15) << 5) | sz];
+    const int L = (int)(e & 31u) + sz;
+    const uint32_t mag = (uint32_t)(v + (v >> 31)) & ((1u << sz) - 1u);
+    o.put(e | (mag << ((32 - L) & 31)), L, acc, n);
+    last = K;
+  }
+}
+
 // One block: DC difference, AC walk, EOB, the partial word (left-aligned).
 // Returns the bit count (32 per completed word + the pending bits); bd = not
 // baseline-codable.
 __device__ __forceinline__ uint32_t es_block(const BlockRegs& r, int diff, const EsTab& es, int cls, EsStage& o,
-                                             bool& bd) {
+                                             bool& bd, int16_t* cz) {
   uint32_t acc = 0u;
   int n = 0;
+  uint32_t mhi = 0u;
+  if constexpr (ES_DENSE < 64) es_hi_stash<ES_DENSE>(r, cz, mhi);
   const int v1 = coef_at<ZZC[1]>(r);
   const int sz1 = es_size(v1 < 0 ? -v1 : v1);
   const uint32_t e1 = es.ac[cls][sz1];  // run 0
@@ -732,6 +779,7 @@ __device__ __forceinline__ uint32_t es_block(const BlockRegs& r, int diff, const
   o.put(ed | (md << ((32 - Ld) & 31)), Ld, acc, n);
   int aor = 0, last = 0;
   es_ac<1>(r, 0, aor, es.ac[cls], es.zrl[cls], acc, n, o, e1, v1, sz1, last);
+  if constexpr (ES_DENSE < 64) es_hi_code(cz, mhi, last, aor, es.ac[cls], es.zrl[cls], acc, n, o);
   const uint32_t eb = es.eob[cls];
   const int Le = last < 63 ? (int)(eb & 31u) : 0;  // EOB unless coefficient 63 is set
   o.put(eb, Le, acc, n);
@@ -819,7 +867,16 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
     const int nout = (int)(tw - hw);
     if (own_head && !single) put_word(hw, hv);
     uint32_t prev = s0;
-    for (int j = 1; j < nout; ++j) {
+    int j = 1;
+    for (; j + 3 < nout; j += 4) {  // four staged words requested before any is used
+      const uint32_t c0 = stw(j), c1 = stw(j + 1), c2 = stw(j + 2), c3 = stw(j + 3);
+      put_word(hw + j, __builtin_amdgcn_alignbit(prev, c0, (uint32_t)sh));
+      put_word(hw + j + 1, __builtin_amdgcn_alignbit(c0, c1, (uint32_t)sh));
+      put_word(hw + j + 2, __builtin_amdgcn_alignbit(c1, c2, (uint32_t)sh));
+      put_word(hw + j + 3, __builtin_amdgcn_alignbit(c2, c3, (uint32_t)sh));
+      prev = c3;
+    }
+    for (; j < nout; ++j) {
       const uint32_t cur = stw(j);
       put_word(hw + j, __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh));
       prev = cur;
@@ -851,6 +908,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
                                                             unsigned long long* __restrict__ bad) {
   __shared__ EsTab es;
   __shared__ uint32_t stage[ES_WAVES][ES_SW][64];
+  __shared__ int16_t czs[ES_WAVES][ES_HI > 0 ? ES_HI : 1][64];
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(gt);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&es);
@@ -858,6 +916,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int16_t* cz = &czs[wv][0][lane];
   // Segments in launch order: a workgroup waits only for segments of lower
   // index, and each XCD dispatches its workgroups in index order, so the
   // lowest unfinished segment is always resident (no ticket: one
@@ -882,7 +941,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   bool bd = false;
   if (valid) {
     EsStage o{st, ov};
-    nb = es_block(rg, dc - pred, es, cls, o, bd);
+    nb = es_block(rg, dc - pred, es, cls, o, bd, cz);
     k = (int)((nb + 31u) >> 5);
   }
   if (bd) bad[q.f] = 1ull;  // not baseline-codable: the frame is reported
@@ -959,9 +1018,10 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
 __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per_eu(JDS_ENT_WPE))) k_ent_walk(
     const EntGeo e, const int nseg, const int16_t* __restrict__ coeffs, const EsTab* __restrict__ gt,
     uint32_t* __restrict__ gst, uint32_t* __restrict__ nbits, unsigned long long* __restrict__ agg,
-    unsigned long long* __restrict__ bad) {
+    uint32_t* __restrict__ badseg, unsigned long long* __restrict__ ffs) {
   __shared__ EsTab es;
   __shared__ uint32_t stage[ES_WAVES][ES_SW][64];
+  __shared__ int16_t czs[ES_WAVES][ES_HI > 0 ? ES_HI : 1][64];
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(gt);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&es);
@@ -969,6 +1029,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int16_t* cz = &czs[wv][0][lane];
   const int g = blockIdx.x * ES_WAVES + wv;
   if (g >= nseg) return;  // (whole wave; no barrier follows)
   const EsSeg q = es_seg(e, g);
@@ -986,10 +1047,10 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   bool bd = false;
   if (valid) {
     EsStage o{st, ov};
-    nb = es_block(rg, dc - pred, es, q.s ? 1 : 0, o, bd);
+    nb = es_block(rg, dc - pred, es, q.s ? 1 : 0, o, bd, cz);
     k = (int)((nb + 31u) >> 5);
   }
-  if (bd) bad[q.f] = 1ull;
+  const bool any_bad = __ballot(bd) != 0ull;
   // the LDS slots to the segment's global area (one 256-B row per slot)
   int kmax = k < ES_SW ? k : ES_SW;
 #pragma unroll
@@ -1003,7 +1064,14 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   unsigned long long a = nb;
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) a += __shfl_xor(a, d, 64);
-  if (lane == 0) agg[g] = a;
+  if (lane == 0) {
+    agg[g] = a;
+    badseg[g] = any_bad ? 1u : 0u;  // not baseline-codable: the frame is reported (k_ent_frame3)
+    if (g == nseg - 1) {            // the scans' closing zeros (no memsets)
+      agg[nseg] = 0ull;
+      ffs[nseg] = 0ull;
+    }
+  }
 }
 
 // segoff = exclusive prefix of agg over all segments; incl[g] = the segment's
@@ -1084,11 +1152,24 @@ __device__ __forceinline__ int es_ff_mem(uint32_t x, int nvb) {
 // assembled in the wave's LDS buffer at the output's alignment, then written
 // out as aligned dwords (bytes at the two partial ends).
 constexpr int EM_CHUNK = 1024;
+// each segment's first output byte (k_ent_emit3's one dependent lookup)
+__global__ void k_ent_offs(const EntGeo e, const int nseg, const unsigned long long* __restrict__ desc,
+                           const unsigned long long* __restrict__ info, const unsigned long long* __restrict__ ffx,
+                           unsigned long long* __restrict__ outoff) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nseg) return;
+  const EsSeg q = es_seg(e, g);
+  const unsigned long long W0 = q.seg ? (desc[g - 1] & ES_VAL) : 0ull;
+  const unsigned long long b0 = 4 * ((W0 + 31) >> 5);
+  outoff[g] = (unsigned long long)es_scan_out(e, q.f, q.s, info, ffx) + b0 +
+              (ffx[g] - ffx[(long long)q.f * e.sfirst[3] + e.sfirst[q.s]]);
+}
+
 __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nseg,
                                                    const unsigned long long* __restrict__ desc,
                                                    const unsigned long long* __restrict__ info,
                                                    const uint32_t* __restrict__ raw,
-                                                   const unsigned long long* __restrict__ ffx,
+                                                   const unsigned long long* __restrict__ outoff,
                                                    uint8_t* __restrict__ out, long long stride) {
   __shared__ uint32_t sbuf[4][(2 * EM_CHUNK + 8) / 4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1100,8 +1181,7 @@ __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nse
   const unsigned long long fw = (W0 + 31) >> 5, lw = (W1 - 1) >> 5;
   if (fw > lw) return;
   const unsigned long long b0 = 4 * fw, b1 = (4 * lw + 4 < nbytes) ? 4 * lw + 4 : nbytes;
-  uint8_t* dst = out + (long long)q.f * stride + es_scan_out(e, q.f, q.s, info, ffx) + (long long)b0 +
-                 (long long)(ffx[g] - ffx[(long long)q.f * e.sfirst[3] + e.sfirst[q.s]]);
+  uint8_t* dst = out + (long long)q.f * stride + (long long)outoff[g];
   const uint32_t* w = raw + raw_base(e, q.f, q.s);
   uint8_t* lb = reinterpret_cast<uint8_t*>(sbuf[wv]);
   for (unsigned long long i0 = b0; i0 < b1; i0 += EM_CHUNK) {
@@ -1170,6 +1250,39 @@ __global__ void k_ent_frame2(const EntGeo e, const uint8_t* __restrict__ hdr, co
     dst[end] = 0xFF;
     dst[end + 1] = 0xD9;
     if (lengths) lengths[f] = bad[f] ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
+  }
+}
+
+__global__ void k_ent_frame3(const EntGeo e, const uint8_t* __restrict__ hdr, const unsigned long long* __restrict__ info,
+                             const unsigned long long* __restrict__ ffx, uint8_t* __restrict__ out, long long stride,
+                             unsigned long long* __restrict__ lengths, const uint32_t* __restrict__ badseg) {
+  __shared__ int s_bad;
+  const int f = blockIdx.x;
+  if (threadIdx.x == 0) s_bad = 0;
+  __syncthreads();
+  {
+    int b = 0;
+    for (int i = threadIdx.x; i < e.sfirst[3]; i += blockDim.x) b |= (int)badseg[(long long)f * e.sfirst[3] + i];
+    if (b) s_bad = 1;
+  }
+  __syncthreads();
+  uint8_t* dst = out + (long long)f * stride;
+  for (int i = threadIdx.x; i < e.hdr; i += blockDim.x) dst[i] = hdr[(long long)f * e.hdr + i];
+  if (threadIdx.x < 3) {
+    const int s = threadIdx.x;
+    uint8_t* m = dst + es_scan_out(e, f, s, info, ffx) - ENT_SOS;
+    const uint8_t sos[ENT_SOS] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(s + 1), (uint8_t)(s == 0 ? 0x00 : 0x11),
+                                  0x00, 0x3F, 0x00};
+    for (int i = 0; i < ENT_SOS; ++i) m[i] = sos[i];
+  }
+  if (threadIdx.x == 0) {
+    const long long g0 = (long long)f * e.sfirst[3];
+    const unsigned long long nb = (info[2 * (f * 3 + 2) + 1] + 7) >> 3;
+    const unsigned long long ff = ffx[g0 + e.sfirst[3]] - ffx[g0 + e.sfirst[2]];
+    const long long end = es_scan_out(e, f, 2, info, ffx) + (long long)(nb + ff);
+    dst[end] = 0xFF;
+    dst[end + 1] = 0xD9;
+    if (lengths) lengths[f] = s_bad ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
   }
 }
 
@@ -1330,7 +1443,7 @@ void ent_sizes(const Geo& g, int n, size_t* sz) {
   if (JDS_ENT_FUSED) {
     const long long nseg = (long long)n * e.sfirst[3];
     sz[0] = sizeof(unsigned long long) * (nseg + 2) + sizeof(uint32_t) * (nseg + 1);
-    sz[0] += sizeof(uint32_t) + sizeof(unsigned long long) * 2 * (nseg + 1) + sizeof(uint32_t) * 64 * nseg;  // JDS_ENT_SPLIT: agg, segoff, nbits
+    sz[0] += sizeof(uint32_t) + sizeof(unsigned long long) * 2 * (nseg + 1) + sizeof(uint32_t) * 65 * nseg;  // JDS_ENT_SPLIT: agg, segoff, nbits, badseg
     sz[1] = sizeof(uint32_t) * ES_MAXW * 64 * nseg;
     sz[4] = sizeof(unsigned long long) * (nseg + 1);
     sz[5] = sizeof(unsigned long long) * (nseg + 1);
@@ -1373,18 +1486,21 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
   ent_sizes(g, n, sz);
   unsigned long long* bad = info + 6 * n;
   hipError_t err;
-  // every descriptor's flag starts at zero; ffs[nseg] closes the scan
-  if ((err = hipMemsetAsync(buf[0], 0, sizeof(unsigned long long) * (nseg + 1), s)) != hipSuccess) return err;
-  if ((err = hipMemsetAsync(ffs + nseg, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
-  if ((err = hipMemsetAsync(bad, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) return err;
+  if (!JDS_ENT_SPLIT) {
+    // every descriptor's flag starts at zero; ffs[nseg] closes the scan
+    if ((err = hipMemsetAsync(buf[0], 0, sizeof(unsigned long long) * (nseg + 1), s)) != hipSuccess) return err;
+    if ((err = hipMemsetAsync(ffs + nseg, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
+    if ((err = hipMemsetAsync(bad, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) return err;
+  }
+  auto* badseg = (uint32_t*)((unsigned long long*)(headw + ((nseg + 2) & ~1)) + 2 * (nseg + 1)) + 64 * (size_t)nseg;
   const unsigned wg = (unsigned)((nseg + ES_WAVES - 1) / ES_WAVES);
   const EsTab* est = reinterpret_cast<const EsTab*>((const char*)tab_dev + sizeof(EntTab));
   if (JDS_ENT_SPLIT) {
     auto* agg = (unsigned long long*)(headw + ((nseg + 2) & ~1));  // 8-B aligned
     auto* segoff = agg + nseg + 1;
     auto* nbits = (uint32_t*)(segoff + nseg + 1);
-    if ((err = hipMemsetAsync(agg + nseg, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
-    hipLaunchKernelGGL(k_ent_walk, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, ovf, nbits, agg, bad);
+    hipLaunchKernelGGL(k_ent_walk, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, ovf, nbits, agg, badseg,
+                       ffs);
     if ((err = hipGetLastError()) != hipSuccess) return err;
     size_t tb0 = sz[7];
     if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb0, agg, segoff, nseg + 1, s)) != hipSuccess) return err;
@@ -1398,8 +1514,14 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
   hipLaunchKernelGGL(k_ent_fix, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, headw, raw, ffs);
   size_t tb = sz[7];
   if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, ffs, ffx, nseg + 1, s)) != hipSuccess) return err;
-  hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, ffx, out, stride);
-  hipLaunchKernelGGL(k_ent_frame2, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, bad);
+  auto* outoff = (unsigned long long*)(headw + ((nseg + 2) & ~1));  // (the split path's segment totals, consumed)
+  hipLaunchKernelGGL(k_ent_offs, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, info, ffx,
+                     outoff);
+  hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
+  if (JDS_ENT_SPLIT)
+    hipLaunchKernelGGL(k_ent_frame3, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, badseg);
+  else
+    hipLaunchKernelGGL(k_ent_frame2, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, bad);
   return hipGetLastError();
 }
 
