@@ -1066,7 +1066,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   for (int d = 32; d > 0; d >>= 1) a += __shfl_xor(a, d, 64);
   if (lane == 0) {
     agg[g] = a;
-    badseg[g] = any_bad ? 1u : 0u;  // not baseline-codable: the frame is reported (k_ent_frame3)
+    badseg[g] = any_bad ? 1u : 0u;  // not baseline-codable: the frame is reported (k_ent_frame4)
     if (g == nseg - 1) {            // the scans' closing zeros (no memsets)
       agg[nseg] = 0ull;
       ffs[nseg] = 0ull;
@@ -1165,6 +1165,110 @@ __global__ void k_ent_offs(const EntGeo e, const int nseg, const unsigned long l
               (ffx[g] - ffx[(long long)q.f * e.sfirst[3] + e.sfirst[q.s]]);
 }
 
+// Per-frame exclusive prefix of a per-segment u64 array (one 1024-thread
+// workgroup per frame; frames' segment ranges are independent): out[g] is
+// frame-relative, tot[f] the frame's total.  OFFS: also each segment's first
+// output byte (what k_ent_offs computes), from the frame's own prefixes.
+// Replaces a hipCUB scan (two launches) and k_ent_offs.
+template <bool OFFS>
+__global__ void __launch_bounds__(1024) k_ent_fscan(const EntGeo e, const unsigned long long* __restrict__ in,
+                                                    unsigned long long* __restrict__ out,
+                                                    unsigned long long* __restrict__ tot,
+                                                    const unsigned long long* __restrict__ desc,
+                                                    const unsigned long long* __restrict__ info,
+                                                    unsigned long long* __restrict__ outoff) {
+  __shared__ unsigned long long s_w[16];
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int n = e.sfirst[3];
+  const long long g0 = (long long)f * n;
+  const int C = (n + 1023) / 1024, i0 = t * C, i1 = min(n, i0 + C);
+  unsigned long long loc = 0ull;
+  for (int i = i0; i < i1; ++i) loc += in[g0 + i];
+  unsigned long long inc = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  unsigned long long base = 0ull, all = 0ull;
+  for (int w = 0; w < 16; ++w) {
+    base += w < wv ? s_w[w] : 0ull;
+    all += s_w[w];
+  }
+  unsigned long long run = base + inc - loc;
+  for (int i = i0; i < i1; ++i) {
+    const unsigned long long v = in[g0 + i];
+    out[g0 + i] = run;
+    run += v;
+  }
+  if (t == 0) tot[f] = all;
+  if constexpr (OFFS) {
+    __syncthreads();  // the frame's prefixes (global, this workgroup's writes) are visible
+    long long so[3];
+    long long p = e.hdr + ENT_SOS;
+    for (int s2 = 0; s2 < 3; ++s2) {
+      so[s2] = p;
+      const unsigned long long nb = (info[2 * (f * 3 + s2) + 1] + 7) >> 3;
+      const unsigned long long ffe = s2 < 2 ? out[g0 + e.sfirst[s2 + 1]] : all;
+      p += (long long)(nb + ffe - out[g0 + e.sfirst[s2]]) + ENT_SOS;
+    }
+    for (int i = t; i < n; i += 1024) {
+      const long long g = g0 + i;
+      const int s2 = i < e.sfirst[1] ? 0 : (i < e.sfirst[2] ? 1 : 2);
+      const int seg = i - e.sfirst[s2];
+      const unsigned long long W0 = seg ? (desc[g - 1] & ES_VAL) : 0ull;
+      outoff[g] = (unsigned long long)so[s2] + 4 * ((W0 + 31) >> 5) + (out[g] - out[g0 + e.sfirst[s2]]);
+    }
+  }
+}
+
+// k_ent_frame with the 0xFF prefixes frame-relative (k_ent_fscan) and the
+// per-segment error flags
+__global__ void k_ent_frame4(const EntGeo e, const uint8_t* __restrict__ hdr, const unsigned long long* __restrict__ info,
+                             const unsigned long long* __restrict__ ffx, const unsigned long long* __restrict__ fftot,
+                             uint8_t* __restrict__ out, long long stride, unsigned long long* __restrict__ lengths,
+                             const uint32_t* __restrict__ badseg) {
+  __shared__ int s_bad;
+  const int f = blockIdx.x;
+  if (threadIdx.x == 0) s_bad = 0;
+  __syncthreads();
+  {
+    int b = 0;
+    for (int i = threadIdx.x; i < e.sfirst[3]; i += blockDim.x) b |= (int)badseg[(long long)f * e.sfirst[3] + i];
+    if (b) s_bad = 1;
+  }
+  __syncthreads();
+  uint8_t* dst = out + (long long)f * stride;
+  for (int i = threadIdx.x; i < e.hdr; i += blockDim.x) dst[i] = hdr[(long long)f * e.hdr + i];
+  const long long g0 = (long long)f * e.sfirst[3];
+  long long so[4];
+  {
+    long long p = e.hdr + ENT_SOS;
+    for (int s2 = 0; s2 < 3; ++s2) {
+      so[s2] = p;
+      const unsigned long long nb = (info[2 * (f * 3 + s2) + 1] + 7) >> 3;
+      const unsigned long long ffe = s2 < 2 ? ffx[g0 + e.sfirst[s2 + 1]] : fftot[f];
+      p += (long long)(nb + ffe - ffx[g0 + e.sfirst[s2]]) + ENT_SOS;
+    }
+    so[3] = p;  // where a fourth scan's data would start
+  }
+  if (threadIdx.x < 3) {
+    const int s2 = threadIdx.x;
+    uint8_t* m = dst + so[s2] - ENT_SOS;
+    const uint8_t sos[ENT_SOS] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(s2 + 1), (uint8_t)(s2 == 0 ? 0x00 : 0x11),
+                                  0x00, 0x3F, 0x00};
+    for (int i = 0; i < ENT_SOS; ++i) m[i] = sos[i];
+  }
+  if (threadIdx.x == 0) {
+    const long long end = so[3] - ENT_SOS;  // end of the Cr scan
+    dst[end] = 0xFF;
+    dst[end + 1] = 0xD9;
+    if (lengths) lengths[f] = s_bad ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
+  }
+}
+
 __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nseg,
                                                    const unsigned long long* __restrict__ desc,
                                                    const unsigned long long* __restrict__ info,
@@ -1250,39 +1354,6 @@ __global__ void k_ent_frame2(const EntGeo e, const uint8_t* __restrict__ hdr, co
     dst[end] = 0xFF;
     dst[end + 1] = 0xD9;
     if (lengths) lengths[f] = bad[f] ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
-  }
-}
-
-__global__ void k_ent_frame3(const EntGeo e, const uint8_t* __restrict__ hdr, const unsigned long long* __restrict__ info,
-                             const unsigned long long* __restrict__ ffx, uint8_t* __restrict__ out, long long stride,
-                             unsigned long long* __restrict__ lengths, const uint32_t* __restrict__ badseg) {
-  __shared__ int s_bad;
-  const int f = blockIdx.x;
-  if (threadIdx.x == 0) s_bad = 0;
-  __syncthreads();
-  {
-    int b = 0;
-    for (int i = threadIdx.x; i < e.sfirst[3]; i += blockDim.x) b |= (int)badseg[(long long)f * e.sfirst[3] + i];
-    if (b) s_bad = 1;
-  }
-  __syncthreads();
-  uint8_t* dst = out + (long long)f * stride;
-  for (int i = threadIdx.x; i < e.hdr; i += blockDim.x) dst[i] = hdr[(long long)f * e.hdr + i];
-  if (threadIdx.x < 3) {
-    const int s = threadIdx.x;
-    uint8_t* m = dst + es_scan_out(e, f, s, info, ffx) - ENT_SOS;
-    const uint8_t sos[ENT_SOS] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(s + 1), (uint8_t)(s == 0 ? 0x00 : 0x11),
-                                  0x00, 0x3F, 0x00};
-    for (int i = 0; i < ENT_SOS; ++i) m[i] = sos[i];
-  }
-  if (threadIdx.x == 0) {
-    const long long g0 = (long long)f * e.sfirst[3];
-    const unsigned long long nb = (info[2 * (f * 3 + 2) + 1] + 7) >> 3;
-    const unsigned long long ff = ffx[g0 + e.sfirst[3]] - ffx[g0 + e.sfirst[2]];
-    const long long end = es_scan_out(e, f, 2, info, ffx) + (long long)(nb + ff);
-    dst[end] = 0xFF;
-    dst[end + 1] = 0xD9;
-    if (lengths) lengths[f] = s_bad ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
   }
 }
 
@@ -1446,7 +1517,7 @@ void ent_sizes(const Geo& g, int n, size_t* sz) {
     sz[0] += sizeof(uint32_t) + sizeof(unsigned long long) * 2 * (nseg + 1) + sizeof(uint32_t) * 65 * nseg;  // JDS_ENT_SPLIT: agg, segoff, nbits, badseg
     sz[1] = sizeof(uint32_t) * ES_MAXW * 64 * nseg;
     sz[4] = sizeof(unsigned long long) * (nseg + 1);
-    sz[5] = sizeof(unsigned long long) * (nseg + 1);
+    sz[5] = sizeof(unsigned long long) * (nseg + 1 + n);  // + the frame totals (k_ent_fscan)
     size_t t1 = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                            (int)(nseg + 1));
@@ -1502,8 +1573,7 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
     hipLaunchKernelGGL(k_ent_walk, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, ovf, nbits, agg, badseg,
                        ffs);
     if ((err = hipGetLastError()) != hipSuccess) return err;
-    size_t tb0 = sz[7];
-    if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb0, agg, segoff, nseg + 1, s)) != hipSuccess) return err;
+    hipLaunchKernelGGL(k_ent_fscan<false>, dim3(n), dim3(1024), 0, s, e, agg, segoff, ffx, nullptr, nullptr, nullptr);
     hipLaunchKernelGGL(k_ent_place, dim3(wg), dim3(256), 0, s, e, nseg, ovf, nbits, segoff, desc, raw, headw, ffs,
                        info, scan_bits);
   } else {
@@ -1512,16 +1582,22 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
   }
   if ((err = hipGetLastError()) != hipSuccess) return err;
   hipLaunchKernelGGL(k_ent_fix, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, headw, raw, ffs);
-  size_t tb = sz[7];
-  if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, ffs, ffx, nseg + 1, s)) != hipSuccess) return err;
   auto* outoff = (unsigned long long*)(headw + ((nseg + 2) & ~1));  // (the split path's segment totals, consumed)
-  hipLaunchKernelGGL(k_ent_offs, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, info, ffx,
-                     outoff);
-  hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
-  if (JDS_ENT_SPLIT)
-    hipLaunchKernelGGL(k_ent_frame3, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, badseg);
-  else
+  if (JDS_ENT_SPLIT) {
+    // frame-relative 0xFF prefixes and each segment's output offset in one launch; frame totals in ffs[nseg ..]
+    unsigned long long* fftot = ffx + nseg + 1;
+    hipLaunchKernelGGL(k_ent_fscan<true>, dim3(n), dim3(1024), 0, s, e, ffs, ffx, fftot, desc, info, outoff);
+    hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
+    hipLaunchKernelGGL(k_ent_frame4, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, fftot, out, stride, lengths,
+                       badseg);
+  } else {
+    size_t tb = sz[7];
+    if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, ffs, ffx, nseg + 1, s)) != hipSuccess) return err;
+    hipLaunchKernelGGL(k_ent_offs, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, info, ffx,
+                       outoff);
+    hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
     hipLaunchKernelGGL(k_ent_frame2, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, bad);
+  }
   return hipGetLastError();
 }
 
