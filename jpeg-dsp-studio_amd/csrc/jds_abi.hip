@@ -592,8 +592,14 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
   }
   // Border tiles run on the plan's own stream after the interior tiles unless
   // JDS_SIDE_STREAM=1 asks for the fork/join onto a side stream (A/B: tools/ab_probe.py).
+  // JDS_REDUCE_SIDE=1 runs the statistics reduction beside the fix-up on the
+  // side stream (A/B: 0.627 vs 0.617 ms per 64 x 1080p step -- the fork / join
+  // costs more than the overlap returns; off by default).
   const char* side_env = getenv("JDS_SIDE_STREAM");
-  if (side_env && side_env[0] == '1' &&
+  const char* red_env = getenv("JDS_REDUCE_SIDE");
+  p->side.border = side_env && side_env[0] == '1';
+  p->side.reduce = red_env && red_env[0] == '1';
+  if ((p->side.border || p->side.reduce) &&
       ((e = hipStreamCreateWithFlags(&p->side.stream, hipStreamNonBlocking)) != hipSuccess ||
        (e = hipEventCreateWithFlags(&p->side.fork, hipEventDisableTiming)) != hipSuccess ||
        (e = hipEventCreateWithFlags(&p->side.join, hipEventDisableTiming)) != hipSuccess)) {

@@ -1955,7 +1955,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   hipError_t e;
   if (split) {
     const int nin = (rect.y - rect.x + 1) * (rect.w - rect.z + 1), nout = g.tiles_y * g.tiles_x - nin;
-    const bool fork = side && side->stream && nout > 0;
+    const bool fork = side && side->stream && side->border && nout > 0;
     hipStream_t sb = fork ? side->stream : s;
     if (fork && ((e = hipEventRecord(side->fork, s)) != hipSuccess ||
                  (e = hipStreamWaitEvent(sb, side->fork, 0)) != hipSuccess))
@@ -2004,15 +2004,26 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ptiles + FIX_RED_TILES - 1) / FIX_RED_TILES, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk,
                        st, fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ptiles, gx);
 #else
+    // the reduction and the fix-up are independent (both add into the frame
+    // stats with atomics; the fix-up reads only its list): the reduction runs
+    // on the plan's side stream beside the latency-bound fix-up, joined before
+    // the next launch on s
+    const bool rfork = side && side->stream && side->reduce;
+    hipStream_t rs = rfork ? side->stream : s;
+    if (rfork && ((e = hipEventRecord(side->fork, s)) != hipSuccess ||
+                  (e = hipStreamWaitEvent(rs, side->fork, 0)) != hipSuccess))
+      return e;
     if constexpr (FLUSH_ROWS && C::TF < JDS_FLUSH_BARRIER_TF) {
       hipLaunchKernelGGL(k_fwd_reduce_rows<4 * (C::TF / 64)>, dim3((ptiles + RROWS_TILES - 1) / RROWS_TILES, n),
-                         dim3(256), 0, s, g, st, part, ptiles);
+                         dim3(256), 0, rs, g, st, part, ptiles);
       if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else if ((e = launch_fwd_reduce(n, st, part, ptiles, s)) != hipSuccess) {
+    } else if ((e = launch_fwd_reduce(n, st, part, ptiles, rs)) != hipSuccess) {
       return e;
     }
+    if (rfork && (e = hipEventRecord(side->join, rs)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
+    if (rfork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
 #endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;

@@ -70,6 +70,8 @@ __host__ __device__ inline int fix_wpi(const Geo& g) { return (int)((g.cpf / 64 
 struct Side {
   hipStream_t stream = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  bool border = false;  // border tiles beside the interior tiles (JDS_SIDE_STREAM=1)
+  bool reduce = false;  // statistics reduction beside the fix-up (JDS_REDUCE_SIDE=1; measured slower, off)
 };
 
 // Buffers of the certified 16x16 forward (jds_fast16.hip): per-frame fp32
