@@ -8,25 +8,25 @@
 // Cr; a non-interleaved scan's raster block order is exactly the reference's
 // block order).  Byte-for-byte definition: oracle/jpeg_entropy.py.
 //
-// Integer / byte work, HBM-bound by design.  Pipeline per batch of frames:
-//   k_ent_bits   one lane per 8x8 block: coefficients in registers, the
-//                zigzag walk unrolled at compile time, Huffman code lengths
-//                from LDS tables -> bits per block.  Coefficients the
-//                baseline tables cannot code are clamped (bounded output)
-//                and flag the frame.
-//   scan         exclusive prefix of block bits (hipCUB) -> bit offsets.
-//   k_ent_info   per scan: start offset, bit and byte counts.
-//   k_ent_zero   zero each block's first/last 32-bit word of the packed scan.
-//   k_ent_pack   the same walk, packing MSB-first into 32-bit words from the
-//                block's bit offset: plain stores for the block's own words,
-//                atomic OR for the first / last word it may share with
-//                neighbouring blocks.
-//   k_ent_ff     per 1 KiB chunk of a scan: 0xFF bytes (after the 1-bit pad).
-//   scan         exclusive prefix of the 0xFF counts -> stuffed offsets.
-//   k_ent_emit   chunk bytes -> the JFIF at their stuffed offsets (0x00 after
-//                every 0xFF).
-//   k_ent_frame  headers (host-built template: SOI, APP0, DQT, SOF0, DHT),
+// Integer / byte work.  Pipeline per batch of frames (segments = 64
+// consecutive blocks of one scan, one wave each; DESIGN.md §4 "Round 4: one
+// pass"):
+//   k_ent_walk   each lane codes its block (zigzag walk, T.81 Annex K tables,
+//                left-aligned symbols appended by funnel shifts) into staging
+//                words; per-lane bit counts and per-segment totals.
+//   k_ent_fscan  per frame: each segment's bit offset within its scan.
+//   k_ent_place  each lane's words shifted into place in the packed scan
+//                (shared words combined by a segmented OR across the wave),
+//                the scan's pad bits, the 0xFF bytes per segment.
+//   k_ent_fix    words whose first bit the previous segment holds.
+//   k_ent_fscan  per frame: 0xFF prefixes and every segment's output offset.
+//   k_ent_emit3  stuffed copy to the file (0x00 after every 0xFF).
+//   k_ent_frame4 headers (host-built template: SOI, APP0, DQT, SOF0, DHT),
 //                the three SOS markers, EOI, file length.
+// (The rounds 1-3 multi-pass coder -- a counting walk, a block scan, a packing
+// walk with LDS atomics, per-chunk stuffing -- measured 0.54 ms per 64 x 1080p
+// against this one's 0.30; it is retired.  JDS_ENT_SPLIT=0 keeps the one-launch
+// form with a decoupled look-back, k_ent_seg.)
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -164,21 +164,11 @@ struct EntGeo {
   int sfirst[4];   // single-pass coder: first 64-block segment of each scan within the frame, sfirst[3] = per frame
   int cap_w[3];    // packed-scan capacity in 32-bit words (worst case 1660 bits per block)
   long long raw_w; // packed words per frame
-  int chunks;      // 1 KiB chunks per scan (worst-case Y scan)
   long long hdr;   // header template bytes per frame
 };
 
-__device__ __forceinline__ int scan_of(const EntGeo& e, int b) { return b < e.first[1] ? 0 : (b < e.first[2] ? 1 : 2); }
-
 __device__ __forceinline__ long long raw_base(const EntGeo& e, int frame, int s) {
   return (long long)frame * e.raw_w + (s == 0 ? 0 : (s == 1 ? e.cap_w[0] : e.cap_w[0] + e.cap_w[1]));
-}
-
-__device__ __forceinline__ void load_tab(const EntTab* __restrict__ g, EntTab* s) {
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(s);
-  for (int i = threadIdx.x; i < (int)(sizeof(EntTab) / 4); i += blockDim.x) dst[i] = src[i];
-  __syncthreads();
 }
 
 // The code of lane k (zigzag position k) of a block: `v` its coefficient,
@@ -220,402 +210,15 @@ __device__ __forceinline__ int coef_at(const BlockRegs& r) {
   return (int)(int16_t)((IDX & 1) ? (r.w[IDX >> 1] >> 16) : (r.w[IDX >> 1] & 0xFFFFu));
 }
 
-// Bit sink: COUNT only counts; otherwise bits are packed MSB-first into 32-bit
-// words starting `n` bits into word *dst.
-//  * global target: the first and the last (partial) word may be shared with
-//    neighbouring blocks -> atomic OR (k_ent_zero cleared them); the words in
-//    between are this block's alone -> plain stores (byte-swapped: stream order).
-//  * LDS target (wave window): every word is OR-ed (ds_or_b32), native order.
-enum SinkMode { SINK_COUNT = 0, SINK_GLOBAL = 1, SINK_LDS = 2 };
-
-template <int MODE>
-struct BitSink {
-  uint64_t acc = 0;
-  int n = 0;
-  int total = 0;
-  uint32_t* dst = nullptr;
-  bool first = true;
-  __device__ __forceinline__ void put(uint32_t v, int len) {
-    total += len;
-    if constexpr (MODE != SINK_COUNT) {
-      acc = (acc << len) | v;
-      n += len;
-      if (n >= 32) {
-        n -= 32;
-        const uint32_t word = (uint32_t)(acc >> n);
-        if constexpr (MODE == SINK_LDS) {
-          atomicOr(dst, word);
-        } else {
-          const uint32_t sw = __builtin_bswap32(word);  // byte 0 of the stream first
-          if (first) atomicOr(dst, sw); else *dst = sw;
-        }
-        first = false;
-        ++dst;
-      }
-    }
-  }
-  __device__ __forceinline__ void finish() {
-    if constexpr (MODE == SINK_LDS) {
-      if (n > 0) atomicOr(dst, (uint32_t)(acc << (32 - n)));
-    } else if constexpr (MODE == SINK_GLOBAL) {
-      if (n > 0) atomicOr(dst, __builtin_bswap32((uint32_t)(acc << (32 - n))));
-    }
-  }
-};
-
 constexpr uint8_t ZZC[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
                              12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
                              35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                              58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-template <int K, int MODE>
-__device__ __forceinline__ void code_ac(const BlockRegs& r, int& last, const uint32_t* act, BitSink<MODE>& o,
-                                        bool& bad) {
-  if constexpr (K < 64) {
-    const int v = coef_at<ZZC[K]>(r);
-    if (v != 0) {
-      const int run = K - last - 1;
-      const uint32_t z = act[0xF0];
-      for (int i = 0; i < (run >> 4); ++i) o.put(z & 0xFFFFu, (int)(z >> 16));  // ZRL: 16 zeros
-      const int a = v < 0 ? -v : v;
-      int s = 32 - __clz(a);
-      bad |= s > 10;
-      s = s > 10 ? 10 : s;
-      const uint32_t e = act[((run & 15) << 4) | s];
-      o.put(e & 0xFFFFu, (int)(e >> 16));
-      o.put((uint32_t)((v < 0 ? v - 1 : v) & ((1 << s) - 1)), s);
-      last = K;
-    }
-    code_ac<K + 1, MODE>(r, last, act, o, bad);
-  }
-}
-
-// T.81 F.1.2 for one block; `pred` = the DC of the previous block of the scan (0 at its start)
-template <int MODE>
-__device__ __forceinline__ void code_block(const BlockRegs& r, int pred, const uint32_t* dct, const uint32_t* act,
-                                           BitSink<MODE>& o, bool& bad) {
-  const int diff = coef_at<0>(r) - pred;
-  const int a = diff < 0 ? -diff : diff;
-  int s = a ? 32 - __clz(a) : 0;
-  bad = s > 11;
-  s = s > 11 ? 11 : s;
-  const uint32_t e = dct[s];
-  o.put(e & 0xFFFFu, (int)(e >> 16));
-  o.put((uint32_t)((diff < 0 ? diff - 1 : diff) & ((1 << s) - 1)), s);
-  int last = 0;
-  code_ac<1, MODE>(r, last, act, o, bad);
-  if (last < 63) {  // EOB
-    const uint32_t eob = act[0x00];
-    o.put(eob & 0xFFFFu, (int)(eob >> 16));
-  }
-  o.finish();
-}
-
-template <int K>
-__device__ __forceinline__ void ac_bits(const BlockRegs& r, int& last, int& amax, uint32_t& nb, const uint16_t* tb) {
-  if constexpr (K < 64) {
-    const int v = coef_at<ZZC[K]>(r);
-    const int a = v < 0 ? -v : v;
-    amax = a > amax ? a : amax;
-    const int sz = a ? 32 - __clz(a) : 0;
-    nb += tb[((K - 1 - last) << 5) | sz];
-    last = a ? K : last;
-    ac_bits<K + 1>(r, last, amax, nb, tb);
-  }
-}
-
-__global__ void __launch_bounds__(256) k_ent_bits(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
-                                                  const EntTab* __restrict__ gt, unsigned long long* __restrict__ bits,
-                                                  unsigned long long* __restrict__ bad) {
-  __shared__ EntTab t;
-  load_tab(gt, &t);  // once per workgroup: the grid strides over the blocks
-  for (long long gb = (long long)blockIdx.x * blockDim.x + threadIdx.x; gb < nblk; gb += (long long)gridDim.x * blockDim.x) {
-    const int frame = (int)(gb / e.nb), b = (int)(gb - (long long)frame * e.nb);
-    const int s = scan_of(e, b);
-    const BlockRegs r = load_block(coeffs + gb * 64);
-    const int pred = b == e.first[s] ? 0 : (int)coeffs[(gb - 1) * 64];
-    BitSink<SINK_COUNT> o;
-    bool bd;
-    code_block<SINK_COUNT>(r, pred, t.dc[s ? 1 : 0], t.ac[s ? 1 : 0], o, bd);
-    bits[gb] = (unsigned long long)o.total;
-    if (bd) bad[frame] = 1ull;  // not baseline-codable: the frame is reported
-  }
-}
-
-// k_ent_bits2: the same bit counts without the walk's branches.  Per table
-// class, bl[run * 32 + s] = the bits a nonzero coefficient of size s after
-// `run` zeros costs: (run >> 4) ZRL codes + the (run & 15, min(s, 10)) code +
-// min(s, 10) magnitude bits (the clamp of code_ac); bl[run * 32 + 0] = 0, so a
-// zero coefficient adds nothing and every zigzag position runs the same
-// branch-free ops: size, one LDS lookup, an add, a select for the last
-// nonzero.  The AC error flag comes from the largest magnitude.
-#ifndef JDS_ENT_BITS_TABLE
-#define JDS_ENT_BITS_TABLE 1
-#endif
-constexpr int ENT_BL = 64 * 32;  // entries per table class
-
-__global__ void __launch_bounds__(256) k_ent_bits2(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
-                                                   const EntTab* __restrict__ gt, unsigned long long* __restrict__ bits,
-                                                   unsigned long long* __restrict__ bad) {
-  __shared__ EntTab t;
-  __shared__ uint16_t bl[2][ENT_BL];
-  load_tab(gt, &t);
-  for (int i = threadIdx.x; i < 2 * ENT_BL; i += blockDim.x) {
-    const int c = i / ENT_BL, run = (i % ENT_BL) >> 5, sz = i & 31;
-    uint32_t v = 0;
-    if (sz) {
-      const int sc = sz > 10 ? 10 : sz;
-      const uint32_t code = t.ac[c][((run & 15) << 4) | sc], zrl = t.ac[c][0xF0];
-      v = (uint32_t)(run >> 4) * (zrl >> 16) + (code >> 16) + (uint32_t)sc;
-    }
-    bl[c][i % ENT_BL] = (uint16_t)v;
-  }
-  __syncthreads();
-  for (long long gb = (long long)blockIdx.x * blockDim.x + threadIdx.x; gb < nblk; gb += (long long)gridDim.x * blockDim.x) {
-    const int frame = (int)(gb / e.nb), b = (int)(gb - (long long)frame * e.nb);
-    const int s = scan_of(e, b);
-    const BlockRegs r = load_block(coeffs + gb * 64);
-    const int pred = b == e.first[s] ? 0 : (int)coeffs[(gb - 1) * 64];
-    const uint16_t* tb = bl[s ? 1 : 0];
-    const uint32_t* dct = t.dc[s ? 1 : 0];
-    const int diff = coef_at<0>(r) - pred;
-    const int da = diff < 0 ? -diff : diff;
-    int ds = da ? 32 - __clz(da) : 0;
-    bool bd = ds > 11;
-    ds = ds > 11 ? 11 : ds;
-    uint32_t nb = (dct[ds] >> 16) + (uint32_t)ds;
-    int last = 0, amax = 0;
-    ac_bits<1>(r, last, amax, nb, tb);
-    if (last < 63) nb += t.ac[s ? 1 : 0][0x00] >> 16;  // EOB
-    bd |= amax > 1023;                                  // size > 10
-    bits[gb] = (unsigned long long)nb;
-    if (bd) bad[frame] = 1ull;  // not baseline-codable: the frame is reported
-  }
-}
-
-// info[(f*3+s)*2 + 0] = scan start (global bit prefix), [1] = scan bits
-__global__ void k_ent_info(const EntGeo e, int n, const unsigned long long* __restrict__ excl,
-                           unsigned long long* __restrict__ info, unsigned long long* __restrict__ scan_bits) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n * 3) return;
-  const int f = i / 3, s = i - f * 3;
-  const unsigned long long a = excl[(long long)f * e.nb + e.first[s]], b = excl[(long long)f * e.nb + e.first[s + 1]];
-  info[2 * i] = a;
-  info[2 * i + 1] = b - a;
-  if (scan_bits) scan_bits[i] = b - a;
-}
-
-__global__ void __launch_bounds__(256) k_ent_zero(const EntGeo e, long long nblk, const unsigned long long* __restrict__ bits,
-                                                  const unsigned long long* __restrict__ excl,
-                                                  const unsigned long long* __restrict__ info, uint32_t* __restrict__ raw) {
-  const long long gb = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gb >= nblk) return;
-  const int f = (int)(gb / e.nb), s = scan_of(e, (int)(gb - (long long)f * e.nb));
-  const unsigned long long rel = excl[gb] - info[2 * (f * 3 + s)];
-  uint32_t* w = raw + raw_base(e, f, s);
-  w[rel >> 5] = 0u;
-  w[(rel + bits[gb] - 1) >> 5] = 0u;
-}
-
-
-// One lane per block, 64 consecutive blocks per wave.  Their bits are
-// contiguous within a scan, so the wave assembles them in an LDS window
-// (ds_or: neighbouring lanes share boundary words) and writes the window with
-// coalesced stores; only the window's first and last words, shared with the
-// neighbouring waves, need global atomics.  Waves that straddle a scan
-// boundary or overflow the window write each block straight to global memory.
-constexpr int ENT_WIN = 2048;  // words per wave (64 blocks at <= 1024 bits each)
-
-__global__ void __launch_bounds__(256) k_ent_pack(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
-                                                  const EntTab* __restrict__ gt,
-                                                  const unsigned long long* __restrict__ bits,
-                                                  const unsigned long long* __restrict__ excl,
-                                                  const unsigned long long* __restrict__ info,
-                                                  uint32_t* __restrict__ raw) {
-  __shared__ EntTab t;
-  __shared__ uint32_t s_win[4][ENT_WIN];
-  load_tab(gt, &t);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t* win = s_win[wv];
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long g0 = ((long long)blockIdx.x * 4 + wv) * 64; g0 < nblk; g0 += stride) {
-    const long long gb = g0 + lane;
-    const bool valid = gb < nblk;
-    const long long gl = (nblk - g0 < 64 ? nblk : g0 + 64) - 1;  // last block of the wave
-    const int frame = (int)((valid ? gb : gl) / e.nb), b = (int)((valid ? gb : gl) - (long long)frame * e.nb);
-    const int s = scan_of(e, b);
-    const unsigned long long base = info[2 * (frame * 3 + s)];
-    const unsigned long long rel = (valid ? excl[gb] : excl[gl]) - base;
-    // wave-uniform: one scan, and the window holds the wave's words?
-    const int f0 = (int)(g0 / e.nb), fl = (int)(gl / e.nb);
-    const int s0 = scan_of(e, (int)(g0 - (long long)f0 * e.nb)), sl = scan_of(e, (int)(gl - (long long)fl * e.nb));
-    const unsigned long long rel0 = __shfl(rel, 0, 64);
-    const unsigned long long end = excl[gl] + bits[gl] - base;  // same scan as lane 0 when f0 == fl && s0 == sl
-    const long long w0 = (long long)(rel0 >> 5), nw = (long long)((end + 31) >> 5) - w0;
-    const bool fast = f0 == fl && s0 == sl && nw <= ENT_WIN;
-    BlockRegs r;
-    int pred = 0;
-    if (valid) {
-      r = load_block(coeffs + gb * 64);
-      pred = b == e.first[s] ? 0 : (int)coeffs[(gb - 1) * 64];
-    }
-    bool bd;
-    if (fast) {
-      for (int i = lane; i < nw; i += 64) win[i] = 0u;
-      __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations execute in order
-      asm volatile("" ::: "memory");
-      if (valid) {
-        BitSink<SINK_LDS> o;
-        o.dst = win + ((long long)(rel >> 5) - w0);
-        o.n = (int)(rel & 31);
-        code_block<SINK_LDS>(r, pred, t.dc[s ? 1 : 0], t.ac[s ? 1 : 0], o, bd);
-      }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");
-      uint32_t* dst = raw + raw_base(e, f0, s0) + w0;
-      for (int i = lane; i < nw; i += 64) {
-        const uint32_t w = __builtin_bswap32(win[i]);
-        if (i == 0 || i == nw - 1) atomicOr(dst + i, w); else dst[i] = w;
-      }
-      __builtin_amdgcn_wave_barrier();  // the window is reused by the next iteration
-      asm volatile("" ::: "memory");
-    } else if (valid) {
-      BitSink<SINK_GLOBAL> o;
-      o.dst = raw + raw_base(e, frame, s) + (rel >> 5);
-      o.n = (int)(rel & 31);
-      code_block<SINK_GLOBAL>(r, pred, t.dc[s ? 1 : 0], t.ac[s ? 1 : 0], o, bd);
-    }
-  }
-}
-
-// k_ent_pack2: k_ent_pack's wave windows with the walk made branch-free for
-// the common symbols.  Per table class, pk[run * 32 + s] = (length << 16) |
-// code of the (run, s) symbol for run < 16 (s clamped to 10 as code_ac does),
-// 0 for s = 0: a zero coefficient appends nothing.  Every zigzag position
-// appends code << s | magnitude (<= 26 bits) to a 64-bit accumulator and
-// ORs one window word (0 when fewer than 32 bits are pending: no branch); only
-// ZRL codes (a nonzero after >= 16 zeros) take a branch.
-#ifndef JDS_ENT_PACK_TABLE
-#define JDS_ENT_PACK_TABLE 1
-#endif
-struct PackAcc {
-  uint64_t acc;
-  int n;
-  uint32_t* dst;
-  __device__ __forceinline__ void put(uint32_t v, int len) {  // len <= 32
-    acc = (acc << len) | v;
-    n += len;
-    const bool f = n >= 32;
-    const uint32_t w = (uint32_t)(acc >> (f ? n - 32 : 0));
-    atomicOr(dst, f ? w : 0u);  // ds_or_b32
-    dst += f ? 1 : 0;
-    n -= f ? 32 : 0;
-  }
-};
-
-template <int K>
-__device__ __forceinline__ void ac_pack(const BlockRegs& r, int& last, PackAcc& o, const uint32_t* pk, uint32_t zrl) {
-  if constexpr (K < 64) {
-    const int v = coef_at<ZZC[K]>(r);
-    const int a = v < 0 ? -v : v;
-    int sz = a ? 32 - __clz(a) : 0;
-    sz = sz > 10 ? 10 : sz;
-    int run = K - 1 - last;
-    if (a && run >= 16) {  // rare: one ZRL code per 16 zeros first
-      for (; run >= 16; run -= 16) o.put(zrl & 0xFFFFu, (int)(zrl >> 16));
-    }
-    const uint32_t e = pk[((run & 15) << 5) | sz];
-    const uint32_t mag = (uint32_t)(v < 0 ? v - 1 : v) & ((1u << sz) - 1u);
-    o.put(((e & 0xFFFFu) << sz) | mag, (int)(e >> 16) + sz);
-    last = a ? K : last;
-    ac_pack<K + 1>(r, last, o, pk, zrl);
-  }
-}
-
-__global__ void __launch_bounds__(256) k_ent_pack2(const EntGeo e, long long nblk, const int16_t* __restrict__ coeffs,
-                                                   const EntTab* __restrict__ gt,
-                                                   const unsigned long long* __restrict__ bits,
-                                                   const unsigned long long* __restrict__ excl,
-                                                   const unsigned long long* __restrict__ info,
-                                                   uint32_t* __restrict__ raw) {
-  __shared__ EntTab t;
-  __shared__ uint32_t pkt[2][16 * 32];
-  __shared__ uint32_t s_win[4][ENT_WIN];
-  load_tab(gt, &t);
-  for (int i = threadIdx.x; i < 2 * 16 * 32; i += blockDim.x) {
-    const int c = i >> 9, run = (i >> 5) & 15, sz = i & 31;
-    pkt[c][i & 511] = sz ? t.ac[c][(run << 4) | (sz > 10 ? 10 : sz)] : 0u;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t* win = s_win[wv];
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long g0 = ((long long)blockIdx.x * 4 + wv) * 64; g0 < nblk; g0 += stride) {
-    const long long gb = g0 + lane;
-    const bool valid = gb < nblk;
-    const long long gl = (nblk - g0 < 64 ? nblk : g0 + 64) - 1;  // last block of the wave
-    const int frame = (int)((valid ? gb : gl) / e.nb), b = (int)((valid ? gb : gl) - (long long)frame * e.nb);
-    const int s = scan_of(e, b);
-    const unsigned long long base = info[2 * (frame * 3 + s)];
-    const unsigned long long rel = (valid ? excl[gb] : excl[gl]) - base;
-    const int f0 = (int)(g0 / e.nb), fl = (int)(gl / e.nb);
-    const int s0 = scan_of(e, (int)(g0 - (long long)f0 * e.nb)), sl = scan_of(e, (int)(gl - (long long)fl * e.nb));
-    const unsigned long long rel0 = __shfl(rel, 0, 64);
-    const unsigned long long end = excl[gl] + bits[gl] - base;
-    const long long w0 = (long long)(rel0 >> 5), nw = (long long)((end + 31) >> 5) - w0;
-    const bool fast = f0 == fl && s0 == sl && nw <= ENT_WIN;
-    BlockRegs r;
-    int pred = 0;
-    if (valid) {
-      r = load_block(coeffs + gb * 64);
-      pred = b == e.first[s] ? 0 : (int)coeffs[(gb - 1) * 64];
-    }
-    bool bd;
-    if (fast) {
-      for (int i = lane; i < nw; i += 64) win[i] = 0u;
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");
-      if (valid) {
-        const int cls = s ? 1 : 0;
-        PackAcc o{0ull, (int)(rel & 31), win + ((long long)(rel >> 5) - w0)};
-        const int diff = coef_at<0>(r) - pred;
-        const int da = diff < 0 ? -diff : diff;
-        int ds = da ? 32 - __clz(da) : 0;
-        ds = ds > 11 ? 11 : ds;
-        const uint32_t dc = t.dc[cls][ds];
-        o.put(((dc & 0xFFFFu) << ds) | ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << ds) - 1u)),
-              (int)(dc >> 16) + ds);
-        int last = 0;
-        ac_pack<1>(r, last, o, pkt[cls], t.ac[cls][0xF0]);
-        if (last < 63) {
-          const uint32_t eob = t.ac[cls][0x00];
-          o.put(eob & 0xFFFFu, (int)(eob >> 16));
-        }
-        if (o.n > 0) atomicOr(o.dst, (uint32_t)(o.acc << (32 - o.n)));
-      }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");
-      uint32_t* dst = raw + raw_base(e, f0, s0) + w0;
-      for (int i = lane; i < nw; i += 64) {
-        const uint32_t w = __builtin_bswap32(win[i]);
-        if (i == 0 || i == nw - 1) atomicOr(dst + i, w); else dst[i] = w;
-      }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");
-    } else if (valid) {
-      BitSink<SINK_GLOBAL> o;
-      o.dst = raw + raw_base(e, frame, s) + (rel >> 5);
-      o.n = (int)(rel & 31);
-      code_block<SINK_GLOBAL>(r, pred, t.dc[s ? 1 : 0], t.ac[s ? 1 : 0], o, bd);
-    }
-  }
-}
-
 // ------------------------------------------------ single pass (round 4) --
 //
-// k_ent_seg replaces k_ent_bits, the block scan, k_ent_info, k_ent_zero and
-// k_ent_pack (JDS_ENT_FUSED): one wave per segment of 64 consecutive blocks of
-// one scan, segments in launch order.
+// k_ent_seg (JDS_ENT_SPLIT=0): one wave per segment of 64 consecutive blocks
+// of one scan, segments in launch order.
 //  * walk: each lane packs its block MSB-first into lane-private staging
 //    words (LDS, word-major across the wave's lanes so every store hits its
 //    own bank; words past ES_SW spill to a per-block global area), so the
@@ -636,9 +239,6 @@ __global__ void __launch_bounds__(256) k_ent_pack2(const EntGeo e, long long nbl
 //    with 1-bits (T.81 F.1.2.3), so the stuffing pass reads final words.
 // A segment that is not the last of its scan holds >= 256 bits (every block
 // costs >= 4), so only consecutive segments share a word.
-#ifndef JDS_ENT_FUSED
-#define JDS_ENT_FUSED 1
-#endif
 #ifndef JDS_ENT_WPE
 #define JDS_ENT_WPE 4  // waves per SIMD the walk's registers are held to (the scheduler hoists lookups freely)
 #endif
@@ -1357,124 +957,6 @@ __global__ void k_ent_frame2(const EntGeo e, const uint8_t* __restrict__ hdr, co
   }
 }
 
-constexpr int ENT_CH = 1024;  // bytes per stuffing chunk (256 threads x 4)
-
-// byte i of scan (f, s) with the 1-bit pad applied (T.81 F.1.2.3)
-__device__ __forceinline__ uint32_t scan_word(const uint32_t* w, int i4, unsigned long long nbits) {
-  const unsigned long long nbytes = (nbits + 7) >> 3;
-  uint32_t x = w[i4];
-  const unsigned long long last = nbytes - 1;
-  if ((nbits & 7) && (unsigned long long)i4 == (last >> 2)) {
-    const int pad = 8 - (int)(nbits & 7);
-    x |= ((1u << pad) - 1u) << (8 * (int)(last & 3));
-  }
-  return x;
-}
-
-// grid (CG, 3, n): workgroups stride over the chunks a scan actually has (ffc
-// is zeroed beforehand for the rest)
-__global__ void __launch_bounds__(256) k_ent_ff(const EntGeo e, const unsigned long long* __restrict__ info,
-                                                const uint32_t* __restrict__ raw, unsigned long long* __restrict__ ffc) {
-  __shared__ int s_red[2][4];
-  const int s = blockIdx.y, f = blockIdx.z;
-  const unsigned long long nbits = info[2 * (f * 3 + s) + 1], nbytes = (nbits + 7) >> 3;
-  const long long nch = (long long)((nbytes + ENT_CH - 1) / ENT_CH);
-  const uint32_t* w = raw + raw_base(e, f, s);
-  int par = 0;
-  for (long long c = blockIdx.x; c < nch; c += gridDim.x, par ^= 1) {
-    const long long i0 = c * ENT_CH + 4 * threadIdx.x;
-    int cnt = 0;
-    if ((unsigned long long)i0 < nbytes) {
-      const uint32_t x = scan_word(w, (int)(i0 >> 2), nbits);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        cnt += ((unsigned long long)(i0 + k) < nbytes && ((x >> (8 * k)) & 255u) == 255u) ? 1 : 0;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-    if ((threadIdx.x & 63) == 0) s_red[par][threadIdx.x >> 6] = cnt;  // double-buffered: one barrier per chunk
-    __syncthreads();
-    if (threadIdx.x == 0)
-      ffc[((long long)f * 3 + s) * e.chunks + c] =
-          (unsigned long long)(s_red[par][0] + s_red[par][1] + s_red[par][2] + s_red[par][3]);
-  }
-}
-
-// output offset of scan s of frame f (after its SOS marker)
-__device__ __forceinline__ long long scan_out(const EntGeo& e, int f, int s, const unsigned long long* info,
-                                              const unsigned long long* ffx) {
-  long long p = e.hdr + ENT_SOS;
-  for (int j = 0; j < s; ++j) {
-    const unsigned long long nb = (info[2 * (f * 3 + j) + 1] + 7) >> 3;
-    const unsigned long long ff = ffx[((long long)f * 3 + j + 1) * e.chunks] - ffx[((long long)f * 3 + j) * e.chunks];
-    p += (long long)(nb + ff) + ENT_SOS;
-  }
-  return p;
-}
-
-__global__ void __launch_bounds__(256) k_ent_emit(const EntGeo e, const unsigned long long* __restrict__ info,
-                                                  const uint32_t* __restrict__ raw,
-                                                  const unsigned long long* __restrict__ ffx, uint8_t* __restrict__ out,
-                                                  long long stride) {
-  __shared__ int s_w[2][4];
-  const int s = blockIdx.y, f = blockIdx.z;
-  const unsigned long long nbits = info[2 * (f * 3 + s) + 1], nbytes = (nbits + 7) >> 3;
-  const long long nch = (long long)((nbytes + ENT_CH - 1) / ENT_CH);
-  const uint32_t* w = raw + raw_base(e, f, s);
-  const long long cidx = ((long long)f * 3 + s) * e.chunks;
-  const long long sbase = scan_out(e, f, s, info, ffx);
-  uint8_t* dst = out + (long long)f * stride;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int par = 0;
-  for (long long c = blockIdx.x; c < nch; c += gridDim.x, par ^= 1) {
-    const long long i0 = c * ENT_CH + 4 * threadIdx.x;
-    uint32_t x = 0;
-    int nv = 0, ff = 0;
-    if ((unsigned long long)i0 < nbytes) {
-      x = scan_word(w, (int)(i0 >> 2), nbits);
-      nv = nbytes - i0 < 4 ? (int)(nbytes - i0) : 4;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ff += (k < nv && ((x >> (8 * k)) & 255u) == 255u) ? 1 : 0;
-    }
-    // exclusive prefix of ff over the workgroup (double-buffered partials: one barrier per chunk)
-    const int ex = wave_excl_sum(ff, lane);
-    if (lane == 63) s_w[par][wv] = ex + ff;
-    __syncthreads();
-    int base = 0;
-    for (int i = 0; i < wv; ++i) base += s_w[par][i];
-    long long o = sbase + i0 + (long long)(ffx[cidx + c] - ffx[cidx]) + base + ex;
-    for (int k = 0; k < nv; ++k) {
-      const uint8_t b = (uint8_t)(x >> (8 * k));
-      dst[o++] = b;
-      if (b == 0xFF) dst[o++] = 0x00;
-    }
-  }
-}
-
-__global__ void k_ent_frame(const EntGeo e, const uint8_t* __restrict__ hdr, const unsigned long long* __restrict__ info,
-                            const unsigned long long* __restrict__ ffx, uint8_t* __restrict__ out, long long stride,
-                            unsigned long long* __restrict__ lengths, const unsigned long long* __restrict__ bad) {
-  const int f = blockIdx.x;
-  uint8_t* dst = out + (long long)f * stride;
-  for (int i = threadIdx.x; i < e.hdr; i += blockDim.x) dst[i] = hdr[(long long)f * e.hdr + i];
-  if (threadIdx.x < 3) {
-    const int s = threadIdx.x;
-    uint8_t* m = dst + scan_out(e, f, s, info, ffx) - ENT_SOS;
-    const uint8_t sos[ENT_SOS] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(s + 1), (uint8_t)(s == 0 ? 0x00 : 0x11),
-                                  0x00, 0x3F, 0x00};
-    for (int i = 0; i < ENT_SOS; ++i) m[i] = sos[i];
-  }
-  if (threadIdx.x == 0) {
-    // end of the Cr scan = start of a fourth scan minus its SOS
-    const unsigned long long nb = (info[2 * (f * 3 + 2) + 1] + 7) >> 3;
-    const unsigned long long ff = ffx[((long long)f * 3 + 3) * e.chunks] - ffx[((long long)f * 3 + 2) * e.chunks];
-    const long long end = scan_out(e, f, 2, info, ffx) + (long long)(nb + ff);
-    dst[end] = 0xFF;
-    dst[end + 1] = 0xD9;
-    if (lengths) lengths[f] = bad[f] ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
-  }
-}
-
 // ------------------------------------------------------------ driver --
 
 EntGeo ent_geo(const Geo& g) {
@@ -1490,7 +972,6 @@ EntGeo ent_geo(const Geo& g) {
   e.cap_w[0] = (int)(((long long)ny * 1660 + 31) / 32) + 2;
   e.cap_w[1] = e.cap_w[2] = (int)(((long long)nc * 1660 + 31) / 32) + 2;
   e.raw_w = (long long)e.cap_w[0] + 2LL * e.cap_w[1];
-  e.chunks = (int)(((long long)e.cap_w[0] * 4 + ENT_CH - 1) / ENT_CH);
   e.hdr = ENT_HDR;
   return e;
 }
@@ -1501,40 +982,26 @@ long long ent_capacity(const Geo& g) {
   return e.hdr + 3 * ENT_SOS + 2 * 4 * e.raw_w + 2;
 }
 
-// scratch sizes (bytes).  Multi-pass coder: [0] bits, [1] excl, [2] info, [3] raw,
-// [4] ffc, [5] ffx, [6] hdr, [7] cub temp.  Single pass (JDS_ENT_FUSED): [0]
-// segment descriptors (from the second word) + head words, [1] spill words, [2] info, [3]
-// raw, [4] 0xFF counts per segment, [5] their prefix, [6] hdr, [7] cub temp.
+// scratch sizes (bytes): [0] segment descriptors / end bits (from the second
+// word), head words, segment totals, their prefix, per-lane bit counts,
+// per-segment error flags; [1] staged words (word-major per segment); [2]
+// info; [3] packed scans; [4] 0xFF counts per segment; [5] their prefix and
+// the frame totals; [6] headers; [7] hipCUB temp (JDS_ENT_SPLIT=0 only).
 void ent_sizes(const Geo& g, int n, size_t* sz) {
   const EntGeo e = ent_geo(g);
-  const long long nblk = (long long)n * e.nb;
   sz[2] = sizeof(unsigned long long) * 7 * n;  // 6 per frame (scan start / bits) + the frame's error flag
   sz[3] = sizeof(uint32_t) * e.raw_w * n;
   sz[6] = (size_t)e.hdr * n;
-  if (JDS_ENT_FUSED) {
-    const long long nseg = (long long)n * e.sfirst[3];
-    sz[0] = sizeof(unsigned long long) * (nseg + 2) + sizeof(uint32_t) * (nseg + 1);
-    sz[0] += sizeof(uint32_t) + sizeof(unsigned long long) * 2 * (nseg + 1) + sizeof(uint32_t) * 65 * nseg;  // JDS_ENT_SPLIT: agg, segoff, nbits, badseg
-    sz[1] = sizeof(uint32_t) * ES_MAXW * 64 * nseg;
-    sz[4] = sizeof(unsigned long long) * (nseg + 1);
-    sz[5] = sizeof(unsigned long long) * (nseg + 1 + n);  // + the frame totals (k_ent_fscan)
-    size_t t1 = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                           (int)(nseg + 1));
-    sz[7] = t1 + 256;
-    return;
-  }
-  const long long nch = (long long)n * 3 * e.chunks;
-  sz[0] = sizeof(unsigned long long) * (nblk + 1);
-  sz[1] = sizeof(unsigned long long) * (nblk + 1);
-  sz[4] = sizeof(unsigned long long) * (nch + 1);
-  sz[5] = sizeof(unsigned long long) * (nch + 1);
-  size_t t1 = 0, t2 = 0;
+  const long long nseg = (long long)n * e.sfirst[3];
+  sz[0] = sizeof(unsigned long long) * (nseg + 2) + sizeof(uint32_t) * (nseg + 1);
+  sz[0] += sizeof(uint32_t) + sizeof(unsigned long long) * 2 * (nseg + 1) + sizeof(uint32_t) * 65 * nseg;
+  sz[1] = sizeof(uint32_t) * ES_MAXW * 64 * nseg;
+  sz[4] = sizeof(unsigned long long) * (nseg + 1);
+  sz[5] = sizeof(unsigned long long) * (nseg + 1 + n);  // + the frame totals (k_ent_fscan)
+  size_t t1 = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                         (int)(nblk + 1));
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                         (int)(nch + 1));
-  sz[7] = (t1 > t2 ? t1 : t2) + 256;
+                                         (int)(nseg + 1));
+  sz[7] = t1 + 256;
 }
 
 // single pass: segments, fix-up of the shared words, stuffing
@@ -1604,48 +1071,7 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
 hipError_t launch_entropy(const Geo& g, int n, const int16_t* coeffs, void* const* buf, const uint8_t* hdr_dev,
                           const void* tab_dev, uint8_t* out, long long stride, unsigned long long* lengths,
                           unsigned long long* scan_bits, hipStream_t s) {
-  if (JDS_ENT_FUSED)
-    return launch_entropy_fused(g, n, coeffs, buf, hdr_dev, tab_dev, out, stride, lengths, scan_bits, s);
-  const EntGeo e = ent_geo(g);
-  const long long nblk = (long long)n * e.nb;
-  const long long nch = (long long)n * 3 * e.chunks;
-  auto* bits = (unsigned long long*)buf[0];
-  auto* excl = (unsigned long long*)buf[1];
-  auto* info = (unsigned long long*)buf[2];
-  auto* raw = (uint32_t*)buf[3];
-  auto* ffc = (unsigned long long*)buf[4];
-  auto* ffx = (unsigned long long*)buf[5];
-  void* temp = buf[7];
-  size_t sz[8];
-  ent_sizes(g, n, sz);
-  const EntTab* tab = (const EntTab*)tab_dev;
-  hipError_t err;
-  const long long gw_need = (nblk + 255) / 256;
-  const unsigned gw = (unsigned)(gw_need < 2048 ? gw_need : 2048);  // 8 per CU, grid-stride beyond
-  unsigned long long* bad = info + 6 * n;
-  if ((err = hipMemsetAsync(bits + nblk, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
-  if ((err = hipMemsetAsync(bad, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) return err;
-  if (JDS_ENT_BITS_TABLE)
-    hipLaunchKernelGGL(k_ent_bits2, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, bad);
-  else
-    hipLaunchKernelGGL(k_ent_bits, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, bad);
-  if ((err = hipGetLastError()) != hipSuccess) return err;
-  size_t tb = sz[7];
-  if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, bits, excl, (int)(nblk + 1), s)) != hipSuccess) return err;
-  hipLaunchKernelGGL(k_ent_info, dim3((3 * n + 63) / 64), dim3(64), 0, s, e, n, excl, info, scan_bits);
-  hipLaunchKernelGGL(k_ent_zero, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, e, nblk, bits, excl, info, raw);
-  if (JDS_ENT_PACK_TABLE)
-    hipLaunchKernelGGL(k_ent_pack2, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, excl, info, raw);
-  else
-    hipLaunchKernelGGL(k_ent_pack, dim3(gw), dim3(256), 0, s, e, nblk, coeffs, tab, bits, excl, info, raw);
-  const dim3 cg(e.chunks < 64 ? e.chunks : 64, 3, n);
-  if ((err = hipMemsetAsync(ffc, 0, sizeof(unsigned long long) * (nch + 1), s)) != hipSuccess) return err;
-  hipLaunchKernelGGL(k_ent_ff, cg, dim3(256), 0, s, e, info, raw, ffc);
-  tb = sz[7];
-  if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, ffc, ffx, (int)(nch + 1), s)) != hipSuccess) return err;
-  hipLaunchKernelGGL(k_ent_emit, cg, dim3(256), 0, s, e, info, raw, ffx, out, stride);
-  hipLaunchKernelGGL(k_ent_frame, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, bad);
-  return hipGetLastError();
+  return launch_entropy_fused(g, n, coeffs, buf, hdr_dev, tab_dev, out, stride, lengths, scan_bits, s);
 }
 
 }  // namespace jds
