@@ -4,5 +4,5 @@ set -e
 cd "$(dirname "$0")/.."
 rm -f tools/bin/ab/*.so tools/bin/ab/*.o
 python3 tools/build_variant.py A "" jds_entropy.hip
-python3 tools/build_variant.py D64 "-DES_DENSE=64" jds_entropy.hip
-python3 tools/build_variant.py D40 "-DES_DENSE=40" jds_entropy.hip
+python3 tools/build_variant.py S0 "-DES_SW_DEF=0" jds_entropy.hip
+python3 tools/build_variant.py S8 "-DES_SW_DEF=8" jds_entropy.hip
