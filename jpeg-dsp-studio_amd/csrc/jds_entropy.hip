@@ -16,13 +16,14 @@
 //                words; per-lane bit counts and per-segment totals.
 //   k_ent_fscan  per frame: each segment's bit offset within its scan.
 //   k_ent_place  each lane's words shifted into place in the packed scan
-//                (shared words combined by a segmented OR across the wave),
-//                the scan's pad bits, the 0xFF bytes per segment.
-//   k_ent_fix    words whose first bit the previous segment holds.
-//   k_ent_fscan  per frame: 0xFF prefixes and every segment's output offset.
-//   k_ent_emit3  stuffed copy to the file (0x00 after every 0xFF).
-//   k_ent_frame4 headers (host-built template: SOI, APP0, DQT, SOF0, DHT),
+//                (shared words combined by a segmented OR across the wave,
+//                the word shared with the next segment completed from that
+//                segment's leading bits), the scan's pad bits, the 0xFF bytes
+//                per segment.
+//   k_ent_fscan  per frame: 0xFF prefixes, every segment's output offset, the
+//                headers (host-built template: SOI, APP0, DQT, SOF0, DHT),
 //                the three SOS markers, EOI, file length.
+//   k_ent_emit3  stuffed copy to the file (0x00 after every 0xFF).
 // (The rounds 1-3 multi-pass coder -- a counting walk, a block scan, a packing
 // walk with LDS atomics, per-chunk stuffing -- measured 0.54 ms per 64 x 1080p
 // against this one's 0.30; it is retired.  JDS_ENT_SPLIT=0 keeps the one-launch
@@ -422,12 +423,16 @@ __device__ __forceinline__ int es_ff(uint32_t v, int nbytes) {  // 0xFF bytes am
 // Placement of a segment's staged words at scan bit offset pre (lane bits at
 // pre + excl): see k_ent_seg.  st: the lane's LDS staging (slots < ES_SW),
 // ov: its global words (slots >= ES_SW, or all slots when st is null).
+// fuse (not the scan's last segment): tailx holds the next segment's bits that
+// share this segment's final word, so that word is written whole here (no
+// k_ent_fix); Wn: the scan's end bit when the next segment ends in that word.
 __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g, int lane, bool valid, int nvalid,
                                          bool last_seg, uint32_t nb, uint32_t excl, unsigned long long pre,
                                          unsigned long long A, const uint32_t* st, const uint32_t* ov, int k,
                                          uint32_t* __restrict__ raw, uint32_t* __restrict__ headw,
                                          unsigned long long* __restrict__ ffs, unsigned long long* __restrict__ info,
-                                         unsigned long long* __restrict__ scan_bits) {
+                                         unsigned long long* __restrict__ scan_bits, bool fuse = false,
+                                         uint32_t tailx = 0u, unsigned long long Wn = 0ull, bool fuse_prev = false) {
   const unsigned long long W1 = pre + A;
   auto stw = [&](int j) -> uint32_t { return j >= k ? 0u : ((st == nullptr || j >= ES_SW) ? ov[j * 64] : st[j * 64]); };
   const unsigned long long o = pre + excl;  // the lane's first bit in the scan
@@ -437,10 +442,15 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
   const uint32_t s0 = stw(0);
   const uint32_t hv = s0 >> sh;
   // the next lane starts inside this lane's tail word
-  const bool c = valid && ((o + nb) & 31ull) != 0ull && lane + 1 < nvalid;
+  // (fuse: lane 63's "next lane" is the next segment, whose bits are tailx)
+  const bool c = valid && ((o + nb) & 31ull) != 0ull && (lane + 1 < nvalid || fuse);
   // X = this lane's head word bits | those of the following lanes that share it
   uint32_t X = valid ? hv : 0u;
   int F = (valid && single && c) ? 1 : 0;
+  if (fuse && lane == 63 && F) {
+    X |= tailx;
+    F = 0;
+  }
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t Xn = __shfl_down(X, d, 64);
@@ -451,14 +461,15 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
     }
   }
   const uint32_t X1 = __shfl_down(X, 1, 64);
-  const uint32_t in_tail = c ? X1 : 0u;
+  const uint32_t in_tail = c ? ((fuse && lane == 63) ? tailx : X1) : 0u;
   uint32_t* rs = raw + raw_base(e, q.f, q.s);
   const unsigned long long wlast = (W1 - 1ull) >> 5;
-  const bool open_end = !last_seg && (W1 & 31ull);
+  const bool open_end = !fuse && !last_seg && (W1 & 31ull);
+  const unsigned long long Wend = last_seg ? W1 : Wn;  // the scan ends in word wlast (0: it does not)
   int ffc = 0;
   auto put_word = [&](unsigned long long widx, uint32_t v) {
     int nb4 = 4;
-    if (last_seg && widx == wlast) nb4 = es_pad(v, W1, widx);
+    if (Wend && widx == wlast) nb4 = es_pad(v, Wend, widx);
     rs[widx] = __builtin_bswap32(v);  // byte 0 of the stream first
     if (!(open_end && widx == wlast)) ffc += es_ff(v, nb4);
   };
@@ -483,7 +494,7 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
     }
     const uint32_t tv = single ? hv : __builtin_amdgcn_alignbit(prev, stw(nout), (uint32_t)sh);
     if (!single || own_head) put_word(tw, tv | in_tail);
-    if (lane == 0 && !own_head) headw[g] = X;  // the previous segment holds this word's first bit
+    if (lane == 0 && !own_head && !fuse_prev) headw[g] = X;  // the previous segment holds this word's first bit
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) ffc += __shfl_xor(ffc, d, 64);
@@ -615,6 +626,9 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
 #ifndef JDS_ENT_SPLIT
 #define JDS_ENT_SPLIT 1
 #endif
+#ifndef JDS_ENT_NOFIX
+#define JDS_ENT_NOFIX 1  // k_ent_place completes the words segments share (no k_ent_fix)
+#endif
 __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per_eu(JDS_ENT_WPE))) k_ent_walk(
     const EntGeo e, const int nseg, const int16_t* __restrict__ coeffs, const EsTab* __restrict__ gt,
     uint32_t* __restrict__ gst, uint32_t* __restrict__ nbits, unsigned long long* __restrict__ agg,
@@ -666,7 +680,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   for (int d = 32; d > 0; d >>= 1) a += __shfl_xor(a, d, 64);
   if (lane == 0) {
     agg[g] = a;
-    badseg[g] = any_bad ? 1u : 0u;  // not baseline-codable: the frame is reported (k_ent_frame4)
+    badseg[g] = any_bad ? 1u : 0u;  // not baseline-codable: the frame is reported (k_ent_fscan)
     if (g == nseg - 1) {            // the scans' closing zeros (no memsets)
       agg[nseg] = 0ull;
       ffs[nseg] = 0ull;
@@ -690,18 +704,40 @@ __global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nse
   const bool valid = q.seg * 64 + lane < q.nbs;
   const int nvalid = q.nbs - q.seg * 64 < 64 ? q.nbs - q.seg * 64 : 64;
   const bool last_seg = q.seg == q.nseg_s - 1;
+  const bool fuse = JDS_ENT_NOFIX && !last_seg;
+  const int gn = fuse ? g + 1 : g;  // the next segment of the scan (its head bits)
   const uint32_t nb = nbits[(size_t)g * 64 + lane];
-  uint32_t inc = nb;
+  const uint32_t nbn = nbits[(size_t)gn * 64 + lane];
+  const uint32_t w0n = gst[(size_t)gn * ES_MAXW * 64 + lane];  // (row 0; garbage where nbn == 0)
+  const unsigned long long pre = segoff[g] - segoff[g - q.seg];
+  uint32_t inc = nb, incn = nbn;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
+    const uint32_t yn = __shfl_up(incn, o, 64);
+    if (lane >= o) {
+      inc += y;
+      incn += yn;
+    }
   }
   const unsigned long long A = __shfl(inc, 63, 64);
-  const unsigned long long pre = segoff[g] - segoff[g - q.seg];
-  if (lane == 0) incl[g] = pre + A;
+  const unsigned long long W1 = pre + A;
+  if (lane == 0) incl[g] = W1;
+  uint32_t tailx = 0u;
+  unsigned long long Wn = 0ull;
+  if (fuse) {
+    // the next segment's lanes starting inside this segment's final word: each
+    // one's bits there are its first staged word's leading bits
+    const uint32_t sh = (uint32_t)(W1 & 31ull), p = sh + (incn - nbn);
+    tailx = (sh && nbn && p < 32u) ? w0n >> p : 0u;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) tailx |= __shfl_xor(tailx, d, 64);
+    const unsigned long long An = __shfl(incn, 63, 64);
+    if (q.seg + 2 == q.nseg_s && sh && ((W1 + An - 1ull) >> 5) == ((W1 - 1ull) >> 5)) Wn = W1 + An;
+  }
   es_place(e, q, g, lane, valid, nvalid, last_seg, nb, inc - nb, pre, A, nullptr,
-           gst + (size_t)g * ES_MAXW * 64 + lane, (int)((nb + 31u) >> 5), raw, headw, ffs, info, scan_bits);
+           gst + (size_t)g * ES_MAXW * 64 + lane, (int)((nb + 31u) >> 5), raw, headw, ffs, info, scan_bits, fuse,
+           tailx, Wn, JDS_ENT_NOFIX && q.seg > 0);
 }
 
 // the first word of segment g when segment g - 1 holds its first bit: OR in
@@ -776,8 +812,12 @@ __global__ void __launch_bounds__(1024) k_ent_fscan(const EntGeo e, const unsign
                                                     unsigned long long* __restrict__ tot,
                                                     const unsigned long long* __restrict__ desc,
                                                     const unsigned long long* __restrict__ info,
-                                                    unsigned long long* __restrict__ outoff) {
+                                                    unsigned long long* __restrict__ outoff,
+                                                    const uint8_t* __restrict__ hdr, uint8_t* __restrict__ file,
+                                                    long long stride, unsigned long long* __restrict__ lengths,
+                                                    const uint32_t* __restrict__ badseg) {
   __shared__ unsigned long long s_w[16];
+  __shared__ int s_bad;
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n = e.sfirst[3];
   const long long g0 = (long long)f * n;
@@ -814,58 +854,34 @@ __global__ void __launch_bounds__(1024) k_ent_fscan(const EntGeo e, const unsign
       const unsigned long long ffe = s2 < 2 ? out[g0 + e.sfirst[s2 + 1]] : all;
       p += (long long)(nb + ffe - out[g0 + e.sfirst[s2]]) + ENT_SOS;
     }
+    int b = 0;
     for (int i = t; i < n; i += 1024) {
       const long long g = g0 + i;
       const int s2 = i < e.sfirst[1] ? 0 : (i < e.sfirst[2] ? 1 : 2);
       const int seg = i - e.sfirst[s2];
       const unsigned long long W0 = seg ? (desc[g - 1] & ES_VAL) : 0ull;
       outoff[g] = (unsigned long long)so[s2] + 4 * ((W0 + 31) >> 5) + (out[g] - out[g0 + e.sfirst[s2]]);
+      b |= (int)badseg[g];
     }
-  }
-}
-
-// k_ent_frame with the 0xFF prefixes frame-relative (k_ent_fscan) and the
-// per-segment error flags
-__global__ void k_ent_frame4(const EntGeo e, const uint8_t* __restrict__ hdr, const unsigned long long* __restrict__ info,
-                             const unsigned long long* __restrict__ ffx, const unsigned long long* __restrict__ fftot,
-                             uint8_t* __restrict__ out, long long stride, unsigned long long* __restrict__ lengths,
-                             const uint32_t* __restrict__ badseg) {
-  __shared__ int s_bad;
-  const int f = blockIdx.x;
-  if (threadIdx.x == 0) s_bad = 0;
-  __syncthreads();
-  {
-    int b = 0;
-    for (int i = threadIdx.x; i < e.sfirst[3]; i += blockDim.x) b |= (int)badseg[(long long)f * e.sfirst[3] + i];
+    // the frame's markers (what k_ent_frame4 does; k_ent_emit3 writes only the scans' bytes)
+    if (t == 0) s_bad = 0;
+    __syncthreads();
     if (b) s_bad = 1;
-  }
-  __syncthreads();
-  uint8_t* dst = out + (long long)f * stride;
-  for (int i = threadIdx.x; i < e.hdr; i += blockDim.x) dst[i] = hdr[(long long)f * e.hdr + i];
-  const long long g0 = (long long)f * e.sfirst[3];
-  long long so[4];
-  {
-    long long p = e.hdr + ENT_SOS;
-    for (int s2 = 0; s2 < 3; ++s2) {
-      so[s2] = p;
-      const unsigned long long nb = (info[2 * (f * 3 + s2) + 1] + 7) >> 3;
-      const unsigned long long ffe = s2 < 2 ? ffx[g0 + e.sfirst[s2 + 1]] : fftot[f];
-      p += (long long)(nb + ffe - ffx[g0 + e.sfirst[s2]]) + ENT_SOS;
+    uint8_t* dst = file + (long long)f * stride;
+    for (int i = t; i < e.hdr; i += 1024) dst[i] = hdr[(long long)f * e.hdr + i];
+    if (t < 3) {
+      uint8_t* m = dst + so[t] - ENT_SOS;
+      const uint8_t sos[ENT_SOS] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(t + 1), (uint8_t)(t == 0 ? 0x00 : 0x11),
+                                    0x00, 0x3F, 0x00};
+      for (int i = 0; i < ENT_SOS; ++i) m[i] = sos[i];
     }
-    so[3] = p;  // where a fourth scan's data would start
-  }
-  if (threadIdx.x < 3) {
-    const int s2 = threadIdx.x;
-    uint8_t* m = dst + so[s2] - ENT_SOS;
-    const uint8_t sos[ENT_SOS] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(s2 + 1), (uint8_t)(s2 == 0 ? 0x00 : 0x11),
-                                  0x00, 0x3F, 0x00};
-    for (int i = 0; i < ENT_SOS; ++i) m[i] = sos[i];
-  }
-  if (threadIdx.x == 0) {
-    const long long end = so[3] - ENT_SOS;  // end of the Cr scan
-    dst[end] = 0xFF;
-    dst[end + 1] = 0xD9;
-    if (lengths) lengths[f] = s_bad ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
+    __syncthreads();
+    if (t == 0) {
+      const long long end = p - ENT_SOS;  // end of the Cr scan
+      dst[end] = 0xFF;
+      dst[end + 1] = 0xD9;
+      if (lengths) lengths[f] = s_bad ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
+    }
   }
 }
 
@@ -1040,7 +1056,8 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
     hipLaunchKernelGGL(k_ent_walk, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, ovf, nbits, agg, badseg,
                        ffs);
     if ((err = hipGetLastError()) != hipSuccess) return err;
-    hipLaunchKernelGGL(k_ent_fscan<false>, dim3(n), dim3(1024), 0, s, e, agg, segoff, ffx, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL(k_ent_fscan<false>, dim3(n), dim3(1024), 0, s, e, agg, segoff, ffx, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, 0ll, nullptr, nullptr);
     hipLaunchKernelGGL(k_ent_place, dim3(wg), dim3(256), 0, s, e, nseg, ovf, nbits, segoff, desc, raw, headw, ffs,
                        info, scan_bits);
   } else {
@@ -1048,15 +1065,16 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
                        ffs, info, scan_bits, bad);
   }
   if ((err = hipGetLastError()) != hipSuccess) return err;
-  hipLaunchKernelGGL(k_ent_fix, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, headw, raw, ffs);
+  if (!(JDS_ENT_SPLIT && JDS_ENT_NOFIX))
+    hipLaunchKernelGGL(k_ent_fix, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, headw, raw,
+                       ffs);
   auto* outoff = (unsigned long long*)(headw + ((nseg + 2) & ~1));  // (the split path's segment totals, consumed)
   if (JDS_ENT_SPLIT) {
     // frame-relative 0xFF prefixes and each segment's output offset in one launch; frame totals in ffs[nseg ..]
     unsigned long long* fftot = ffx + nseg + 1;
-    hipLaunchKernelGGL(k_ent_fscan<true>, dim3(n), dim3(1024), 0, s, e, ffs, ffx, fftot, desc, info, outoff);
+    hipLaunchKernelGGL(k_ent_fscan<true>, dim3(n), dim3(1024), 0, s, e, ffs, ffx, fftot, desc, info, outoff, hdr_dev,
+                       out, stride, lengths, badseg);
     hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
-    hipLaunchKernelGGL(k_ent_frame4, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, fftot, out, stride, lengths,
-                       badseg);
   } else {
     size_t tb = sz[7];
     if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, ffs, ffx, nseg + 1, s)) != hipSuccess) return err;

@@ -1,10 +1,11 @@
 """Host model of the single-pass entropy coder's placement (csrc/jds_entropy.hip:
-es_place, k_ent_fix): segments of up to 64 blocks, each lane's bit string
+es_place, k_ent_place, k_ent_fix): segments of up to 64 blocks, each lane's bit string
 placed at its offset, words shared by several lanes written once by the lane
 holding their first bit with the others' bits gathered by the segmented OR,
 a segment's first word handed to the fix-up when the previous segment holds
-its first bit, the scan's last byte padded with 1-bits and the 0xFF bytes
-counted per owning segment.  The model follows the kernel's index arithmetic
+its first bit (or, fused as k_ent_place does by default, completed by the
+previous segment from this segment's leading bits), the scan's last byte
+padded with 1-bits and the 0xFF bytes counted per owning segment.  The model follows the kernel's index arithmetic
 step for step; the test checks that the assembled words equal the plain
 concatenated stream and that the 0xFF counts add up, over ragged block counts
 and bit lengths (blocks of 4 bits -- several per word -- up to 300 bits).
@@ -14,7 +15,7 @@ import random
 import pytest
 
 
-def _place_scan(nbits_list, seed):
+def _place_scan(nbits_list, seed, fuse=False):
     rng = random.Random(seed)
     blocks = [[rng.randint(0, 1) for _ in range(nb)] for nb in nbits_list]
     # make 0xFF bytes common enough to exercise the counts
@@ -36,6 +37,22 @@ def _place_scan(nbits_list, seed):
         ranges.append((W0, W1))
         last_seg = g == nseg - 1
         nv = len(blk)
+        fz = fuse and not last_seg
+        tailx, Wn = 0, 0
+        if fz:  # k_ent_place: the next segment's lanes that start inside word W1 >> 5
+            nbl = blocks[(g + 1) * 64:(g + 2) * 64]
+            nbn = [len(b) for b in nbl] + [0] * (64 - len(nbl))
+            sh1 = W1 & 31
+            ex = 0
+            for l in range(64):
+                p = sh1 + ex
+                if sh1 and nbn[l] and p < 32:
+                    w0 = int(''.join(map(str, (nbl[l] + [0] * 32)[:32])), 2)
+                    tailx |= w0 >> p
+                ex += nbn[l]
+            An = sum(nbn)
+            if g + 2 == nseg and sh1 and ((W1 + An - 1) >> 5) == ((W1 - 1) >> 5):
+                Wn = W1 + An
         o = [W0 + sum(nb[:l]) for l in range(nv)]
 
         def words(l):
@@ -50,9 +67,12 @@ def _place_scan(nbits_list, seed):
         tw = [(o[l] + nb[l] - 1) >> 5 for l in range(nv)]
         single = [hw[l] == tw[l] for l in range(nv)]
         hv = [stw(l, 0) >> sh[l] for l in range(nv)]
-        c = [((o[l] + nb[l]) & 31) != 0 and l + 1 < nv for l in range(nv)]
+        c = [((o[l] + nb[l]) & 31) != 0 and (l + 1 < nv or fz) for l in range(nv)]
         X = hv + [0] * (64 - nv)
         F = [1 if (single[l] and c[l]) else 0 for l in range(nv)] + [0] * (64 - nv)
+        if fz and F[63]:
+            X[63] |= tailx
+            F[63] = 0
         d = 1
         while d < 64:  # log-step segmented suffix OR (the kernel's shuffles)
             Xn = [X[l + d] if l + d < 64 else X[l] for l in range(64)]
@@ -63,11 +83,12 @@ def _place_scan(nbits_list, seed):
                     F[l] = Fn[l]
             d *= 2
         wlast = (W1 - 1) >> 5
-        open_end = (not last_seg) and (W1 & 31)
+        open_end = (not fz) and (not last_seg) and (W1 & 31)
+        Wend = W1 if last_seg else Wn
         ffc = 0
 
         def pad(v, widx):
-            used = W1 - 32 * widx
+            used = Wend - 32 * widx
             pb = (8 - (used & 7)) & 7
             if pb:
                 v |= ((1 << pb) - 1) << (32 - used - pb)
@@ -79,14 +100,14 @@ def _place_scan(nbits_list, seed):
         def put(widx, v):
             nonlocal ffc
             n4 = 4
-            if last_seg and widx == wlast:
+            if Wend and widx == wlast:
                 v, n4 = pad(v, widx)
             assert raw[widx] is None, ('word written twice', widx)
             raw[widx] = v
             if not (open_end and widx == wlast):
                 ffc += ff(v, n4)
         for l in range(nv):
-            in_tail = X[l + 1] if c[l] else 0
+            in_tail = (tailx if (fz and l == 63) else X[l + 1]) if c[l] else 0
             own_head = sh[l] == 0
             nout = tw[l] - hw[l]
             if own_head and not single[l]:
@@ -99,11 +120,11 @@ def _place_scan(nbits_list, seed):
             tv = hv[l] if single[l] else ((prev << 32 | stw(l, nout)) >> sh[l]) & 0xFFFFFFFF
             if not single[l] or own_head:
                 put(tw[l], tv | in_tail)
-            if l == 0 and not own_head:
+            if l == 0 and not own_head and not (fuse and g > 0):
                 headw[g] = X[0]
         ffs[g] = ffc
         pre = W1
-    for g in range(1, nseg):  # k_ent_fix
+    for g in range(1, nseg if not fuse else 1):  # k_ent_fix
         W0, W1 = ranges[g]
         if W0 & 31:
             w = W0 >> 5
@@ -123,8 +144,9 @@ def _place_scan(nbits_list, seed):
     return got, ref, sum(ffs)
 
 
+@pytest.mark.parametrize('fuse', [False, True])
 @pytest.mark.parametrize('seed', range(60))
-def test_placement_model_equals_concatenation(seed):
+def test_placement_model_equals_concatenation(seed, fuse):
     rng = random.Random(seed)
     nblk = rng.choice([1, 2, 63, 64, 65, 127, 128, 129, 200, 300])
     kind = rng.choice(['small', 'mixed', 'big'])
@@ -134,6 +156,6 @@ def test_placement_model_equals_concatenation(seed):
         nb = [rng.randint(30, 300) for _ in range(nblk)]
     else:
         nb = [rng.choice([4, 5, 6, 31, 32, 33, 64, 100]) for _ in range(nblk)]
-    got, ref, nff = _place_scan(nb, seed)
+    got, ref, nff = _place_scan(nb, seed, fuse)
     assert got == ref
     assert nff == ref.count(0xFF)

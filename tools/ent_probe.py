@@ -36,7 +36,7 @@ def main():
     lengths = torch.zeros(B, dtype=torch.int64, device=dev)
     for _ in range(3):
         ent.run(cf.data_ptr(), files.data_ptr(), ent.capacity, lengths.data_ptr(), 0, s.cuda_stream)
-    reps = 20
+    reps = int(os.environ.get('REPS', '20'))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(reps):
