@@ -81,8 +81,13 @@ struct EntTab {
 };
 
 // left-aligned symbols: code << (32 - len) | len (len <= 16 sits below the code)
+#ifndef ES_RS_DEF
+#define ES_RS_DEF 11  // AC table row stride: (run, size) at run * 11 + size spreads a wave's lookups over the LDS banks
+#endif
+constexpr int ES_RS = ES_RS_DEF;  // (32: 0.271 vs 11: 0.258 ms per 64 x 1080p; a stride of 32 put every even run on the same 11 banks)
+static_assert(ES_RS >= 11, "sizes 0..10");
 struct EsTab {
-  uint32_t ac[2][16 * 32];  // (run & 15, size) -> AC symbol, size clamped to 10 (code_ac's clamp); 0 for size 0
+  uint32_t ac[2][16 * ES_RS];  // (run & 15, size) -> AC symbol, size clamped to 10 (code_ac's clamp); 0 for size 0
   uint32_t dc[2][16];
   uint32_t zrl[2], eob[2];
 };
@@ -113,8 +118,8 @@ void ent_build_tables(EntTab* t) {
   // the single-pass coder's left-aligned symbols follow the table (ent_tab_size)
   EsTab* es = reinterpret_cast<EsTab*>(t + 1);
   for (int c = 0; c < 2; ++c) {
-    for (int i = 0; i < 16 * 32; ++i) {
-      const int run = i >> 5, sz = i & 31;
+    for (int i = 0; i < 16 * ES_RS; ++i) {
+      const int run = i / ES_RS, sz = i % ES_RS;
       es->ac[c][i] = sz ? es_left(t->ac[c][(run << 4) | (sz > 10 ? 10 : sz)]) : 0u;
     }
     for (int i = 0; i < 16; ++i) es->dc[c][i] = es_left(t->dc[c][i]);
@@ -306,7 +311,7 @@ __device__ __forceinline__ void es_ac(const BlockRegs& r, int last, int& aor, co
     if constexpr (K + 1 < ES_DENSE) {
       v1 = coef_at<ZZC[K + 1]>(r);
       sz1 = es_size(v1 < 0 ? -v1 : v1);
-      e1 = ac[((K - nlast) & 15) << 5 | sz1];
+      e1 = ac[((K - nlast) & 15) * ES_RS + sz1];
     }
     if (a && run >= 16) {  // rare: one ZRL code per 16 zeros first
       const int zl = (int)(zrl & 31u);
@@ -350,7 +355,7 @@ __device__ __forceinline__ void es_hi_code(const int16_t* cz, uint32_t m, int& l
       const int zl = (int)(zrl & 31u);
       for (int i = 0; i < (run >> 4); ++i) o.put(zrl, zl, acc, n);
     }
-    const uint32_t e = ac[((run & 15) << 5) | sz];
+    const uint32_t e = ac[(run & 15) * ES_RS + sz];
     const int L = (int)(e & 31u) + sz;
     const uint32_t mag = (uint32_t)(v + (v >> 31)) & ((1u << sz) - 1u);
     o.put(e | (mag << ((32 - L) & 31)), L, acc, n);
