@@ -177,17 +177,30 @@ __device__ __forceinline__ long long raw_base(const EntGeo& e, int frame, int s)
   return (long long)frame * e.raw_w + (s == 0 ? 0 : (s == 1 ? e.cap_w[0] : e.cap_w[0] + e.cap_w[1]));
 }
 
-// The code of lane k (zigzag position k) of a block: `v` its coefficient,
-// `nzm` the wave's nonzero mask, `diff` the DC difference (lane 0).
-// T.81 F.1.2.1 / F.1.2.2; returns the bit count, the bits right-aligned in *val.
-__device__ __forceinline__ int wave_excl_sum(int x, int lane) {
-  int inc = x;
+// Inclusive prefix sum over the wave (every lane active): row_shr 1, 2, 4, 8
+// within the 16-lane rows, then row_bcast 15 / 31 across them -- six DPP adds
+// (JDS_ENT_SHFL_SCAN: the log-step shuffle form, six ds_bpermute round trips).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
+#ifdef JDS_ENT_SHFL_SCAN
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
   }
-  return inc - x;
+#else
+  (void)lane;
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+#endif
+  return v;
+}
+
+__device__ __forceinline__ int wave_excl_sum(int x, int lane) {
+  return (int)(wave_incl_sum((uint32_t)x, lane) - (uint32_t)x);
 }
 
 // One LANE per block: its 64 coefficients sit in 32 VGPRs (packed int16
@@ -563,12 +576,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   if (bd) bad[q.f] = 1ull;  // not baseline-codable: the frame is reported
 
   // ---- offset: the wave's prefix, then the look-back over the scan's segments
-  uint32_t inc = nb;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
-  }
+  const uint32_t inc = wave_incl_sum(nb, lane);
   const uint32_t excl = inc - nb;
   const unsigned long long A = __shfl(inc, 63, 64);
   unsigned long long pre = 0ull;
@@ -715,16 +723,7 @@ __global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nse
   const uint32_t nbn = nbits[(size_t)gn * 64 + lane];
   const uint32_t w0n = gst[(size_t)gn * ES_MAXW * 64 + lane];  // (row 0; garbage where nbn == 0)
   const unsigned long long pre = segoff[g] - segoff[g - q.seg];
-  uint32_t inc = nb, incn = nbn;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o, 64);
-    const uint32_t yn = __shfl_up(incn, o, 64);
-    if (lane >= o) {
-      inc += y;
-      incn += yn;
-    }
-  }
+  const uint32_t inc = wave_incl_sum(nb, lane), incn = wave_incl_sum(nbn, lane);
   const unsigned long long A = __shfl(inc, 63, 64);
   const unsigned long long W1 = pre + A;
   if (lane == 0) incl[g] = W1;
@@ -793,6 +792,9 @@ __device__ __forceinline__ int es_ff_mem(uint32_t x, int nvb) {
 // assembled in the wave's LDS buffer at the output's alignment, then written
 // out as aligned dwords (bytes at the two partial ends).
 constexpr int EM_CHUNK = 1024;
+#ifndef JDS_EM_INTERLEAVE
+#define JDS_EM_INTERLEAVE 1
+#endif
 // each segment's first output byte (k_ent_emit3's one dependent lookup)
 __global__ void k_ent_offs(const EntGeo e, const int nseg, const unsigned long long* __restrict__ desc,
                            const unsigned long long* __restrict__ info, const unsigned long long* __restrict__ ffx,
@@ -910,6 +912,42 @@ __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nse
   const uint32_t* w = raw + raw_base(e, q.f, q.s);
   uint8_t* lb = reinterpret_cast<uint8_t*>(sbuf[wv]);
   for (unsigned long long i0 = b0; i0 < b1; i0 += EM_CHUNK) {
+#if JDS_EM_INTERLEAVE
+    // lane l takes the chunk's dwords l, l + 64, l + 128, l + 192: coalesced
+    // loads, and a wave's byte stores land on consecutive LDS words (16 B per
+    // lane put lanes 16 apart on one bank)
+    uint32_t x[4];
+    int nvk[4], lk[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned long long i = i0 + 4 * (64 * k + lane);
+      nvk[k] = i < b1 ? (b1 - i < 4 ? (int)(b1 - i) : 4) : 0;
+      x[k] = nvk[k] ? w[i >> 2] : 0u;
+      lk[k] = nvk[k] + es_ff_mem(x[k], nvk[k]);  // <= 8
+    }
+    // two packed scans (16-bit fields: a field's wave sum is <= 512)
+    const uint32_t pa = (uint32_t)lk[0] | ((uint32_t)lk[1] << 16), pb = (uint32_t)lk[2] | ((uint32_t)lk[3] << 16);
+    const uint32_t ia = wave_incl_sum(pa, lane), ib = wave_incl_sum(pb, lane);
+    const uint32_t ta = __shfl(ia, 63, 64), tb = __shfl(ib, 63, 64);
+    const uint32_t ea = ia - pa, eb = ib - pb;
+    const int t0 = (int)(ta & 0xFFFFu), t1 = (int)(ta >> 16), t2 = (int)(tb & 0xFFFFu), t3 = (int)(tb >> 16);
+    const int tot = t0 + t1 + t2 + t3;
+    const int sh0 = (int)((uintptr_t)dst & 3u);  // LDS byte sh0 <-> dst[0]
+    const int pk[4] = {sh0 + (int)(ea & 0xFFFFu), sh0 + t0 + (int)(ea >> 16), sh0 + t0 + t1 + (int)(eb & 0xFFFFu),
+                       sh0 + t0 + t1 + t2 + (int)(eb >> 16)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int p = pk[k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < nvk[k]) {
+          const uint8_t b = (uint8_t)(x[k] >> (8 * j));
+          lb[p++] = b;
+          if (b == 0xFF) lb[p++] = 0x00;
+        }
+      }
+    }
+#else
     const unsigned long long i = i0 + 16 * lane;
     uint32_t x[4] = {0u, 0u, 0u, 0u};
     int nv = 0, ff = 0;
@@ -934,6 +972,7 @@ __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nse
         if (b == 0xFF) lb[p++] = 0x00;
       }
     }
+#endif
     __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations execute in order
     asm volatile("" ::: "memory");
     // out: global bytes dst[0 .. tot) <- LDS bytes [sh0, sh0 + tot); dword d covers LDS [4d, 4d + 4)
