@@ -203,6 +203,31 @@ __device__ __forceinline__ int wave_excl_sum(int x, int lane) {
   return (int)(wave_incl_sum((uint32_t)x, lane) - (uint32_t)x);
 }
 
+__device__ __forceinline__ uint32_t lane63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
+
+// wave-wide totals (every lane active), read from lane 63 of the DPP scan
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane63(wave_incl_sum(v, (int)__lane_id())); }
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  return lane63(v);
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+  return lane63(v);
+}
+
 // One LANE per block: its 64 coefficients sit in 32 VGPRs (packed int16
 // pairs) and the zigzag walk is unrolled at compile time, so every register
 // index is a constant; the per-coefficient work is a handful of integer ops
@@ -469,8 +494,11 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
     X |= tailx;
     F = 0;
   }
+  // (every block costs >= 4 bits, so at most 7 lanes in a row lie inside one
+  // word and share the next lane's word: spans of 8 lanes suffice; the host
+  // model fails with spans of 4)
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
+  for (int d = 1; d < 8; d <<= 1) {
     const uint32_t Xn = __shfl_down(X, d, 64);
     const int Fn = __shfl_down(F, d, 64);
     if (F && lane + d < 64) {
@@ -514,8 +542,7 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
     if (!single || own_head) put_word(tw, tv | in_tail);
     if (lane == 0 && !own_head && !fuse_prev) headw[g] = X;  // the previous segment holds this word's first bit
   }
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) ffc += __shfl_xor(ffc, d, 64);
+  ffc = (int)wave_sum((uint32_t)ffc);
   if (lane == 0) {
     ffs[g] = (unsigned long long)ffc;
     if (last_seg) {
@@ -578,7 +605,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   // ---- offset: the wave's prefix, then the look-back over the scan's segments
   const uint32_t inc = wave_incl_sum(nb, lane);
   const uint32_t excl = inc - nb;
-  const unsigned long long A = __shfl(inc, 63, 64);
+  const unsigned long long A = lane63(inc);
   unsigned long long pre = 0ull;
 #ifdef JDS_ENT_PROBE_NOLB  // timing probe (wrong output): no look-back
   if (true) {
@@ -679,18 +706,11 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   }
   const bool any_bad = __ballot(bd) != 0ull;
   // the LDS slots to the segment's global area (one 256-B row per slot)
-  int kmax = k < ES_SW ? k : ES_SW;
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    const int y = __shfl_xor(kmax, d, 64);
-    kmax = y > kmax ? y : kmax;
-  }
+  const int kmax = (int)wave_max((uint32_t)(k < ES_SW ? k : ES_SW));
   for (int j = 0; j < kmax; ++j)
     if (j < k) ov[j * 64] = st[j * 64];
   nbits[(size_t)g * 64 + lane] = nb;
-  unsigned long long a = nb;
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) a += __shfl_xor(a, d, 64);
+  const unsigned long long a = wave_sum(nb);  // (<= 64 * 1660 bits)
   if (lane == 0) {
     agg[g] = a;
     badseg[g] = any_bad ? 1u : 0u;  // not baseline-codable: the frame is reported (k_ent_fscan)
@@ -724,7 +744,7 @@ __global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nse
   const uint32_t w0n = gst[(size_t)gn * ES_MAXW * 64 + lane];  // (row 0; garbage where nbn == 0)
   const unsigned long long pre = segoff[g] - segoff[g - q.seg];
   const uint32_t inc = wave_incl_sum(nb, lane), incn = wave_incl_sum(nbn, lane);
-  const unsigned long long A = __shfl(inc, 63, 64);
+  const unsigned long long A = lane63(inc);
   const unsigned long long W1 = pre + A;
   if (lane == 0) incl[g] = W1;
   uint32_t tailx = 0u;
@@ -734,9 +754,8 @@ __global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nse
     // one's bits there are its first staged word's leading bits
     const uint32_t sh = (uint32_t)(W1 & 31ull), p = sh + (incn - nbn);
     tailx = (sh && nbn && p < 32u) ? w0n >> p : 0u;
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) tailx |= __shfl_xor(tailx, d, 64);
-    const unsigned long long An = __shfl(incn, 63, 64);
+    tailx = wave_or(tailx);
+    const unsigned long long An = lane63(incn);
     if (q.seg + 2 == q.nseg_s && sh && ((W1 + An - 1ull) >> 5) == ((W1 - 1ull) >> 5)) Wn = W1 + An;
   }
   es_place(e, q, g, lane, valid, nvalid, last_seg, nb, inc - nb, pre, A, nullptr,
@@ -928,7 +947,7 @@ __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nse
     // two packed scans (16-bit fields: a field's wave sum is <= 512)
     const uint32_t pa = (uint32_t)lk[0] | ((uint32_t)lk[1] << 16), pb = (uint32_t)lk[2] | ((uint32_t)lk[3] << 16);
     const uint32_t ia = wave_incl_sum(pa, lane), ib = wave_incl_sum(pb, lane);
-    const uint32_t ta = __shfl(ia, 63, 64), tb = __shfl(ib, 63, 64);
+    const uint32_t ta = lane63(ia), tb = lane63(ib);
     const uint32_t ea = ia - pa, eb = ib - pb;
     const int t0 = (int)(ta & 0xFFFFu), t1 = (int)(ta >> 16), t2 = (int)(tb & 0xFFFFu), t3 = (int)(tb >> 16);
     const int tot = t0 + t1 + t2 + t3;
@@ -961,7 +980,7 @@ __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nse
     }
     const int len = nv + ff;
     const int ex = wave_excl_sum(len, lane);
-    const int tot = __shfl(ex + len, 63, 64);
+    const int tot = (int)lane63((uint32_t)(ex + len));
     const int sh0 = (int)((uintptr_t)dst & 3u);  // LDS byte sh0 <-> dst[0]
     int p = sh0 + ex;
 #pragma unroll

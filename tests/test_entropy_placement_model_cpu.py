@@ -74,7 +74,7 @@ def _place_scan(nbits_list, seed, fuse=False):
             X[63] |= tailx
             F[63] = 0
         d = 1
-        while d < 64:  # log-step segmented suffix OR (the kernel's shuffles)
+        while d < 8:  # log-step segmented suffix OR (the kernel's shuffles; spans of 8 lanes)
             Xn = [X[l + d] if l + d < 64 else X[l] for l in range(64)]
             Fn = [F[l + d] if l + d < 64 else F[l] for l in range(64)]
             for l in range(64):
@@ -149,8 +149,10 @@ def _place_scan(nbits_list, seed, fuse=False):
 def test_placement_model_equals_concatenation(seed, fuse):
     rng = random.Random(seed)
     nblk = rng.choice([1, 2, 63, 64, 65, 127, 128, 129, 200, 300])
-    kind = rng.choice(['small', 'mixed', 'big'])
-    if kind == 'small':
+    kind = rng.choice(['small', 'mixed', 'big', 'min'])
+    if kind == 'min':  # every block at the 4-bit minimum: 8 lanes inside one word (the longest OR chains)
+        nb = [4 if rng.random() < 0.9 else rng.randint(5, 40) for _ in range(nblk)]
+    elif kind == 'small':
         nb = [rng.randint(4, 12) for _ in range(nblk)]
     elif kind == 'big':
         nb = [rng.randint(30, 300) for _ in range(nblk)]
