@@ -205,6 +205,16 @@ __device__ __forceinline__ int wave_excl_sum(int x, int lane) {
 
 __device__ __forceinline__ uint32_t lane63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
 
+// lane l <- lane l + 1 across the whole wave (DPP wave_shl:1; lane 63 <- 0)
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);
+}
+// lane l <- lane l - 1 (DPP wave_shr:1; lane 0 <- 0)
+__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, true); }
+#ifndef JDS_ENT_DPP_CHAIN
+#define JDS_ENT_DPP_CHAIN 1
+#endif
+
 // wave-wide totals (every lane active), read from lane 63 of the DPP scan
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane63(wave_incl_sum(v, (int)__lane_id())); }
 
@@ -497,6 +507,16 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
   // (every block costs >= 4 bits, so at most 7 lanes in a row lie inside one
   // word and share the next lane's word: spans of 8 lanes suffice; the host
   // model fails with spans of 4)
+#if JDS_ENT_DPP_CHAIN
+  {  // X_l = own_l | (F_l ? X_{l+1} : 0), one lane further per DPP wave shift (lane 63 never chains)
+    // (a mask, not a select: the shifts must run with every lane active, and
+    // the compiler turns a select into a branch around them)
+    const uint32_t own = X, fm = 0u - (uint32_t)F;
+#pragma unroll
+    for (int it = 0; it < 7; ++it) X = own | (wave_shl1(X) & fm);
+  }
+  const uint32_t X1 = wave_shl1(X);
+#else
 #pragma unroll
   for (int d = 1; d < 8; d <<= 1) {
     const uint32_t Xn = __shfl_down(X, d, 64);
@@ -507,6 +527,7 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
     }
   }
   const uint32_t X1 = __shfl_down(X, 1, 64);
+#endif
   const uint32_t in_tail = c ? ((fuse && lane == 63) ? tailx : X1) : 0u;
   uint32_t* rs = raw + raw_base(e, q.f, q.s);
   const unsigned long long wlast = (W1 - 1ull) >> 5;
@@ -587,7 +608,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   const long long gb = (long long)q.f * e.nb + e.first[q.s] + (valid ? bi : q.nbs - 1);
   const BlockRegs rg = load_block(coeffs + gb * 64);
   const int dc = coef_at<0>(rg);
-  int pred = __shfl_up(dc, 1, 64);
+  int pred = wave_shr1(dc);
   if (lane == 0) pred = q.seg ? (int)coeffs[(gb - 1) * 64] : 0;
   const int cls = q.s ? 1 : 0;
   uint32_t* st = &stage[wv][0][lane];
@@ -692,7 +713,7 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   const long long gb = (long long)q.f * e.nb + e.first[q.s] + (valid ? bi : q.nbs - 1);
   const BlockRegs rg = load_block(coeffs + gb * 64);
   const int dc = coef_at<0>(rg);
-  int pred = __shfl_up(dc, 1, 64);
+  int pred = wave_shr1(dc);
   if (lane == 0) pred = q.seg ? (int)coeffs[(gb - 1) * 64] : 0;
   uint32_t* st = &stage[wv][0][lane];
   uint32_t* ov = gst + (size_t)g * ES_MAXW * 64 + lane;
