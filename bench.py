@@ -690,7 +690,7 @@ def main():
         nbytes = int(lengths.sum().item())
         moved = B * cpf * 2 + nbytes  # algorithmic: coefficients in, files out
         result['entropy'] = {
-            'kernels': 'k_ent_walk, k_ent_fscan (segment bit totals), k_ent_place (shared words completed), k_ent_fscan (0xFF counts, output offsets, markers), k_ent_emit3', 'ms_per_step': round(t_ent, 4),
+            'kernels': 'k_ent_walk, k_ent_place (segment offsets, shared words completed), k_ent_fscan (0xFF counts, output offsets, markers), k_ent_emit3', 'ms_per_step': round(t_ent, 4),
             'Mpixels_per_s': round(px_per_step / (t_ent * 1e-3) / 1e6 * world, 2),
             'file_bytes_per_frame': round(nbytes / B, 1), 'bpp': round(8 * nbytes / px_per_step, 4),
             'bpp_estimate_no_entropy': None,

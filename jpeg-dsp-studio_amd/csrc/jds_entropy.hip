@@ -14,8 +14,8 @@
 //   k_ent_walk   each lane codes its block (zigzag walk, T.81 Annex K tables,
 //                left-aligned symbols appended by funnel shifts) into staging
 //                words; per-lane bit counts and per-segment totals.
-//   k_ent_fscan  per frame: each segment's bit offset within its scan.
-//   k_ent_place  each lane's words shifted into place in the packed scan
+//   k_ent_place  each segment's bit offset within its scan (the sum of the
+//                scan's earlier segment totals); each lane's words shifted into place in the packed scan
 //                (shared words combined by a segmented OR across the wave,
 //                the word shared with the next segment completed from that
 //                segment's leading bits), the scan's pad bits, the 0xFF bytes
@@ -687,6 +687,9 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
 #ifndef JDS_ENT_SPLIT
 #define JDS_ENT_SPLIT 1
 #endif
+#ifndef JDS_ENT_SELFPRE
+#define JDS_ENT_SELFPRE 1  // k_ent_place sums its scan's earlier segment totals (no k_ent_fscan<false>)
+#endif
 #ifndef JDS_ENT_NOFIX
 #define JDS_ENT_NOFIX 1  // k_ent_place completes the words segments share (no k_ent_fix)
 #endif
@@ -763,7 +766,30 @@ __global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nse
   const uint32_t nb = nbits[(size_t)g * 64 + lane];
   const uint32_t nbn = nbits[(size_t)gn * 64 + lane];
   const uint32_t w0n = gst[(size_t)gn * ES_MAXW * 64 + lane];  // (row 0; garbage where nbn == 0)
+#if JDS_ENT_SELFPRE
+  // the segment's bit offset in its scan: the scan's earlier totals (agg, every
+  // one final when this launch starts), summed across the wave -- no scan
+  // launch between the walk and the placement.  Lane sums are < 2^32 (<= 1024
+  // totals of <= 64 * 1660 bits); the wave sum in two DPP scans of 8 / 24 bits.
+  unsigned long long pre;
+  {
+    const unsigned long long* a0 = segoff + (g - q.seg);  // (segoff is agg here)
+    uint32_t ps = 0u;
+    for (int j0 = 0; j0 < q.seg; j0 += 512) {  // eight loads in flight per lane
+      uint32_t t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + 64 * u + lane;
+        t[u] = j < q.seg ? (uint32_t)a0[j] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) ps += t[u];
+    }
+    pre = ((unsigned long long)wave_sum(ps >> 8) << 8) + wave_sum(ps & 255u);
+  }
+#else
   const unsigned long long pre = segoff[g] - segoff[g - q.seg];
+#endif
   const uint32_t inc = wave_incl_sum(nb, lane), incn = wave_incl_sum(nbn, lane);
   const unsigned long long A = lane63(inc);
   const unsigned long long W1 = pre + A;
@@ -1140,9 +1166,11 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
     hipLaunchKernelGGL(k_ent_walk, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, ovf, nbits, agg, badseg,
                        ffs);
     if ((err = hipGetLastError()) != hipSuccess) return err;
-    hipLaunchKernelGGL(k_ent_fscan<false>, dim3(n), dim3(1024), 0, s, e, agg, segoff, ffx, nullptr, nullptr, nullptr,
-                       nullptr, nullptr, 0ll, nullptr, nullptr);
-    hipLaunchKernelGGL(k_ent_place, dim3(wg), dim3(256), 0, s, e, nseg, ovf, nbits, segoff, desc, raw, headw, ffs,
+    if (!JDS_ENT_SELFPRE)
+      hipLaunchKernelGGL(k_ent_fscan<false>, dim3(n), dim3(1024), 0, s, e, agg, segoff, ffx, nullptr, nullptr, nullptr,
+                         nullptr, nullptr, 0ll, nullptr, nullptr);
+    hipLaunchKernelGGL(k_ent_place, dim3(wg), dim3(256), 0, s, e, nseg, ovf, nbits, JDS_ENT_SELFPRE ? agg : segoff,
+                       desc, raw, headw, ffs,
                        info, scan_bits);
   } else {
     hipLaunchKernelGGL(k_ent_seg, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, desc, ovf, raw, headw,
