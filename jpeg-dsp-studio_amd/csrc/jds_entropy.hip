@@ -466,11 +466,16 @@ __device__ __forceinline__ int es_pad(uint32_t& v, unsigned long long W1, unsign
   return (used + 7) >> 3;
 }
 
+// 0xFF bytes of a word as loaded from memory (byte j = bits 8j..8j+7), among its first nvb bytes
+__device__ __forceinline__ int es_ff_mem(uint32_t x, int nvb) {
+  const uint32_t y = ~x;
+  const uint32_t hi = ~((((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) | 0x7F7F7F7Fu);  // bit 8j+7: byte j == 0xFF
+  const uint32_t vm = nvb >= 4 ? 0x80808080u : (((1u << (8 * (nvb < 0 ? 0 : nvb))) - 1u) & 0x80808080u);
+  return __popc(hi & vm);
+}
+
 __device__ __forceinline__ int es_ff(uint32_t v, int nbytes) {  // 0xFF bytes among the first nbytes (stream order)
-  int c = 0;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) c += (b < nbytes && ((v >> (24 - 8 * b)) & 255u) == 255u) ? 1 : 0;
-  return c;
+  return es_ff_mem(__builtin_bswap32(v), nbytes);
 }
 
 // Placement of a segment's staged words at scan bit offset pre (lane bits at
@@ -530,37 +535,41 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
 #endif
   const uint32_t in_tail = c ? ((fuse && lane == 63) ? tailx : X1) : 0u;
   uint32_t* rs = raw + raw_base(e, q.f, q.s);
-  const unsigned long long wlast = (W1 - 1ull) >> 5;
+  // word indices within the scan fit 32 bits (< 2^28 words)
+  const uint32_t wlast = (uint32_t)((W1 - 1ull) >> 5);
   const bool open_end = !fuse && !last_seg && (W1 & 31ull);
   const unsigned long long Wend = last_seg ? W1 : Wn;  // the scan ends in word wlast (0: it does not)
+  const uint32_t padw = Wend ? wlast : 0xFFFFFFFFu;     // the word that takes the pad bits
+  const uint32_t skipw = open_end ? wlast : 0xFFFFFFFFu;  // the word the next segment counts
   int ffc = 0;
-  auto put_word = [&](unsigned long long widx, uint32_t v) {
+  auto put_word = [&](uint32_t widx, uint32_t v) {
     int nb4 = 4;
-    if (Wend && widx == wlast) nb4 = es_pad(v, Wend, widx);
+    if (widx == padw) nb4 = es_pad(v, Wend, widx);
     rs[widx] = __builtin_bswap32(v);  // byte 0 of the stream first
-    if (!(open_end && widx == wlast)) ffc += es_ff(v, nb4);
+    if (widx != skipw) ffc += es_ff(v, nb4);
   };
   if (valid) {
     const bool own_head = sh == 0;
     const int nout = (int)(tw - hw);
-    if (own_head && !single) put_word(hw, hv);
+    const uint32_t hw32 = (uint32_t)hw, tw32 = (uint32_t)tw;
+    if (own_head && !single) put_word(hw32, hv);
     uint32_t prev = s0;
     int j = 1;
     for (; j + 3 < nout; j += 4) {  // four staged words requested before any is used
       const uint32_t c0 = stw(j), c1 = stw(j + 1), c2 = stw(j + 2), c3 = stw(j + 3);
-      put_word(hw + j, __builtin_amdgcn_alignbit(prev, c0, (uint32_t)sh));
-      put_word(hw + j + 1, __builtin_amdgcn_alignbit(c0, c1, (uint32_t)sh));
-      put_word(hw + j + 2, __builtin_amdgcn_alignbit(c1, c2, (uint32_t)sh));
-      put_word(hw + j + 3, __builtin_amdgcn_alignbit(c2, c3, (uint32_t)sh));
+      put_word(hw32 + j, __builtin_amdgcn_alignbit(prev, c0, (uint32_t)sh));
+      put_word(hw32 + j + 1, __builtin_amdgcn_alignbit(c0, c1, (uint32_t)sh));
+      put_word(hw32 + j + 2, __builtin_amdgcn_alignbit(c1, c2, (uint32_t)sh));
+      put_word(hw32 + j + 3, __builtin_amdgcn_alignbit(c2, c3, (uint32_t)sh));
       prev = c3;
     }
     for (; j < nout; ++j) {
       const uint32_t cur = stw(j);
-      put_word(hw + j, __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh));
+      put_word(hw32 + j, __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh));
       prev = cur;
     }
     const uint32_t tv = single ? hv : __builtin_amdgcn_alignbit(prev, stw(nout), (uint32_t)sh);
-    if (!single || own_head) put_word(tw, tv | in_tail);
+    if (!single || own_head) put_word(tw32, tv | in_tail);
     if (lane == 0 && !own_head && !fuse_prev) headw[g] = X;  // the previous segment holds this word's first bit
   }
   ffc = (int)wave_sum((uint32_t)ffc);
@@ -844,13 +853,6 @@ __device__ __forceinline__ long long es_scan_out(const EntGeo& e, int f, int s, 
   return p;
 }
 
-// 0xFF bytes of a word as loaded from memory (byte j = bits 8j..8j+7), among its first nvb bytes
-__device__ __forceinline__ int es_ff_mem(uint32_t x, int nvb) {
-  const uint32_t y = ~x;
-  const uint32_t hi = ~((((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) | 0x7F7F7F7Fu);  // bit 8j+7: byte j == 0xFF
-  const uint32_t vm = nvb >= 4 ? 0x80808080u : (((1u << (8 * (nvb < 0 ? 0 : nvb))) - 1u) & 0x80808080u);
-  return __popc(hi & vm);
-}
 
 // One wave per segment: the bytes of the words it finalised, stuffed (0x00
 // after every 0xFF) at their place in the file.  Per 1 KiB of input (16 B per

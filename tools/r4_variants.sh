@@ -5,7 +5,6 @@ set -e
 cd "$(dirname "$0")/.."
 rm -f tools/bin/ab/*.so tools/bin/ab/*.o
 python3 tools/build_variant.py A "" jds_entropy.hip
-python3 tools/build_variant.py P0 "-DJDS_ENT_SELFPRE=0" jds_entropy.hip
 python3 tools/build_variant.py S0 "-DJDS_ENT_SPLIT=0" jds_entropy.hip
 git show HEAD:jpeg-dsp-studio_amd/csrc/jds_entropy.hip > /tmp/ent_head.hip
 O=jpeg-dsp-studio_amd/jds/_obj
