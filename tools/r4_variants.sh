@@ -4,6 +4,4 @@ set -e
 cd "$(dirname "$0")/.."
 rm -f tools/bin/ab/*.so tools/bin/ab/*.o
 python3 tools/build_variant.py A "" jds_entropy.hip
-python3 tools/build_variant.py W0 "-DES_SW_DEF=0" jds_entropy.hip
-python3 tools/build_variant.py W4 "-DES_SW_DEF=4" jds_entropy.hip
-python3 tools/build_variant.py W16 "-DES_SW_DEF=16" jds_entropy.hip
+python3 tools/build_variant.py P0 "-DJDS_ENT_HI_PIPE=0" jds_entropy.hip
