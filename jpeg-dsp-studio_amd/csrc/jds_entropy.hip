@@ -318,10 +318,31 @@ constexpr unsigned long long ES_FA = 1ull << 62, ES_FP = 2ull << 62, ES_VAL = ES
 // words apart, so a wave's stores hit 64 banks), slots >= ES_SW to the
 // segment's global area (same word-major layout: word k of lane l at
 // (g * ES_MAXW + k) * 64 + l).
+#ifndef JDS_ENT_LEFT
+#define JDS_ENT_LEFT 1  // pending bits left-aligned: an append is one shift and one OR
+#endif
+// a table symbol without its length field (JDS_ENT_LEFT needs clean symbols)
+__device__ __forceinline__ uint32_t es_code(uint32_t e) { return JDS_ENT_LEFT ? (e & ~31u) : e; }
 struct EsStage {
   uint32_t* st;
   uint32_t* ov;
   int k = 0;
+#if JDS_ENT_LEFT
+  // acc: the n pending bits left-aligned (the rest zero); symL clean (zero
+  // below its L bits, 0 when L = 0)
+  __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
+    const int t = n + L;
+    const uint32_t w = acc | (symL >> n);
+    if (t >= 32) {
+      if (k < ES_SW) st[k * 64] = w; else ov[k * 64] = w;
+      ++k;
+      acc = __builtin_amdgcn_alignbit(symL, 0u, (uint32_t)n);  // the bits that did not fit (0 when n = 0)
+    } else {
+      acc = w;
+    }
+    n = t & 31;
+  }
+#else
   __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
     const int t = n + L;
     if (t >= 32) {
@@ -332,6 +353,7 @@ struct EsStage {
     acc = L ? __builtin_amdgcn_alignbit(acc, symL, (uint32_t)(32 - L)) : acc;  // (acc << L) | sym
     n = t & 31;
   }
+#endif
   __device__ __forceinline__ void store(uint32_t w) {
     if (k < ES_SW) st[k * 64] = w; else ov[k * 64] = w;
   }
@@ -363,11 +385,11 @@ __device__ __forceinline__ void es_ac(const BlockRegs& r, int last, int& aor, co
     }
     if (a && run >= 16) {  // rare: one ZRL code per 16 zeros first
       const int zl = (int)(zrl & 31u);
-      for (int i = 0; i < (run >> 4); ++i) o.put(zrl, zl, acc, n);
+      for (int i = 0; i < (run >> 4); ++i) o.put(es_code(zrl), zl, acc, n);
     }
     const int L = (int)(e & 31u) + sz;
     const uint32_t mag = (uint32_t)(v + (v >> 31)) & ((1u << sz) - 1u);  // v, or v - 1 for v < 0, in sz bits
-    o.put(e | (mag << ((32 - L) & 31)), L, acc, n);
+    o.put(es_code(e) | (mag << ((32 - L) & 31)), L, acc, n);
     es_ac<K + 1>(r, nlast, aor, ac, zrl, acc, n, o, e1, v1, sz1, lastK);
   } else {
     lastK = last;
@@ -401,12 +423,12 @@ __device__ __forceinline__ void es_hi_code(const int16_t* cz, uint32_t m, int& l
     const int run = K - 1 - last;
     if (run >= 16) {  // one ZRL code per 16 zeros first
       const int zl = (int)(zrl & 31u);
-      for (int i = 0; i < (run >> 4); ++i) o.put(zrl, zl, acc, n);
+      for (int i = 0; i < (run >> 4); ++i) o.put(es_code(zrl), zl, acc, n);
     }
     const uint32_t e = ac[(run & 15) * ES_RS + sz];
     const int L = (int)(e & 31u) + sz;
     const uint32_t mag = (uint32_t)(v + (v >> 31)) & ((1u << sz) - 1u);
-    o.put(e | (mag << ((32 - L) & 31)), L, acc, n);
+    o.put(es_code(e) | (mag << ((32 - L) & 31)), L, acc, n);
     last = K;
   }
 }
@@ -430,16 +452,16 @@ __device__ __forceinline__ uint32_t es_block(const BlockRegs& r, int diff, const
   const uint32_t ed = es.dc[cls][ds];
   const int Ld = (int)(ed & 31u) + ds;
   const uint32_t md = (uint32_t)(diff + (diff >> 31)) & ((1u << ds) - 1u);
-  o.put(ed | (md << ((32 - Ld) & 31)), Ld, acc, n);
+  o.put(es_code(ed) | (md << ((32 - Ld) & 31)), Ld, acc, n);
   int aor = 0, last = 0;
   es_ac<1>(r, 0, aor, es.ac[cls], es.zrl[cls], acc, n, o, e1, v1, sz1, last);
   if constexpr (ES_DENSE < 64) es_hi_code(cz, mhi, last, aor, es.ac[cls], es.zrl[cls], acc, n, o);
   const uint32_t eb = es.eob[cls];
   const int Le = last < 63 ? (int)(eb & 31u) : 0;  // EOB unless coefficient 63 is set
-  o.put(eb, Le, acc, n);
+  o.put(Le ? es_code(eb) : 0u, Le, acc, n);
   bd |= aor > 1023;  // AC size > 10
   const uint32_t nb = 32u * (uint32_t)o.k + (uint32_t)n;
-  o.store(n ? acc << (32 - n) : 0u);
+  o.store(JDS_ENT_LEFT ? acc : (n ? acc << (32 - n) : 0u));
   return nb;
 }
 
