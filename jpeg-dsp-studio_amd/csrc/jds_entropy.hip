@@ -312,9 +312,10 @@ constexpr int ES_MAXW = 53;              // words per block at most (1660 bits +
 constexpr int ES_WAVES = 4;
 constexpr unsigned long long ES_FA = 1ull << 62, ES_FP = 2ull << 62, ES_VAL = ES_FA - 1ull;
 
-// Append the L (<= 32) bits of symL (left-aligned; bits below the symbol are
-// ignored) to the pending word acc (n bits, right-aligned; bits above n are
-// ignored); a completed word goes to the lane's LDS staging slot k (slots 64
+// Append the L (< 32) bits of symL (left-aligned) to the pending word acc (n
+// bits; JDS_ENT_LEFT: left-aligned with zeros below and a clean symbol, else
+// right-aligned with the bits outside ignored); a completed word goes to the
+// lane's LDS staging slot k (slots 64
 // words apart, so a wave's stores hit 64 banks), slots >= ES_SW to the
 // segment's global area (same word-major layout: word k of lane l at
 // (g * ES_MAXW + k) * 64 + l).
