@@ -4,5 +4,6 @@ set -e
 cd "$(dirname "$0")/.."
 rm -f tools/bin/ab/*.so tools/bin/ab/*.o
 python3 tools/build_variant.py A "" jds_entropy.hip
-python3 tools/build_variant.py L0 "-DJDS_ENT_LEFT=0" jds_entropy.hip
-python3 tools/build_variant.py S0 "-DJDS_ENT_SPLIT=0" jds_entropy.hip
+python3 tools/build_variant.py P3 "-DJDS_ENT_WPE=3" jds_entropy.hip
+python3 tools/build_variant.py P5 "-DJDS_ENT_WPE=5" jds_entropy.hip
+python3 tools/build_variant.py P6 "-DJDS_ENT_WPE=6" jds_entropy.hip
