@@ -16,11 +16,14 @@ broadcast from rank 0, the barrier, the max-over-ranks time and the per-rank
 frame-0 parity gather (`parity_ranks`).
 
 Prints ONE JSON line (rank 0).  The roofline object describes the dominant
-kernel (longer average launch) with ALGORITHMIC bytes: k_fwd reads 3 B/px RGB and
-writes 2*S B/px int16 coefficients, k_inv the reverse (S = coefficients per
-pixel, 1.5037 at 1080p 4:2:0).  Launch durations come from torch.cuda.Events on
-the stream the kernels run on, in a serial (non-overlapped) calibration pass
-after the timed region.  `traffic` (HBM bytes/launch from rocprofv3 PMC)
+kernel -- the single longest launch of a step -- with ALGORITHMIC bytes: a
+forward front end (k_fwd32i) reads 3 B/px RGB and writes 2*S B/px int16
+coefficients, an inverse (k_inv_fast) the reverse (S = coefficients per pixel,
+1.5037 at 1080p 4:2:0).  Launch durations (`kernels_ms`) come from the plan
+itself: K more steps exactly as timed, right after the timed region, with
+jds_plan_profile's event marks after every launch on the launch stream; the
+intervals tile the profiled span, so they sum to the step time.  `traffic`
+(HBM bytes/launch of that kernel from rocprofv3 FETCH_SIZE / WRITE_SIZE PMC)
 is read from profiles/pmc_traffic.json when it matches this configuration.
 """
 import argparse
@@ -80,7 +83,83 @@ def parse():
                     help='1: image-stream pipelining, two buffer sets; the forward of batch k+1 runs beside the '
                          'inverse of batch k on a second stream (measured no faster: the launches share CUs at '
                          'workgroup granularity).  0 (default): one jds_plan_run (forward then inverse) per step')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='launcher check without a GPU: each rank joins the process group (gloo), one all-reduce, '
+                         'rank 0 prints the world it saw (tests/test_bench_launch_cpu.py)')
     return ap.parse_args()
+
+
+def launch_decision(gpus, env, visible_gpus, dry_run=False):
+    """How `bench.py --gpus N` runs (--gpus must never be
+    ignored).  Returns (action, detail):
+      * ('run', None): this process is the whole job (N = 1) or one rank of a
+        torchrun job whose WORLD_SIZE equals N;
+      * ('spawn', backend): N > 1 without torchrun -- start N ranks as child
+        processes (torch.distributed.run) before any GPU call: 'nccl' with one
+        rank per GPU when N GPUs are visible, 'gloo' sharing the visible GPU(s)
+        when JDS_BENCH_REHEARSE=1 asks for the rehearsal (or for --dry-run);
+      * ('error', message): a mismatch -- exit non-zero, print nothing as JSON."""
+    if gpus < 1:
+        return 'error', f'--gpus must be >= 1, got {gpus}'
+    ws = env.get('WORLD_SIZE')
+    if ws is not None:
+        if int(ws) != gpus:
+            return 'error', (f'--gpus {gpus} but WORLD_SIZE={ws}: launch with torchrun --nproc-per-node {gpus} '
+                             f'(or without torchrun and let bench.py start the ranks)')
+        return 'run', None
+    if gpus == 1:
+        return 'run', None
+    if dry_run:
+        return 'spawn', 'gloo'
+    if visible_gpus >= gpus:
+        return 'spawn', 'nccl'
+    if env.get('JDS_BENCH_REHEARSE') == '1':
+        return 'spawn', 'gloo'
+    return 'error', (f'--gpus {gpus} but only {visible_gpus} GPU(s) visible; set JDS_BENCH_REHEARSE=1 to rehearse '
+                     f'{gpus} ranks sharing them over gloo (the line is then marked as a rehearsal)')
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(gpus, backend, argv):
+    """Start `gpus` ranks of this script under torch.distributed.run as a child
+    process (never exec: the parent has touched no GPU, and a child keeps the
+    launcher's exit status) and return its exit code."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    if backend == 'gloo':
+        env['JDS_BENCH_BACKEND'] = 'gloo'
+        env['JDS_BENCH_SHARE_GPU'] = '1'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={gpus}',
+           '--master-addr=127.0.0.1', f'--master-port={_free_port()}', os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run_main(args):
+    """One all-reduce over the ranks (gloo, no GPU); rank 0 prints what it saw."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    if world > 1:
+        dist.init_process_group('gloo')
+    t = torch.tensor([rank + 1.0])
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({'dry_run': True, 'gpus_flag': args.gpus, 'world_size': world,
+                          'rank_sum': float(t.item()), 'backend': os.environ.get('JDS_BENCH_BACKEND', 'nccl')}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 PREWARM_S = 0.3
@@ -270,7 +349,12 @@ def metric_name(q, mode):
 def dist_info(world, backend):
     import torch.distributed as dist
     if world > 1 and dist.is_initialized():
-        return {'world_size': dist.get_world_size(), 'backend': dist.get_backend()}
+        d = {'world_size': dist.get_world_size(), 'backend': dist.get_backend()}
+        if os.environ.get('JDS_BENCH_SHARE_GPU') == '1':
+            # ranks share the visible GPU(s): a rehearsal of the N > 1 path, not an N-GPU measurement
+            import torch
+            d['rehearsal_shared_gpus'] = torch.cuda.device_count()
+        return d
     return {'world_size': 1, 'backend': None}
 
 
@@ -500,17 +584,39 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    # Per-kernel launch durations from a serial calibration pass (outside the
-    # timed region): with pipelining the forward and inverse launches overlap,
-    # so their in-stream durations would not describe either kernel alone.
-    # Forward phase = k_fwd32i (+ k_fwd32 border tiles) + k_fwd_reduce + k_fix_fwd.
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    torch.cuda.synchronize(dev)
-    for k in range(args.steps):
-        step(k * NS, evs[k], si=s_f)
-    torch.cuda.synchronize(dev)
-    t_fwd = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    t_inv = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
+    # Per-kernel launch durations of the same runs (outside the timed region):
+    # K more steps exactly as timed, with the plan marking its stream after
+    # every launch (jds_plan_profile); the intervals between marks tile the
+    # span, so they sum to the profiled step time.  With pipelining (two
+    # streams) the phases overlap: then a serial pass with events per phase.
+    kernels, kprof = {}, None
+    if NS == 1:
+        plans[0].profile(True)
+        torch.cuda.synchronize(dev)
+        for k in range(args.steps):
+            run_step(nwarm + args.steps + k)
+        kt, span = plans[0].profile_read()
+        plans[0].profile(False)
+        kernels = {name: {'ms_per_step': tot / args.steps, 'launches_per_step': cnt / args.steps,
+                          'avg_launch_ms': tot / cnt} for name, (tot, cnt) in kt.items()}
+        kprof = {'profiled_step_ms': span / args.steps,
+                 'sum_ms': sum(v['ms_per_step'] for v in kernels.values()),
+                 'timing': 'jds_plan_profile: an event after every launch of the plan\'s runs, K steps after the '
+                           'timed region on the same stream; "(between runs)" = host gaps between runs'}
+        fwd_keys = [k for k in kernels if k.startswith(FWD_PREFIXES)]
+        inv_keys = [k for k in kernels if k.startswith(INV_PREFIXES)]
+        t_fwd = sum(kernels[k]['ms_per_step'] for k in fwd_keys)
+        t_inv = sum(kernels[k]['ms_per_step'] for k in inv_keys)
+    else:
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+        torch.cuda.synchronize(dev)
+        for k in range(args.steps):
+            step(k * NS, evs[k], si=s_f)
+        torch.cuda.synchronize(dev)
+        t_fwd = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+        t_inv = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
+        kernels = {'forward phase': {'ms_per_step': t_fwd, 'launches_per_step': 1, 'avg_launch_ms': t_fwd},
+                   'inverse phase': {'ms_per_step': t_inv, 'launches_per_step': 1, 'avg_launch_ms': t_inv}}
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev, backend)
 
@@ -519,45 +625,26 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
     S = cpf / (H * W)
     bytes_fwd = int(px_per_step * 3 + px_per_step * S * 2)  # one launch processes one batch
     bytes_inv = int(px_per_step * S * 2 + px_per_step * 3)
-    dom = 'k_fwd' if t_fwd >= t_inv else 'k_inv'
-    t_dom = max(t_fwd, t_inv)
-    achieved = (bytes_fwd if dom == 'k_fwd' else bytes_inv) / (t_dom * 1e-3) / 1e9
-    mcode = {"4:2:0": 2, "4:2:2": 1, "4:4:4": 0}[mode]
-    pfs = 'true' if (pf and mcode != 0) else 'false'
-    if block == 16:
-        if dom == 'k_fwd':
-            kname = f'k_fwd16<{mcode},{pfs}>' if args.exact else f'k_fwd16f<{mcode},{pfs}> + k_fix_fwd16<{mcode},{pfs}>'
-        else:
-            # the plan's 16x16 inverse: the certified k_inv16_fast (4:2:x); the
-            # exact k_inv16s with --exact-inv
-            kname = ((f'k_inv16_fast<{mcode}>' if not (args.exact or args.exact_inv)
-                      else f'k_inv16s<{mcode},0>') if mcode
-                     else f'k_chroma16<{mcode}> + k_inv16<{mcode}>')
-    else:
-        # the plan's inverse choice (jds_abi.hip inv_fast_ok): the certified fast
-        # kernel for 4:2:x with a DC quantiser <= 60 and the wave-local
-        # k_inv_fast444 at every 4:4:4 quality, k_inv2 otherwise
-        inv_fast = (mcode == 0 or float(qt[0][0]) <= 60.0 or args.inv_fast) and not (args.exact or args.exact_inv)
-        # (k_fwd32 runs only for border tiles k_fwd32i cannot take: fold_rows in jds_fast.hip)
-        fwd_name = ('k_fwd444w + k_fwd_reduce + k_fix_fwd' if mcode == 0 and not args.exact else
-                    f'k_fwd32i<{mcode},{pfs}> (+ k_fwd32 border tiles if any) + k_fwd_reduce_rows + k_fix_fwd')
-        kname = (fwd_name
-                 if dom == 'k_fwd' else ((('k_inv_fast444' if mcode == 0 else f'k_inv_fast<{mcode},0>') if inv_fast
-                                          else f'k_inv2<{mcode},0>')))
-    traffic = None
+    # the dominant kernel: the single longest launch of the step, with its own
+    # algorithmic bytes (front-end kernels: RGB in + coefficients out; inverse
+    # kernels: coefficients in + RGB out; both per launch over the whole batch)
+    cand = {k: v for k, v in kernels.items() if not k.startswith('(')}
+    kname = max(cand, key=lambda k: cand[k]['avg_launch_ms'])
+    t_dom = cand[kname]['avg_launch_ms']
+    dom = 'k_inv' if kname.startswith(INV_PREFIXES) or kname == 'inverse phase' else 'k_fwd'
+    dom_bytes = bytes_inv if dom == 'k_inv' else bytes_fwd
+    achieved = dom_bytes / (t_dom * 1e-3) / 1e9
+    traffic, traffic_src = None, None
     tf = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(tf):
         try:
             rec = json.load(open(tf))
             base = (f'{W}x{H}_q{quality}_{mode}_pf{int(bool(pf))}' + ('_B16' if block == 16 else '') + '_b')
-            nl = B  # frames per launch
-            if base + str(nl) in rec:
-                traffic = rec[base + str(nl)].get(dom)
-            else:  # bytes scale with frames per launch; recorded for other launch sizes
-                for kk, vv in rec.items():
-                    if kk.startswith(base) and vv.get(dom):
-                        traffic = int(vv[dom] * nl / int(kk[len(base):]))
-                        break
+            for kk, vv in rec.items():  # bytes scale with frames per launch (recorded for some launch size)
+                if kk.startswith(base) and kname in vv.get('kernels', {}):
+                    traffic = int(vv['kernels'][kname] * B / int(kk[len(base):]))
+                    traffic_src = vv.get('source')
+                    break
         except Exception:
             traffic = None
 
@@ -605,21 +692,35 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
                    'parallelism': f'frame-shard x{world}', **dist_info(world, backend)},
         'roofline': {'bound': bound, 'kernel': kname, 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                     'traffic_source': traffic_src,
                      'frac_vs_measured_copy_bw': round(achieved / HBM_COPY_GBS, 4),
-                     'algorithmic_bytes_per_launch': bytes_fwd if dom == 'k_fwd' else bytes_inv,
+                     'algorithmic_bytes_per_launch': dom_bytes,
+                     'algorithmic_bytes_note': (f'{B} frames x {H}x{W} px x ' +
+                                                (f'(2 x {S:.4f} B coefficients in + 3 B RGB out)' if dom == 'k_inv'
+                                                 else f'(3 B RGB in + 2 x {S:.4f} B coefficients out)')),
                      'avg_launch_ms': round(t_dom, 4),
-                     'timing': 'HIP events on the launch stream, serial calibration pass after the timed region',
+                     'timing': ('jds_plan_profile marks (kernels_ms)' if kprof else
+                                'HIP events per phase, serial calibration pass after the timed region'),
                      'valu': valu,
-                     'note': ('achieved / peak / frac: the HBM roofline by algorithmic bytes; bound: the resource '
-                              'with the larger fraction (valu.frac: issue cycles / SIMD cycles, DESIGN.md section 4 '
-                              'floor table)')},
-        'kernels_ms': {'k_fwd': round(t_fwd, 4), 'k_inv': round(t_inv, 4)},
+                     'note': ('kernel: the longest single launch of the step; achieved / peak / frac: the HBM '
+                              'roofline by its algorithmic bytes; bound: the resource with the larger fraction '
+                              '(valu.frac: issue cycles / SIMD cycles, DESIGN.md section 4 floor table)')},
+        'kernels_ms': {k: round(v['ms_per_step'], 4) for k, v in kernels.items()},
+        'kernels_profile': kprof and {**{k: round(v, 4) if isinstance(v, float) else v for k, v in kprof.items()},
+                                      'avg_launch_ms': {k: round(v['avg_launch_ms'], 4) for k, v in kernels.items()},
+                                      'phases_ms': {'forward': round(t_fwd, 4), 'inverse': round(t_inv, 4)}},
         'fixups_last_step': {'fwd_blocks': int(plans[0].fix_counts()[0]), 'inv_tiles': int(plans[0].fix_counts()[1])},
         'pipeline_roofline_frac': round(value / world * 1e6 * (6 + 2 * S) / (HBM_PEAK_GBS * 1e9), 4),
     }
     state = {'plans': plans, 'rgb': rgbs[0], 'out': outs[0], 'coeffs': coefs[0], 'stats': stats_l[0], 's_f': s_f,
              'cpf': cpf, 'qt': qt}
     return result, state
+
+
+# launch-mark names (jds_plan_profile) by phase: the forward front ends,
+# reductions and fix-ups; the inverse kernels and their per-frame tail
+FWD_PREFIXES = ('k_fwd', 'k_fix_fwd', 'k_quant_mq')
+INV_PREFIXES = ('k_inv', 'k_chroma16', 'k_finalize', 'k_sel_')
 
 
 def frame0_parity(state, quality, mode, pf, block):
@@ -643,6 +744,18 @@ NORTH_STAR = dict(B=16, H=2160, W=3840, quality=50, mode='4:2:0', pf=1)  # BASEL
 
 def main():
     args = parse()
+    visible = 0
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ and not args.dry_run:
+        import torch  # (counting devices does not initialise the GPU on this image)
+        visible = torch.cuda.device_count()
+    action, detail = launch_decision(args.gpus, os.environ, visible, args.dry_run)
+    if action == 'error':
+        print(f'bench.py: {detail}', file=sys.stderr, flush=True)
+        sys.exit(2)
+    if action == 'spawn':
+        sys.exit(spawn_ranks(args.gpus, detail, sys.argv[1:]))
+    if args.dry_run:
+        return dry_run_main(args)
     if args.sweep:
         return sweep_main(args)
     import torch
@@ -730,7 +843,7 @@ def main():
         nqt = broadcast_tables([ns['quality']])[0]
         r_ns, st_ns = run_point(args, dev, world, backend, rank, ns['B'], ns['H'], ns['W'], ns['quality'],
                                 ns['mode'], ns['pf'], 8, nqt, seed=3000)
-        keep = ('metric', 'value', 'unit', 'ms_per_step', 'warmup_steps_run', 'roofline', 'kernels_ms',
+        keep = ('metric', 'value', 'unit', 'ms_per_step', 'warmup_steps_run', 'roofline', 'kernels_ms', 'kernels_profile',
                 'fixups_last_step', 'pipeline_roofline_frac')
         result['north_star'] = {k: r_ns[k] for k in keep}
         result['north_star']['config'] = {'workload': r_ns['config']['workload'],

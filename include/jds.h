@@ -145,6 +145,24 @@ int jds_plan_geometry(const jds_plan* plan, jds_geometry* out);
 int jds_plan_fix_counts(const jds_plan* plan, uint32_t* counts);
 void jds_plan_destroy(jds_plan* plan);
 
+/* Launch-level timing of jds_plan_run itself (bench.py's roofline; no reference
+ * counterpart -- the reference's Timer covers only the colour conversions,
+ * utils/metrics.py:31-48).  While profiling is on, every run of the plan marks
+ * its stream before its first launch and after each kernel launch with an event;
+ * jds_plan_profile_read waits for the last mark and returns, per kernel name (in
+ * first-seen order), the summed time between the mark before it and its own
+ * mark, and the number of launches.  "(between runs)" is the time from one run's
+ * last mark to the next run's first (host gaps).  The intervals tile the span
+ * from the first mark to the last, so their sum equals *span_ms.  Reading resets
+ * the record; jds_plan_profile(plan, 0) stops marking. */
+typedef struct {
+  char name[64];
+  double total_ms;
+  int64_t launches;
+} jds_kernel_time;
+int jds_plan_profile(jds_plan* plan, int enable);
+int jds_plan_profile_read(jds_plan* plan, jds_kernel_time* out, int max, int* n_out, double* span_ms);
+
 /* Host-buffer path: the drop-in for engines.pipeline.compress_reconstruct
  * (engines/pipeline.py:17-167).  Synchronous.  rgb: HxWx3 u8, C-contiguous.
  * Outputs (caller-allocated, all but rgb_out/stats nullable):

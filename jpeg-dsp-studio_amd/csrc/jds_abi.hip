@@ -223,7 +223,42 @@ struct jds_plan {
   DevBuf ent[8], ent_hdr, ent_tab;  // entropy coder scratch, allocated by the first jds_plan_entropy
   DevBuf gen_tab, gen_sub, gen_rec;  // general-geometry path (jds_gen.hip)
   GenBufs gen() const { return {(const AreaTap*)gen_tab.p, (double*)gen_sub.p, (double*)gen_rec.p}; }
+  // jds_plan_profile: the launch marks of profiled runs (event pool + names)
+  bool prof_on = false;
+  KMarks marks;
 };
+
+namespace jds {
+thread_local KMarks* t_kmarks = nullptr;
+
+void kmark(hipStream_t s, const char* fmt, ...) {
+  KMarks* m = t_kmarks;
+  if (!m || m->n >= m->cap) return;
+  if (hipEventRecord(m->ev[m->n], s) != hipSuccess) return;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(m->name[m->n], sizeof m->name[0], fmt, ap);
+  va_end(ap);
+  m->n++;
+}
+}  // namespace jds
+
+// Marks the runs of a profiled plan on this thread (jds_plan_run's scope).
+struct MarkScope {
+  explicit MarkScope(jds_plan* p, hipStream_t s) {
+    if (!p->prof_on) return;
+    t_kmarks = &p->marks;
+    kmark(s, "(between runs)");
+  }
+  ~MarkScope() { t_kmarks = nullptr; }
+};
+
+static void marks_release(KMarks& m) {
+  for (int i = 0; i < m.cap; ++i) (void)hipEventDestroy(m.ev[i]);
+  free(m.ev);
+  free(m.name);
+  m = KMarks{};
+}
 
 // ------------------------------------------------------------- geometry --
 
@@ -660,6 +695,7 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   if (((uintptr_t)rgb | (uintptr_t)rgb_out | (uintptr_t)coeffs | (uintptr_t)stats) & 15u)
     return fail(JDS_EINVAL, "rgb, rgb_out, coeffs and stats must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream (torch's default stream)
+  const MarkScope marks_(p, s);         // jds_plan_profile: launch marks of this run
   int phases = (flags & JDS_RUN_FWD ? 1 : 0) | (flags & JDS_RUN_INV ? 2 : 0);
   if (!phases) phases = 3;
   const bool exact = (flags & JDS_RUN_EXACT) != 0;
@@ -732,6 +768,69 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   return JDS_OK;
 }
 
+int jds_plan_profile(jds_plan* p, int enable) {
+  if (!p) return fail(JDS_EINVAL, "null argument");
+  if (enable && !p->marks.cap) {
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    const int cap = 8192;  // marks until the next read: ~7 per run
+    KMarks m;
+    m.ev = (hipEvent_t*)calloc(cap, sizeof(hipEvent_t));
+    m.name = (char(*)[64])calloc(cap, sizeof *m.name);
+    if (!m.ev || !m.name) {
+      free(m.ev);
+      free(m.name);
+      return fail(JDS_ENOMEM, "host allocation failed");
+    }
+    for (; m.cap < cap; ++m.cap) {
+      hipError_t e = hipEventCreate(&m.ev[m.cap]);
+      if (e != hipSuccess) {
+        marks_release(m);
+        return fail(JDS_EHIP, "hipEventCreate: %s", hipGetErrorString(e));
+      }
+    }
+    p->marks = m;
+  }
+  p->prof_on = enable != 0;
+  p->marks.n = 0;
+  return JDS_OK;
+}
+
+int jds_plan_profile_read(jds_plan* p, jds_kernel_time* out, int max, int* n_out, double* span_ms) {
+  if (!p || !n_out || (max > 0 && !out)) return fail(JDS_EINVAL, "null argument");
+  KMarks& m = p->marks;
+  *n_out = 0;
+  if (span_ms) *span_ms = 0.0;
+  if (m.n < 2) {
+    m.n = 0;
+    return JDS_OK;
+  }
+  HIP_TRY(hipSetDevice(p->ctx->device));
+  HIP_TRY(hipEventSynchronize(m.ev[m.n - 1]));
+  int k = 0;
+  for (int i = 1; i < m.n; ++i) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, m.ev[i - 1], m.ev[i]));
+    int j = 0;
+    while (j < k && strncmp(out[j].name, m.name[i], sizeof out[j].name) != 0) ++j;
+    if (j == k) {
+      if (k == max) continue;  // more distinct names than the caller's array holds
+      memset(&out[k], 0, sizeof out[k]);
+      snprintf(out[k].name, sizeof out[k].name, "%s", m.name[i]);
+      ++k;
+    }
+    out[j].total_ms += ms;
+    out[j].launches += 1;
+  }
+  if (span_ms) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, m.ev[0], m.ev[m.n - 1]));
+    *span_ms = ms;
+  }
+  *n_out = k;
+  m.n = 0;
+  return JDS_OK;
+}
+
 void jds_plan_destroy(jds_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
@@ -755,6 +854,7 @@ void jds_plan_destroy(jds_plan* p) {
   p->ent_hdr.release();
   p->ent_tab.release();
   free(p->qt);
+  marks_release(p->marks);
   if (p->side.stream) (void)hipStreamDestroy(p->side.stream);
   if (p->side.fork) (void)hipEventDestroy(p->side.fork);
   if (p->side.join) (void)hipEventDestroy(p->side.join);

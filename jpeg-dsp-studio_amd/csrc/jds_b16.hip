@@ -756,6 +756,7 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
       hipLaunchKernelGGL((k_fwd16<MODE, (MODE != M444)>), grid, dim3(C::TF), 0, s, g, rgb, coeffs, fq, gk, st);
     else
       hipLaunchKernelGGL((k_fwd16<MODE, false>), grid, dim3(C::TF), 0, s, g, rgb, coeffs, fq, gk, st);
+    if (!ff) kmark(s, "k_fwd16<%d,%d>", MODE, (int)(MODE != M444 && pf));
     if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_fwd_finish(g, n, st, nullptr, 0, s)) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
@@ -785,15 +786,18 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
       else
         hipLaunchKernelGGL((K_INV16<MODE, 0>), gi, bi, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, nullptr,
                            nullptr);
+      kmark(s, "k_inv16s<%d,%d>", MODE, err_y ? 2 : rin ? 1 : 0);
 #undef K_INV16
       if ((e = hipGetLastError()) != hipSuccess) return e;
       }
     } else {
       const int cblocks = 2 * g.ncy * g.ncx;
       hipLaunchKernelGGL((k_chroma16<MODE>), dim3((cblocks + 15) / 16, n), dim3(256), 0, s, g, coeffs, fq, planes);
+      kmark(s, "k_chroma16<%d>", MODE);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       hipLaunchKernelGGL((k_inv16<MODE>), grid, dim3(C::TI), 0, s, g, coeffs, fq, planes, rin, rgb_out, st, part,
                          err_y, err_rgb);
+      kmark(s, "k_inv16<%d>", MODE);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;

@@ -566,6 +566,7 @@ __global__ void k_fwd_finish(const Geo g, jds_frame_stats* st) {
 
 hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s) {
   hipLaunchKernelGGL(k_fwd_reduce, dim3((ptiles + 63) / 64, n), dim3(512), 0, s, st, part, ptiles);
+  kmark(s, "k_fwd_reduce");
   return hipGetLastError();
 }
 
@@ -576,6 +577,7 @@ hipError_t launch_fwd_finish(const Geo& g, int n, jds_frame_stats* st, const uin
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_fwd_finish, dim3(n), dim3(64), 0, s, g, st);
+  kmark(s, "k_fwd_finish");
   return hipGetLastError();
 }
 
@@ -598,6 +600,7 @@ __global__ void k_finalize(const Geo g, jds_frame_stats* st, const double* __res
 hipError_t launch_finalize(const Geo& g, int n, jds_frame_stats* st, const double* part, int tiles, bool with_sse,
                            hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, tiles, (int)with_sse, 0);
+  kmark(s, "k_finalize");
   return hipGetLastError();
 }
 
@@ -610,6 +613,7 @@ static hipError_t launch_fwd_t(const Geo& g, int n, const uint8_t* rgb, int16_t*
   dim3 grid(g.tiles_y * g.tiles_x, n);
   hipLaunchKernelGGL((k_fwd<MODE, PF>), grid, dim3(Cfg<MODE>::TF), 0, s, g, rgb, coeffs, fq, gk, st, sel,
                      sel ? 0 : -1, sel_blk, in_div);
+  kmark(s, "k_fwd<%d,%d>", MODE, (int)PF);
   return hipGetLastError();
 }
 
@@ -621,6 +625,7 @@ static hipError_t launch_inv_t(const Geo& g, int n, const int16_t* coeffs, const
   dim3 grid(g.tiles_y * g.tiles_x, n);
   hipLaunchKernelGGL((k_inv<MODE>), grid, dim3(Cfg<MODE>::TI), 0, s, g, coeffs, fq, rgb_in, rgb_out, st, part,
                      err_y, err_rgb, sel, sel ? 0 : -1, sel_blk, in_div);
+  kmark(s, "k_inv<%d>", MODE);
   return hipGetLastError();
 }
 
@@ -660,9 +665,11 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
     if (e != hipSuccess || !(phases & 2)) return e;
     if (sel) {
       hipLaunchKernelGGL(k_sel_dequant, dim3(1), dim3(64), 0, s, coeffs, fq, sel, sel_blk);
+      kmark(s, "k_sel_dequant");
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, gen_px_tiles(g), (int)(rin != nullptr), 0);
+    kmark(s, "k_finalize");
     return hipGetLastError();
   }
   if (phases & 1) {
@@ -713,12 +720,14 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
     if (e != hipSuccess || (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess)) return e;
     if (sel) {
       hipLaunchKernelGGL(k_sel_dequant, dim3(1), dim3(64), 0, s, coeffs, fq, sel, sel_blk);
+      kmark(s, "k_sel_dequant");
       if ((e = hipGetLastError()) != hipSuccess) return e;
       if (!(phases & 4) && (e = launch_sel_recon(coeffs, fq, sel, sel_blk, s)) != hipSuccess) return e;
     }
     if (!fused_fin) {
       hipLaunchKernelGGL(k_finalize, dim3(n), dim3(64), 0, s, g, st, part, tiles,
                          (int)(rin != nullptr), (phases & 8) ? 1 : 0);
+      kmark(s, "k_finalize");
       e = hipGetLastError();
     }
   }

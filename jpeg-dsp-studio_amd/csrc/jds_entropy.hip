@@ -26,10 +26,9 @@
 //   k_ent_emit3  stuffed copy to the file (0x00 after every 0xFF).
 // (The rounds 1-3 multi-pass coder -- a counting walk, a block scan, a packing
 // walk with LDS atomics, per-chunk stuffing -- measured 0.54 ms per 64 x 1080p
-// against this one's 0.30; it is retired.  JDS_ENT_SPLIT=0 keeps the one-launch
-// form with a decoupled look-back, k_ent_seg.)
+// against this one's 0.30, and a one-launch form with a decoupled look-back
+// 0.386 ms; both are retired, their A/Bs are in DESIGN.md §4.)
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <string.h>
 
@@ -81,10 +80,10 @@ struct EntTab {
 };
 
 // left-aligned symbols: code << (32 - len) | len (len <= 16 sits below the code)
-#ifndef ES_RS_DEF
-#define ES_RS_DEF 11  // AC table row stride: (run, size) at run * 11 + size spreads a wave's lookups over the LDS banks
-#endif
-constexpr int ES_RS = ES_RS_DEF;  // (32: 0.271 vs 11: 0.258 ms per 64 x 1080p; a stride of 32 put every even run on the same 11 banks)
+// AC table row stride: (run, size) at run * 11 + size spreads a wave's lookups
+// over the LDS banks (32: 0.271 vs 11: 0.258 ms per 64 x 1080p; a stride of 32
+// put every even run on the same 11 banks)
+constexpr int ES_RS = 11;
 static_assert(ES_RS >= 11, "sizes 0..10");
 struct EsTab {
   uint32_t ac[2][16 * ES_RS];  // (run & 15, size) -> AC symbol, size clamped to 10 (code_ac's clamp); 0 for size 0
@@ -179,15 +178,8 @@ __device__ __forceinline__ long long raw_base(const EntGeo& e, int frame, int s)
 
 // Inclusive prefix sum over the wave (every lane active): row_shr 1, 2, 4, 8
 // within the 16-lane rows, then row_bcast 15 / 31 across them -- six DPP adds
-// (JDS_ENT_SHFL_SCAN: the log-step shuffle form, six ds_bpermute round trips).
+// (the log-step shuffle form, six ds_bpermute round trips, measured slower).
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
-#ifdef JDS_ENT_SHFL_SCAN
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
-#else
   (void)lane;
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
@@ -195,7 +187,6 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
-#endif
   return v;
 }
 
@@ -211,9 +202,6 @@ __device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {
 }
 // lane l <- lane l - 1 (DPP wave_shr:1; lane 0 <- 0)
 __device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, true); }
-#ifndef JDS_ENT_DPP_CHAIN
-#define JDS_ENT_DPP_CHAIN 1
-#endif
 
 // wave-wide totals (every lane active), read from lane 63 of the DPP scan
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return lane63(wave_incl_sum(v, (int)__lane_id())); }
@@ -269,66 +257,48 @@ constexpr uint8_t ZZC[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
                              35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                              58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-// ------------------------------------------------ single pass (round 4) --
+// ------------------------------------------------ one pass (round 4) --
 //
-// k_ent_seg (JDS_ENT_SPLIT=0): one wave per segment of 64 consecutive blocks
-// of one scan, segments in launch order.
-//  * walk: each lane packs its block MSB-first into lane-private staging
-//    words (LDS, word-major across the wave's lanes so every store hits its
-//    own bank; words past ES_SW spill to a per-block global area), so the
+// Segments of 64 consecutive blocks of one scan, one wave each.
+//  * walk (k_ent_walk): each lane packs its block MSB-first into lane-private
+//    staging words (LDS, word-major across the wave's lanes so every store hits
+//    its own bank; words past ES_SW go to the segment's global rows), so the
 //    block's bit count comes out of the same walk that packs it.  Appending a
-//    symbol is two funnel shifts (v_alignbit) on a 32-bit pending word.
-//  * offset: a wave-wide prefix of the lanes' bit counts, then a decoupled
-//    look-back over the scan's earlier segments (each publishes its
-//    aggregate, then its inclusive prefix; the single-pass scan of Merrill and
-//    Garland), 64 descriptors per probe.
-//  * placement: each lane writes its words shifted into place.  Words it
-//    alone covers: plain stores.  A word shared by several lanes is written
-//    once, by the lane holding its first bit, with the others' bits gathered
-//    by a segmented OR across the wave.  The segment's first word, when the
-//    previous segment holds its first bit, goes to headw[g]; k_ent_fix ORs it
-//    in afterwards (no zeroed memory, no global atomics on the stream).
-//  * the 0xFF bytes of every word the segment finalises are counted here
-//    (k_ent_fix counts the shared words), and each scan's last byte is padded
-//    with 1-bits (T.81 F.1.2.3), so the stuffing pass reads final words.
+//    symbol is one shift and one OR on a left-aligned 32-bit pending word.
+//  * offset: the segment's bit offset within its scan is the sum of the scan's
+//    earlier segment totals (k_ent_place sums them itself for short scans, a
+//    per-frame prefix launch gives them for long ones).
+//  * placement (k_ent_place): each lane writes its words shifted into place.
+//    Words it alone covers: plain stores.  A word shared by several lanes is
+//    written once, by the lane holding its first bit, with the others' bits
+//    gathered by a segmented OR across the wave; the word a segment shares with
+//    the next is completed from the next segment's leading bits.
+//  * the 0xFF bytes of every word the segment finalises are counted there,
+//    and each scan's last byte is padded with 1-bits (T.81 F.1.2.3), so the
+//    stuffing pass reads final words.
 // A segment that is not the last of its scan holds >= 256 bits (every block
 // costs >= 4), so only consecutive segments share a word.
-#ifndef JDS_ENT_WPE
-#define JDS_ENT_WPE 4  // waves per SIMD the walk's registers are held to (the scheduler hoists lookups freely)
-#endif
-#ifndef ES_LB
-#define ES_LB 1  // look-back descriptors per lane and probe (4: 0.473, 8: 0.545 vs 1: 0.386 ms per 64 x 1080p; device-coherent loads)
-#endif
-#ifndef ES_DENSE
-#define ES_DENSE 32  // zigzag positions coded by the unrolled walk; the rest by the nonzero loop (64: none)
-#endif
-static_assert(ES_DENSE >= 32 && ES_DENSE <= 64, "the nonzero loop's mask is 32 bits");
-#ifndef ES_SW_DEF
-#define ES_SW_DEF (ES_DENSE < 64 ? 8 : 32)  // 16: 0.303, 0: 0.295, 8: 0.292 ms per 64 x 1080p (LDS -> 5 workgroups per CU)
-#endif
-constexpr int ES_SW = ES_SW_DEF;         // LDS staging words per lane (more spill to global)
+constexpr int ES_WPE = 4;     // waves per SIMD the walk's registers are held to (3..6: no difference)
+constexpr int ES_DENSE = 32;  // zigzag positions coded by the unrolled walk; the rest by the nonzero loop
+// LDS staging words per lane (more go to global): 16: 0.303, 0: 0.295, 8: 0.292
+// ms per 64 x 1080p (LDS -> 5 workgroups per CU)
+constexpr int ES_SW = 8;
 constexpr int ES_HI = 64 - ES_DENSE;     // positions of the nonzero loop
 constexpr int ES_MAXW = 53;              // words per block at most (1660 bits + the partial word): the spill area
 constexpr int ES_WAVES = 4;
-constexpr unsigned long long ES_FA = 1ull << 62, ES_FP = 2ull << 62, ES_VAL = ES_FA - 1ull;
 
-// Append the L (< 32) bits of symL (left-aligned) to the pending word acc (n
-// bits; JDS_ENT_LEFT: left-aligned with zeros below and a clean symbol, else
-// right-aligned with the bits outside ignored); a completed word goes to the
-// lane's LDS staging slot k (slots 64
-// words apart, so a wave's stores hit 64 banks), slots >= ES_SW to the
-// segment's global area (same word-major layout: word k of lane l at
-// (g * ES_MAXW + k) * 64 + l).
-#ifndef JDS_ENT_LEFT
-#define JDS_ENT_LEFT 1  // pending bits left-aligned: an append is one shift and one OR
-#endif
-// a table symbol without its length field (JDS_ENT_LEFT needs clean symbols)
-__device__ __forceinline__ uint32_t es_code(uint32_t e) { return JDS_ENT_LEFT ? (e & ~31u) : e; }
+// Append the L (< 32) bits of symL (left-aligned, zero below) to the pending
+// word acc (n bits, left-aligned with zeros below: an append is one shift and
+// one OR; right-aligned pending bits measured 0.2405 against 0.2385 ms); a
+// completed word goes to the lane's LDS staging slot k (slots 64 words apart,
+// so a wave's stores hit 64 banks), slots >= ES_SW to the segment's global
+// area (same word-major layout: word k of lane l at (g * ES_MAXW + k) * 64 + l).
+// a table symbol without its length field
+__device__ __forceinline__ uint32_t es_code(uint32_t e) { return e & ~31u; }
 struct EsStage {
   uint32_t* st;
   uint32_t* ov;
   int k = 0;
-#if JDS_ENT_LEFT
   // acc: the n pending bits left-aligned (the rest zero); symL clean (zero
   // below its L bits, 0 when L = 0)
   __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
@@ -343,18 +313,6 @@ struct EsStage {
     }
     n = t & 31;
   }
-#else
-  __device__ __forceinline__ void put(uint32_t symL, int L, uint32_t& acc, int& n) {
-    const int t = n + L;
-    if (t >= 32) {
-      const uint32_t w = __builtin_amdgcn_alignbit(acc, symL, (uint32_t)n);  // the top 32 bits of acc . sym
-      if (k < ES_SW) st[k * 64] = w; else ov[k * 64] = w;
-      ++k;
-    }
-    acc = L ? __builtin_amdgcn_alignbit(acc, symL, (uint32_t)(32 - L)) : acc;  // (acc << L) | sym
-    n = t & 31;
-  }
-#endif
   __device__ __forceinline__ void store(uint32_t w) {
     if (k < ES_SW) st[k * 64] = w; else ov[k * 64] = w;
   }
@@ -462,7 +420,7 @@ __device__ __forceinline__ uint32_t es_block(const BlockRegs& r, int diff, const
   o.put(Le ? es_code(eb) : 0u, Le, acc, n);
   bd |= aor > 1023;  // AC size > 10
   const uint32_t nb = 32u * (uint32_t)o.k + (uint32_t)n;
-  o.store(JDS_ENT_LEFT ? acc : (n ? acc << (32 - n) : 0u));
+  o.store(acc);
   return nb;
 }
 
@@ -502,18 +460,18 @@ __device__ __forceinline__ int es_ff(uint32_t v, int nbytes) {  // 0xFF bytes am
 }
 
 // Placement of a segment's staged words at scan bit offset pre (lane bits at
-// pre + excl): see k_ent_seg.  st: the lane's LDS staging (slots < ES_SW),
-// ov: its global words (slots >= ES_SW, or all slots when st is null).
+// pre + excl): see "one pass" above.  st: the lane's LDS staging (slots <
+// ES_SW), ov: its global words (slots >= ES_SW, or all slots when st is null).
 // fuse (not the scan's last segment): tailx holds the next segment's bits that
-// share this segment's final word, so that word is written whole here (no
-// k_ent_fix); Wn: the scan's end bit when the next segment ends in that word.
+// share this segment's final word, so that word is written whole here; Wn: the
+// scan's end bit when the next segment ends in that word.
 __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g, int lane, bool valid, int nvalid,
                                          bool last_seg, uint32_t nb, uint32_t excl, unsigned long long pre,
                                          unsigned long long A, const uint32_t* st, const uint32_t* ov, int k,
-                                         uint32_t* __restrict__ raw, uint32_t* __restrict__ headw,
-                                         unsigned long long* __restrict__ ffs, unsigned long long* __restrict__ info,
-                                         unsigned long long* __restrict__ scan_bits, bool fuse = false,
-                                         uint32_t tailx = 0u, unsigned long long Wn = 0ull, bool fuse_prev = false) {
+                                         uint32_t* __restrict__ raw, unsigned long long* __restrict__ ffs,
+                                         unsigned long long* __restrict__ info,
+                                         unsigned long long* __restrict__ scan_bits, bool fuse, uint32_t tailx,
+                                         unsigned long long Wn) {
   const unsigned long long W1 = pre + A;
   auto stw = [&](int j) -> uint32_t { return j >= k ? 0u : ((st == nullptr || j >= ES_SW) ? ov[j * 64] : st[j * 64]); };
   const unsigned long long o = pre + excl;  // the lane's first bit in the scan
@@ -535,7 +493,6 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
   // (every block costs >= 4 bits, so at most 7 lanes in a row lie inside one
   // word and share the next lane's word: spans of 8 lanes suffice; the host
   // model fails with spans of 4)
-#if JDS_ENT_DPP_CHAIN
   {  // X_l = own_l | (F_l ? X_{l+1} : 0), one lane further per DPP wave shift (lane 63 never chains)
     // (a mask, not a select: the shifts must run with every lane active, and
     // the compiler turns a select into a branch around them)
@@ -544,18 +501,6 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
     for (int it = 0; it < 7; ++it) X = own | (wave_shl1(X) & fm);
   }
   const uint32_t X1 = wave_shl1(X);
-#else
-#pragma unroll
-  for (int d = 1; d < 8; d <<= 1) {
-    const uint32_t Xn = __shfl_down(X, d, 64);
-    const int Fn = __shfl_down(F, d, 64);
-    if (F && lane + d < 64) {
-      X |= Xn;
-      F = Fn;
-    }
-  }
-  const uint32_t X1 = __shfl_down(X, 1, 64);
-#endif
   const uint32_t in_tail = c ? ((fuse && lane == 63) ? tailx : X1) : 0u;
   uint32_t* rs = raw + raw_base(e, q.f, q.s);
   // word indices within the scan fit 32 bits (< 2^28 words)
@@ -593,7 +538,6 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
     }
     const uint32_t tv = single ? hv : __builtin_amdgcn_alignbit(prev, stw(nout), (uint32_t)sh);
     if (!single || own_head) put_word(tw32, tv | in_tail);
-    if (lane == 0 && !own_head && !fuse_prev) headw[g] = X;  // the previous segment holds this word's first bit
   }
   ffc = (int)wave_sum((uint32_t)ffc);
   if (lane == 0) {
@@ -606,126 +550,10 @@ __device__ __forceinline__ void es_place(const EntGeo& e, const EsSeg& q, int g,
   }
 }
 
-__global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per_eu(JDS_ENT_WPE))) k_ent_seg(const EntGeo e, const int nseg, const int16_t* __restrict__ coeffs,
-                                                            const EsTab* __restrict__ gt,
-                                                            unsigned long long* __restrict__ desc,
-                                                            uint32_t* __restrict__ ovf, uint32_t* __restrict__ raw,
-                                                            uint32_t* __restrict__ headw,
-                                                            unsigned long long* __restrict__ ffs,
-                                                            unsigned long long* __restrict__ info,
-                                                            unsigned long long* __restrict__ scan_bits,
-                                                            unsigned long long* __restrict__ bad) {
-  __shared__ EsTab es;
-  __shared__ uint32_t stage[ES_WAVES][ES_SW > 0 ? ES_SW : 1][64];
-  __shared__ int16_t czs[ES_WAVES][ES_HI > 0 ? ES_HI : 1][64];
-  {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(gt);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&es);
-    for (int i = threadIdx.x; i < (int)(sizeof(EsTab) / 4); i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int16_t* cz = &czs[wv][0][lane];
-  // Segments in launch order: a workgroup waits only for segments of lower
-  // index, and each XCD dispatches its workgroups in index order, so the
-  // lowest unfinished segment is always resident (no ticket: one
-  // device-scope counter for every wave serialised the launch).
-  const int g = blockIdx.x * ES_WAVES + wv;
-  if (g >= nseg) return;  // (whole wave; no barrier follows)
-  const EsSeg q = es_seg(e, g);
-  const int bi = q.seg * 64 + lane;  // block within the scan
-  const bool valid = bi < q.nbs;
-  const int nvalid = q.nbs - q.seg * 64 < 64 ? q.nbs - q.seg * 64 : 64;
-  const bool last_seg = q.seg == q.nseg_s - 1;
-  const long long gb = (long long)q.f * e.nb + e.first[q.s] + (valid ? bi : q.nbs - 1);
-  const BlockRegs rg = load_block(coeffs + gb * 64);
-  const int dc = coef_at<0>(rg);
-  int pred = wave_shr1(dc);
-  if (lane == 0) pred = q.seg ? (int)coeffs[(gb - 1) * 64] : 0;
-  const int cls = q.s ? 1 : 0;
-  uint32_t* st = &stage[wv][0][lane];
-  uint32_t* ov = ovf + (size_t)g * ES_MAXW * 64 + lane;
-  uint32_t nb = 0u;
-  int k = 0;
-  bool bd = false;
-  if (valid) {
-    EsStage o{st, ov};
-    nb = es_block(rg, dc - pred, es, cls, o, bd, cz);
-    k = (int)((nb + 31u) >> 5);
-  }
-  if (bd) bad[q.f] = 1ull;  // not baseline-codable: the frame is reported
-
-  // ---- offset: the wave's prefix, then the look-back over the scan's segments
-  const uint32_t inc = wave_incl_sum(nb, lane);
-  const uint32_t excl = inc - nb;
-  const unsigned long long A = lane63(inc);
-  unsigned long long pre = 0ull;
-#ifdef JDS_ENT_PROBE_NOLB  // timing probe (wrong output): no look-back
-  if (true) {
-    if (lane == 0) __hip_atomic_store(&desc[g], ES_FP | A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else
-#endif
-  if (q.seg == 0) {
-    if (lane == 0) __hip_atomic_store(&desc[g], ES_FP | A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    if (lane == 0) __hip_atomic_store(&desc[g], ES_FA | A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int lo = g - q.seg;  // the scan's first segment (publishes its prefix at once)
-    // each probe reads ES_LB descriptors per lane: segments base - ES_LB * lane - r, r = 0 .. ES_LB - 1,
-    // i.e. 64 * ES_LB predecessors per round trip
-    int base = g - 1, spins = 0;
-    while (true) {
-      int rp = ES_LB;        // the lane's first inclusive prefix (index r), ES_LB if none
-      bool zb = false;       // a not-yet-published descriptor before it
-      unsigned long long v = 0ull;
-#pragma unroll
-      for (int r = 0; r < ES_LB; ++r) {
-        const int j = base - ES_LB * lane - r;
-        const unsigned long long d =
-            j >= lo ? __hip_atomic_load(&desc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ES_FP;
-        const unsigned long long fl = d >> 62;
-        if (rp == ES_LB) {
-          zb |= fl == 0ull;
-          v += d & ES_VAL;
-          if (fl == 2ull) rp = r;
-        }
-      }
-      const unsigned long long pm = __ballot(rp < ES_LB);
-      const int p = pm ? (int)__builtin_ctzll(pm) : 64;
-      const unsigned long long upto = p >= 63 ? ~0ull : ((2ull << p) - 1ull);
-      if (__ballot(zb) & upto) {  // a predecessor has not published yet
-        if (++spins > (1 << 22)) {  // never expected: give up rather than hang (the frame reports failure)
-          bad[q.f] = 1ull;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-        continue;
-      }
-      v = lane <= p ? v : 0ull;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      pre += v;
-      if (p < 64) break;
-      base -= 64 * ES_LB;
-    }
-    if (lane == 0) __hip_atomic_store(&desc[g], ES_FP | (pre + A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  es_place(e, q, g, lane, valid, nvalid, last_seg, nb, excl, pre, A, st, ov, k, raw, headw, ffs, info, scan_bits);
-}
-
-// JDS_ENT_SPLIT: the same work without the look-back.  k_ent_walk packs
-// each segment's blocks and stores the staged words (word-major per segment),
-// the lanes' bit counts and the segment's total; a hipCUB scan over the
-// totals gives every segment's offset; k_ent_place places the words.
-#ifndef JDS_ENT_SPLIT
-#define JDS_ENT_SPLIT 1
-#endif
-#ifndef JDS_ENT_SELFPRE
-#define JDS_ENT_SELFPRE 1  // k_ent_place sums its scan's earlier segment totals (no k_ent_fscan<false>)
-#endif
-#ifndef JDS_ENT_NOFIX
-#define JDS_ENT_NOFIX 1  // k_ent_place completes the words segments share (no k_ent_fix)
-#endif
-__global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per_eu(JDS_ENT_WPE))) k_ent_walk(
+// k_ent_walk packs each segment's blocks and stores the staged words
+// (word-major per segment), the lanes' bit counts and the segment's total;
+// k_ent_place places the words at the segment's offset.
+__global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per_eu(ES_WPE))) k_ent_walk(
     const EntGeo e, const int nseg, const int16_t* __restrict__ coeffs, const EsTab* __restrict__ gt,
     uint32_t* __restrict__ gst, uint32_t* __restrict__ nbits, unsigned long long* __restrict__ agg,
     uint32_t* __restrict__ badseg, unsigned long long* __restrict__ ffs) {
@@ -777,13 +605,26 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
   }
 }
 
-// segoff = exclusive prefix of agg over all segments; incl[g] = the segment's
-// end bit within its scan (k_ent_fix / k_ent_emit3 read it as desc)
+// The segment's bit offset within its scan is the sum of the scan's earlier
+// segment totals.  Scans of at most ES_SELF_MAX segments (1080p: 507 luma, 128
+// chroma) sum them here -- every total is final when this launch starts -- and
+// need no prefix launch between the walk and the placement (0.245 -> 0.244 ms
+// per 64 x 1080p); longer scans (4K: 2025 luma segments) would re-sum O(n^2)
+// totals across their waves, so their frames get a per-frame exclusive prefix
+// (k_ent_fscan<false>, segoff) before this launch.
+#ifndef JDS_AB_ENT_SELF_MAX  // (temporary A/B hook)
+#define JDS_AB_ENT_SELF_MAX 512
+#endif
+constexpr int ES_SELF_MAX = JDS_AB_ENT_SELF_MAX;
+
+// incl[g] = the segment's end bit within its scan (k_ent_fscan / k_ent_emit3
+// read it as desc)
 __global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nseg, const uint32_t* __restrict__ gst,
                                                    const uint32_t* __restrict__ nbits,
+                                                   const unsigned long long* __restrict__ agg,
                                                    const unsigned long long* __restrict__ segoff,
                                                    unsigned long long* __restrict__ incl, uint32_t* __restrict__ raw,
-                                                   uint32_t* __restrict__ headw, unsigned long long* __restrict__ ffs,
+                                                   unsigned long long* __restrict__ ffs,
                                                    unsigned long long* __restrict__ info,
                                                    unsigned long long* __restrict__ scan_bits) {
   const int lane = threadIdx.x & 63;
@@ -793,19 +634,16 @@ __global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nse
   const bool valid = q.seg * 64 + lane < q.nbs;
   const int nvalid = q.nbs - q.seg * 64 < 64 ? q.nbs - q.seg * 64 : 64;
   const bool last_seg = q.seg == q.nseg_s - 1;
-  const bool fuse = JDS_ENT_NOFIX && !last_seg;
+  const bool fuse = !last_seg;      // this segment completes the word it shares with the next
   const int gn = fuse ? g + 1 : g;  // the next segment of the scan (its head bits)
   const uint32_t nb = nbits[(size_t)g * 64 + lane];
   const uint32_t nbn = nbits[(size_t)gn * 64 + lane];
   const uint32_t w0n = gst[(size_t)gn * ES_MAXW * 64 + lane];  // (row 0; garbage where nbn == 0)
-#if JDS_ENT_SELFPRE
-  // the segment's bit offset in its scan: the scan's earlier totals (agg, every
-  // one final when this launch starts), summed across the wave -- no scan
-  // launch between the walk and the placement.  Lane sums are < 2^32 (<= 1024
-  // totals of <= 64 * 1660 bits); the wave sum in two DPP scans of 8 / 24 bits.
   unsigned long long pre;
-  {
-    const unsigned long long* a0 = segoff + (g - q.seg);  // (segoff is agg here)
+  if (q.nseg_s <= ES_SELF_MAX) {  // (uniform: the scan's length)
+    // lane sums are < 2^32 (<= 8 totals of <= 64 * 1660 bits); the wave sum in
+    // two DPP scans of 8 / 24 bits
+    const unsigned long long* a0 = agg + (g - q.seg);
     uint32_t ps = 0u;
     for (int j0 = 0; j0 < q.seg; j0 += 512) {  // eight loads in flight per lane
       uint32_t t[8];
@@ -818,10 +656,9 @@ __global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nse
       for (int u = 0; u < 8; ++u) ps += t[u];
     }
     pre = ((unsigned long long)wave_sum(ps >> 8) << 8) + wave_sum(ps & 255u);
+  } else {
+    pre = segoff[g] - segoff[g - q.seg];  // (frame-relative prefixes)
   }
-#else
-  const unsigned long long pre = segoff[g] - segoff[g - q.seg];
-#endif
   const uint32_t inc = wave_incl_sum(nb, lane), incn = wave_incl_sum(nbn, lane);
   const unsigned long long A = lane63(inc);
   const unsigned long long W1 = pre + A;
@@ -838,44 +675,8 @@ __global__ void __launch_bounds__(256) k_ent_place(const EntGeo e, const int nse
     if (q.seg + 2 == q.nseg_s && sh && ((W1 + An - 1ull) >> 5) == ((W1 - 1ull) >> 5)) Wn = W1 + An;
   }
   es_place(e, q, g, lane, valid, nvalid, last_seg, nb, inc - nb, pre, A, nullptr,
-           gst + (size_t)g * ES_MAXW * 64 + lane, (int)((nb + 31u) >> 5), raw, headw, ffs, info, scan_bits, fuse,
-           tailx, Wn, JDS_ENT_NOFIX && q.seg > 0);
+           gst + (size_t)g * ES_MAXW * 64 + lane, (int)((nb + 31u) >> 5), raw, ffs, info, scan_bits, fuse, tailx, Wn);
 }
-
-// the first word of segment g when segment g - 1 holds its first bit: OR in
-// g's bits, pad if it is its scan's final word, count its 0xFF bytes for g - 1
-__global__ void k_ent_fix(const EntGeo e, const int nseg, const unsigned long long* __restrict__ desc,
-                          const uint32_t* __restrict__ headw, uint32_t* __restrict__ raw,
-                          unsigned long long* __restrict__ ffs) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nseg) return;
-  const EsSeg q = es_seg(e, g);
-  if (q.seg == 0) return;
-  const unsigned long long W0 = desc[g - 1] & ES_VAL, W1 = desc[g] & ES_VAL;
-  if (!(W0 & 31ull)) return;
-  const unsigned long long w = W0 >> 5;
-  uint32_t* rs = raw + raw_base(e, q.f, q.s);
-  uint32_t v = __builtin_bswap32(rs[w]) | headw[g];
-  int nb4 = 4;
-  if (q.seg == q.nseg_s - 1 && ((W1 - 1ull) >> 5) == w) nb4 = es_pad(v, W1, w);
-  rs[w] = __builtin_bswap32(v);
-  ffs[g - 1] += (unsigned long long)es_ff(v, nb4);
-}
-
-// output offset of scan s of frame f (after its SOS marker); ffx = exclusive
-// prefix of the segments' 0xFF counts
-__device__ __forceinline__ long long es_scan_out(const EntGeo& e, int f, int s, const unsigned long long* info,
-                                                 const unsigned long long* ffx) {
-  long long p = e.hdr + ENT_SOS;
-  const long long g0 = (long long)f * e.sfirst[3];
-  for (int j = 0; j < s; ++j) {
-    const unsigned long long nb = (info[2 * (f * 3 + j) + 1] + 7) >> 3;
-    const unsigned long long ff = ffx[g0 + e.sfirst[j + 1]] - ffx[g0 + e.sfirst[j]];
-    p += (long long)(nb + ff) + ENT_SOS;
-  }
-  return p;
-}
-
 
 // One wave per segment: the bytes of the words it finalised, stuffed (0x00
 // after every 0xFF) at their place in the file.  Per 1 KiB of input (16 B per
@@ -883,27 +684,11 @@ __device__ __forceinline__ long long es_scan_out(const EntGeo& e, int f, int s, 
 // assembled in the wave's LDS buffer at the output's alignment, then written
 // out as aligned dwords (bytes at the two partial ends).
 constexpr int EM_CHUNK = 1024;
-#ifndef JDS_EM_INTERLEAVE
-#define JDS_EM_INTERLEAVE 1
-#endif
-// each segment's first output byte (k_ent_emit3's one dependent lookup)
-__global__ void k_ent_offs(const EntGeo e, const int nseg, const unsigned long long* __restrict__ desc,
-                           const unsigned long long* __restrict__ info, const unsigned long long* __restrict__ ffx,
-                           unsigned long long* __restrict__ outoff) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nseg) return;
-  const EsSeg q = es_seg(e, g);
-  const unsigned long long W0 = q.seg ? (desc[g - 1] & ES_VAL) : 0ull;
-  const unsigned long long b0 = 4 * ((W0 + 31) >> 5);
-  outoff[g] = (unsigned long long)es_scan_out(e, q.f, q.s, info, ffx) + b0 +
-              (ffx[g] - ffx[(long long)q.f * e.sfirst[3] + e.sfirst[q.s]]);
-}
-
 // Per-frame exclusive prefix of a per-segment u64 array (one 1024-thread
 // workgroup per frame; frames' segment ranges are independent): out[g] is
 // frame-relative, tot[f] the frame's total.  OFFS: also each segment's first
-// output byte (what k_ent_offs computes), from the frame's own prefixes.
-// Replaces a hipCUB scan (two launches) and k_ent_offs.
+// output byte, from the frame's own prefixes, and the frame's markers.
+// (Replaced a hipCUB scan -- two launches -- and a per-segment offset launch.)
 template <bool OFFS>
 __global__ void __launch_bounds__(1024) k_ent_fscan(const EntGeo e, const unsigned long long* __restrict__ in,
                                                     unsigned long long* __restrict__ out,
@@ -957,11 +742,11 @@ __global__ void __launch_bounds__(1024) k_ent_fscan(const EntGeo e, const unsign
       const long long g = g0 + i;
       const int s2 = i < e.sfirst[1] ? 0 : (i < e.sfirst[2] ? 1 : 2);
       const int seg = i - e.sfirst[s2];
-      const unsigned long long W0 = seg ? (desc[g - 1] & ES_VAL) : 0ull;
+      const unsigned long long W0 = seg ? desc[g - 1] : 0ull;
       outoff[g] = (unsigned long long)so[s2] + 4 * ((W0 + 31) >> 5) + (out[g] - out[g0 + e.sfirst[s2]]);
       b |= (int)badseg[g];
     }
-    // the frame's markers (what k_ent_frame4 does; k_ent_emit3 writes only the scans' bytes)
+    // the frame's markers (k_ent_emit3 writes only the scans' bytes)
     if (t == 0) s_bad = 0;
     __syncthreads();
     if (b) s_bad = 1;
@@ -994,7 +779,7 @@ __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nse
   const int g = blockIdx.x * 4 + wv;
   if (g >= nseg) return;
   const EsSeg q = es_seg(e, g);
-  const unsigned long long W0 = q.seg ? (desc[g - 1] & ES_VAL) : 0ull, W1 = desc[g] & ES_VAL;
+  const unsigned long long W0 = q.seg ? desc[g - 1] : 0ull, W1 = desc[g];
   const unsigned long long nbytes = (info[2 * (q.f * 3 + q.s) + 1] + 7) >> 3;
   const unsigned long long fw = (W0 + 31) >> 5, lw = (W1 - 1) >> 5;
   if (fw > lw) return;
@@ -1003,7 +788,6 @@ __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nse
   const uint32_t* w = raw + raw_base(e, q.f, q.s);
   uint8_t* lb = reinterpret_cast<uint8_t*>(sbuf[wv]);
   for (unsigned long long i0 = b0; i0 < b1; i0 += EM_CHUNK) {
-#if JDS_EM_INTERLEAVE
     // lane l takes the chunk's dwords l, l + 64, l + 128, l + 192: coalesced
     // loads, and a wave's byte stores land on consecutive LDS words (16 B per
     // lane put lanes 16 apart on one bank)
@@ -1038,32 +822,6 @@ __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nse
         }
       }
     }
-#else
-    const unsigned long long i = i0 + 16 * lane;
-    uint32_t x[4] = {0u, 0u, 0u, 0u};
-    int nv = 0, ff = 0;
-    if (i < b1) {
-      nv = b1 - i < 16 ? (int)(b1 - i) : 16;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        x[j] = 4 * j < nv ? w[(i >> 2) + j] : 0u;
-        ff += es_ff_mem(x[j], nv - 4 * j);
-      }
-    }
-    const int len = nv + ff;
-    const int ex = wave_excl_sum(len, lane);
-    const int tot = (int)lane63((uint32_t)(ex + len));
-    const int sh0 = (int)((uintptr_t)dst & 3u);  // LDS byte sh0 <-> dst[0]
-    int p = sh0 + ex;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (j < nv) {
-        const uint8_t b = (uint8_t)(x[j >> 2] >> (8 * (j & 3)));
-        lb[p++] = b;
-        if (b == 0xFF) lb[p++] = 0x00;
-      }
-    }
-#endif
     __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations execute in order
     asm volatile("" ::: "memory");
     // out: global bytes dst[0 .. tot) <- LDS bytes [sh0, sh0 + tot); dword d covers LDS [4d, 4d + 4)
@@ -1081,30 +839,6 @@ __global__ void __launch_bounds__(256) k_ent_emit3(const EntGeo e, const int nse
     __builtin_amdgcn_wave_barrier();  // the buffer is reused by the next iteration
     asm volatile("" ::: "memory");
     dst += tot;
-  }
-}
-
-__global__ void k_ent_frame2(const EntGeo e, const uint8_t* __restrict__ hdr, const unsigned long long* __restrict__ info,
-                             const unsigned long long* __restrict__ ffx, uint8_t* __restrict__ out, long long stride,
-                             unsigned long long* __restrict__ lengths, const unsigned long long* __restrict__ bad) {
-  const int f = blockIdx.x;
-  uint8_t* dst = out + (long long)f * stride;
-  for (int i = threadIdx.x; i < e.hdr; i += blockDim.x) dst[i] = hdr[(long long)f * e.hdr + i];
-  if (threadIdx.x < 3) {
-    const int s = threadIdx.x;
-    uint8_t* m = dst + es_scan_out(e, f, s, info, ffx) - ENT_SOS;
-    const uint8_t sos[ENT_SOS] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(s + 1), (uint8_t)(s == 0 ? 0x00 : 0x11),
-                                  0x00, 0x3F, 0x00};
-    for (int i = 0; i < ENT_SOS; ++i) m[i] = sos[i];
-  }
-  if (threadIdx.x == 0) {
-    const long long g0 = (long long)f * e.sfirst[3];
-    const unsigned long long nb = (info[2 * (f * 3 + 2) + 1] + 7) >> 3;
-    const unsigned long long ff = ffx[g0 + e.sfirst[3]] - ffx[g0 + e.sfirst[2]];
-    const long long end = es_scan_out(e, f, 2, info, ffx) + (long long)(nb + ff);
-    dst[end] = 0xFF;
-    dst[end + 1] = 0xD9;
-    if (lengths) lengths[f] = bad[f] ? 0ull : (unsigned long long)(end + 2);  // 0: not baseline-codable
   }
 }
 
@@ -1133,29 +867,28 @@ long long ent_capacity(const Geo& g) {
   return e.hdr + 3 * ENT_SOS + 2 * 4 * e.raw_w + 2;
 }
 
-// scratch sizes (bytes): [0] segment descriptors / end bits (from the second
-// word), head words, segment totals, their prefix, per-lane bit counts,
-// per-segment error flags; [1] staged words (word-major per segment); [2]
-// info; [3] packed scans; [4] 0xFF counts per segment; [5] their prefix and
-// the frame totals; [6] headers; [7] hipCUB temp (JDS_ENT_SPLIT=0 only).
+// scratch sizes (bytes): [0] segment end bits (desc, from the second word),
+// segment totals (agg; reused for the output offsets once placed), their
+// per-frame prefix (segoff), per-lane bit counts, per-segment error flags; [1]
+// staged words (word-major per segment); [2] info; [3] packed scans; [4] 0xFF
+// counts per segment; [5] their prefix and the frame totals; [6] headers; [7]
+// unused.
 void ent_sizes(const Geo& g, int n, size_t* sz) {
   const EntGeo e = ent_geo(g);
   sz[2] = sizeof(unsigned long long) * 7 * n;  // 6 per frame (scan start / bits) + the frame's error flag
   sz[3] = sizeof(uint32_t) * e.raw_w * n;
   sz[6] = (size_t)e.hdr * n;
   const long long nseg = (long long)n * e.sfirst[3];
-  sz[0] = sizeof(unsigned long long) * (nseg + 2) + sizeof(uint32_t) * (nseg + 1);
-  sz[0] += sizeof(uint32_t) + sizeof(unsigned long long) * 2 * (nseg + 1) + sizeof(uint32_t) * 65 * nseg;
+  sz[0] = sizeof(unsigned long long) * (nseg + 2) + sizeof(unsigned long long) * 2 * (nseg + 1) +
+          sizeof(uint32_t) * 65 * nseg;
   sz[1] = sizeof(uint32_t) * ES_MAXW * 64 * nseg;
   sz[4] = sizeof(unsigned long long) * (nseg + 1);
   sz[5] = sizeof(unsigned long long) * (nseg + 1 + n);  // + the frame totals (k_ent_fscan)
-  size_t t1 = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                         (int)(nseg + 1));
-  sz[7] = t1 + 256;
+  sz[7] = 0;
 }
 
-// single pass: segments, fix-up of the shared words, stuffing
+// walk, (per-frame segment prefix for long scans,) placement, per-frame
+// offsets and markers, stuffing: 4 or 5 launches per batch of frames
 static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeffs, void* const* buf,
                                        const uint8_t* hdr_dev, const void* tab_dev, uint8_t* out, long long stride,
                                        unsigned long long* lengths, unsigned long long* scan_bits, hipStream_t s) {
@@ -1164,62 +897,42 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
   if (nseg_l >= (1ll << 31)) return hipErrorInvalidValue;
   const int nseg = (int)nseg_l;
   auto* desc = (unsigned long long*)buf[0] + 1;
-  auto* headw = (uint32_t*)(desc + nseg + 1);
+  auto* agg = desc + nseg + 1;
+  auto* segoff = agg + nseg + 1;
+  auto* nbits = (uint32_t*)(segoff + nseg + 1);
+  auto* badseg = nbits + 64 * (size_t)nseg;
+  auto* outoff = agg;  // (the segment totals, consumed by the placement)
   auto* ovf = (uint32_t*)buf[1];
   auto* info = (unsigned long long*)buf[2];
   auto* raw = (uint32_t*)buf[3];
   auto* ffs = (unsigned long long*)buf[4];
   auto* ffx = (unsigned long long*)buf[5];
-  void* temp = buf[7];
-  size_t sz[8];
-  ent_sizes(g, n, sz);
-  unsigned long long* bad = info + 6 * n;
-  hipError_t err;
-  if (!JDS_ENT_SPLIT) {
-    // every descriptor's flag starts at zero; ffs[nseg] closes the scan
-    if ((err = hipMemsetAsync(buf[0], 0, sizeof(unsigned long long) * (nseg + 1), s)) != hipSuccess) return err;
-    if ((err = hipMemsetAsync(ffs + nseg, 0, sizeof(unsigned long long), s)) != hipSuccess) return err;
-    if ((err = hipMemsetAsync(bad, 0, sizeof(unsigned long long) * n, s)) != hipSuccess) return err;
-  }
-  auto* badseg = (uint32_t*)((unsigned long long*)(headw + ((nseg + 2) & ~1)) + 2 * (nseg + 1)) + 64 * (size_t)nseg;
   const unsigned wg = (unsigned)((nseg + ES_WAVES - 1) / ES_WAVES);
   const EsTab* est = reinterpret_cast<const EsTab*>((const char*)tab_dev + sizeof(EntTab));
-  if (JDS_ENT_SPLIT) {
-    auto* agg = (unsigned long long*)(headw + ((nseg + 2) & ~1));  // 8-B aligned
-    auto* segoff = agg + nseg + 1;
-    auto* nbits = (uint32_t*)(segoff + nseg + 1);
-    hipLaunchKernelGGL(k_ent_walk, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, ovf, nbits, agg, badseg,
-                       ffs);
-    if ((err = hipGetLastError()) != hipSuccess) return err;
-    if (!JDS_ENT_SELFPRE)
-      hipLaunchKernelGGL(k_ent_fscan<false>, dim3(n), dim3(1024), 0, s, e, agg, segoff, ffx, nullptr, nullptr, nullptr,
-                         nullptr, nullptr, 0ll, nullptr, nullptr);
-    hipLaunchKernelGGL(k_ent_place, dim3(wg), dim3(256), 0, s, e, nseg, ovf, nbits, JDS_ENT_SELFPRE ? agg : segoff,
-                       desc, raw, headw, ffs,
-                       info, scan_bits);
-  } else {
-    hipLaunchKernelGGL(k_ent_seg, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, desc, ovf, raw, headw,
-                       ffs, info, scan_bits, bad);
+  hipLaunchKernelGGL(k_ent_walk, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, ovf, nbits, agg, badseg,
+                     ffs);
+  kmark(s, "k_ent_walk");
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  bool long_scan = false;
+  for (int c = 0; c < 3; ++c) long_scan = long_scan || e.sfirst[c + 1] - e.sfirst[c] > ES_SELF_MAX;
+  if (long_scan) {
+    hipLaunchKernelGGL(k_ent_fscan<false>, dim3(n), dim3(1024), 0, s, e, agg, segoff, ffx, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, 0ll, nullptr, nullptr);
+    kmark(s, "k_ent_fscan<0>");
   }
+  hipLaunchKernelGGL(k_ent_place, dim3(wg), dim3(256), 0, s, e, nseg, ovf, nbits, agg, segoff, desc, raw, ffs, info,
+                     scan_bits);
+  kmark(s, "k_ent_place");
   if ((err = hipGetLastError()) != hipSuccess) return err;
-  if (!(JDS_ENT_SPLIT && JDS_ENT_NOFIX))
-    hipLaunchKernelGGL(k_ent_fix, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, headw, raw,
-                       ffs);
-  auto* outoff = (unsigned long long*)(headw + ((nseg + 2) & ~1));  // (the split path's segment totals, consumed)
-  if (JDS_ENT_SPLIT) {
-    // frame-relative 0xFF prefixes and each segment's output offset in one launch; frame totals in ffs[nseg ..]
-    unsigned long long* fftot = ffx + nseg + 1;
-    hipLaunchKernelGGL(k_ent_fscan<true>, dim3(n), dim3(1024), 0, s, e, ffs, ffx, fftot, desc, info, outoff, hdr_dev,
-                       out, stride, lengths, badseg);
-    hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
-  } else {
-    size_t tb = sz[7];
-    if ((err = hipcub::DeviceScan::ExclusiveSum(temp, tb, ffs, ffx, nseg + 1, s)) != hipSuccess) return err;
-    hipLaunchKernelGGL(k_ent_offs, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, e, nseg, desc, info, ffx,
-                       outoff);
-    hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
-    hipLaunchKernelGGL(k_ent_frame2, dim3(n), dim3(256), 0, s, e, hdr_dev, info, ffx, out, stride, lengths, bad);
-  }
+  // frame-relative 0xFF prefixes, each segment's output offset and the frame's
+  // markers in one launch; frame totals in ffx[nseg + 1 ..]
+  unsigned long long* fftot = ffx + nseg + 1;
+  hipLaunchKernelGGL(k_ent_fscan<true>, dim3(n), dim3(1024), 0, s, e, ffs, ffx, fftot, desc, info, outoff, hdr_dev,
+                     out, stride, lengths, badseg);
+  kmark(s, "k_ent_fscan<1>");
+  hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
+  kmark(s, "k_ent_emit3");
   return hipGetLastError();
 }
 

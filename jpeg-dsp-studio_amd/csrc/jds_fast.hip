@@ -1924,23 +1924,27 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   if (MODE == M444 && !mq && !fwd444_tiled) {
     const int ng = fwd444w_groups(g);
     hipLaunchKernelGGL(k_fwd444w, dim3(ng, n), dim3(64 * F444_WAVES), 0, s, g, rgb, coeffs, fq32, part, fixlist, fc, st);
+    kmark(s, "k_fwd444w");
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
 #if JDS_FIX_REDUCE
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ng + FIX_RED_TILES - 1) / FIX_RED_TILES, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st,
                        fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ng, gx);
+    kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
 #else
     if constexpr (FLUSH_ROWS) {
       static_assert(F444_WAVES * 4 == 16, "16 row records per k_fwd444w workgroup");
       hipLaunchKernelGGL((k_fwd_reduce_rows<16, 1>), dim3((ng + RROWS_TILES - 1) / RROWS_TILES, n), dim3(256), 0, s, g,
                          st, part, ng);
+      kmark(s, "k_fwd_reduce_rows<16,1>");
       if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if ((e = launch_fwd_reduce(n, st, part, ng, s)) != hipSuccess) {
       return e;
     }
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
+    kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
 #endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
@@ -1967,6 +1971,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
       else
         hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(nout, n), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32, part,
                            fixlist, fc, 1, rect, nullptr, nullptr, 1);
+      kmark(sb, "k_fwd32<%d,%d%s>", MODE, (int)PF, mq ? ",mq" : "");
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (fork && (e = hipEventRecord(side->join, sb)) != hipSuccess) return e;
@@ -1976,6 +1981,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     else
       hipLaunchKernelGGL((k_fwd32i<MODE, PF>), dim3(nin, n), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32, part,
                          fixlist, fc, rect, nullptr, st, 1);
+    kmark(s, "k_fwd32i<%d,%d%s>", MODE, (int)PF, mq ? ",mq" : "");
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (fork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
   } else {
@@ -1985,12 +1991,14 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     else
       hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(g.tiles_y * g.tiles_x, n), dim3(C::TF), 0, s, g, rgb, coeffs,
                          fq32, gk32, part, fixlist, fc, 0, rect, nullptr, st, 1);
+    kmark(s, "k_fwd32<%d,%d%s>", MODE, (int)PF, mq ? ",mq" : "");
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   int ptiles = g.tiles_y * g.tiles_x;
   if (mq) {
     ptiles = quant_mq_tiles(g);
     hipLaunchKernelGGL(k_quant_mq, dim3(ptiles, nf), dim3(256), 0, s, g, nq, dct32, coeffs, fq32, part, fixbits);
+    kmark(s, "k_quant_mq");
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
@@ -2003,6 +2011,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
 #if JDS_FIX_REDUCE
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ptiles + FIX_RED_TILES - 1) / FIX_RED_TILES, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk,
                        st, fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ptiles, gx);
+    kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
 #else
     // the reduction and the fix-up are independent (both add into the frame
     // stats with atomics; the fix-up reads only its list): the reduction runs
@@ -2016,6 +2025,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     if constexpr (FLUSH_ROWS && C::TF < JDS_FLUSH_BARRIER_TF) {
       hipLaunchKernelGGL(k_fwd_reduce_rows<4 * (C::TF / 64)>, dim3((ptiles + RROWS_TILES - 1) / RROWS_TILES, n),
                          dim3(256), 0, rs, g, st, part, ptiles);
+      kmark(rs, "k_fwd_reduce_rows<%d>", 4 * (C::TF / 64));
       if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if ((e = launch_fwd_reduce(n, st, part, ptiles, rs)) != hipSuccess) {
       return e;
@@ -2023,6 +2033,7 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     if (rfork && (e = hipEventRecord(side->join, rs)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
+    kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
     if (rfork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
 #endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -2032,13 +2043,16 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   // at fixcount[n + item] (zeroed by the front-end launch)
   hipLaunchKernelGGL(k_fwd_reduce_fix, dim3((ptiles + 63) / 64, n), dim3(512), 0, s, g, st, part, ptiles,
                      fixbits, fixlist, fixcount);
+  kmark(s, "k_fwd_reduce_fix");
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (n < 8192) {  // one flat grid over every item's list (list starts in <= 32 KB of LDS)
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(FIX_GRID), dim3(64), sizeof(unsigned) * (n + 1), s, g, rgb,
                        coeffs, fq, gk, st, fixlist, fixcount + n, nq, n, nullptr);
+    kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
   } else {
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + n, nq, 0, nullptr);
+    kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;

@@ -940,10 +940,12 @@ static hipError_t fast16_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coe
   const int tiles = g.tiles_y * g.tiles_x;
   hipLaunchKernelGGL((k_fwd16f<MODE, PF>), dim3(tiles, n), dim3(C::TF), 0, s, g, rgb, coeffs, (const FastQ16*)fq16,
                      gk32, part, fixlist, counters + parity, counters + (parity ^ 1), cap, fix_all);
+  kmark(s, "k_fwd16f<%d,%d>", MODE, (int)PF);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_fix_fwd16<MODE, PF>), dim3(FIX16_GRID), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                      counters + parity, counters + 2, cap);
+  kmark(s, "k_fix_fwd16<%d,%d>", MODE, (int)PF);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return launch_fwd_reduce(n, st, part, tiles, s);  // the per-tile partials (order-free: u64 atomics)
 }

@@ -143,6 +143,18 @@ struct Cfg {
   static constexpr int TI = 384;                      // inverse threads
 };
 
+// Launch marks (jds_plan_profile): while a profiled plan run is on this
+// thread, each launch site records an event on its stream right after its
+// launch, named after the kernel; jds_plan_profile_read turns consecutive marks
+// into per-kernel durations.  No marks (a null pointer test) otherwise.
+struct KMarks {
+  hipEvent_t* ev = nullptr;
+  char (*name)[64] = nullptr;
+  int n = 0, cap = 0;
+};
+extern thread_local KMarks* t_kmarks;
+void kmark(hipStream_t s, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
 // Per-frame constants of the statistics and, when the forward deferred it,
 // the histogram's zero bin (k_fwd_finish, k_finalize, k_inv_fast's fused tail).
 __device__ inline void finalize_frame(const Geo& g, jds_frame_stats* s, int zero_bin) {

@@ -97,6 +97,7 @@ static hipError_t inv2_t(const Geo& g, int n, const int16_t* coeffs, const Frame
   else
     hipLaunchKernelGGL((k_inv2<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, nullptr,
                        nullptr, in_div);
+  kmark(s, "k_inv2<%d,%d>", MODE, err_y ? 2 : rgb_in ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -113,6 +114,7 @@ hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, con
 hipError_t launch_sel_recon(const int16_t* coeffs, const FrameQ* fq, jds_selected_block* sel, int sel_blk,
                             hipStream_t s) {
   hipLaunchKernelGGL(k_sel_recon, dim3(1), dim3(64), 0, s, coeffs, fq, sel, sel_blk);
+  kmark(s, "k_sel_recon");
   return hipGetLastError();
 }
 

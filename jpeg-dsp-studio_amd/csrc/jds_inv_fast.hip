@@ -1274,6 +1274,7 @@ hipError_t launch_inv16_fast(int mode, const Geo& g, int n, const int16_t* coeff
     const int tx = (g.W + TW - 1) / TW, ty = (g.H + TH - 1) / TH;
     hipLaunchKernelGGL(kern, dim3(ty * tx, n), dim3(256), 0, s, g, tx, coeffs, fq, rgb_out, fx.count + fx.parity,
                        fx.count + (fx.parity ^ 1), fx.item, fx.rot, fx.fix_all);
+    kmark(s, "k_inv16_fast<%d>", mode);
     return hipGetLastError();
   };
   if (mode == M420) return go(k_inv16_fast<M420>, Inv16<M420>::TH, Inv16<M420>::TW);
@@ -1295,6 +1296,7 @@ static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const F
   (void)rgb_in;  // SSE runs take the exact kernel (launch_codec)
   hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, cnt, nxt,
                      fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
+  kmark(s, "k_inv_fast<%d,0>", MODE);
   return hipGetLastError();
 }
 
@@ -1313,6 +1315,7 @@ hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs,
       const dim3 grid((unsigned)((nblk + 8 * I444_WAVES - 1) / (8 * I444_WAVES)), n), blk(64 * I444_WAVES);
       hipLaunchKernelGGL(k_inv_fast444, grid, blk, 0, s, g, coeffs, fq, rgb_out, st, fx.count + fx.parity,
                          fx.count + (fx.parity ^ 1), fx.item, fx.rot, fx.fix_all, fin);
+      kmark(s, "k_inv_fast444");
       return hipGetLastError();
     }
   }

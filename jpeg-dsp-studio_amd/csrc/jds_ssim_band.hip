@@ -92,6 +92,7 @@ struct SsimBatch {
   long long ns;           // cropped map size (H - 6) * (W - 6)
   long long ns_pitch;     // map stride per (item, channel): ns rounded up to 64 (16-B aligned buffers)
   long long n_pitch;      // luma plane stride: H * W rounded up to 64
+  long long ck_pitch;     // checkpoint stride per item: 5 * NB * W rounded up to 64
   int nch_s, nch_y;       // 8192-element buffers of the map / of the luma MSE stream
   double c1, c2, cov_norm;
   double* yplanes;        // [item][2][n_pitch]: Y of a, Y of b (H x W each)
@@ -246,7 +247,7 @@ __global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
   const int item = blockIdx.z;
   const double* X = B.yplanes + (size_t)item * 2 * B.n_pitch;
   const double* Y = X + B.n_pitch;
-  double* ck = B.ck + ((size_t)item * 5 + blockIdx.y) * (size_t)B.NB * B.W;
+  double* ck = B.ck + (size_t)item * B.ck_pitch + (size_t)blockIdx.y * B.NB * B.W;
   switch (blockIdx.y) {
     case 0: ychk_lane<0, BH>(X, Y, B.H, B.W, j, B.NB, ck); break;
     case 1: ychk_lane<1, BH>(X, Y, B.H, B.W, j, B.NB, ck); break;
@@ -487,7 +488,7 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   const SsimPair pr = B.pairs[item];
   const double* X = B.yplanes + (size_t)item * 2 * B.n_pitch;
   const double* Y = X + B.n_pitch;
-  const double* ck = B.ck + (size_t)item * 5 * B.NB * W;
+  const double* ck = B.ck + (size_t)item * B.ck_pitch;
   double* smap = B.smap + ((size_t)item * 4 + c) * B.ns_pitch;
   const int jend = W - 3;  // axis-1 steps j = 0 .. W - 4 (outputs 3 .. W - 4)
   const int nchunks = (jend + SB_CW - 1) / SB_CW;
@@ -697,10 +698,11 @@ __global__ void __launch_bounds__(256) k_ss_final(SsimBatch B) {
 
 // ------------------------------------------------------------------ host --
 
-#ifndef JDS_SSIM_BH
-#define JDS_SSIM_BH 8
-#endif
-constexpr int SB_BH = JDS_SSIM_BH;  // band height (rows per workgroup; 8 or 16)
+// band height (rows per workgroup): the RGB staging holds 16 rows per image
+// (b4[2][4][...]: four rows per word), i.e. the band plus its 6-row window
+// (BH = 16 measured 0.40 against 0.34 ms per pair, and does not fit it)
+constexpr int SB_BH = 8;
+static_assert(SB_BH + 6 <= 16, "k_ss_band's RGB staging holds 16 rows per image");
 
 int ssim_bands(int H) { return (H - 6 + SB_BH - 1) / SB_BH; }
 
@@ -761,6 +763,9 @@ static void pw_tree(int m, PwTree* T) {
 
 static long long ns_pitch_of(int H, int W) { return (((long long)(H - 6) * (W - 6)) + 63) & ~63LL; }
 static long long n_pitch_of(int H, int W) { return ((long long)H * W + 63) & ~63LL; }
+// the axis-0 checkpoints' doubles per item (5 quantities x bands x W), rounded up
+// to 64 so the maps after them stay 16-B aligned (k_ss_chunks' double2 loads)
+static long long ck_pitch_of(int H, int W) { return (5LL * ssim_bands(H) * W + 63) & ~63LL; }
 
 int ssim_batch_max_items() { return SB_MAX_ITEMS; }
 
@@ -768,7 +773,7 @@ int ssim_batch_max_items() { return SB_MAX_ITEMS; }
 size_t ssim_batch_scratch_doubles(int H, int W) {
   const size_t n = (size_t)H * W;
   const size_t nch = (n + SB_NP_BUF - 1) / SB_NP_BUF;  // n > ns
-  return 2 * (size_t)n_pitch_of(H, W) + 5 * (size_t)ssim_bands(H) * W + 4 * (size_t)ns_pitch_of(H, W) + 5 * nch;
+  return 2 * (size_t)n_pitch_of(H, W) + (size_t)ck_pitch_of(H, W) + 4 * (size_t)ns_pitch_of(H, W) + 5 * nch;
 }
 
 // SSIM R, G, B, Y and the luma MSE of `items` (<= SB_MAX_ITEMS) pairs (device
@@ -799,7 +804,8 @@ hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const*
   B.cov_norm = 49.0 / 48.0;
   B.yplanes = scratch;
   B.ck = B.yplanes + (size_t)items * 2 * B.n_pitch;
-  B.smap = B.ck + (size_t)items * 5 * B.NB * W;
+  B.ck_pitch = ck_pitch_of(H, W);
+  B.smap = B.ck + (size_t)items * B.ck_pitch;
   B.chunks = B.smap + (size_t)items * 4 * B.ns_pitch;
   B.out = out;
   B.out_stride = out_stride;

@@ -63,6 +63,10 @@ class SelectedBlock(C.Structure):
                 ('reconstructed', C.c_double * 64)]
 
 
+class KernelTime(C.Structure):
+    _fields_ = [('name', C.c_char * 64), ('total_ms', C.c_double), ('launches', C.c_int64)]
+
+
 class JDSError(RuntimeError):
     pass
 
@@ -85,6 +89,9 @@ _SIGS = {
     'jds_plan_geometry': (C.c_int, [_P, C.POINTER(Geometry)]),
     'jds_plan_fix_counts': (C.c_int, [_P, _P]),
     'jds_plan_destroy': (None, [_P]),
+    'jds_plan_profile': (C.c_int, [_P, C.c_int]),
+    'jds_plan_profile_read': (C.c_int, [_P, C.POINTER(KernelTime), C.c_int, C.POINTER(C.c_int),
+                                        C.POINTER(C.c_double)]),
     'jds_compress_reconstruct': (C.c_int, [_P, C.POINTER(Params), _P, C.c_int64, C.c_int64, _P, _P,
                                            C.POINTER(FrameStats), _P, _P, C.c_int32, C.c_int32,
                                            C.POINTER(SelectedBlock), C.POINTER(C.c_int32)]),
@@ -310,6 +317,18 @@ class Plan:
         c = np.zeros(2, np.uint32)
         check(lib().jds_plan_fix_counts(self.handle, c.ctypes.data))
         return c
+
+    def profile(self, enable: bool = True):
+        """Launch marks on every following run of this plan (jds_plan_profile)."""
+        check(lib().jds_plan_profile(self.handle, 1 if enable else 0))
+
+    def profile_read(self):
+        """(per-kernel {name: (total_ms, launches)} in first-seen order, span_ms) of the
+        runs since the last read; the intervals sum to span_ms."""
+        arr = (KernelTime * 64)()
+        n, span = C.c_int(0), C.c_double(0.0)
+        check(lib().jds_plan_profile_read(self.handle, arr, 64, C.byref(n), C.byref(span)))
+        return {arr[i].name.decode(): (arr[i].total_ms, int(arr[i].launches)) for i in range(n.value)}, span.value
 
     def close(self):
         if self.handle:

@@ -158,7 +158,7 @@ def test_struct_layouts_match_the_c_header(tmp_path):
     """ctypes mirrors == the C compiler's view of include/jds.h (sizes and offsets)."""
     from jds import _abi
     structs = {'jds_params': _abi.Params, 'jds_frame_stats': _abi.FrameStats, 'jds_geometry': _abi.Geometry,
-               'jds_selected_block': _abi.SelectedBlock}
+               'jds_selected_block': _abi.SelectedBlock, 'jds_kernel_time': _abi.KernelTime}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "jds.h"', 'int main(void) {']
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

@@ -108,6 +108,78 @@ def test_gpu_plan_entropy_batch():
     plan.close()
 
 
+def test_gpu_plan_entropy_64_frame_1080p_batch_matches_oracle():
+    """The bench's entropy leg exactly: PlanEntropy over a 64-frame 1080p Q50 4:2:0
+    batch (507 luma segments per scan, every frame in one launch) against the
+    oracle encoder on the same coefficients, frame by frame."""
+    import multiprocessing as mp
+    import os
+    import torch
+    from jds import _abi, codec, entropy
+    H, W, mode, q, B = 1080, 1920, '4:2:0', 50, 64
+    qt = cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q)
+    params = [_abi.make_params(q, qt, mode, True, codec.gaussian_kernel3())] * B
+    plan = _abi.Plan(_abi.context(0), params, H, W)
+    ent = entropy.PlanEntropy(plan)
+    dev = torch.device('cuda:0')
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(77)
+    rgb = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=gen)
+    out = torch.empty_like(rgb)
+    cf = torch.empty((B, plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+    st = torch.zeros((B, _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    files = torch.empty((B, ent.capacity), dtype=torch.uint8, device=dev)
+    lengths = torch.zeros(B, dtype=torch.int64, device=dev)
+    sbits = torch.zeros((B, 3), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), 0, s)
+    ent.run(cf.data_ptr(), files.data_ptr(), ent.capacity, lengths.data_ptr(), sbits.data_ptr(), s)
+    torch.cuda.synchronize()
+    ny, nc = counts(H, W, mode)
+    cfh, n_h, bits_h = cf.cpu().numpy(), lengths.cpu().numpy(), sbits.cpu().numpy()
+    files_h = files.cpu().numpy()
+    plan.close()
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    with mp.get_context('spawn').Pool(workers) as pool:
+        # (oracle worker processes: no GPU; ~5 s of Python per 1080p frame)
+        refs = pool.starmap(je.encode_jfif, [(cfh[i], H, W, mode, qt, ny, nc) for i in range(B)])
+    for i, (data, bits) in enumerate(refs):
+        assert int(n_h[i]) == len(data), i
+        assert files_h[i, :len(data)].tobytes() == data, i
+        assert bits_h[i].tolist() == bits, i
+
+
+@pytest.mark.parametrize('nblk,rows,seed', [(65, 1, 1), (129, 1, 2), (65, 2, 3), (66, 1, 6), (193, 1, 5)])
+def test_gpu_jfif_short_last_segment(nblk, rows, seed):
+    """Scans whose last segment (nblk mod 64 blocks) is short and mostly zero
+    blocks, with a few nonzero DC values so the segment boundary is not word
+    aligned: the last segment fits inside the previous segment's final word
+    (k_ent_place's fused-pad path and the skipped head word)."""
+    from jds import entropy
+    h, w, mode = 8 * rows, 8 * nblk, '4:4:4'
+    ny, nc = counts(h, w, mode)
+    rng = np.random.default_rng(seed)
+    blk = np.zeros((ny + 2 * nc, 64), np.int64)
+    pick = rng.choice(len(blk), max(1, len(blk) // 9), replace=False)
+    blk[pick, 0] = rng.integers(-40, 41, len(pick))
+    cf = blk.astype(np.int16).reshape(-1)
+    qt = np.ones((8, 8))
+    ref, ref_bits = je.encode_jfif(cf, h, w, mode, qt, ny, nc)
+    got, bits = entropy.encode_jfif(cf, h, w, mode, qt)
+    assert bits == ref_bits and got == ref
+    # the case is the one asked for: some scan's last segment starts off a word
+    # boundary and ends inside the same 32-bit word
+    n = ny
+    inside = []
+    for c in range(3):
+        bb = je.block_bits(blk[c * n:(c + 1) * n], c > 0)
+        cum = np.concatenate([[0], np.cumsum(bb)])
+        s0, e0 = int(cum[64 * ((n - 1) // 64)]), int(cum[n])
+        inside.append(s0 % 32 != 0 and s0 // 32 == (e0 - 1) // 32)
+    assert any(inside)
+    assert np.array_equal(je.decode_jfif(got)['coeffs'], cf)
+
+
 def test_gpu_jfif_rejects_non_baseline_coefficients():
     from jds import entropy
     h, w, mode = 16, 16, '4:4:4'

@@ -76,6 +76,17 @@ def test_cfg5_4k_q50_422_plan_matches_reference_golden():
     _golden_check('cfg5_rand4k_s0_q50_422_nopf', [0, _abi.RUN_INV_FIXALL, _abi.RUN_EXACT])
 
 
+def test_cfg2_1080p_plan_default_route_matches_reference_golden():
+    """configs[1], the headline: the plan's default route (flags = 0: k_fwd32i +
+    k_fwd_reduce_rows + k_fix_fwd, then the certified k_inv_fast with its
+    in-launch exact tile fallback -- exactly what bench.py times) against the
+    reference-run cfg2 digest; then the fallback forced on every tile and the
+    exact kernels (the cfg2 golden had only been checked
+    through the drop-in's exact kernels and the SSE route)."""
+    from jds import _abi
+    _golden_check('cfg2_rand1080p_s0_q50_420_pf', [0, _abi.RUN_INV_FIXALL, _abi.RUN_EXACT])
+
+
 def test_north_star_4k_q50_420_prefilter_plan_equals_exact_and_oracle():
     """The north-star point (BASELINE.json north_star: 4K / Q50 / 4:2:0, prefilter
     on): default == RUN_EXACT == RUN_INV_FIXALL, bit for bit (coefficients,

@@ -37,7 +37,7 @@ def _pair(h, w, seed, kind):
 
 
 SIZES = [(7, 7), (7, 40), (40, 7), (8, 9), (13, 8), (14, 14), (15, 39), (23, 70), (31, 37), (64, 64),
-         (100, 37), (129, 131), (255, 257), (518, 931), (1080, 1920)]
+         (100, 37), (129, 131), (135, 131), (255, 257), (518, 931), (1080, 1920)]  # 135x131: odd NB, W, items
 
 
 @pytest.mark.parametrize('h,w', SIZES)

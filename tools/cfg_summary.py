@@ -34,6 +34,21 @@ bench = json.loads(open(os.path.join(src, 'bench.json')).read().strip().splitlin
 json.dump(bench, open(os.path.join(prof, f'{name}_bench.json'), 'w'), indent=1)
 shutil.copy(os.path.join(src, 'stats', 'run_kernel_stats.csv'), os.path.join(prof, f'{name}_kernel_stats.csv'))
 
+def mark_name(k):
+    """rocprofv3's kernel name -> the plan's launch-mark name (jds_plan_profile):
+    'void jds::k_fwd32i<2, true, false>' -> 'k_fwd32i<2,1>'."""
+    k = k.replace('void ', '').replace('jds::', '').replace(' ', '').replace('true', '1').replace('false', '0')
+    if '<' not in k:
+        return k
+    base, args = k.split('<', 1)
+    a = args.rstrip('>').split(',')
+    if base in ('k_fwd32i', 'k_fwd32') and len(a) == 3:
+        a = a[:2] + (['mq'] if a[2] == '1' else [])
+    if base == 'k_fwd_reduce_rows' and len(a) == 2 and a[1] == '0':
+        a = a[:1]
+    return f'{base}<{",".join(a)}>'
+
+
 FWD = ('k_fwd32i', 'k_fwd32<', 'k_fix_fwd', 'k_fwd_reduce', 'k_fwd16', 'k_fwd<', 'k_fwdq', 'k_quant_mq')
 INV = ('k_inv2', 'k_inv<', 'k_inv_fast', 'k_inv16', 'k_chroma16', 'k_inv32', 'k_fix_inv')
 pmc = collections.defaultdict(dict)
@@ -57,12 +72,18 @@ if pmc:
             fwd += (f + w) * 1024
         elif any(t in k for t in INV):
             inv += (2 * f + w) * 1024
+    per_kernel = {}
+    for k, m in pmc.items():
+        f, w = m.get('FETCH_SIZE_KB', 0.0), m.get('WRITE_SIZE_KB', 0.0)
+        inv_k = any(t in k for t in INV)
+        per_kernel[mark_name(k)] = int(((2 * f if inv_k else f) + w) * 1024)
     cfg = bench['config']
     key = sys.argv[3] if len(sys.argv) > 3 else cfg.get('traffic_key')
     if key:
         tf = os.path.join(prof, 'pmc_traffic.json')
         rec = json.load(open(tf)) if os.path.exists(tf) else {}
-        rec[key] = {'k_fwd': int(fwd), 'k_inv': int(inv), 'method': __doc__.split('\n\n', 2)[2].replace('\n', ' '),
+        rec[key] = {'k_fwd': int(fwd), 'k_inv': int(inv), 'kernels': per_kernel,
+                    'method': __doc__.split('\n\n', 2)[2].replace('\n', ' '),
                     'source': f'profiles/{name}_pmc.json'}
         json.dump(rec, open(tf, 'w'), indent=1)
     print(f'{name}: fwd {fwd / 1e6:.1f} MB/launch, inv {inv / 1e6:.1f} MB/launch')

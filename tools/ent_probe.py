@@ -1,5 +1,5 @@
 """Time the JPEG entropy coder (jds_plan_entropy) on one 64 x 1080p Q50 4:2:0
-batch of codec coefficients; prints one JSON line with ms per batch and a
+batch of codec coefficients (FRAMES / HEIGHT / WIDTH override the batch); prints one JSON line with ms per batch and a
 digest of the files (A/B builds must produce the same digest).  Run with
 JDS_LIB_PATH=... for a variant build."""
 import hashlib
@@ -18,7 +18,8 @@ from utils.constants import JPEG_LUMA_Q50  # noqa: E402
 
 
 def main():
-    B, H, W = int(os.environ.get('FRAMES', '64')), 1080, 1920
+    B = int(os.environ.get('FRAMES', '64'))
+    H, W = int(os.environ.get('HEIGHT', '1080')), int(os.environ.get('WIDTH', '1920'))
     dev = torch.device('cuda', 0)
     prm = _abi.make_params(50, scale_quant_matrix(JPEG_LUMA_Q50, 50), '4:2:0', True, codec.gaussian_kernel3())
     plan = _abi.Plan(_abi.context(0), [prm] * B, H, W)
@@ -49,7 +50,7 @@ def main():
     for i in range(B):
         h.update(fh[i, :ln[i]].numpy().tobytes())
     print(json.dumps({'lib': os.environ.get('JDS_LIB_PATH', 'default'), 'ms_per_batch': e0.elapsed_time(e1) / reps,
-                      'frames': B, 'bytes': int(sum(ln)), 'sha16': h.hexdigest()[:16]}))
+                      'frames': B, 'H': H, 'W': W, 'bytes': int(sum(ln)), 'sha16': h.hexdigest()[:16]}))
     plan.close()
 
 
