@@ -5,7 +5,7 @@ Workload (BASELINE.json configs[1]): 1920x1080 uniform-random RGB frames, Q=50,
 4:2:0, prefilter ON, through the fused HIP kernels (forward phase: k_fwd32i +
 k_fwd_reduce_rows + k_fix_fwd, RGB -> int16 coefficients + statistics; inverse
 phase: the certified k_inv_fast, coefficients -> RGB, with its in-launch exact
-tile fix-up; k_inv2 where the plan's certificate does not pay).  One step = one pass over a batch of
+tile fix-up).  One step = one pass over a batch of
 `--frames` device-resident 1080p frames per GPU (default 64, the size of the
 reference's cfg4 batch sweep); inputs are generated on the device before the
 timed region.  A step is one jds_plan_run (forward then inverse) on one stream;
@@ -57,8 +57,8 @@ def parse():
                     help='16 = the configs[4] 16x16 stretch path (jds_fast16.hip certified fp32 forward, '
                          'jds_b16.hip fp64 inverse)')
     ap.add_argument('--inv-fast', action='store_true',
-                    help='A/B: force the certified fast inverse (JDS_RUN_INV_FAST) where the plan would pick k_inv2 '
-                         '(coarse tables) or k_inv16s (16x16 blocks: k_inv16_fast)')
+                    help='A/B: coarse tables (DC quantiser > 60): the certified fast inverse with its plain '
+                         'certificate (JDS_RUN_INV_FAST) instead of the exact-value variant the plan picks')
     ap.add_argument('--exact-inv', action='store_true',
                     help='A/B: force the exact replayed-order inverse (JDS_RUN_EXACT_INV: k_inv2 / k_inv16s)')
     ap.add_argument('--exact', action='store_true',

@@ -43,8 +43,9 @@ extern "C" {
                                  inverse + tile fix-up (same bytes; A/B and tests) */
 #define JDS_RUN_INV_FIXALL 32u /* test: the certified fast inverse flags every tile, so the exact
                                   tile code recomputes the whole frame (exercises the fix-up path) */
-#define JDS_RUN_INV_FAST 128u /* test: the certified fast inverse even where the plan picks k_inv2
-                                (4:4:4, coarse tables: DESIGN.md section 3) */
+#define JDS_RUN_INV_FAST 128u /* A/B and tests, coarse tables (DC quantiser > 60): the certified fast
+                                inverse with its plain certificate instead of the variant that takes
+                                values exact in both orders out of it */
 #define JDS_RUN_FWD_FIXALL 64u /* test, 16x16 plans: the certified fp32 forward lists every block, so
                                   k_fix_fwd16 recomputes the whole frame (exercises the fix-up path) */
 

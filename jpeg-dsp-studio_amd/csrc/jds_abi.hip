@@ -528,8 +528,10 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
     return fail(JDS_ENOMEM, "host allocation failed");
   }
   for (int i = 0; i < n; ++i) memcpy(p->qt + 64 * i, params[i].qtable, 64 * sizeof(double));
-  // the certified fast inverse where it measured faster than k_inv2: 4:4:4
-  // always (the wave-local k_inv_fast444), 4:2:x with fine tables
+  // coarse tables (DC quantiser > 60, quality below ~14): the certified fast
+  // inverse takes values exact in both orders out of its certificate
+  // (k_inv_fast<.., EX>); without that, most tiles of such frames fell back and
+  // k_inv2 was faster (4K 4:2:0 Q10: 396 vs 373 us)
   p->inv_fast_ok = true;
   if (mode != JDS_SS_444)
     for (int i = 0; i < n; ++i) p->inv_fast_ok = p->inv_fast_ok && params[i].qtable[0] <= 60.0;
@@ -754,8 +756,10 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   }
   InvFix fx = p->inv_fix();
   fx.fix_all = (flags & JDS_RUN_INV_FIXALL) ? 1 : 0;
-  const bool exact_inv =
-      exact || (flags & JDS_RUN_EXACT_INV) != 0 || (!p->inv_fast_ok && !(flags & JDS_RUN_INV_FAST));
+  // coarse tables: the exact-value tracking variant unless JDS_RUN_INV_FAST asks
+  // for the plain certificate (A/B and tests)
+  fx.ex = (!p->inv_fast_ok && !(flags & JDS_RUN_INV_FAST)) ? 1 : 0;
+  const bool exact_inv = exact || (flags & JDS_RUN_EXACT_INV) != 0;
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,

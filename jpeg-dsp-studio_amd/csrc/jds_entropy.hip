@@ -611,11 +611,11 @@ __global__ void __launch_bounds__(64 * ES_WAVES) __attribute__((amdgpu_waves_per
 // need no prefix launch between the walk and the placement (0.245 -> 0.244 ms
 // per 64 x 1080p); longer scans (4K: 2025 luma segments) would re-sum O(n^2)
 // totals across their waves, so their frames get a per-frame exclusive prefix
-// (k_ent_fscan<false>, segoff) before this launch.
-#ifndef JDS_AB_ENT_SELF_MAX  // (temporary A/B hook)
-#define JDS_AB_ENT_SELF_MAX 512
-#endif
-constexpr int ES_SELF_MAX = JDS_AB_ENT_SELF_MAX;
+// (k_ent_fscan<false>, segoff) before this launch.  Measured
+// (tools/ent_probe.py, profiles/r05_entropy_selfpre_ab.jsonl): 16 x 4K, every
+// scan summing itself 0.2585 ms, every scan from the prefix launch 0.2517,
+// this threshold 0.2547; 64 x 1080p 0.2518 / 0.2523 / 0.2528 (noise).
+constexpr int ES_SELF_MAX = 512;
 
 // incl[g] = the segment's end bit within its scan (k_ent_fscan / k_ent_emit3
 // read it as desc)

@@ -110,6 +110,7 @@ struct InvFix {
   int parity;
   int rot;
   int probe;
+  int ex = 0;  // coarse tables: values exact in both orders leave the certificate (k_inv_fast<.., EX>)
 };
 
 // Per-frame quantiser: q16 = 16*Q (pocketfft's first-axis fct = 1/16 folded in), q = Q.

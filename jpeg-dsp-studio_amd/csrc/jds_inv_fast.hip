@@ -198,7 +198,7 @@ __device__ __forceinline__ void fast_col(const Col16& in, const double* __restri
 // 255) - 128 = clip(x, -128, 127)): the chroma window holds the shifted samples
 // directly and the luma's +128 rides on the magic constant; fewer roundings and
 // smaller magnitudes than the +128-folded form tools/inv_bound.py models.
-template <int LO = 0>
+template <int LO = 0, bool CLIP = true>
 __device__ __forceinline__ void fast_row(const double* __restrict__ src, int u, double (&c)[8]) {
   const int sw = u & 3;
 #pragma unroll
@@ -208,8 +208,10 @@ __device__ __forceinline__ void fast_row(const double* __restrict__ src, int u, 
     c[2 * p + 1] = d.y;
   }
   aan8(c);
+  if constexpr (CLIP) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) c[k] = fmin(fmax(c[k], (double)LO), (double)(LO + 255));
+    for (int k = 0; k < 8; ++k) c[k] = fmin(fmax(c[k], (double)LO), (double)(LO + 255));
+  }
 }
 
 // One plane's upsampled (chroma - 128) at the lane's 8 pixels (cv2
@@ -271,6 +273,37 @@ __device__ __forceinline__ uint32_t byte_cert_y(double y, uint32_t& lo_min, uint
   return c > MAGIC_HI + 255u ? MAGIC_HI + 255u : c;  // v_med3_u32; the byte is bits 0-7
 }
 
+// The same for a value known exact in both orders (EX, below): its fraction
+// word is replaced by a neutral one (half-way between integers) so it cannot
+// trip the certificate.
+__device__ __forceinline__ uint32_t byte_cert_y(double y, uint32_t& lo_min, uint32_t& lo_max, bool exact) {
+  const uint32_t lo = exact ? 0x80000000u : (uint32_t)__double2loint(y), hi = (uint32_t)__double2hiint(y);
+  lo_min = lo_min < lo ? lo_min : lo;
+  lo_max = lo_max > lo ? lo_max : lo;
+  const uint32_t c = hi < MAGIC_HI ? MAGIC_HI : hi;
+  return c > MAGIC_HI + 255u ? MAGIC_HI + 255u : c;
+}
+
+// OR of v over the 8 lanes of a block's lane group (lanes 8k .. 8k + 7):
+// quad_perm xor 1, xor 2, then row_half_mirror (lane i with 7 - i)
+__device__ __forceinline__ int or8(int v) {
+  v |= __builtin_amdgcn_update_dpp(0, v, 0xb1, 0xf, 0xf, true);
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x4e, 0xf, 0xf, true);
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, true);
+  return v;
+}
+__device__ __forceinline__ int col_nonzero(const Col16& c) {
+  int v = 0;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) v |= (int)c.q[r];
+  return v;
+}
+// bits of window columns [lo, hi) that fall in 32-bit word w
+__device__ __forceinline__ uint32_t colbits(int lo, int hi, int w) {
+  const int a = max(lo - 32 * w, 0), b = min(hi - 32 * w, 32);
+  return a >= b ? 0u : (b - a == 32 ? 0xffffffffu : ((1u << (b - a)) - 1u) << a);
+}
+
 // Four bytes (bits 0-7 of a, b, c, d) into one word: two byte permutes and an or.
 __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   const uint32_t ab = __builtin_amdgcn_perm(b, a, 0x0c0c0400u);  // a.b0 | b.b0 << 8
@@ -310,29 +343,62 @@ __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, ui
 #ifndef JDS_INV_ONE_BARRIER
 #define JDS_INV_ONE_BARRIER 0  // every thread deciding without the second barrier measured slower (312 vs 309 us)
 #endif
-template <int SH>
-__device__ __forceinline__ void cert_row_step(uint32_t& mn, uint32_t& mx, uint32_t& qm) {
+template <int SH, bool EX>
+__device__ __forceinline__ void cert_row_step(uint32_t& mn, uint32_t& mx, uint32_t& qm, uint32_t& em) {
   const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)mn, 0x110 + SH, 0xf, 0xf, false);
   const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x110 + SH, 0xf, 0xf, false);
   const uint32_t c = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)qm, 0x110 + SH, 0xf, 0xf, false);
   mn = mn < a ? mn : a;
   mx = mx > b ? mx : b;
   qm = qm > c ? qm : c;
+  if constexpr (EX) {
+    const uint32_t d = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)em, 0x110 + SH, 0xf, 0xf, false);
+    em = em < d ? em : d;
+  }
 }
-__device__ __forceinline__ void cert_to_lds(uint32_t mn, uint32_t mx, uint32_t qm, uint32_t* s_cert) {
-  cert_row_step<1>(mn, mx, qm);
-  cert_row_step<2>(mn, mx, qm);
-  cert_row_step<4>(mn, mx, qm);
-  cert_row_step<8>(mn, mx, qm);  // lane 15 of each row: the row's min / max
+// em (EX): the smallest clip margin of the values taken as exact, as the bits
+// of a non-negative float (ordered like the floats), or 0x7f800000 (+inf)
+template <bool EX = false>
+__device__ __forceinline__ void cert_to_lds(uint32_t mn, uint32_t mx, uint32_t qm, uint32_t* s_cert,
+                                            uint32_t em = 0x7f800000u) {
+  cert_row_step<1, EX>(mn, mx, qm, em);
+  cert_row_step<2, EX>(mn, mx, qm, em);
+  cert_row_step<4, EX>(mn, mx, qm, em);
+  cert_row_step<8, EX>(mn, mx, qm, em);  // lane 15 of each row: the row's min / max
   if ((threadIdx.x & 15) == 15) {
     atomicMin(&s_cert[0], mn);
     atomicMax(&s_cert[1], mx);
     atomicMax(&s_cert[2], qm);
+    if constexpr (EX) atomicMin(&s_cert[3], em);
   }
 }
 
 // The fast pass over one tile (sets sh.redo when the tile must be recomputed).
-template <int MODE, int XTRA>
+//
+// EX (coarse tables): values that are exact in both orders
+// are taken out of the certificate.  At coarse tables many luma samples clip
+// (|Y - 128| > 128 before the reference's per-block clip) and many chroma
+// blocks quantise to all zeros; a value whose luma sample is exactly known and
+// whose chroma term is exactly zero is then an exact integer in both orders
+// (the certificate, which only sees distances to integers, cannot tell it from
+// a value E away from one):
+//   * luma exactly known: its block is all zeros (Y - 128 = 0 in both orders:
+//     the IDCT of zeros is zeros) or the fast value lies beyond the clip
+//     boundary by more than E -- E bounds |v_fast - v_ref| of the whole chain,
+//     which includes the luma term with weight 1, so the reference's value
+//     lies beyond it too and both clip to -128 / 127 exactly;
+//   * chroma term exactly zero: every window sample the pixel's taps read
+//     comes from an all-zero chroma block (the reference's samples are then
+//     exactly 128: IDCT of zeros + 128, clip, and cv2's blends with weights
+//     summing to 1 keep 128; the fast window holds +-0 and its blends keep
+//     +-0), so 1.402 (Cr - 128) etc. is exactly 0 in both, R = G = B = Y;
+//     the lane's 8 pixels are judged together (all 6 columns, both rows);
+//   * then v_ref = v_fast = Y (+128), an integer: the bytes agree.
+// Such values do not enter the fraction-word certificate; instead the tile
+// is uncertain if the smallest clip margin among them is <= E.  Window
+// samples' sources are tracked as bits (s_zb: one bit per window sample, set
+// by the chroma task that writes the sample from an all-zero block).
+template <int MODE, int XTRA, bool EX = false>
 __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const Geo& g, const int tiles_x,
                                               const int frame, const int tile, const int16_t* __restrict__ coeffs,
                                               const FrameQ* __restrict__ fq, const uint8_t* __restrict__ rgb_in,
@@ -347,7 +413,9 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   __shared__ double s_qmax;
   __shared__ double s_red[I::NT / 64], s_dq[I::NT / 64];
   __shared__ uint32_t s_lmin[I::NT / 64], s_lmax[I::NT / 64];
-  __shared__ uint32_t s_cert[3];  // JDS_INV_CERT_DPP: min / max fraction word, max |q|
+  __shared__ uint32_t s_cert[4];  // min / max fraction word, max |q|, (EX) smallest clip margin (float bits)
+  constexpr int ZW = (I::CWC + 31) / 32;  // EX: words per window row of zero-source bits
+  __shared__ uint32_t s_zb[EX ? 2 * I::CWR * ZW : 1];
 #if JDS_INV_WIN_SEL
   __shared__ double s_dummy[64];  // the window stores' sink for ring columns outside it
 #endif
@@ -381,6 +449,7 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
         s_cert[0] = 0xffffffffu;
         s_cert[1] = 0u;
         s_cert[2] = 0u;
+        s_cert[3] = 0x7f800000u;
       }
 #else
       double m = q;
@@ -395,6 +464,9 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
 #endif
     }
     if (XTRA && tid == 0) s_sse = 0ull;
+    if constexpr (EX) {
+      for (int i = tid; i < 2 * I::CWR * ZW; i += I::NT) s_zb[i] = 0u;
+    }
     __syncthreads();
   };
 #if !JDS_INV_EARLY_LOADS
@@ -411,6 +483,28 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   auto chroma_task = [&](const int p, const int i, const int by, const int bx, const Col16& cur) {
     const bool need = !I::RY || (i == 0 ? lv == 7 : (i == I::CBR - 1 ? lv == 0 : true));
     fast_col(cur, s_qs, lv, s_mid + lb * MS, qhi, qlo);
+    if constexpr (EX) {
+      // an all-zero block: the window samples this lane writes (its row, the
+      // ring column and the replicated edge columns below) are exact zeros
+      const bool zero = or8(col_nonzero(cur)) == 0;
+      if (zero && need) {
+        const int wc0 = bx * 8 - cwx0, wr = by * 8 + lv - cwy0;
+        int elo = 1 << 30, ehi = 0;  // replicated columns past the plane's right end
+        if constexpr (I::SX == 2) {
+          const int ke = g.wc - 1 - bx * 8;
+          if ((unsigned)ke < 8u) {
+            elo = wc0 + ke + 1;
+            ehi = I::CWC;
+          }
+        }
+        const int lo = (I::SX == 2 && bx == 0 && wc0 >= 1) ? wc0 - 1 : wc0;
+#pragma unroll
+        for (int w = 0; w < ZW; ++w) {
+          const uint32_t m = colbits(lo, wc0 + 8, w) | colbits(elo, ehi, w);
+          if (m) atomicOr(&s_zb[(p * I::CWR + wr) * ZW + w], m);
+        }
+      }
+    }
     if (need) {
       double c[8];
       fast_row<-128>(s_mid + lb * MS, lv, c);
@@ -506,6 +600,7 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   // ---- 2. luma rounds: IDCT, upsample, colour, certify, store ----------------
   // the certificate: smallest / largest fraction word of the lane's outputs
   uint32_t lo_min = 0xffffffffu, lo_max = 0u;
+  double em = 1e300;  // EX: the smallest clip margin among the values taken as exact
   unsigned long long sse = 0ull;
   double ssy = 0.0;
   const uint8_t* in_f = XTRA ? rgb_in + (size_t)(frame / in_div) * g.H * g.W * 3 : nullptr;
@@ -524,10 +619,22 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       lq = load_col(cf, ((long long)by1 * g.nbx + bx1) * 64, lv, ok1);
     }
     if (bvalid) fast_col(cur, s_qs, lv, s_mid + lb * MS, qhi, qlo);
+    // EX: the luma block is all zeros (all 8 lanes of the block group take part)
+    const bool yzero = EX && or8(col_nonzero(cur)) == 0;
     const int y = by * 8 + lv, x0 = bx * 8;
     if (bvalid && y < g.H && x0 < g.W) {
       double Yv[8];
-      fast_row<-128>(s_mid + lb * MS, lv, Yv);  // Y - 128
+      double ym[8];  // EX: how far beyond the clip range the fast luma lies (> 0: clipped)
+      if constexpr (EX) {
+        fast_row<-128, false>(s_mid + lb * MS, lv, Yv);  // Y - 128, unclipped
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          ym[k] = yzero ? 1e300 : fmax(-128.0 - Yv[k], Yv[k] - 127.0);
+          Yv[k] = fmin(fmax(Yv[k], -128.0), 127.0);  // (fast_row's clip)
+        }
+      } else {
+        fast_row<-128>(s_mid + lb * MS, lv, Yv);  // Y - 128
+      }
       int wq, wt = 0;
       if constexpr (I::SY == 2) {
         // output row 2m: rows (m-1, m) weighted (1/4, 3/4); row 2m+1: (m+1, m)
@@ -541,6 +648,19 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
       uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
       const bool wide = nx == 8 && ((((uintptr_t)o) & 7u) == 0);
+      // EX: every window sample of plane p the lane's taps read (6 columns
+      // from c0, rows wq and wt) is an exact zero
+      bool zc[2] = {false, false};
+      if constexpr (EX) {
+        const int c0 = x0 / I::SX - 1 - cwx0, wi = c0 >> 5, sh = c0 & 31;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const uint32_t* zq = s_zb + (p * I::CWR + wq) * ZW + wi;
+          const uint32_t* zt = s_zb + (p * I::CWR + (I::SY == 2 ? wt : wq)) * ZW + wi;
+          const uint64_t bq = ((uint64_t)zq[1] << 32) | zq[0], bt = ((uint64_t)zt[1] << 32) | zt[0];
+          zc[p] = (((bq & bt) >> sh) & 63u) == 63u;
+        }
+      }
       uint32_t pk[6];
       {
         // channel words (byte in bits 0-7) in output order R0 G0 B0 R1 ...
@@ -552,15 +672,28 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
           Yv[k] = Yv[k] + (MAGIC + 128.0);  // Y on byte_cert_y's grid, shared by the three channels
           const double B = col_b(Yv[k], C[k]);
           Gt[k] = col_gt(Yv[k], C[k]);
-          cb[3 * k + 2] = byte_cert_y(B, lo_min, lo_max);
+          if constexpr (EX) {
+            const bool ex = zc[0] && ym[k] > 0.0;
+            cb[3 * k + 2] = byte_cert_y(B, lo_min, lo_max, ex);
+            em = ex ? fmin(em, ym[k]) : em;
+          } else {
+            cb[3 * k + 2] = byte_cert_y(B, lo_min, lo_max);
+          }
         }
         chroma8_fast<MODE>(s_cw[1], x0, cwx0, wq, wt, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const double R = col_r(Yv[k], C[k]);
           const double G = col_g(Gt[k], C[k]);
-          cb[3 * k] = byte_cert_y(R, lo_min, lo_max);
-          cb[3 * k + 1] = byte_cert_y(G, lo_min, lo_max);
+          if constexpr (EX) {
+            const bool exr = zc[1] && ym[k] > 0.0, exg = exr && zc[0];
+            cb[3 * k] = byte_cert_y(R, lo_min, lo_max, exr);
+            cb[3 * k + 1] = byte_cert_y(G, lo_min, lo_max, exg);
+            em = exr ? fmin(em, ym[k]) : em;
+          } else {
+            cb[3 * k] = byte_cert_y(R, lo_min, lo_max);
+            cb[3 * k + 1] = byte_cert_y(G, lo_min, lo_max);
+          }
         }
 #pragma unroll
         for (int w = 0; w < 6; ++w) pk[w] = pack4(cb[4 * w], cb[4 * w + 1], cb[4 * w + 2], cb[4 * w + 3]);
@@ -618,7 +751,9 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   // ---- 3. certification: the tile's closest approach to an integer vs its bound
   int qm = max(qhi, -qlo);  // max |q| this lane read
 #if JDS_INV_CERT_DPP
-  cert_to_lds(lo_min, lo_max, (uint32_t)qm, s_cert);
+  // (EX: the margin as a float rounded down -- a smaller margin is conservative)
+  cert_to_lds<EX>(lo_min, lo_max, (uint32_t)qm, s_cert,
+                  EX ? __float_as_uint(__double2float_rd(fmin(em, 3.0e38))) : 0x7f800000u);
 #else
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -690,7 +825,8 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     // byte_cert); T in units of 2^-32
     const double E = K_LIN * (q * s_qmax) + K_CONST + 0x1p-31;
     const double T = ceil(E * 0x1p+32) + 1.0;
-    const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
+    const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T ||
+                           (EX && (double)__uint_as_float(s_cert[3]) <= E);
     sh.redo = uncertain || fix_all;
     if (sh.redo) {
       atomicAdd(fixcount, 1u);  // tiles recomputed (jds_plan_fix_counts)
@@ -710,8 +846,9 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
 
 // XTRA: 0 = RGB only; 1 = + exact integer SSE and luma SSE partials (sweeps),
 // committed by the fast pass only for certified tiles (the exact tile code
-// commits the others).
-template <int MODE, int XTRA>
+// commits the others).  EX: exact values leave the certificate (coarse tables;
+// inv_fast_tile).
+template <int MODE, int XTRA, bool EX = false>
 __global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(Inv<MODE>::WPE)))
 k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
            const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
@@ -746,8 +883,8 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
     }
   } else {
     sh.redo = 0;
-    redo = inv_fast_tile<MODE, XTRA>(sh, g, tiles_x, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part,
-                                     fixcount, next_count, cnt_now, in_div, fix_all);
+    redo = inv_fast_tile<MODE, XTRA, EX>(sh, g, tiles_x, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part,
+                                         fixcount, next_count, cnt_now, in_div, fix_all);
   }
   // one call site of the exact tile code: items in exact mode, uncertain tiles
 #ifndef JDS_PROBE_NOFALLBACK  // tools/stage_budget.py: the fast path's code alone
@@ -1294,9 +1431,13 @@ static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const F
   unsigned* cnt = fx.count + fx.parity;
   unsigned* nxt = fx.count + (fx.parity ^ 1);
   (void)rgb_in;  // SSE runs take the exact kernel (launch_codec)
-  hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, cnt, nxt,
-                     fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
-  kmark(s, "k_inv_fast<%d,0>", MODE);
+  if (fx.ex)
+    hipLaunchKernelGGL((k_inv_fast<MODE, 0, true>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part,
+                       cnt, nxt, fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
+  else
+    hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, cnt,
+                       nxt, fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
+  kmark(s, "k_inv_fast<%d,0%s>", MODE, fx.ex ? ",ex" : "");
   return hipGetLastError();
 }
 

@@ -7,9 +7,10 @@ a rigorous bound (tools/inv_bound.py); tiles with an uncertain sample go
 through the exact kernel (k_inv2_list).  Bar: bit-identical bytes, SSE and
 luma SSE with the default (fast), JDS_RUN_EXACT_INV (exact) and
 JDS_RUN_INV_FIXALL (fast, then every tile recomputed by the exact tile code).
-Plans pick k_inv2 for coarse 4:2:x tables (measured faster there) and the
-wave-local k_inv_fast444 at 4:4:4; these tests force the fast kernels with
-JDS_RUN_INV_FAST, and the default route is checked separately."""
+Plans take the wave-local k_inv_fast444 at 4:4:4 and, for 4:2:x plans with a
+coarse table, the variant that takes values exact in both orders out of the
+certificate (k_inv_fast<.., EX>); JDS_RUN_INV_FAST asks for the plain
+certificate there.  Both are checked against the exact kernel."""
 import numpy as np
 import pytest
 
@@ -145,13 +146,14 @@ def test_fast_inverse_arbitrary_int16_coefficients(scale):
         _same(fast, exact)
 
 
-@pytest.mark.parametrize('mode,q,fast', [('4:2:0', 50, True), ('4:2:2', 20, True), ('4:2:0', 10, False),
+@pytest.mark.parametrize('mode,q,fast', [('4:2:0', 50, True), ('4:2:2', 20, True), ('4:2:0', 10, True),
                                          ('4:4:4', 50, True), ('4:4:4', 10, True)])
 def test_default_inverse_route(mode, q, fast):
-    """The plan's own choice (fast inverse at 4:4:4 and for 4:2:x with fine
-    tables, k_inv2 otherwise) gives the exact kernel's bytes; the fix-up
-    counter shows which kernel ran (k_inv2 reports none, the fast kernels list
-    the checkerboard's ties)."""
+    """The plan's own choice (the certified fast inverse everywhere: the
+    wave-local k_inv_fast444 at 4:4:4, the exact-value variant for coarse 4:2:x
+    tables) gives the exact kernel's bytes; the fix-up counter shows which
+    kernel ran (k_inv2 reports none, the fast kernels list the checkerboard's
+    ties)."""
     from jds import _abi
     frames = np.stack([cpu_ref.generate_colored_checkerboard(256)] * 2)  # ties: the fast kernel lists tiles
     dflt, exact = _plan(frames, [q, q], mode, mode != '4:4:4', [0, _abi.RUN_EXACT_INV])
@@ -160,3 +162,45 @@ def test_default_inverse_route(mode, q, fast):
         assert dflt[3][1] == 0
     else:
         assert dflt[3][1] > 0
+
+
+def _coarse_frames(h, w, seed):
+    """Random frames plus saturated structure: pure primaries, black and white
+    blocks (clipped luma beside all-zero chroma blocks at coarse tables)."""
+    rnd = cpu_ref.random_image(h, w, seed)
+    prim = np.zeros((h, w, 3), np.uint8)
+    cols = np.array([[255, 0, 0], [0, 255, 0], [0, 0, 255], [255, 255, 255], [0, 0, 0], [255, 255, 0]], np.uint8)
+    yy, xx = np.mgrid[0:h, 0:w]
+    prim[:] = cols[((yy // 24) * 7 + xx // 40) % len(cols)]
+    half = rnd.copy()
+    half[:, : w // 2] = 255
+    half[h // 2:, :, 1:] = 0
+    return [rnd, prim, half]
+
+
+@pytest.mark.parametrize('mode', ['4:2:0', '4:2:2'])
+@pytest.mark.parametrize('h,w', [(256, 384), (136, 200), (1080, 1920)])
+def test_coarse_tables_exact_value_tracking(mode, h, w):
+    """Coarse tables: the default route (k_inv_fast<.., EX>)
+    == the plain certificate (RUN_INV_FAST) == k_inv2 == EX with every tile
+    recomputed == the oracle, on random and saturated frames at Q 1 .. 13; and
+    on random frames the exact-value variant recomputes fewer tiles."""
+    from jds import _abi
+    qs = [1, 5, 10, 13, 10, 5] if h * w < 1e6 else [10, 5]
+    fr = _coarse_frames(h, w, 40)
+    frames = np.stack([fr[i % 3] for i in range(len(qs))])
+    ex, = _plan(frames, qs, mode, False, [0])              # a fresh plan: no adaptive state yet
+    plain, = _plan(frames, qs, mode, False, [_abi.RUN_INV_FAST])
+    exact, fixall = _plan(frames, qs, mode, False, [_abi.RUN_EXACT_INV, _abi.RUN_INV_FIXALL])
+    _same(ex, exact)
+    _same(plain, exact)
+    _same(fixall, exact)
+    for i in (0, 1, 2) if len(qs) > 2 else (0, 1):
+        ref = cpu_ref.compress_reconstruct(frames[i], qs[i], 8, mode, False, metrics=False)
+        assert np.array_equal(ex[0][i], ref['reconstructed']), (i, qs[i])
+    # random frames at Q10: the plain certificate hands most tiles to the exact code
+    rnd = np.stack([cpu_ref.random_image(h, w, 50 + i) for i in range(2)])
+    ex2, = _plan(rnd, [10, 10], mode, False, [0])
+    plain2, = _plan(rnd, [10, 10], mode, False, [_abi.RUN_INV_FAST])
+    _same(ex2, plain2)
+    assert ex2[3][1] < plain2[3][1] or plain2[3][1] == 0, (ex2[3], plain2[3])

@@ -62,10 +62,13 @@ def _golden_check(name, flags_list):
 
 
 def test_cfg3_4k_q10_420_plan_matches_reference_golden():
-    """configs[2]: the plan's default kernels (k_inv2 at this coarse table), the
-    certified fast inverse forced (RUN_INV_FAST) and the all-fp64 kernels."""
+    """configs[2]: the plan's default kernels (at this coarse table the fast
+    inverse's exact-value variant, k_inv_fast<2,0,EX>), that variant with every
+    tile recomputed, the plain certificate (RUN_INV_FAST) with and without
+    FIXALL, the exact inverse and the all-fp64 kernels."""
     from jds import _abi
-    _golden_check('cfg3_rand4k_s0_q10_420_nopf', [0, _abi.RUN_INV_FAST, _abi.RUN_INV_FAST | _abi.RUN_INV_FIXALL,
+    _golden_check('cfg3_rand4k_s0_q10_420_nopf', [0, _abi.RUN_INV_FIXALL, _abi.RUN_INV_FAST,
+                                                  _abi.RUN_INV_FAST | _abi.RUN_INV_FIXALL, _abi.RUN_EXACT_INV,
                                                   _abi.RUN_EXACT])
 
 

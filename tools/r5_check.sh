@@ -46,6 +46,21 @@ if has cfg4k; then
     --no-host-path > gpurun_out/${TAG}_cfg4k.log 2>&1
   rc=$?; echo "cfg4k rc=$rc"; tail -3 gpurun_out/${TAG}_cfg4k.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc
 fi
+if has q10; then
+  # configs[2] (16 x 4K Q10 4:2:0): the exact-value fast inverse (default) vs the plain certificate vs k_inv2
+  for v in default --inv-fast --exact-inv; do
+    a=$v; [ "$v" = default ] && a=""
+    timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --height 2160 --width 3840 --frames 16 --quality 10 \
+      --prefilter 0 --no-north-star --no-host-path --no-entropy --no-cpu-baseline $a >> gpurun_out/${TAG}_q10.jsonl \
+      2>> gpurun_out/${TAG}_q10.err
+    rc=$?; [ $rc -eq 0 ] || { echo "q10 $v rc=$rc"; tail -5 gpurun_out/${TAG}_q10.err; exit $rc; }
+  done
+  python3 -c "
+import json
+for l in open('gpurun_out/${TAG}_q10.jsonl'):
+    d=json.loads(l); print(d['value'], d['ms_per_step'], d['pipeline_roofline_frac'], d['kernels_ms'], d['fixups_last_step'], d['parity'])
+"
+fi
 if has sweep; then
   timeout -k 10 600 python -u bench.py --sweep --steps 10 --warmup 3 > gpurun_out/${TAG}_sweep.json 2> gpurun_out/${TAG}_sweep.err
   rc=$?; echo "sweep rc=$rc"; head -c 1500 gpurun_out/${TAG}_sweep.json; echo; [ $rc -eq 0 ] || exit $rc
