@@ -57,8 +57,8 @@ def parse():
                     help='16 = the configs[4] 16x16 stretch path (jds_fast16.hip certified fp32 forward, '
                          'jds_b16.hip fp64 inverse)')
     ap.add_argument('--inv-fast', action='store_true',
-                    help='A/B: coarse tables (DC quantiser > 60): the certified fast inverse with its plain '
-                         'certificate (JDS_RUN_INV_FAST) instead of the exact-value variant the plan picks')
+                    help='A/B: coarse tables (DC quantiser > 60): the certified fast inverse '
+                         '(JDS_RUN_INV_FAST) instead of the exact k_inv2 the plan picks')
     ap.add_argument('--exact-inv', action='store_true',
                     help='A/B: force the exact replayed-order inverse (JDS_RUN_EXACT_INV: k_inv2 / k_inv16s)')
     ap.add_argument('--exact', action='store_true',

@@ -44,8 +44,8 @@ extern "C" {
 #define JDS_RUN_INV_FIXALL 32u /* test: the certified fast inverse flags every tile, so the exact
                                   tile code recomputes the whole frame (exercises the fix-up path) */
 #define JDS_RUN_INV_FAST 128u /* A/B and tests, coarse tables (DC quantiser > 60): the certified fast
-                                inverse with its plain certificate instead of the variant that takes
-                                values exact in both orders out of it */
+                                inverse instead of the exact k_inv2 such plans run (most tiles of
+                                those frames fall back) */
 #define JDS_RUN_FWD_FIXALL 64u /* test, 16x16 plans: the certified fp32 forward lists every block, so
                                   k_fix_fwd16 recomputes the whole frame (exercises the fix-up path) */
 
@@ -268,12 +268,6 @@ int jds_plan_entropy(jds_plan* plan, const int16_t* coeffs, uint8_t* out, int64_
                      uint64_t* scan_bits, void* stream);
 int jds_encode_jfif(jds_ctx* ctx, const jds_params* p, int64_t H, int64_t W, const int16_t* coeffs, uint8_t* out,
                     int64_t out_cap, int64_t* out_len, uint64_t* scan_bits);
-
-/* Test-only: jds_psnr_ssim_dev through the round-1..3 SSIM kernels
- * (jds_ssim.hip: IEEE divisions, one line per lane), the reference the
- * batched pipeline is compared with bit for bit.  out[0..5] as above. */
-int jds_selftest_psnr_ssim_legacy_dev(jds_ctx* ctx, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W,
-                                      double* out);
 
 /* Test-only: evaluate the device DCT expressions (jds_dct8.hpp) on the host so
  * the CPU test suite can pin them against SciPy without a GPU.  Not used by

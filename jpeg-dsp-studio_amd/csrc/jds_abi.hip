@@ -31,9 +31,6 @@ size_t gen_rec_doubles(const Geo& g);
 int gen_px_tiles(const Geo& g);
 hipError_t stage_area_gen(const double* in, int H, int W, const AreaTap* ytab, const AreaTap* xtab, double* out,
                           int oh, int ow, hipStream_t s);
-hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, double c1, double c2,
-                            double* scratch_planes, double* scratch_smap, double* scratch_chunks, double* out,
-                            hipStream_t s);
 hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const* b, int items, int H, int W,
                                   double c1, double c2, double* scratch, double* out, int out_stride,
                                   unsigned long long* sse, hipStream_t s);
@@ -49,7 +46,7 @@ hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
                            jds_frame_stats* st, uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount,
                            float* dct32,
-                           hipStream_t s, const Side* side, bool finish, int par);
+                           hipStream_t s, bool finish, int par);
 int quant_mq_tiles(const Geo& g);
 int inv16_tiles(int mode, int H, int W);
 constexpr int MAXQ_SHARED = 8;  // jds_fast.hip MAXQ
@@ -141,7 +138,7 @@ struct jds_ctx {
   hipEvent_t xfer_ev = nullptr;
   // host-path scratch
   DevBuf rgb, out, coeffs, stats, part, fq, gk, erry, errrgb, sel;
-  DevBuf ss_planes, ss_map, ss_chunks, ss_out, img_a, img_b;  // ss_planes: k_ss_* scratch; map/chunks: legacy
+  DevBuf ss_planes, ss_out, img_a, img_b;  // ss_planes: k_ss_* scratch
   DevBuf st[5];  // per-stage API staging
   DevBuf chunks;
   DevBuf planes;  // 16x16 path: reconstructed chroma planes
@@ -176,18 +173,6 @@ static int run_ssim(jds_ctx* c, const uint8_t* a, const uint8_t* b, int H, int W
   return run_ssim_batch(c, 1, &a, &b, H, W, dres, 5, nullptr);
 }
 
-// the round-1..3 kernels (k_uf_axis0 / k_uf_axis1_ssim / k_chunks_*): kept as
-// the A/B and test reference of the batched pipeline (jds_selftest_psnr_ssim_legacy_dev)
-static int run_ssim_legacy(jds_ctx* c, const uint8_t* a, const uint8_t* b, int H, int W, double* dres) {
-  const size_t n = (size_t)H * W;
-  HIP_TRY(c->ss_planes.ensure(4 * 5 * n * sizeof(double)));  // the four channels at once
-  HIP_TRY(c->ss_map.ensure(4 * (size_t)(H - 6) * (W - 6) * sizeof(double)));
-  HIP_TRY(c->ss_chunks.ensure(4 * ((n + 8191) / 8192 + 1) * sizeof(double)));
-  HIP_TRY(launch_psnr_ssim(a, b, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_planes.p, (double*)c->ss_map.p,
-                           (double*)c->ss_chunks.p, dres, c->stream));
-  return JDS_OK;
-}
-
 struct jds_plan {
   jds_ctx* ctx = nullptr;
   int n = 0, mode = 0;
@@ -217,7 +202,6 @@ struct jds_plan {
     return {(unsigned*)invfix.p, (unsigned*)invfix.p + 16, 0, (int)(inv_runs & 1u), (int)(inv_runs % 3u),
             (int)(inv_runs % 16u == 15u)};
   }
-  Side side;  // border tiles run beside interior tiles
   DevBuf planes;  // 16x16 path: reconstructed chroma planes (n x 2 x hc x wc f64)
   double* qt = nullptr;  // host copy of the per-frame 8x8 tables (entropy headers)
   DevBuf ent[8], ent_hdr, ent_tab;  // entropy coder scratch, allocated by the first jds_plan_entropy
@@ -460,7 +444,7 @@ void jds_ctx_destroy(jds_ctx* c) {
   }
   if (c->xfer_ev) (void)hipEventDestroy(c->xfer_ev);
   DevBuf* bufs[] = {&c->rgb,     &c->out,    &c->coeffs,    &c->stats,  &c->part,  &c->fq,   &c->gk,  &c->erry,
-                    &c->errrgb,  &c->sel,    &c->ss_planes, &c->ss_map, &c->ss_chunks, &c->ss_out, &c->img_a, &c->img_b};
+                    &c->errrgb,  &c->sel,    &c->ss_planes, &c->ss_out, &c->img_a, &c->img_b};
   for (DevBuf* b : bufs) b->release();
   for (DevBuf& b : c->st) b.release();
   c->chunks.release();
@@ -528,10 +512,11 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
     return fail(JDS_ENOMEM, "host allocation failed");
   }
   for (int i = 0; i < n; ++i) memcpy(p->qt + 64 * i, params[i].qtable, 64 * sizeof(double));
-  // coarse tables (DC quantiser > 60, quality below ~14): the certified fast
-  // inverse takes values exact in both orders out of its certificate
-  // (k_inv_fast<.., EX>); without that, most tiles of such frames fell back and
-  // k_inv2 was faster (4K 4:2:0 Q10: 396 vs 373 us)
+  // coarse tables (DC quantiser > 60, quality below ~14) put most tiles of a
+  // frame on the certified inverse's fallback (reconstructions land on
+  // integers: clipped luma, all-zero chroma), where k_inv2 is faster (16 x 4K
+  // 4:2:0 Q10: 358 vs 410 us; an exact-value certificate variant, 425 us, did
+  // not pay either -- DESIGN.md): such plans run k_inv2 unless JDS_RUN_INV_FAST
   p->inv_fast_ok = true;
   if (mode != JDS_SS_444)
     for (int i = 0; i < n; ++i) p->inv_fast_ok = p->inv_fast_ok && params[i].qtable[0] <= 60.0;
@@ -626,22 +611,6 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
       return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
     }
     free(h32);
-  }
-  // Border tiles run on the plan's own stream after the interior tiles unless
-  // JDS_SIDE_STREAM=1 asks for the fork/join onto a side stream (A/B: tools/ab_probe.py).
-  // JDS_REDUCE_SIDE=1 runs the statistics reduction beside the fix-up on the
-  // side stream (A/B: 0.627 vs 0.617 ms per 64 x 1080p step -- the fork / join
-  // costs more than the overlap returns; off by default).
-  const char* side_env = getenv("JDS_SIDE_STREAM");
-  const char* red_env = getenv("JDS_REDUCE_SIDE");
-  p->side.border = side_env && side_env[0] == '1';
-  p->side.reduce = red_env && red_env[0] == '1';
-  if ((p->side.border || p->side.reduce) &&
-      ((e = hipStreamCreateWithFlags(&p->side.stream, hipStreamNonBlocking)) != hipSuccess ||
-       (e = hipEventCreateWithFlags(&p->side.fork, hipEventDisableTiming)) != hipSuccess ||
-       (e = hipEventCreateWithFlags(&p->side.join, hipEventDisableTiming)) != hipSuccess)) {
-    jds_plan_destroy(p);
-    return fail(JDS_EHIP, "plan stream: %s", hipGetErrorString(e));
   }
   *out = p;
   return JDS_OK;
@@ -749,17 +718,14 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
       HIP_TRY(launch_fast_fwd(p->mode, p->pf, p->g, p->n, p->nq, rgb, coeffs, (const FrameQ*)p->fq.p, p->fq32.p,
                               (const double*)p->gk.p, (const float*)p->gk32.p, stats, (uint32_t*)p->part32.p,
                               (uint32_t*)p->fixbits.p, (uint2*)p->fixlist.p, (unsigned*)p->counters.p,
-                              (float*)p->dct32.p, s, &p->side,
+                              (float*)p->dct32.p, s,
                               phases == 1,  // forward + inverse: k_finalize adds the zero bin
                               (int)(p->fwd8_runs & 1u)));
     if (!exact && p->nq == 1) p->last_fwd8_bank = (int)(p->fwd8_runs++ & 1u);
   }
   InvFix fx = p->inv_fix();
   fx.fix_all = (flags & JDS_RUN_INV_FIXALL) ? 1 : 0;
-  // coarse tables: the exact-value tracking variant unless JDS_RUN_INV_FAST asks
-  // for the plain certificate (A/B and tests)
-  fx.ex = (!p->inv_fast_ok && !(flags & JDS_RUN_INV_FAST)) ? 1 : 0;
-  const bool exact_inv = exact || (flags & JDS_RUN_EXACT_INV) != 0;
+  const bool exact_inv = exact || (flags & JDS_RUN_EXACT_INV) != 0 || (!p->inv_fast_ok && !(flags & JDS_RUN_INV_FAST));
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,
@@ -859,9 +825,6 @@ void jds_plan_destroy(jds_plan* p) {
   p->ent_tab.release();
   free(p->qt);
   marks_release(p->marks);
-  if (p->side.stream) (void)hipStreamDestroy(p->side.stream);
-  if (p->side.fork) (void)hipEventDestroy(p->side.fork);
-  if (p->side.join) (void)hipEventDestroy(p->side.join);
   delete p;
 }
 
@@ -1083,30 +1046,6 @@ int jds_psnr_ssim_batch_dev(jds_ctx* c, int32_t n, const uint8_t* const* a_dev, 
   int rc = wait_after(c, after);
   if (rc) return rc;
   return psnr_ssim_device_batch(c, n, a_dev, b_dev, H, W, out);
-}
-
-int jds_selftest_psnr_ssim_legacy_dev(jds_ctx* c, const uint8_t* a_dev, const uint8_t* b_dev, int64_t H, int64_t W,
-                                      double* out) {
-  int rc = psnr_ssim_args(c, a_dev, b_dev, H, W, out);
-  if (rc) return rc;
-  HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(c->ss_out.ensure(5 * sizeof(double) + sizeof(unsigned long long)));
-  hipStream_t s = c->stream;
-  HIP_TRY(hipMemsetAsync(c->ss_out.p, 0, 5 * sizeof(double) + sizeof(unsigned long long), s));
-  double* dres = (double*)c->ss_out.p;
-  unsigned long long* dsse = (unsigned long long*)(dres + 5);
-  if ((rc = run_ssim_legacy(c, a_dev, b_dev, (int)H, (int)W, dres))) return rc;
-  const size_t nb = (size_t)H * W * 3;
-  HIP_TRY(launch_sse_u8(a_dev, b_dev, (long long)nb, dsse, s));
-  double res[5];
-  unsigned long long sse = 0;
-  HIP_TRY(hipMemcpyAsync(res, dres, sizeof res, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(&sse, dsse, sizeof sse, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  for (int i = 0; i < 5; ++i) out[i] = res[i];
-  out[5] = (double)sse / (double)nb;
-  return JDS_OK;
 }
 
 int jds_magnitude_bits_f32_batch_dev(jds_ctx* c, const int16_t* coeffs_dev, int32_t n_items, int64_t n_coeffs,

@@ -772,11 +772,7 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
       if (fx && !rin) {  // RGB only: the certified fast inverse (jds_inv_fast.hip)
         if ((e = launch_inv16_fast(MODE, g, n, coeffs, fq, rgb_out, *fx, s)) != hipSuccess) return e;
       } else {
-#ifndef JDS_INV16_TWO_WINDOWS
 #define K_INV16 k_inv16s
-#else
-#define K_INV16 k_inv16f
-#endif
       if (err_y)
         hipLaunchKernelGGL((K_INV16<MODE, 2>), gi, bi, 0, s, g, tx, coeffs, fq, rin, rgb_out, st, part, err_y,
                            err_rgb);

@@ -25,36 +25,12 @@
 
 #pragma clang fp contract(off)
 
-// first/last tile rows in k_fwd32i (fold_rows); A/B: -DJDS_FOLD_MODE=0 gives
-// them a border launch.  A uniform per-tile flag that skips the masks on the
-// other rows measured no better (339.6 vs 337.1 us per 64 x 1080p).
-#ifndef JDS_FOLD_MODE
-#define JDS_FOLD_MODE 1
-#endif
-// k_fwd32i's staging pass: ring rows on the lanes after the tile's rows
-#ifndef JDS_RING_LAST
-#define JDS_RING_LAST 1
-#endif
-// k_fwd444w's statistics: one record per wave (rows summed by DPP broadcasts)
-#ifndef JDS_F444_WAVE_REC
-#define JDS_F444_WAVE_REC 1
-#endif
-// single-quality forwards: the statistics partials summed inside k_fix_fwd's launch
-#ifndef JDS_FIX_REDUCE
-#define JDS_FIX_REDUCE 0  // 1 measured level or slower once the 4:2:2 and 4K points were timed (profiles/r03_v29_ab.txt, ab9)
-#endif
-// k_fwd32i (4:2:x): padding of the luma plane's rows in LDS (floats)
-#ifndef JDS_SY_PAD
-#define JDS_SY_PAD 0
-#endif
-// k_fwd32i: the quantiser tables loaded by the wave without staging work
-#ifndef JDS_TABLES_IDLE_WAVE
-#define JDS_TABLES_IDLE_WAVE 1
-#endif
-// k_fwd32i's staging pass: neighbour samples by DPP instead of ds_bpermute
-#ifndef JDS_STAGE_DPP
-#define JDS_STAGE_DPP 1
-#endif
+// Shipped choices whose alternatives were measured and retired (DESIGN.md
+// "Retired A/B switches"): first/last tile rows folded into k_fwd32i
+// (fold_rows; a uniform per-tile flag that skips the masks on the other rows
+// measured no better, 339.6 vs 337.1 us per 64 x 1080p); ring rows staged on
+// the lanes after the tile's rows; neighbour samples by DPP instead of
+// ds_bpermute; the quantiser tables loaded by a wave without staging work.
 
 namespace jds {
 
@@ -151,7 +127,6 @@ template <bool REPL = false>
 __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8], const float (&thr)[8], bool valid,
                                        int (&q)[8], LaneStats& ls, unsigned* s_st) {
   unsigned nrare = 0u;
-#ifndef JDS_QUANT8_CLASSIC
   // |t| <= 1024 (|c| <= 8 * 128, Q >= 1): QMAGIC rounds exactly.
   // Written for gfx950's issue costs (tools/microbench/op_rates.hip): fp32
   // add / sub / mul / fma and integer add / and / or / lshr issue in ~2.5
@@ -174,7 +149,6 @@ __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8]
     const float e = fabsf(t - r) - fmaf(fabsf(t), -0x1p-22f, thr[k]);
     ok &= __float_as_uint(e);
     q[k] = (int)(fb - QMAGIC_BITS);
-#ifndef JDS_PROBE_NOQSTATS  // tools/probe: the per-coefficient statistics removed (timing only)
     const int x = __builtin_amdgcn_frexp_expf(r);  // bit length of |q| (0 for q = 0; <= 11)
     ls.nz += (unsigned)(x + 15) >> 4;
     ls.mb += (unsigned)x;
@@ -184,31 +158,9 @@ __device__ __forceinline__ void quant8(const float (&v)[8], const float (&rq)[8]
     // taken back below
     ls.hn += top >> ((o & 28u) ^ 31u);
     orr |= o;  // any o >= 32 (q outside [-12, 19]) sets a bit >= 5
-#endif
   }
   ls.nflag += (~ok) >> 31;
   nrare = REPL ? orr : (orr >= 32u ? 1u : 0u);
-#else
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float t = v[k] * rq[k];
-    const float r = rintf(t);
-    // |t - r| is exact (Sterbenz); thr[k] holds 0.5 - E/Q - slack, rounded down
-    ls.nflag += fabsf(t - r) >= fmaf(fabsf(t), -0x1p-22f, thr[k]) ? 1u : 0u;
-    q[k] = (int)r;
-    ls.nz += r != 0.0f ? 1u : 0u;
-    ls.mb += (unsigned)__builtin_amdgcn_frexp_expf(r);
-    const unsigned o = (unsigned)(q[k] + 12);
-    ls.hn += 1u << (o & 28u);  // bins 22..29; a rare q lands in some nibble and is taken back below
-    if constexpr (REPL)
-      nrare |= o;  // any o >= 32 sets a bit >= 5
-    else
-      nrare += o >= 32u ? 1u : 0u;
-  }
-#endif
-#ifdef JDS_PROBE_NORARE  // tools/probe: drop the rare-bin atomics
-  nrare = 0u;
-#endif
   if constexpr (REPL) {
     if (nrare >= 32u) {
       const int lane = threadIdx.x & 63;
@@ -282,226 +234,19 @@ __device__ __forceinline__ void flag_block_bits(const LaneStats& ls, bool valid,
     atomicOr(fixbits + (size_t)item * wpi + (gblk >> 5), 1u << (gblk & 31));
 }
 
-// The workgroup's statistics into this tile's slot of the per-tile partials
-// (plain stores; k_fwd_reduce_fix reduces them per frame).  Each lane's eight
-// common-bin nibbles (<= 8 each) go into two words of 8-bit fields, the nonzero
-// count and magnitude bits into a third; three-word row sums (a 16-lane row
-// sums to <= 128 per bin), one LDS record per row, and the last wave decodes
-// and adds the waves' rows to the rare bins the quantiser counted.
-// s_st holds NSTAT + 1 words: the last is the waves' ticket counter.
+// The workgroup's statistics into this tile's slot of the per-tile partials.
+// No workgroup-level step at all: after the 16-lane row sums of the packed
+// counters (8-bit fields: a 16-lane row sums to <= 16 * 8 = 128 per bin; the
+// row's valid-lane count rides in bits 8..15 of the nonzero | magnitude-bits
+// word), lanes 15 / 31 / 47 / 63 store their row's three words straight into
+// the tile's slot (PSLOT words: [wave][row][4]); quant8's rare bins go to the
+// frame's rare row (global atomics; rare values are sparse) behind the tiles'
+// slots, and k_fwd_reduce_rows decodes the records, adds the rare row and
+// re-zeroes it.  (Measured against a workgroup-barrier form, a last-wave
+// ticket form, LDS-atomic and per-wave record forms in round 3: this one saves
+// the row broadcasts, the ticket and the last wave's decode; profiles/r03_*.)
 constexpr int NW_MAX = 8;  // waves per forward workgroup (TF <= 512)
-
-// Two forms, picked per kernel configuration (stats_flush<TF>): the barrier
-// form (wave reductions, LDS atomics, one workgroup barrier) measured faster
-// with 8 waves per workgroup (4:2:2: k_fwd32i 379 vs 418 us per 16 x 4K),
-// the ticket form below with 6 (4:2:0: 325 vs 333 us per 64 x 1080p).
-#ifndef JDS_FLUSH_BARRIER_TF
-#define JDS_FLUSH_BARRIER_TF 1024  // workgroups of at least this many threads take the barrier form (512: see DESIGN)
-#endif
-__device__ __forceinline__ void stats_flush_barrier(LaneStats ls, bool valid, unsigned* s_st,
-                                                    uint32_t* __restrict__ slot) {
-  if (!valid) ls = LaneStats();
-  const unsigned e = ls.hn & 0x0f0f0f0fu, o = (ls.hn >> 4) & 0x0f0f0f0fu;
-  const unsigned w0 = __reduce_add_sync(~0ull, e & 0x00ff00ffu), w1 = __reduce_add_sync(~0ull, (e >> 8) & 0x00ff00ffu);
-  const unsigned w2 = __reduce_add_sync(~0ull, o & 0x00ff00ffu), w3 = __reduce_add_sync(~0ull, (o >> 8) & 0x00ff00ffu);
-  const unsigned wmb = __reduce_add_sync(~0ull, ls.mb), wnz = __reduce_add_sync(~0ull, ls.nz);
-  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&s_st[0], wnz);
-    atomicAdd(&s_st[1], wmb + wnz);
-    const unsigned zeros = 8u * nvalid - wnz;
-    const unsigned c[8] = {w0 & 0xffffu, w2 & 0xffffu, w1 & 0xffffu, (w3 & 0xffffu) - zeros,
-                           w0 >> 16,     w2 >> 16,     w1 >> 16,     w3 >> 16};
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (c[j]) atomicAdd(&s_st[2 + 22 + j], c[j]);
-  }
-  __syncthreads();
-  if (threadIdx.x < NSTAT) slot[threadIdx.x] = s_st[threadIdx.x];
-}
-__device__ __forceinline__ void stats_flush_ticket(LaneStats ls, bool valid, unsigned* s_st,
-                                                   uint32_t* __restrict__ slot) {
-  __shared__ __attribute__((aligned(16))) unsigned s_wave[NW_MAX][4][4];  // [wave][row][word]
-  __shared__ unsigned s_nvalid[NW_MAX];
-  if (!valid) ls = LaneStats();
-#ifdef JDS_PROBE_NOSTATS  // tools/probe: stop before the statistics
-  if (ls.hn == 0x12345u && ls.mb == 7u && ls.nz == 3u) slot[0] = 1u;
-  return;
-#endif
-  // 8-bit fields: a 16-lane row sums to <= 16 * 8 = 128 per bin; even bins
-  // (22, 24, 26, 28) in v[0], odd in v[1], nonzero | magnitude bits << 16 in
-  // v[2] (<= 128 and <= 16 * 88); three row sums of fast and / shift ops
-  const unsigned h = ls.hn;
-  unsigned v[3] = {h & 0x0f0f0f0fu, (h >> 4) & 0x0f0f0f0fu, ls.nz | (ls.mb << 16)};
-  row_sums3(v);
-  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nw = (int)(blockDim.x >> 6);
-  // no workgroup barrier: the four row-total lanes leave the wave's rows, lane 0
-  // takes a ticket, and the last wave of the workgroup (the LDS performs one
-  // wave's operations in order, so everyone's rows and rare-bin atomics
-  // precede the last ticket) decodes and stores the tile's slot
-  if ((lane & 15) == 15) {
-    *reinterpret_cast<uint4*>(&s_wave[w][lane >> 4][0]) = make_uint4(v[0], v[1], v[2], 0u);
-    if (lane == 63) s_nvalid[w] = nvalid;
-  }
-  // (a compiler barrier only: a memory fence would also wait for the wave's
-  // global coefficient stores)
-  __asm__ volatile("" ::: "memory");
-  unsigned ticket = 0u;
-  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
-  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
-  if (ticket != (unsigned)(nw - 1)) return;
-  __asm__ volatile("" ::: "memory");
-  const int t = lane;
-  if (t < NSTAT) {
-    unsigned tot = s_st[t];  // rare bins (quant8's LDS atomics)
-    const int b = t - 2 - 22;  // common bin 22 + b: word b & 1, byte b >> 1
-    const bool odd = (b & 1) != 0;
-    const int sh = 8 * ((b >> 1) & 3);
-    for (int i = 0; i < nw; ++i) {
-      unsigned nz = 0u, mb = 0u, c = 0u;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {  // (per-row fields, unpacked before the rows are added; no branches)
-        const uint4 x = *reinterpret_cast<const uint4*>(&s_wave[i][r][0]);
-        nz += x.z & 0xffffu;
-        mb += x.z >> 16;
-        c += ((odd ? x.y : x.x) >> sh) & 255u;
-      }
-      if (t == 0) {
-        tot += nz;
-      } else if (t == 1) {
-        tot += mb + nz;  // magnitude bits = bit length + 1 per nonzero
-      } else if (b >= 0 && b < 8) {
-        if (b == 3) c -= 8u * s_nvalid[i] - nz;  // zeros fall in bin 25: k_finalize adds them
-        tot += c;
-      }
-    }
-    slot[t] = tot;
-  }
-}
-// The ticket form with the per-row records summed by the LDS instead of by the
-// last wave: each 16-lane row total widens its 8-bit bin fields into four
-// words of 16-bit fields (a workgroup counts <= 384 lanes x 8 = 3072 per bin,
-// nonzero <= 3072, magnitude bits <= 384 x 88 = 33792) and adds them, with the
-// nonzero | magnitude-bits word, into s_st[NSTAT + 1 ..] by LDS atomics (no
-// return); lane 63 adds the wave's valid-lane count.  The last wave then
-// decodes five words once instead of 4 x waves records (the ticket form's
-// loop was ~24 dependent reads and ~200 VALU in one wave per workgroup).
-// s_st holds NST_LDS words (zeroed by the kernel): [0, NSTAT) the tile's
-// record with quant8's rare bins, [NSTAT] the ticket, then the packed sums.
-constexpr int NST_LDS = NSTAT + 8;
-__device__ __forceinline__ void stats_flush_atomic(LaneStats ls, bool valid, unsigned* s_st,
-                                                   uint32_t* __restrict__ slot) {
-  if (!valid) ls = LaneStats();
-  const unsigned h = ls.hn;
-  unsigned v[3] = {h & 0x0f0f0f0fu, (h >> 4) & 0x0f0f0f0fu, ls.nz | (ls.mb << 16)};
-  row_sums3(v);
-  const int lane = threadIdx.x & 63;
-  const int nw = (int)(blockDim.x >> 6);
-  unsigned* pk = s_st + NSTAT + 1;
-  if ((lane & 15) == 15) {
-    // even bins 22, 24, 26, 28 in v[0]'s bytes, odd in v[1]'s: words of
-    // 16-bit fields (22 | 26), (24 | 28), (23 | 27), (25 | 29)
-    atomicAdd(pk + 0, v[0] & 0x00ff00ffu);
-    atomicAdd(pk + 1, (v[0] >> 8) & 0x00ff00ffu);
-    atomicAdd(pk + 2, v[1] & 0x00ff00ffu);
-    atomicAdd(pk + 3, (v[1] >> 8) & 0x00ff00ffu);
-    atomicAdd(pk + 4, v[2]);
-  }
-  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
-  if (lane == 63) atomicAdd(pk + 5, nvalid);
-  // (a compiler barrier only: a memory fence would also wait for the wave's
-  // global coefficient stores; the LDS performs one wave's operations in order)
-  __asm__ volatile("" ::: "memory");
-  unsigned ticket = 0u;
-  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
-  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
-  if (ticket != (unsigned)(nw - 1)) return;
-  __asm__ volatile("" ::: "memory");
-  if (lane < NSTAT) {
-    const unsigned nzmb = pk[4];
-    const unsigned nz = nzmb & 0xffffu, mb = nzmb >> 16;
-    const int b = lane - 2 - 22;  // common bin 22 + b: word 2 (b & 1) + ((b >> 1) & 1), field b >> 2
-    const unsigned w = pk[((b & 1) << 1) | ((b >> 1) & 1)];
-    unsigned add = (b >> 2) ? (w >> 16) : (w & 0xffffu);
-    if (b == 3) add -= 8u * pk[5] - nz;  // zeros fall in bin 25: k_finalize adds them
-    add = lane == 0 ? nz : (lane == 1 ? mb + nz : ((unsigned)b < 8u ? add : 0u));
-    slot[lane] = s_st[lane] + add;
-  }
-}
-
-// The ticket form with the wave's rows summed in the wave: after the row sums
-// the 8-bit fields widen into four words of 16-bit fields plus the nonzero |
-// magnitude-bits word (a wave counts <= 64 x 8 = 512 per bin), two DPP row
-// broadcasts sum the rows into lane 63, which stores one 5-word record; the
-// last wave decodes one record per wave instead of four.
-__device__ __forceinline__ void stats_flush_wave(LaneStats ls, bool valid, unsigned* s_st,
-                                                 uint32_t* __restrict__ slot) {
-  __shared__ __attribute__((aligned(16))) unsigned s_wr[NW_MAX][8];  // [wave][word]: 5 sums, valid lanes
-  if (!valid) ls = LaneStats();
-#ifdef JDS_PROBE_NOSTATS  // tools/probe: stop before the statistics
-  if (ls.hn == 0x12345u && ls.mb == 7u && ls.nz == 3u) slot[0] = 1u;
-  return;
-#endif
-  const unsigned h = ls.hn;
-  unsigned v[3] = {h & 0x0f0f0f0fu, (h >> 4) & 0x0f0f0f0fu, ls.nz | (ls.mb << 16)};
-  row_sums3(v);
-  // words of 16-bit fields: (22 | 26), (24 | 28), (23 | 27), (25 | 29), nz | mb
-  unsigned u[5] = {v[0] & 0x00ff00ffu, (v[0] >> 8) & 0x00ff00ffu, v[1] & 0x00ff00ffu, (v[1] >> 8) & 0x00ff00ffu, v[2]};
-#pragma unroll
-  for (int k = 0; k < 5; ++k) u[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u[k], 0x142, 0xa, 0xf, false);
-#pragma unroll
-  for (int k = 0; k < 5; ++k) u[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u[k], 0x143, 0xc, 0xf, false);
-  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nw = (int)(blockDim.x >> 6);
-#ifdef JDS_PROBE_FLUSH_NOTICKET  // tools/probe: the wave's record straight to the slot, no ticket / decode (timing only)
-  if (lane == 63) {
-    *reinterpret_cast<uint4*>(slot + 8 * w) = make_uint4(u[0], u[1], u[2], u[3]);
-    *reinterpret_cast<uint2*>(slot + 8 * w + 4) = make_uint2(u[4], nvalid);
-  }
-  return;
-#endif
-  if (lane == 63) {
-    *reinterpret_cast<uint4*>(&s_wr[w][0]) = make_uint4(u[0], u[1], u[2], u[3]);
-    *reinterpret_cast<uint2*>(&s_wr[w][4]) = make_uint2(u[4], nvalid);
-  }
-  __asm__ volatile("" ::: "memory");
-  unsigned ticket = 0u;
-  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
-  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
-  if (ticket != (unsigned)(nw - 1)) return;
-  __asm__ volatile("" ::: "memory");
-  if (lane < NSTAT) {
-    // lane 0: nz; lane 1: mb + nz; lanes 24..31: bin 22 + b from word
-    // 2 (b & 1) + ((b >> 1) & 1), field b >> 2; bin 25 less the zeros
-    const int b = lane - 2 - 22;
-    const bool bin = (unsigned)b < 8u;
-    const int k = bin ? ((b & 1) << 1) | ((b >> 1) & 1) : 4;
-    const unsigned sh = bin ? 16u * (unsigned)(b >> 2) : 0u;
-    const unsigned m1 = (lane < 2 || bin) ? 0xffffu : 0u, m2 = lane == 1 ? 0xffffu : 0u;
-    unsigned tot = 0u, zeros = 0u;
-    for (int i = 0; i < nw; ++i) {
-      const unsigned x = s_wr[i][k];
-      tot += ((x >> sh) & m1) + ((x >> 16) & m2);
-      zeros += 8u * s_wr[i][5] - (s_wr[i][4] & 0xffffu);
-    }
-    if (b == 3) tot -= zeros;  // zeros fall in bin 25: k_finalize adds them
-    slot[lane] = s_st[lane] + tot;
-  }
-}
-
-// FORM 5: no workgroup-level step at all.  After the 16-lane row sums of the
-// packed counters (8-bit fields; the row's valid-lane count rides in bits
-// 8..15 of the nonzero | magnitude-bits word), lanes 15 / 31 / 47 / 63 store
-// their row's three words straight into the tile's slot of the partials
-// (PSLOT words: [wave][row][4]); quant8's rare bins go to the frame's rare row
-// (global atomics; rare values are sparse) behind the tiles' slots, and
-// k_fwd_reduce_rows decodes the records, adds the rare row and re-zeroes it.
-// Saves the two row-broadcast passes, the widening, the ticket and the last
-// wave's decode of the wave-record form.
-__device__ __forceinline__ void stats_flush_rows(LaneStats ls, bool valid, uint32_t* __restrict__ slot) {
+__device__ __forceinline__ void stats_flush(LaneStats ls, bool valid, uint32_t* __restrict__ slot) {
   if (!valid) ls = LaneStats();
   const unsigned h = ls.hn;
   unsigned v[3] = {h & 0x0f0f0f0fu, (h >> 4) & 0x0f0f0f0fu, ls.nz | ((valid ? 1u : 0u) << 8) | (ls.mb << 16)};
@@ -511,31 +256,11 @@ __device__ __forceinline__ void stats_flush_rows(LaneStats ls, bool valid, uint3
     *reinterpret_cast<uint4*>(slot + 4 * (4 * w + (lane >> 4))) = make_uint4(v[0], v[1], v[2], 0u);
 }
 
-#ifndef JDS_FLUSH_FORM
-#define JDS_FLUSH_FORM 5  // 5: stats_flush_rows; 3: stats_flush_wave; 2: stats_flush_atomic; 1: stats_flush_ticket (below the barrier TF)
-#endif
-// words per tile slot of the per-tile partials (FORM 5: 8 waves x 4 rows x 4 words)
-constexpr int PSLOT = JDS_FLUSH_FORM == 5 ? 128 : NSTAT;
-constexpr bool FLUSH_ROWS = JDS_FLUSH_FORM == 5;
-// k_fix_fwd's in-launch reduction (JDS_FIX_REDUCE) reads NSTAT-stride slots and
-// never drains the rare-bin row: it does not know FORM 5's row records
-static_assert(!(JDS_FIX_REDUCE && JDS_FLUSH_FORM == 5), "JDS_FIX_REDUCE needs a slot-record flush form (not 5)");
-// FORM 5: the frame's rare-bin row (64 words: [2 + bin]) behind every tile slot
+// words per tile slot of the per-tile partials (8 waves x 4 rows x 4 words)
+constexpr int PSLOT = 128;
+// the frame's rare-bin row (64 words: [2 + bin]) behind every tile slot
 __device__ __forceinline__ unsigned* rare_row(uint32_t* part, const Geo& g, int nframes, int frame) {
   return part + (size_t)nframes * g.tiles_y * g.tiles_x * PSLOT + (size_t)frame * 64;
-}
-template <int TF>
-__device__ __forceinline__ void stats_flush(LaneStats ls, bool valid, unsigned* s_st, uint32_t* __restrict__ slot) {
-  if constexpr (TF >= JDS_FLUSH_BARRIER_TF)
-    stats_flush_barrier(ls, valid, s_st, slot);
-  else if constexpr (JDS_FLUSH_FORM == 5)
-    stats_flush_rows(ls, valid, slot);
-  else if constexpr (JDS_FLUSH_FORM == 3)
-    stats_flush_wave(ls, valid, s_st, slot);
-  else if constexpr (JDS_FLUSH_FORM == 2)
-    stats_flush_atomic(ls, valid, s_st, slot);
-  else
-    stats_flush_ticket(ls, valid, s_st, slot);
 }
 
 // ---- general tiles ------------------------------------------------------------
@@ -566,7 +291,6 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   __shared__ __attribute__((aligned(16))) float s_u[U_F];
   __shared__ __attribute__((aligned(16))) float s_rq[64];
   __shared__ __attribute__((aligned(16))) float s_thr[2][64];
-  __shared__ unsigned s_st[NST_LDS];  // + stats_flush's ticket and packed sums
 
   const int tid = threadIdx.x;
   const int frame = blockIdx.y;
@@ -609,7 +333,6 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
     s_thr[0][tid] = fq[frame].thr[0][tid];
     s_thr[1][tid] = fq[frame].thr[1][tid];
   }
-  if (tid < NST_LDS) s_st[tid] = 0u;
 
   const int blk = tid >> 3, line = tid & 7;
   int plane, by_t, bx_t;
@@ -787,12 +510,12 @@ k_fwd32(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coef
   const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
   int q[8];
   LaneStats ls;
-  quant8(v, rq, thr, valid, q, ls, FLUSH_ROWS && !MQ ? rare_row(part, g, gridDim.y, frame) : s_st);
+  quant8(v, rq, thr, valid, q, ls, rare_row(part, g, gridDim.y, frame));
   if (valid)
     *reinterpret_cast<uint4*>(coeffs + (long long)frame * g.cpf + (plane == 0 ? 0 : (plane == 1 ? g.off_cb : g.off_cr)) +
                               (long long)bidx * 64 + u * 8) = pack_q(q);
   flag_block_list(ls, valid, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
-  stats_flush<C::TF>(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * PSLOT);
+  stats_flush(ls, valid, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * PSLOT);
 }
 
 // ---- interior tiles ------------------------------------------------------------
@@ -827,9 +550,10 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   constexpr bool CPLANE = SUB && PF;
   constexpr int CR = SUB ? (CPLANE ? WR : TH) : TH;  // chroma plane rows
   constexpr int NCD = SUB ? 2 * C::NCB : 1;          // chroma row-DCT blocks (SUB)
-  // luma row stride: JDS_SY_PAD floats of padding (4:2:x) put the 8 rows of a
-  // block's in-place int16 transpose on different banks for the row reads
-  constexpr int YS = SUB ? TW + JDS_SY_PAD : TW;
+  // luma row stride: unpadded (8 or 16 floats of padding, which put the 8
+  // rows of a block's in-place int16 transpose on different banks, measured
+  // level: the forward is VALU-issue bound)
+  constexpr int YS = TW;
   __shared__ __attribute__((aligned(16))) float s_y[TH * YS];       // luma after the row DCT
   // chroma planes (4:4:4: after the row DCT; prefiltered 4:2:x: the horizontal
   // pair sums, TW / 2 per row)
@@ -838,7 +562,6 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   __shared__ __attribute__((aligned(16))) float s_cd[NCD * BS32];   // chroma blocks after the row DCT
   __shared__ __attribute__((aligned(16))) float s_rqT[64];          // 1/Q transposed: [v][k]
   __shared__ __attribute__((aligned(16))) float s_thT[2][64];
-  __shared__ unsigned s_st[NST_LDS];  // + stats_flush's ticket and packed sums
 
   const int tid = threadIdx.x, frame = blockIdx.y;
   const int ncol = rect.w - rect.z + 1;
@@ -853,7 +576,6 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   const int m0y = ty * C::MY - g.ty_off, m0x = tx * C::MX - g.tx_off;
   const int y0 = m0y * C::MH, x0 = m0x * C::MW;
   const uint8_t* img = rgb + (size_t)frame * g.H * g.W * 3;
-#if JDS_TABLES_IDLE_WAVE
   // the quantiser tables by the last wave, which has no staging work: the
   // staging waves do not wait for these loads before their own
   static_assert((TH + 2) * (TW / 8) <= Cfg<MODE>::TF - 64, "the last wave is idle in the staging pass");
@@ -864,29 +586,16 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     s_thT[0][l] = fq[frame].thr[0][t];
     s_thT[1][l] = fq[frame].thr[1][t];
   }
-#else
-  if (!MQ && tid < 64) {
-    const int t = (tid & 7) * 8 + (tid >> 3);  // [v][k] <- [k][v]
-    s_rqT[tid] = fq[frame].rq[t];
-    s_thT[0][tid] = fq[frame].thr[0][t];
-    s_thT[1][tid] = fq[frame].thr[1][t];
-  }
-#endif
-  if (tid < NST_LDS) s_st[tid] = 0u;
   const float k0 = gk32[0], k1 = gk32[1], k2 = gk32[2];
   float* s_cb = s_c;
   float* s_cr = s_c + CR * CW;
 
   // ---- 1. row segments --------------------------------------------------------
   if (tid < WR * SEG) {
-#if JDS_RING_LAST
     // the tile's rows 1..TH on the first TH * SEG lanes (whole waves), the
     // prefilter's ring rows 0 and TH + 1 (chroma only) after them: the wave
     // holding the ring rows skips the luma row DCT as a whole
     const int r = tid < TH * SEG ? 1 + tid / SEG : (tid < (TH + 1) * SEG ? 0 : TH + 1), c = tid % SEG;
-#else
-    const int r = tid / SEG, c = tid % SEG;
-#endif
     if (CPLANE || (r >= 1 && r <= TH)) {  // uniform per row (lane groups of SEG)
       // the tile lies inside the image; only the 1-px ring may leave it:
       // BORDER_REFLECT_101 maps row -1 to 1 and row H to H-2 (columns below)
@@ -895,14 +604,8 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       const uint8_t* p = img + ((size_t)yrow * g.W + x0 + 8 * c) * 3;
       const uint2* p2 = reinterpret_cast<const uint2*>(p);
       const bool left_edge = x0 == 0, right_edge = x0 + TW == g.W;
-#ifndef JDS_PROBE_NOLOAD
       const uint2 a = p2[0], b = p2[1], d = p2[2];
       const uint2 ring = CPLANE ? p2[c == 0 ? (left_edge ? 0 : -1) : (right_edge ? 0 : 3)] : make_uint2(0u, 0u);
-#else  // tools/probe: synthetic bytes instead of the loads
-      const uint32_t hsh = (uint32_t)(tid + 977 * blockIdx.x) * 2654435761u;
-      const uint2 a = make_uint2(hsh, hsh ^ 0x5bd1e995u), b = make_uint2(hsh * 3u, hsh + 17u), d = make_uint2(~hsh, hsh >> 3);
-      const uint2 ring = make_uint2(hsh * 5u, hsh * 7u);
-#endif
       const uint32_t w[6] = {a.x, a.y, b.x, b.y, d.x, d.y};
       float yy[8], cb[8], cr[8];
 #pragma unroll
@@ -936,16 +639,11 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
           dr[1] = make_float4(cr[4], cr[5], cr[6], cr[7]);
         }
       } else if constexpr (CPLANE) {
-#if JDS_STAGE_DPP
         // neighbours' edge samples by DPP row shifts (a 16-lane row holds two
         // segment groups; the lanes whose source lies outside their group,
         // c == 0 and c == SEG - 1, take the ring values below)
         float lb = dpp_f32<0x111>(cb[7]), lr = dpp_f32<0x111>(cr[7]);  // row_shr:1
         float rb = dpp_f32<0x101>(cb[0]), rr = dpp_f32<0x101>(cr[0]);  // row_shl:1
-#else
-        float lb = __shfl_up(cb[7], 1, SEG), lr = __shfl_up(cr[7], 1, SEG);
-        float rb = __shfl_down(cb[0], 1, SEG), rr = __shfl_down(cr[0], 1, SEG);
-#endif
         if (c == 0) {  // bytes 5..7 of the 8 before the segment; pixel 1 at the image edge
           const float R = (float)((ring.y >> 8) & 255u), G = (float)((ring.y >> 16) & 255u), B = (float)(ring.y >> 24);
           lb = left_edge ? cb[1] : cb32(R, G, B);
@@ -986,10 +684,6 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     }
   }
   __syncthreads();
-#ifdef JDS_PROBE_STAGE1  // tools/probe: stop after the staging pass
-  if (s_y[tid] == 1234.5f) coeffs[tid] = 1;
-  return;
-#endif
 
   // ---- 2./3. column passes ------------------------------------------------------
   const int blk = tid >> 3, line = tid & 7;
@@ -1036,7 +730,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     const float rq[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
     const float thr[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
     int q[8];
-    quant8(v, rq, thr, valid, q, ls, FLUSH_ROWS && !MQ ? rare_row(part, g, gridDim.y, frame) : s_st);
+    quant8(v, rq, thr, valid, q, ls, rare_row(part, g, gridDim.y, frame));
     // int16 transpose in place (row k at byte offset k * rs * 4).  Rotating
     // full-width rows across the wave's 8 blocks (so a block's 8 lanes read 8
     // bank groups instead of one) measured 6 us slower: the address math
@@ -1046,11 +740,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     for (int k = 0; k < 8; ++k) tq[k * rs * 2 + line] = (int16_t)q[k];
     __builtin_amdgcn_wave_barrier();  // other lanes' rows: the LDS keeps the wave's order
     const uint4 row = *reinterpret_cast<const uint4*>(tq + line * rs * 2);
-#ifndef JDS_PROBE_NOSTORE
     if (valid) *reinterpret_cast<uint4*>(dst + line * 8) = row;
-#else
-    if (row.x == 0x7eadbeefu && row.y == 0x1234567u) *reinterpret_cast<uint4*>(dst + line * 8) = row;
-#endif
   };
 
   if constexpr (SUB) {
@@ -1136,7 +826,7 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   }
   if constexpr (!MQ) {
     flag_block_list(ls, valid, line, frame, plane, bidx, fixlist, fixcount, g.cpf / 64);
-    stats_flush<C::TF>(ls, valid, s_st, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * PSLOT);
+    stats_flush(ls, valid, part + ((size_t)frame * g.tiles_y * g.tiles_x + ty * g.tiles_x + tx) * PSLOT);
   }
 }
 
@@ -1153,27 +843,20 @@ k_fwd32i(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
 // barrier), certified quantisation, the in-place int16 transpose and 16-byte
 // row stores.  Both pass orders are covered by fast_fwd_thresholds.  A lane
 // quantises 24 coefficients, so its common-bin counts are kept in 16-bit
-// fields (quant8's nibbles are folded after each plane) and the workgroup's
-// statistics go to a per-workgroup partial once (last-wave ticket, as
-// stats_flush_ticket), summed per frame by k_fwd_reduce.  Measured (256 x
-// 512^2, same box): 190 us against k_fwd32i<4:4:4>'s 274 (JDS_FWD444_TILED=1
-// keeps the tiled kernel for A/B); 92 VGPRs, 5 waves per SIMD -- forcing 6
+// fields (quant8's nibbles are folded after each plane) and each 16-lane row
+// stores one 8-word record into the workgroup's slot, decoded per frame by
+// k_fwd_reduce_rows<16, 1>.  Measured (256 x 512^2, same box): 190 us against
+// the tiled k_fwd32i<4:4:4>'s 274; 92 VGPRs, 5 waves per SIMD -- forcing 6
 // spills 10 registers and takes 255 us.
 constexpr int F444_WAVES = 4;
-#ifndef JDS_F444_WPE
-#define JDS_F444_WPE 5
-#endif
 
-__global__ void __launch_bounds__(64 * F444_WAVES) __attribute__((amdgpu_waves_per_eu(JDS_F444_WPE)))
+__global__ void __launch_bounds__(64 * F444_WAVES) __attribute__((amdgpu_waves_per_eu(5)))
 k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs, const FastQ* __restrict__ fq,
           uint32_t* __restrict__ part, uint2* __restrict__ fixlist, unsigned* __restrict__ fixcount,
           jds_frame_stats* __restrict__ stz) {
   __shared__ __attribute__((aligned(16))) float s_blk[8 * F444_WAVES * BS32];
   __shared__ __attribute__((aligned(16))) float s_rqT[64];
   __shared__ __attribute__((aligned(16))) float s_thT[2][64];
-  __shared__ unsigned s_st[NSTAT + 1];  // rare bins (quant8) + the waves' ticket
-  __shared__ unsigned s_rows[F444_WAVES][4][5];
-  __shared__ unsigned s_nvalid[F444_WAVES];
   const int tid = threadIdx.x, lv = tid & 7, lb = tid >> 3;
   const int frame = blockIdx.y;
   if (blockIdx.x == 0) {  // this launch owns the frame statistics' reset (k_fwd_reduce adds after it)
@@ -1186,7 +869,6 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     s_thT[0][tid] = fq[frame].thr[0][t];
     s_thT[1][tid] = fq[frame].thr[1][t];
   }
-  if (tid <= NSTAT) s_st[tid] = 0u;
   __syncthreads();
 
   const int nblk = g.nby * g.nbx;
@@ -1247,9 +929,8 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     int q[8];
     ls.hn = 0u;
     ls.nflag = 0u;
-    // (FORM 5: rare bins to the frame's rare row behind the workgroups' slots)
-    quant8(c, rq, thr, valid, q, ls,
-           FLUSH_ROWS ? part + (size_t)gridDim.y * gridDim.x * PSLOT + (size_t)frame * 64 : s_st);
+    // (rare bins to the frame's rare row behind the workgroups' slots)
+    quant8(c, rq, thr, valid, q, ls, part + (size_t)gridDim.y * gridDim.x * PSLOT + (size_t)frame * 64);
     __builtin_amdgcn_wave_barrier();  // every lane's column read precedes the int16 rows
 #pragma unroll
     for (int k = 0; k < 8; ++k) tq[k * 16 + lv] = (int16_t)q[k];
@@ -1265,7 +946,7 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     __builtin_amdgcn_wave_barrier();  // the rows are read before the next plane writes the slot
   }
 
-  // ---- statistics: row sums, one record per 16-lane row, the last wave decodes
+  // ---- statistics: row sums, one record per 16-lane row
   unsigned r5[4] = {acc[0], acc[1], acc[2], acc[3]};
   unsigned nzmb = ls.nz | (ls.mb << 16);  // <= 24 and <= 24 * 16 per lane
   if (!valid) {
@@ -1277,91 +958,26 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
   nzmb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)nzmb, 0x112, 0xf, 0xf, true);
   nzmb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)nzmb, 0x114, 0xf, 0xf, true);
   nzmb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)nzmb, 0x118, 0xf, 0xf, true);
-  const unsigned nvalid = (unsigned)__popcll(__ballot(valid));
+  // each 16-lane row's sums (and its valid lanes) straight into the
+  // workgroup's slot, decoded by k_fwd_reduce_rows<16, 1>
   const int wv = tid >> 6, lane = tid & 63;
-  if constexpr (FLUSH_ROWS) {
-    // FORM 5: each 16-lane row's sums (and its valid lanes) straight into the
-    // workgroup's slot, decoded by k_fwd_reduce_rows<16, 1>
-    const unsigned long long vb = __ballot(valid);  // (the whole wave's: a ballot inside the branch sees 4 lanes)
-    if ((lane & 15) == 15) {
-      const unsigned rv = (unsigned)__popcll(vb & (0xffffull << (lane & 48)));
-      uint32_t* rec = part + ((size_t)frame * gridDim.x + blockIdx.x) * PSLOT + 8 * (4 * wv + (lane >> 4));
-      *reinterpret_cast<uint4*>(rec) = make_uint4(r5[0], r5[1], r5[2], r5[3]);
-      *reinterpret_cast<uint2*>(rec + 4) = make_uint2(nzmb, rv);
-    }
-    return;
-  }
-#if JDS_F444_WAVE_REC
-  // the four rows into lane 63 by two DPP row broadcasts (a wave counts <= 64 x
-  // 24 = 1536 per field, magnitude bits <= 64 x 384): one record per wave
-  unsigned u5[5] = {r5[0], r5[1], r5[2], r5[3], nzmb};
-#pragma unroll
-  for (int k = 0; k < 5; ++k) u5[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u5[k], 0x142, 0xa, 0xf, false);
-#pragma unroll
-  for (int k = 0; k < 5; ++k) u5[k] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)u5[k], 0x143, 0xc, 0xf, false);
-  if (lane == 63) {
-    unsigned* rr = s_rows[wv][0];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) rr[k] = u5[k];
-    s_nvalid[wv] = nvalid;
-  }
-  constexpr int NREC = 1;
-#else
+  const unsigned long long vb = __ballot(valid);  // (the whole wave's: a ballot inside the branch sees 4 lanes)
   if ((lane & 15) == 15) {
-    unsigned* rr = s_rows[wv][lane >> 4];
-    rr[0] = r5[0];
-    rr[1] = r5[1];
-    rr[2] = r5[2];
-    rr[3] = r5[3];
-    rr[4] = nzmb;
-    if (lane == 63) s_nvalid[wv] = nvalid;
-  }
-  constexpr int NREC = 4;
-#endif
-  __asm__ volatile("" ::: "memory");
-  unsigned ticket = 0u;
-  if (lane == 0) ticket = atomicAdd(&s_st[NSTAT], 1u);
-  ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
-  if (ticket != (unsigned)(F444_WAVES - 1)) return;
-  __asm__ volatile("" ::: "memory");
-  if (lane < NSTAT) {
-    unsigned tot = s_st[lane];  // rare bins (quant8's LDS atomics)
-    for (int i = 0; i < F444_WAVES; ++i) {
-      unsigned nz = 0u, mb = 0u, f[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int r = 0; r < NREC; ++r) {
-        const unsigned* rr = s_rows[i][r];
-        nz += rr[4] & 0xffffu;
-        mb += rr[4] >> 16;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) f[j] += rr[j];  // (per-field sums <= 4 * 384: no carry between fields)
-      }
-      if (lane == 0) {
-        tot += nz;
-      } else if (lane == 1) {
-        tot += mb + nz;  // magnitude bits = bit length + 1 per nonzero
-      } else if (lane >= 2 + 22 && lane < 2 + 30) {
-        const int b = lane - 2 - 22;
-        unsigned c = (f[b >> 1] >> (16 * (b & 1))) & 0xffffu;
-        if (b == 3) c -= 24u * s_nvalid[i] - nz;  // zeros fall in bin 25: k_finalize adds them
-        tot += c;
-      }
-    }
-    part[((size_t)frame * gridDim.x + blockIdx.x) * NSTAT + lane] = tot;
+    const unsigned rv = (unsigned)__popcll(vb & (0xffffull << (lane & 48)));
+    uint32_t* rec = part + ((size_t)frame * gridDim.x + blockIdx.x) * PSLOT + 8 * (4 * wv + (lane >> 4));
+    *reinterpret_cast<uint4*>(rec) = make_uint4(r5[0], r5[1], r5[2], r5[3]);
+    *reinterpret_cast<uint2*>(rec + 4) = make_uint2(nzmb, rv);
   }
 }
 
-// FORM 5's reduction: the row records of 64 tiles of frame blockIdx.y per
+// The forward statistics' reduction: the row records of 64 tiles of frame blockIdx.y per
 // workgroup (nrec = 4 x waves per tile), decoded into the 8 common bins, the
 // nonzero count, the magnitude bits and the zeros (8 coefficients per valid
 // lane, all in bin 25 by the nibble counters: taken back), summed per thread,
 // then per wave (DPP-based __reduce_add_sync) and per workgroup (LDS), and
 // added to the frame stats; workgroup 0 of the frame also adds and re-zeroes
 // the frame's rare-bin row for the next run.
-#ifndef JDS_RROWS_TILES
-#define JDS_RROWS_TILES 64
-#endif
-constexpr int RROWS_TILES = JDS_RROWS_TILES;  // tiles per k_fwd_reduce_rows workgroup
+constexpr int RROWS_TILES = 64;  // tiles per k_fwd_reduce_rows workgroup
 // FMT 0: k_fwd32i's 4-word records (8-bit fields); FMT 1: k_fwd444w's 8-word
 // records (16-bit fields, 24 coefficients per valid lane).  ptiles = slots per frame.
 template <int NREC, int FMT = 0>
@@ -1447,7 +1063,7 @@ k_fwd_reduce_rows(const Geo g, jds_frame_stats* __restrict__ st, uint32_t* __res
 }
 
 // words of the statistics partials a single-quality 8x8 plan needs (tile slots
-// of either flush form, plus FORM 5's rare rows); the buffer starts zeroed
+// of row records, plus the frames' rare-bin rows); the buffer starts zeroed
 size_t fast_part_words(const Geo& g, int n) {
   return ((size_t)PSLOT * g.tiles_y * g.tiles_x + 64) * (size_t)n;
 }
@@ -1514,49 +1130,12 @@ k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ 
 //   many workgroups as it has entries.  Each workgroup prefix-sums the n list
 //   lengths in LDS (dynamic, 4 (n + 1) bytes) and maps its entry index to
 //   (item, slot) by binary search.
-#ifndef JDS_FIX_RED_TILES
-#define JDS_FIX_RED_TILES 32
-#endif
-constexpr int FIX_RED_TILES = JDS_FIX_RED_TILES;  // statistics partials per reducing workgroup of k_fix_fwd
 template <int MODE, bool PF>
-#ifndef JDS_FIX_WPE
-#define JDS_FIX_WPE 5
-#endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(JDS_FIX_WPE)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
           const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq, const int n_flat,
-          unsigned* __restrict__ rearm, const uint32_t* __restrict__ part = nullptr, const int ptiles = 0,
-          const int fix_gx = 0) {
-  // single-quality plans (JDS_FIX_REDUCE): the workgroups past the fix-up's
-  // grid (blockIdx.x >= fix_gx) sum the statistics partials of 8 tiles of
-  // frame blockIdx.y into the frame stats -- k_fwd_reduce's work in the same
-  // launch (both only add to the stats, so the two orders agree)
-  if (ptiles > 0 && (int)blockIdx.x >= fix_gx) {
-    const int f = blockIdx.y, t0 = ((int)blockIdx.x - fix_gx) * FIX_RED_TILES, j = threadIdx.x;
-    if (j < NSTAT) {
-      // FIX_RED_TILES tiles per workgroup: few enough device atomics per stats
-      // word (8 tiles per workgroup measured 41.7 vs 31.8 us at 16 x 4K 4:2:2)
-      unsigned long long a = 0ull;
-#pragma unroll 1
-      for (int i0 = 0; i0 < FIX_RED_TILES; i0 += 8) {
-        unsigned v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int tt = t0 + i0 + i;
-          v[i] = tt < ptiles ? part[((size_t)f * ptiles + tt) * NSTAT + j] : 0u;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a += v[i];
-      }
-      jds_frame_stats* sf = st + f;
-      unsigned long long* dst = j == 0 ? (unsigned long long*)&sf->nonzero
-                                : j == 1 ? (unsigned long long*)&sf->magnitude_bits
-                                         : (unsigned long long*)&sf->hist[j - 2];
-      if (a) atomicAdd(dst, a);
-    }
-    return;
-  }
+          unsigned* __restrict__ rearm) {
   constexpr bool CPLANE = (MODE != M444) && PF;
   constexpr int SY = Cfg<MODE>::SY;
   constexpr int WRR = 8 * SY + 2, WCC = 18;  // prefilter source window of one chroma block
@@ -1603,8 +1182,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     if (rearm != nullptr && blockIdx.x == 0 && t == 0) rearm[blockIdx.y] = 0u;
   }
   const double k[3] = {gk[0], gk[1], gk[2]};
-  const unsigned gstride = fix_gx > 0 ? (unsigned)fix_gx : gridDim.x;
-  for (unsigned e = blockIdx.x; e < count; e += gstride) {
+  for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
     uint2 ent;
     if (n_flat) {  // entry e of the concatenated lists: item = last start <= e
       int lo = 0, hi = n_flat - 1;
@@ -1615,7 +1193,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
       ent = list[(size_t)lo * cap + (e - s_off[lo])];
     } else {
       ent = next;
-      if (e + gstride < count) next = list[e + gstride];
+      if (e + gridDim.x < count) next = list[e + gridDim.x];
     }
     const int frame = (int)ent.x;
     const int plane = (int)(ent.y >> 24);
@@ -1638,11 +1216,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     // chains ~4 dependent load rounds per thread: such blocks set the tail)
     const int wy0 = SY * 8 * gy - 1, wx0 = 16 * gx - 1;
     const bool staged = CPLANE && plane != 0 && gy * 8 + 8 <= g.hc && gx * 8 + 8 <= g.wc;
-#ifdef JDS_PFIX_NOSAMPLE  // tools/probe: constant samples (timing only)
-    if (false) {
-#else
     if (staged) {  // uniform per workgroup
-#endif
       // every window load in flight before the first use (one memory latency)
       constexpr int NWL = (WRR * WCC + 63) / 64;
       uint32_t px[NWL];
@@ -1691,11 +1265,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
         v = (sm[0][0] + sm[0][1]) * 0.5;
       s_b[t] = v - 128.0;
     } else {
-#ifdef JDS_PFIX_NOSAMPLE
-      s_b[t] = (double)(t + (int)(old.x & 7u));
-#else
       s_b[t] = sample64<MODE, PF>(img, g, plane, gy * 8 + i, gx * 8 + j, k) - 128.0;
-#endif
     }
     __syncthreads();
     double v[8];
@@ -1721,11 +1291,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
         const int qn = (int)__builtin_rint(v[c] / fq[frame].q16[u * 8 + c]);
         const int qo = (int16_t)((ow[c >> 1] >> ((c & 1) * 16)) & 0xffffu);
         nw[c >> 1] |= (uint32_t)(uint16_t)qn << ((c & 1) * 16);
-#ifdef JDS_PFIX_NOSTAT
-        if (qn == 0x7fffffff) {
-#else
         if (qn != qo) {
-#endif
           const int mo = qo < 0 ? -qo : qo, mn = qn < 0 ? -qn : qn;
           if (mo) {
             --dnz;
@@ -1896,19 +1462,15 @@ static void fold_rows(const Geo& g, int4& rect) {
   }
 }
 
-hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s);
 // k_fix_fwd workgroups in all (x items, grid-stride over each item's list):
 // typical lists (0.4 % of 3M blocks at Q50) need one block per workgroup
-#ifndef JDS_FIX_GRID
-#define JDS_FIX_GRID 16384
-#endif
-constexpr int FIX_GRID = JDS_FIX_GRID;
+constexpr int FIX_GRID = 16384;
 
 template <int MODE, bool PF>
 static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
                              const FastQ* fq32, const double* gk, const float* gk32, jds_frame_stats* st,
                              uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount, float* dct32, hipStream_t s,
-                             const Side* side, bool finish, int par) {
+                             bool finish, int par) {
   using C = Cfg<MODE>;
   const bool mq = nq > 1;  // sweep plan: front end once per frame into dct32, then k_quant_mq
   const int nf = n / nq;   // frames (n = items)
@@ -1916,36 +1478,25 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   unsigned* const fc = mq ? fixcount : fixcount + par * n;
   // Tiles lying wholly inside the image (no padding blocks, no phantom MCUs;
   // only the 1-px ring may reflect) form a rectangle of tile indices and take
-  // k_fwd32i; the rest run in k_fwd32 beside it on the side stream.
-  // 4:4:4 single-quality plans: the wave-local kernel (k_fwd444w) for every block
-  // (A/B knob read once per process: every plan of the process leaves its
-  // rare-bin row where its own forward kind put it)
-  static const bool fwd444_tiled = getenv("JDS_FWD444_TILED") != nullptr;
-  if (MODE == M444 && !mq && !fwd444_tiled) {
+  // k_fwd32i; the rest run in k_fwd32 before it on the same stream (a side
+  // stream for them measured no gain: the fork / join costs what the overlap
+  // returns).  4:4:4 single-quality plans: the wave-local kernel (k_fwd444w)
+  // for every block.
+  if (MODE == M444 && !mq) {
     const int ng = fwd444w_groups(g);
     hipLaunchKernelGGL(k_fwd444w, dim3(ng, n), dim3(64 * F444_WAVES), 0, s, g, rgb, coeffs, fq32, part, fixlist, fc, st);
     kmark(s, "k_fwd444w");
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
-#if JDS_FIX_REDUCE
-    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ng + FIX_RED_TILES - 1) / FIX_RED_TILES, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st,
-                       fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ng, gx);
-    kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
-#else
-    if constexpr (FLUSH_ROWS) {
-      static_assert(F444_WAVES * 4 == 16, "16 row records per k_fwd444w workgroup");
-      hipLaunchKernelGGL((k_fwd_reduce_rows<16, 1>), dim3((ng + RROWS_TILES - 1) / RROWS_TILES, n), dim3(256), 0, s, g,
-                         st, part, ng);
-      kmark(s, "k_fwd_reduce_rows<16,1>");
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else if ((e = launch_fwd_reduce(n, st, part, ng, s)) != hipSuccess) {
-      return e;
-    }
+    static_assert(F444_WAVES * 4 == 16, "16 row records per k_fwd444w workgroup");
+    hipLaunchKernelGGL((k_fwd_reduce_rows<16, 1>), dim3((ng + RROWS_TILES - 1) / RROWS_TILES, n), dim3(256), 0, s, g,
+                       st, part, ng);
+    kmark(s, "k_fwd_reduce_rows<16,1>");
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
     kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
-#endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
   }
@@ -1955,26 +1506,20 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   rect.z = (g.tx_off * C::MW > 0) ? 1 : 0;
   rect.w = (g.W / C::MW + g.tx_off) / C::MX - 1;
   const bool split = (g.W % 8) == 0 && g.H >= 2 && g.W >= 2 && rect.y >= rect.x && rect.w >= rect.z;
-  if (split && JDS_FOLD_MODE >= 1) fold_rows<MODE>(g, rect);
+  if (split) fold_rows<MODE>(g, rect);
   hipError_t e;
   if (split) {
     const int nin = (rect.y - rect.x + 1) * (rect.w - rect.z + 1), nout = g.tiles_y * g.tiles_x - nin;
-    const bool fork = side && side->stream && side->border && nout > 0;
-    hipStream_t sb = fork ? side->stream : s;
-    if (fork && ((e = hipEventRecord(side->fork, s)) != hipSuccess ||
-                 (e = hipStreamWaitEvent(sb, side->fork, 0)) != hipSuccess))
-      return e;
     if (nout > 0) {
       if (mq)
-        hipLaunchKernelGGL((k_fwd32<MODE, PF, true>), dim3(nout, nf), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32,
+        hipLaunchKernelGGL((k_fwd32<MODE, PF, true>), dim3(nout, nf), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32,
                            part, fixlist, fixcount, 1, rect, dct32, nullptr, nq);
       else
-        hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(nout, n), dim3(C::TF), 0, sb, g, rgb, coeffs, fq32, gk32, part,
+        hipLaunchKernelGGL((k_fwd32<MODE, PF>), dim3(nout, n), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32, part,
                            fixlist, fc, 1, rect, nullptr, nullptr, 1);
-      kmark(sb, "k_fwd32<%d,%d%s>", MODE, (int)PF, mq ? ",mq" : "");
+      kmark(s, "k_fwd32<%d,%d%s>", MODE, (int)PF, mq ? ",mq" : "");
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (fork && (e = hipEventRecord(side->join, sb)) != hipSuccess) return e;
     if (mq)
       hipLaunchKernelGGL((k_fwd32i<MODE, PF, true>), dim3(nin, nf), dim3(C::TF), 0, s, g, rgb, coeffs, fq32, gk32,
                          part, fixlist, fixcount, rect, dct32, st, nq);
@@ -1983,7 +1528,6 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
                          fixlist, fc, rect, nullptr, st, 1);
     kmark(s, "k_fwd32i<%d,%d%s>", MODE, (int)PF, mq ? ",mq" : "");
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (fork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
   } else {
     if (mq)
       hipLaunchKernelGGL((k_fwd32<MODE, PF, true>), dim3(g.tiles_y * g.tiles_x, nf), dim3(C::TF), 0, s, g, rgb,
@@ -2007,35 +1551,17 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     // the front-end launch above); k_fix_fwd reads the live counter bank `par`
     // the front end appended to and re-arms the other bank.  (Reducing the
     // partials inside k_fix_fwd instead of this launch measured slower: 49.4
-    // vs 29.1 + 5.4 us per 64 x 1080p.)
-#if JDS_FIX_REDUCE
-    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx + (ptiles + FIX_RED_TILES - 1) / FIX_RED_TILES, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk,
-                       st, fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ptiles, gx);
-    kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
-#else
-    // the reduction and the fix-up are independent (both add into the frame
-    // stats with atomics; the fix-up reads only its list): the reduction runs
-    // on the plan's side stream beside the latency-bound fix-up, joined before
-    // the next launch on s
-    const bool rfork = side && side->stream && side->reduce;
-    hipStream_t rs = rfork ? side->stream : s;
-    if (rfork && ((e = hipEventRecord(side->fork, s)) != hipSuccess ||
-                  (e = hipStreamWaitEvent(rs, side->fork, 0)) != hipSuccess))
-      return e;
-    if constexpr (FLUSH_ROWS && C::TF < JDS_FLUSH_BARRIER_TF) {
-      hipLaunchKernelGGL(k_fwd_reduce_rows<4 * (C::TF / 64)>, dim3((ptiles + RROWS_TILES - 1) / RROWS_TILES, n),
-                         dim3(256), 0, rs, g, st, part, ptiles);
-      kmark(rs, "k_fwd_reduce_rows<%d>", 4 * (C::TF / 64));
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else if ((e = launch_fwd_reduce(n, st, part, ptiles, rs)) != hipSuccess) {
-      return e;
-    }
-    if (rfork && (e = hipEventRecord(side->join, rs)) != hipSuccess) return e;
+    // vs 29.1 + 5.4 us per 64 x 1080p; the reduction on a side stream beside
+    // the fix-up, 0.627 vs 0.617 ms per step: the fork / join costs more than
+    // the overlap returns.)
+    static_assert(C::TF <= 64 * NW_MAX, "row records fit the tile slot");
+    hipLaunchKernelGGL(k_fwd_reduce_rows<4 * (C::TF / 64)>, dim3((ptiles + RROWS_TILES - 1) / RROWS_TILES, n),
+                       dim3(256), 0, s, g, st, part, ptiles);
+    kmark(s, "k_fwd_reduce_rows<%d>", 4 * (C::TF / 64));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
                        fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
     kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
-    if (rfork && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
-#endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
   }
@@ -2061,17 +1587,17 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
 hipError_t launch_fast_fwd(int mode, bool pf, const Geo& g, int n, int nq, const uint8_t* rgb, int16_t* coeffs,
                            const FrameQ* fq, const void* fq32, const double* gk, const float* gk32,
                            jds_frame_stats* st, uint32_t* part, uint32_t* fixbits, uint2* fixlist, unsigned* fixcount, float* dct32,
-                           hipStream_t s, const Side* side, bool finish, int par) {
+                           hipStream_t s, bool finish, int par) {
   const FastQ* f = (const FastQ*)fq32;
   switch (mode) {
     case M420:
-      return pf ? fast_fwd_t<M420, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par)
-                : fast_fwd_t<M420, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par);
+      return pf ? fast_fwd_t<M420, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, finish, par)
+                : fast_fwd_t<M420, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, finish, par);
     case M422:
-      return pf ? fast_fwd_t<M422, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par)
-                : fast_fwd_t<M422, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par);
+      return pf ? fast_fwd_t<M422, true>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, finish, par)
+                : fast_fwd_t<M422, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, finish, par);
     default:
-      return fast_fwd_t<M444, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, side, finish, par);
+      return fast_fwd_t<M444, false>(g, n, nq, rgb, coeffs, fq, f, gk, gk32, st, part, fixbits, fixlist, fixcount, dct32, s, finish, par);
   }
 }
 

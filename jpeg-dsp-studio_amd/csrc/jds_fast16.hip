@@ -114,14 +114,11 @@ constexpr int BS16F = 272;  // floats per 16x16 block in LDS (256 + 16 pad: colu
 // k_fwd_finish / k_finalize add bin 25's zeros from the nonzero count.
 constexpr int NW16 = 6;  // waves per k_fwd16f workgroup (TF <= 384)
 
-// The wave-record form (JDS_FLUSH16_WAVE): the bin bytes widen into four words
+// The wave-record form: the bin bytes widen into four words
 // of 16-bit fields (a wave counts <= 64 x 16 = 1024 per bin) plus nonzero |
 // magnitude bits << 16 (<= 1024, <= 64 x 240), summed over the whole wave by
 // DPP (row shifts, then two row broadcasts) into lane 63, one record per
 // wave; the last wave decodes one record per wave instead of four.
-#ifndef JDS_FLUSH16_WAVE
-#define JDS_FLUSH16_WAVE 1
-#endif
 __device__ __forceinline__ void stats_flush16_wave(unsigned h0, unsigned h1, unsigned nz, unsigned mb, bool valid,
                                                    unsigned* s_st, uint32_t* __restrict__ slot) {
   __shared__ __attribute__((aligned(16))) unsigned s_wr[NW16][8];  // [wave][word]: 5 sums, valid lanes
@@ -168,10 +165,8 @@ __device__ __forceinline__ void stats_flush16_wave(unsigned h0, unsigned h1, uns
 
 __device__ __forceinline__ void stats_flush16(unsigned h0, unsigned h1, unsigned nz, unsigned mb, bool valid,
                                               unsigned* s_st, uint32_t* __restrict__ slot) {
-#if JDS_FLUSH16_WAVE
   stats_flush16_wave(h0, h1, nz, mb, valid, s_st, slot);
   return;
-#endif
   __shared__ __attribute__((aligned(16))) unsigned s_row[NW16][4][4];  // [wave][row][word]
   __shared__ unsigned s_nvalid[NW16];
   const unsigned e = (h0 & 0x0f0f0f0fu) + (h1 & 0x0f0f0f0fu);                 // bins 0, 2, 4, 6 (bytes)
@@ -250,11 +245,7 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   // 4:2:0 with the prefilter reads them from global memory instead: holding
   // them in registers across its sampling cost a wave per SIMD (94 -> 100
   // VGPRs); staging them saves ~6 us elsewhere.
-#ifndef JDS_Q16_GLOBAL
   constexpr bool QLDS = !(MODE == M420 && CPLANE);
-#else
-  constexpr bool QLDS = false;
-#endif
   constexpr int QR = 20, TABF = 3 * 16 * QR;
   static_assert(WN >= TABF, "tables fit the RGB window");
   __shared__ __attribute__((aligned(16))) float s_tab_own[(CPLANE || !QLDS) ? 4 : TABF];
@@ -276,11 +267,7 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
   // chroma planes: each window row holds its even columns, then its odd ones
   // (the sample loop reads columns 2m+1 and 2m+2 of lane m: unit stride)
   static_assert(WC % 2 == 0, "even window width");
-#ifndef JDS_NO_CSPLIT
   auto cidx = [](int r, int c) { return r * WC + (c & 1) * (WC / 2) + (c >> 1); };
-#else
-  auto cidx = [](int r, int c) { return r * WC + c; };
-#endif
   if (tid <= NSTAT) s_st[tid] = 0u;
   float4 tabv = make_float4(0.f, 0.f, 0.f, 0.f);  // 3 tables x 16 rows x 4 float4: one per thread < 192
   const int tab_t = tid >> 6, tab_r = (tid >> 2) & 15, tab_q = tid & 3;
@@ -440,10 +427,6 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     }
   }
 
-#ifdef JDS_P16_ST1  // tools/probe: stop after staging (timing only)
-  if (s_u[tid] == 1234.5f && s_rgb[tid] == 77u) coeffs[tid] = 1;
-  return;
-#endif
   const int blk = tid >> 4, line = tid & 15;
   int plane, gy, gx;
   if (blk < C::NYB) {
@@ -521,9 +504,7 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
       sample_col(std::integral_constant<bool, true>());
     else
       sample_col(std::integral_constant<bool, false>());
-#ifndef JDS_P16_NODCT
     fdct16_f32(v);  // axis 0 (columns) first
-#endif
   }
   if constexpr (CPLANE) {
     __syncthreads();  // the block buffer aliases the chroma planes; s_rgb is free
@@ -543,9 +524,7 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     const int u = line;
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = s_blk[u * 17 + k];
-#ifndef JDS_P16_NODCT
     fdct16_f32(v);
-#endif
     float rqv[16], thv[16];
     if constexpr (QLDS) {
 #pragma unroll
@@ -570,10 +549,6 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     asm("v_mov_b32 %0, 0x80000000" : "=v"(top));  // opaque 2^31 (keeps the right shift below)
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-#ifdef JDS_P16_NOQ  // tools/probe: truncation instead of the certified quantiser (timing only)
-      q[k] = (int)v[k];
-      continue;
-#endif
       const float t = v[k] * rqv[k];
       const float f = t + QMAGIC;
       const float r = f - QMAGIC;  // rintf(t)
@@ -622,11 +597,7 @@ k_fwd16f(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coe
     const bool mine = valid && line == 0 && ((fm >> (lane & ~15)) & 0xffffull);
     const unsigned long long lm = __ballot(mine);
     unsigned base = 0u;
-#ifdef JDS_P16_FLAGSPREAD  // tools/probe: the appends spread over 13 counters (timing only)
-    if (lane == __ffsll((long long)lm) - 1) base = atomicAdd(fixcount + 3 + (blockIdx.x % 13), (unsigned)__popcll(lm));
-#else
     if (lane == __ffsll((long long)lm) - 1) base = atomicAdd(fixcount, (unsigned)__popcll(lm));
-#endif
     base = __shfl(base, __ffsll((long long)lm) - 1, 64);
     if (mine) {
       const unsigned slot = base + (unsigned)__popcll(lm & ((1ull << lane) - 1ull));
@@ -813,25 +784,15 @@ __device__ __forceinline__ void fix_column(const uint8_t* __restrict__ img, cons
   }
 }
 
-#ifndef JDS_FIX16_WPE
-#define JDS_FIX16_WPE 3
-#endif
-#ifndef JDS_FIX16_GRID
-#define JDS_FIX16_GRID 4096
-#endif
 template <int MODE, bool PF>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(JDS_FIX16_WPE)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
             const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
             const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, unsigned* __restrict__ fixlen,
             const unsigned cap) {
   __shared__ double s_b[4 * 272];  // four blocks, rows of 17 (jds_b16.hip's BS16 layout)
   const int lane = threadIdx.x, grp = lane >> 4, line = lane & 15;
-#ifdef JDS_P16_FIXNONE  // tools/probe: an empty list (timing only)
-  const unsigned c = *fixcount * 0u;
-#else
   const unsigned c = *fixcount;
-#endif
   const unsigned count = c < cap ? c : cap;
   const double k[3] = {gk[0], gk[1], gk[2]};
   double* const sb = s_b + grp * 272;
@@ -856,15 +817,8 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       dst = reinterpret_cast<uint4*>(coeffs + off);
       o0 = dst[0];
       o1 = dst[1];
-#ifdef JDS_P16FIX_NOSAMPLE  // tools/probe: constant samples (timing only)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = (double)(i * 3 + line + (int)(o0.x & 7u));
-#else
       fix_column<MODE, PF>(rgb + (size_t)frame * g.H * g.W * 3, g, plane, gy, gx, line, k, v, sb + line);
-#endif
-#ifndef JDS_P16FIX_NODCT
       dct2_line16(v);  // axis 0, column `line`
-#endif
 #pragma unroll
       for (int r = 0; r < 16; ++r) sb[r * 17 + line] = v[r];
     }
@@ -873,9 +827,7 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       const int u = line;
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) v[cc] = sb[u * 17 + cc];
-#ifndef JDS_P16FIX_NODCT
       dct2_line16(v);
-#endif
       const uint32_t ow[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
       uint32_t nw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
       long long dnz = 0, dmb = 0;
@@ -885,18 +837,10 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       for (int cc = 0; cc < 16; ++cc) {
         // quantizer.py:22-24: the true quotient of the reference's coefficient
         // (v / 32, exact) by Q16 = Q8[u/2][cc/2]
-#ifdef JDS_P16FIX_NODIV  // tools/probe: a product instead of the division (timing only)
-        const int qn = (int)__builtin_rint(v[cc] * q8[cc >> 1]);
-#else
         const int qn = (int)__builtin_rint(v[cc] / (32.0 * q8[cc >> 1]));
-#endif
         const int qo = (int16_t)((ow[cc >> 1] >> ((cc & 1) * 16)) & 0xffffu);
         nw[cc >> 1] |= (uint32_t)(uint16_t)qn << ((cc & 1) * 16);
-#ifdef JDS_P16FIX_NOSTAT
-        if (qn == 0x7fffffff) {
-#else
         if (qn != qo) {
-#endif
           const int mo = qo < 0 ? -qo : qo, mn = qn < 0 ? -qn : qn;
           if (mo) {
             --dnz;
@@ -928,7 +872,7 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
 // ------------------------------------------------------------ launchers --
 
 hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s);
-constexpr int FIX16_GRID = JDS_FIX16_GRID;  // k_fix_fwd16 workgroups (x 4 blocks in flight)
+constexpr int FIX16_GRID = 4096;  // k_fix_fwd16 workgroups (x 4 blocks in flight)
 
 template <int MODE, bool PF>
 static hipError_t fast16_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,

@@ -65,15 +65,6 @@ struct GenBufs {
 // 8x8 block of the item's coefficient array).
 __host__ __device__ inline int fix_wpi(const Geo& g) { return (int)((g.cpf / 64 + 31) / 32); }
 
-// A second stream with fork/join events: lets a plan run independent launches
-// (border tiles beside interior tiles) concurrently.  All null = serial.
-struct Side {
-  hipStream_t stream = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  bool border = false;  // border tiles beside the interior tiles (JDS_SIDE_STREAM=1)
-  bool reduce = false;  // statistics reduction beside the fix-up (JDS_REDUCE_SIDE=1; measured slower, off)
-};
-
 // Buffers of the certified 16x16 forward (jds_fast16.hip): per-frame fp32
 // tables (FastQ16), the fp32 Gaussian taps, per-tile statistics partials
 // (NSTAT u32 per tile), the list of blocks the exact fix-up recomputes, and
@@ -110,7 +101,6 @@ struct InvFix {
   int parity;
   int rot;
   int probe;
-  int ex = 0;  // coarse tables: values exact in both orders leave the certificate (k_inv_fast<.., EX>)
 };
 
 // Per-frame quantiser: q16 = 16*Q (pocketfft's first-axis fct = 1/16 folded in), q = Q.

@@ -8,12 +8,6 @@
 
 #include "jds_internal.hpp"
 
-#ifndef JDS_CW_PAD
-#define JDS_CW_PAD 1
-#endif
-#ifndef JDS_CW_PAD422
-#define JDS_CW_PAD422 4  // 4:2:2's padding (the model: 6 halves its read conflicts again; A/B in DESIGN)
-#endif
 
 namespace jds {
 
@@ -32,8 +26,8 @@ struct Inv {
   // row stride of the window in LDS: 4 doubles of padding for subsampled planes
   // (66 -> 70) put the 16-lane groups' ds_read_b128 of chroma8_fast on fewer
   // shared banks (a bank model of the two luma rounds: 576 -> 192 extra LDS
-  // cycles per tile; JDS_CW_PAD=0 keeps the unpadded stride)
-  static constexpr int CWS = (JDS_CW_PAD && SX == 2) ? CWC + (SY == 2 ? 4 : JDS_CW_PAD422) : CWC;
+  // cycles per tile)
+  static constexpr int CWS = SX == 2 ? CWC + 4 : CWC;
   static constexpr int NROW = (CBR - 2 * RY) * CBC * 8 + 2 * RY * CBC;     // chroma row tasks per plane
   static constexpr int MB = NCB > RB ? NCB : RB;                           // transpose-buffer blocks
   static constexpr int WPE = (MODE == M444) ? 3 : 4;                       // 2 or 3 workgroups per CU
@@ -54,15 +48,9 @@ __device__ __forceinline__ int tslot(int r, int c) { return r * 8 + ((((c >> 1) 
 // The same with the column's coefficients already loaded (software
 // prefetch: the loads of the next block are issued before this one's math).
 // (held sign-extended: signed 16-bit loads, no per-use extension)
-#ifndef JDS_COL16_INT
 struct Col16 {  // int16 elements: loaded two per VGPR (k_inv2 373 -> 363 us at 4K Q10 vs int)
   int16_t q[8];
 };
-#else
-struct Col16 {
-  int q[8];
-};
-#endif
 // Blocks outside the grid (`ok` false) read block 0 of the plane instead: the
 // caller never transforms them, and unmasked loads need no per-load branches.
 __device__ __forceinline__ Col16 load_col(const int16_t* __restrict__ plane, long long boff, int v, bool ok) {

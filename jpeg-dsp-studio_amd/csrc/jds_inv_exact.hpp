@@ -227,7 +227,6 @@ __device__ __forceinline__ void inv2_tile(InvShared<MODE, XTRA>& sh, const Geo& 
     const bool ok = luma_blk(0, by, bx);
     lq = load_col(cf, ((long long)by * g.nbx + bx) * 64, lv, ok);
   }
-#ifndef JDS_PROBE_NOCHROMA  // tools/probe: skip the chroma window
   if (tid < I::NCB * 8) {
     const int i = lb / I::CBC, j = lb - i * I::CBC;
     const int by = cby0 + i, bx = cbx0 + j;
@@ -254,7 +253,6 @@ __device__ __forceinline__ void inv2_tile(InvShared<MODE, XTRA>& sh, const Geo& 
     }
   }
   __syncthreads();
-#endif
   // ---- 2. luma rounds: IDCT, upsample, colour, store --------------------------
   const bool want_in = XTRA > 0;
   unsigned long long sse = 0ull;
@@ -322,11 +320,7 @@ __device__ __forceinline__ void inv2_tile(InvShared<MODE, XTRA>& sh, const Geo& 
         double C[8], Gt[8];
         // floor(clip(v, 0, 255)) == clamp(trunc(v), 0, 255) for |v| < 2^31:
         // one conversion and integer min/max instead of two fp64 ops
-#ifndef JDS_PROBE_NOUPS
         chroma8<MODE>(s_cw[0], g, x0, cwx0, wq, wt, C);
-#else
-        for (int k = 0; k < 8; ++k) C[k] = Yv[k] * 0.5;
-#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const double B = Yv[k] + 1.772 * (C[k] - 128.0);
@@ -335,11 +329,7 @@ __device__ __forceinline__ void inv2_tile(InvShared<MODE, XTRA>& sh, const Geo& 
           const int b = 3 * k + 2;
           pk[b >> 2] |= (uint32_t)clampi((int)B, 0, 255) << (8 * (b & 3));
         }
-#ifndef JDS_PROBE_NOUPS
         chroma8<MODE>(s_cw[1], g, x0, cwx0, wq, wt, C);
-#else
-        for (int k = 0; k < 8; ++k) C[k] = Yv[k] * 0.25;
-#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const double R = Yv[k] + 1.402 * (C[k] - 128.0);

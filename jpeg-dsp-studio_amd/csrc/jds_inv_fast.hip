@@ -11,9 +11,10 @@
 //   * AAN IDCT (5 multiplies per 8-point line) with the AAN scales and the 1/8
 //     normalisation folded into the dequantisation (one product per
 //     coefficient: q * Qs[u][v]), no +128: both planes clip to [-128, 127];
-//   * the bilinear upsample as a vertical blend of the lane's 6 chroma columns
-//     followed by a difference-form horizontal blend (3 operations per pixel
-//     and plane);
+//   * the bilinear upsample unnormalised: a vertical sum a + 3b of the lane's
+//     6 chroma columns, then a horizontal far + 3 near per pixel (one fma
+//     each: 14 per lane, row and plane at 4:2:0), the result 16x (4:2:0) or 4x
+//     (4:2:2) the blend, the scale folded into the colour constants;
 //   * the colour terms added onto Y + 1.5 * 2^20 + 128 (one fma per term), so
 //     each output lands on a grid of spacing 2^-32 whose words give both the
 //     byte and the certificate (byte_cert_y).
@@ -59,14 +60,14 @@
 
 namespace jds {
 
-// tools/inv_bound.py (the v24 chain as it stands in this file): e_fast + e_ref
-// <= K_LIN * Dmax + K_CONST off the magic grid, x2 safety included
-// (tests/test_inv_bound_cpu.py asserts kernel >= model)
-constexpr double K_LIN = 1.103043e-12 * 1.01;
-constexpr double K_CONST = 1.081459e-12 * 1.01;
+// tools/inv_bound.py (the v25 chain as it stands in this file: unnormalised
+// upsample): e_fast + e_ref <= K_LIN * Dmax + K_CONST off the magic grid, x2
+// safety included (tests/test_inv_bound_cpu.py asserts kernel >= model)
+constexpr double K_LIN = 8.762155e-13 * 1.01;
+constexpr double K_CONST = 1.024801e-12 * 1.01;
 // the same for 16x16 blocks (fidct16 vs dct3_line16, tools/inv_bound.py --b16)
-constexpr double K_LIN16 = 4.268828e-12 * 1.01;
-constexpr double K_CONST16 = 1.081459e-12 * 1.01;
+constexpr double K_LIN16 = 3.345910e-12 * 1.01;
+constexpr double K_CONST16 = 1.024801e-12 * 1.01;
 
 // AAN scale factors a_k = sqrt(2) cos(k pi / 16), a_0 = 1 (correctly rounded;
 // tools/inv_bound.py reads them from this list and prices their representation
@@ -132,43 +133,46 @@ __host__ __device__ __forceinline__ void aan8(double (&v)[8]) {
   v[4] = e3 - o4;
 }
 
-// cv2 INTER_LINEAR's blends at an exact 2x scale, in the certified order:
-// vertical a * 1/4 + b * 3/4 (a the "quarter" row), horizontal in difference
-// form near + (far - near) * (+-1/4)
+// cv2 INTER_LINEAR's blends at an exact 2x scale, unnormalised: the vertical
+// a * 1/4 + b * 3/4 (a the "quarter" row) as a + 3b, the horizontal (far 1/4,
+// near 3/4) as far + 3 near -- one fma each; every blended axis scales the
+// chroma by 4, which the colour constants take back (USC<SH> = 2^-SH, exact)
 template <class M = MadDev>
-__host__ __device__ __forceinline__ double fvblend(double a, double b) { return M::mad(a, 0.25, b * 0.75); }
+__host__ __device__ __forceinline__ double fvsum(double a, double b) { return M::mad(b, 3.0, a); }
 template <class M = MadDev>
-__host__ __device__ __forceinline__ double fhblend(double d, double w, double near) { return M::mad(d, w, near); }
+__host__ __device__ __forceinline__ double fhsum(double far, double near) { return M::mad(near, 3.0, far); }
+template <int SH>
+constexpr double USC = SH == 0 ? 1.0 : (SH == 2 ? 0.25 : 0.0625);
+// SH of a subsampling: 2 per blended axis
+template <int SY, int SX>
+constexpr int USH = (SY == 2 ? 2 : 0) + (SX == 2 ? 2 : 0);
 
-// The colour terms onto Y + MAGIC + 128 (byte_cert_y's grid): out = B, Gt, R, G
-template <class M = MadDev>
-__host__ __device__ __forceinline__ double col_b(double yv, double cb) { return M::mad(cb, 1.772, yv); }
-template <class M = MadDev>
-__host__ __device__ __forceinline__ double col_gt(double yv, double cb) { return M::mad(cb, -0.344136, yv); }
-template <class M = MadDev>
-__host__ __device__ __forceinline__ double col_r(double yv, double cr) { return M::mad(cr, 1.402, yv); }
-template <class M = MadDev>
-__host__ __device__ __forceinline__ double col_g(double gt, double cr) { return M::mad(cr, -0.714136, gt); }
+// The colour terms onto Y + MAGIC + 128 (byte_cert_y's grid): out = B, Gt, R,
+// G; the chroma operand at scale 2^SH (fvsum / fhsum)
+template <class M = MadDev, int SH = 0>
+__host__ __device__ __forceinline__ double col_b(double yv, double cb) { return M::mad(cb, 1.772 * USC<SH>, yv); }
+template <class M = MadDev, int SH = 0>
+__host__ __device__ __forceinline__ double col_gt(double yv, double cb) { return M::mad(cb, -0.344136 * USC<SH>, yv); }
+template <class M = MadDev, int SH = 0>
+__host__ __device__ __forceinline__ double col_r(double yv, double cr) { return M::mad(cr, 1.402 * USC<SH>, yv); }
+template <class M = MadDev, int SH = 0>
+__host__ __device__ __forceinline__ double col_g(double gt, double cr) { return M::mad(cr, -0.714136 * USC<SH>, gt); }
 
 // Axis-0 pass of column v of one block: dequantise with the folded table,
 // AAN, into the transpose buffer (no +128: fast_row clips to [-128, 127] and
 // the luma's +128 rides on the magic constant, see byte_cert_y).
 // qhi / qlo track the largest and smallest q the lane read (integer max3 /
 // min3 chains: cheaper than an fp64 max of |q| per coefficient).
-// The folded table is held transposed in LDS (JDS_INV_QS_T: column v's eight
+// The folded table is held transposed in LDS (column v's eight
 // entries contiguous, rows padded to QS_STRIDE doubles so the 8 columns' 16-B
 // slots fall on disjoint banks): four ds_read_b128 per column instead of four
 // ds_read2_b64 (8 LDS cycles each at 32-bank granularity, MI355X_MICROARCH.md).
-#ifndef JDS_INV_QS_T
-#define JDS_INV_QS_T 1
-#endif
 constexpr int QS_STRIDE = 10;
-constexpr int QS_WORDS = JDS_INV_QS_T ? 8 * QS_STRIDE : 64;
-__device__ __forceinline__ int qs_index(int r, int v) { return JDS_INV_QS_T ? v * QS_STRIDE + r : r * 8 + v; }
+constexpr int QS_WORDS = 1 ? 8 * QS_STRIDE : 64;
+__device__ __forceinline__ int qs_index(int r, int v) { return 1 ? v * QS_STRIDE + r : r * 8 + v; }
 __device__ __forceinline__ void fast_col(const Col16& in, const double* __restrict__ qs, int v,
                                          double* __restrict__ dst, int& qhi, int& qlo) {
   double c[8];
-#if JDS_INV_QS_T
   double t[8];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -176,17 +180,12 @@ __device__ __forceinline__ void fast_col(const Col16& in, const double* __restri
     t[2 * p] = d.x;
     t[2 * p + 1] = d.y;
   }
-#endif
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const double qd = (double)in.q[r];
     qhi = max(qhi, (int)in.q[r]);
     qlo = min(qlo, (int)in.q[r]);
-#if JDS_INV_QS_T
     c[r] = qd * t[r];
-#else
-    c[r] = qd * qs[r * 8 + v];
-#endif
   }
   aan8(c);
 #pragma unroll
@@ -214,13 +213,13 @@ __device__ __forceinline__ void fast_row(const double* __restrict__ src, int u, 
   }
 }
 
-// One plane's upsampled (chroma - 128) at the lane's 8 pixels (cv2
-// INTER_LINEAR at an exact 2x scale: pixel 2m weights (1/4, 3/4) on chroma
-// columns (m-1, m), pixel 2m+1 (3/4, 1/4) on (m, m+1); rows likewise with
-// clamped indices).  cv2 copies the edge column at the two image-edge pixels;
-// here the window holds that column replicated into the ring (see the window
-// writes), so the same blend gives the same real value: no per-pixel selects.
-// Horizontal blend in difference form: C = s_near + (s_far - s_near) / 4.
+// One plane's upsampled (chroma - 128) at the lane's 8 pixels, times 2^USH
+// (cv2 INTER_LINEAR at an exact 2x scale: pixel 2m weights (1/4, 3/4) on
+// chroma columns (m-1, m), pixel 2m+1 (3/4, 1/4) on (m, m+1); rows likewise
+// with clamped indices; fvsum / fhsum).  cv2 copies the edge column at the two
+// image-edge pixels; here the window holds that column replicated into the
+// ring (see the window writes), so the same blend gives the same real value:
+// no per-pixel selects.
 template <int MODE>
 __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int x0, int cwx0, int wq, int wt,
                                              double (&C)[8]) {
@@ -234,17 +233,14 @@ __device__ __forceinline__ void chroma8_fast(const double* __restrict__ cw, int 
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       if constexpr (I::SY == 2)
-        vb[j] = fvblend(cw[wq * I::CWS + c0 + j], cw[wt * I::CWS + c0 + j]);
+        vb[j] = fvsum(cw[wq * I::CWS + c0 + j], cw[wt * I::CWS + c0 + j]);
       else
         vb[j] = cw[wq * I::CWS + c0 + j];
     }
-    double d[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) d[j] = vb[j] - vb[j + 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      C[2 * i] = fhblend(d[i], 0.25, vb[i + 1]);       // (1/4, 3/4) on (m-1, m)
-      C[2 * i + 1] = fhblend(d[i + 1], -0.25, vb[i + 1]);  // (3/4, 1/4) on (m, m+1)
+      C[2 * i] = fhsum(vb[i], vb[i + 1]);          // (1/4, 3/4) on (m-1, m)
+      C[2 * i + 1] = fhsum(vb[i + 2], vb[i + 1]);  // (3/4, 1/4) on (m, m+1)
     }
   }
 }
@@ -273,35 +269,26 @@ __device__ __forceinline__ uint32_t byte_cert_y(double y, uint32_t& lo_min, uint
   return c > MAGIC_HI + 255u ? MAGIC_HI + 255u : c;  // v_med3_u32; the byte is bits 0-7
 }
 
-// The same for a value known exact in both orders (EX, below): its fraction
-// word is replaced by a neutral one (half-way between integers) so it cannot
-// trip the certificate.
-__device__ __forceinline__ uint32_t byte_cert_y(double y, uint32_t& lo_min, uint32_t& lo_max, bool exact) {
-  const uint32_t lo = exact ? 0x80000000u : (uint32_t)__double2loint(y), hi = (uint32_t)__double2hiint(y);
+// The same without the clamp: the high word itself, whose low 16 bits are
+// floor(v') as an int16 (|v'| < 2^15), for pack4s.
+__device__ __forceinline__ uint32_t cert_hi(double y, uint32_t& lo_min, uint32_t& lo_max) {
+  const uint32_t lo = (uint32_t)__double2loint(y), hi = (uint32_t)__double2hiint(y);
   lo_min = lo_min < lo ? lo_min : lo;
   lo_max = lo_max > lo ? lo_max : lo;
-  const uint32_t c = hi < MAGIC_HI ? MAGIC_HI : hi;
-  return c > MAGIC_HI + 255u ? MAGIC_HI + 255u : c;
+  return hi;
 }
-
-// OR of v over the 8 lanes of a block's lane group (lanes 8k .. 8k + 7):
-// quad_perm xor 1, xor 2, then row_half_mirror (lane i with 7 - i)
-__device__ __forceinline__ int or8(int v) {
-  v |= __builtin_amdgcn_update_dpp(0, v, 0xb1, 0xf, 0xf, true);
-  v |= __builtin_amdgcn_update_dpp(0, v, 0x4e, 0xf, 0xf, true);
-  v |= __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, true);
-  return v;
+// Four bytes clamp(int16 low half, 0, 255) of cert_hi words a, b, c, d into one
+// word: the int16 pairs by two byte permutes, v_sat_pk_u8_i16 clamps and packs
+// each pair, one shift-or joins them (5 operations instead of 4 med3 + 3).
+__device__ __forceinline__ uint32_t sat_pk_u8_i16(uint32_t x) {
+  uint32_t r;
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(x));
+  return r;
 }
-__device__ __forceinline__ int col_nonzero(const Col16& c) {
-  int v = 0;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) v |= (int)c.q[r];
-  return v;
-}
-// bits of window columns [lo, hi) that fall in 32-bit word w
-__device__ __forceinline__ uint32_t colbits(int lo, int hi, int w) {
-  const int a = max(lo - 32 * w, 0), b = min(hi - 32 * w, 32);
-  return a >= b ? 0u : (b - a == 32 ? 0xffffffffu : ((1u << (b - a)) - 1u) << a);
+__device__ __forceinline__ uint32_t pack4s(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t ab = sat_pk_u8_i16(__builtin_amdgcn_perm(b, a, 0x05040100u));  // a.lo16 | b.lo16 << 16
+  const uint32_t cd = sat_pk_u8_i16(__builtin_amdgcn_perm(d, c, 0x05040100u));
+  return ab | (cd << 16);
 }
 
 // Four bytes (bits 0-7 of a, b, c, d) into one word: two byte permutes and an or.
@@ -311,94 +298,39 @@ __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, ui
   return ab | cd;
 }
 
-// The tile certificate's reduction (JDS_INV_CERT_DPP): per 16-lane row by four
+// The tile certificate's reduction: per 16-lane row by four
 // DPP row shifts (lanes without a source keep the identity), then the row
 // totals into three LDS words by LDS min / max atomics (no return): thread 0
 // reads three words instead of looping over every wave's record, and the
 // waves skip six cross-lane permutes per value.
-#ifndef JDS_INV_CERT_DPP
-#define JDS_INV_CERT_DPP 1
-#endif
-#ifndef JDS_INV_WIN_SEL
-#define JDS_INV_WIN_SEL 1
-#endif
-#ifndef JDS_INV_EARLY_LOADS
-#define JDS_INV_EARLY_LOADS 1
-#endif
-#ifndef JDS_INV_QMAX_FQ
-#define JDS_INV_QMAX_FQ 1
-#endif
-#ifndef JDS_INV_MIX_PLANES
-#define JDS_INV_MIX_PLANES 1
-#endif
-// loop unrolling of the chroma plane loop (4:2:0 / 4:4:0) and the luma
-// rounds: 1 keeps the loops (the software-prefetched column is copied per
-// iteration), 2 unrolls them (A/B knobs)
-#ifndef JDS_INV_UNROLL_C
-#define JDS_INV_UNROLL_C 1
-#endif
-#ifndef JDS_INV_UNROLL_Y
-#define JDS_INV_UNROLL_Y 1
-#endif
-#ifndef JDS_INV_ONE_BARRIER
-#define JDS_INV_ONE_BARRIER 0  // every thread deciding without the second barrier measured slower (312 vs 309 us)
-#endif
-template <int SH, bool EX>
-__device__ __forceinline__ void cert_row_step(uint32_t& mn, uint32_t& mx, uint32_t& qm, uint32_t& em) {
+template <int SH>
+__device__ __forceinline__ void cert_row_step(uint32_t& mn, uint32_t& mx, uint32_t& qm) {
   const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)mn, 0x110 + SH, 0xf, 0xf, false);
   const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x110 + SH, 0xf, 0xf, false);
   const uint32_t c = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)qm, 0x110 + SH, 0xf, 0xf, false);
   mn = mn < a ? mn : a;
   mx = mx > b ? mx : b;
   qm = qm > c ? qm : c;
-  if constexpr (EX) {
-    const uint32_t d = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)em, 0x110 + SH, 0xf, 0xf, false);
-    em = em < d ? em : d;
-  }
 }
-// em (EX): the smallest clip margin of the values taken as exact, as the bits
-// of a non-negative float (ordered like the floats), or 0x7f800000 (+inf)
-template <bool EX = false>
-__device__ __forceinline__ void cert_to_lds(uint32_t mn, uint32_t mx, uint32_t qm, uint32_t* s_cert,
-                                            uint32_t em = 0x7f800000u) {
-  cert_row_step<1, EX>(mn, mx, qm, em);
-  cert_row_step<2, EX>(mn, mx, qm, em);
-  cert_row_step<4, EX>(mn, mx, qm, em);
-  cert_row_step<8, EX>(mn, mx, qm, em);  // lane 15 of each row: the row's min / max
+__device__ __forceinline__ void cert_to_lds(uint32_t mn, uint32_t mx, uint32_t qm, uint32_t* s_cert) {
+  cert_row_step<1>(mn, mx, qm);
+  cert_row_step<2>(mn, mx, qm);
+  cert_row_step<4>(mn, mx, qm);
+  cert_row_step<8>(mn, mx, qm);  // lane 15 of each row: the row's min / max
   if ((threadIdx.x & 15) == 15) {
     atomicMin(&s_cert[0], mn);
     atomicMax(&s_cert[1], mx);
     atomicMax(&s_cert[2], qm);
-    if constexpr (EX) atomicMin(&s_cert[3], em);
   }
 }
 
 // The fast pass over one tile (sets sh.redo when the tile must be recomputed).
-//
-// EX (coarse tables): values that are exact in both orders
-// are taken out of the certificate.  At coarse tables many luma samples clip
-// (|Y - 128| > 128 before the reference's per-block clip) and many chroma
-// blocks quantise to all zeros; a value whose luma sample is exactly known and
-// whose chroma term is exactly zero is then an exact integer in both orders
-// (the certificate, which only sees distances to integers, cannot tell it from
-// a value E away from one):
-//   * luma exactly known: its block is all zeros (Y - 128 = 0 in both orders:
-//     the IDCT of zeros is zeros) or the fast value lies beyond the clip
-//     boundary by more than E -- E bounds |v_fast - v_ref| of the whole chain,
-//     which includes the luma term with weight 1, so the reference's value
-//     lies beyond it too and both clip to -128 / 127 exactly;
-//   * chroma term exactly zero: every window sample the pixel's taps read
-//     comes from an all-zero chroma block (the reference's samples are then
-//     exactly 128: IDCT of zeros + 128, clip, and cv2's blends with weights
-//     summing to 1 keep 128; the fast window holds +-0 and its blends keep
-//     +-0), so 1.402 (Cr - 128) etc. is exactly 0 in both, R = G = B = Y;
-//     the lane's 8 pixels are judged together (all 6 columns, both rows);
-//   * then v_ref = v_fast = Y (+128), an integer: the bytes agree.
-// Such values do not enter the fraction-word certificate; instead the tile
-// is uncertain if the smallest clip margin among them is <= E.  Window
-// samples' sources are tracked as bits (s_zb: one bit per window sample, set
-// by the chroma task that writes the sample from an all-zero block).
-template <int MODE, int XTRA, bool EX = false>
+// (Round 5 tried an exact-value variant for coarse tables: values exact in
+// both orders -- luma clipped beyond E or from an all-zero block, every chroma
+// tap from an all-zero block -- taken out of the certificate.  It left 62 of
+// 16320 tiles uncertain at 16 x 4K Q10 instead of 12449, but its bookkeeping
+// made the kernel slower than k_inv2 there: 425 vs 358 us; DESIGN.md.)
+template <int MODE, int XTRA>
 __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const Geo& g, const int tiles_x,
                                               const int frame, const int tile, const int16_t* __restrict__ coeffs,
                                               const FrameQ* __restrict__ fq, const uint8_t* __restrict__ rgb_in,
@@ -407,25 +339,22 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
                                               unsigned* __restrict__ next_count, unsigned* __restrict__ cnt_now,
                                               const int in_div, const int fix_all) {
   using I = Inv<MODE>;
+  constexpr int USH_ = USH<I::SY, I::SX>;  // chroma8_fast's scale
   double* s_mid = sh.mid;
   double (*s_cw)[I::CWR * I::CWS] = sh.cw;
   __shared__ __attribute__((aligned(16))) double s_qs[QS_WORDS];  // Q[u][v] * a_u * a_v / 8 at qs_index(u, v)
   __shared__ double s_qmax;
   __shared__ double s_red[I::NT / 64], s_dq[I::NT / 64];
   __shared__ uint32_t s_lmin[I::NT / 64], s_lmax[I::NT / 64];
-  __shared__ uint32_t s_cert[4];  // min / max fraction word, max |q|, (EX) smallest clip margin (float bits)
-  constexpr int ZW = (I::CWC + 31) / 32;  // EX: words per window row of zero-source bits
-  __shared__ uint32_t s_zb[EX ? 2 * I::CWR * ZW : 1];
-#if JDS_INV_WIN_SEL
+  __shared__ uint32_t s_cert[3];  // min / max fraction word, max |q|
   __shared__ double s_dummy[64];  // the window stores' sink for ring columns outside it
-#endif
   __shared__ unsigned long long s_sse;
   const int tid = threadIdx.x, lv = tid & 7, lb = tid >> 3;
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int Y0 = ty * I::TH, X0 = tx * I::TW;
   const int16_t* cf = coeffs + (size_t)frame * g.cpf;
   // the tile's first coefficient loads are issued before the table set-up and
-  // its barrier (JDS_INV_EARLY_LOADS), so their latency overlaps it
+  // its barrier, so their latency overlaps it
   int qhi = 0, qlo = 0;  // max / min q this lane read (max |q| = max(qhi, -qlo))
 
   // ---- 1. chroma window: (clip(IDCT) - 128) of the blocks the tile reaches --
@@ -442,36 +371,17 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     if (tid < 64) {
       const double q = fq[frame].q[tid];
       s_qs[qs_index(tid >> 3, tid & 7)] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
-#if JDS_INV_QMAX_FQ
       // max Q from the host's FrameQ::qmax (a scalar load at the end): no
       // cross-lane reduction before the barrier
       if (tid == 0) {
         s_cert[0] = 0xffffffffu;
         s_cert[1] = 0u;
         s_cert[2] = 0u;
-        s_cert[3] = 0x7f800000u;
       }
-#else
-      double m = q;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-      if (tid == 0) {
-        s_qmax = m;
-        s_cert[0] = 0xffffffffu;
-        s_cert[1] = 0u;
-        s_cert[2] = 0u;
-      }
-#endif
     }
     if (XTRA && tid == 0) s_sse = 0ull;
-    if constexpr (EX) {
-      for (int i = tid; i < 2 * I::CWR * ZW; i += I::NT) s_zb[i] = 0u;
-    }
     __syncthreads();
   };
-#if !JDS_INV_EARLY_LOADS
-  table_setup();
-#endif
   Col16 lq;
   {
     int by, bx;
@@ -483,44 +393,16 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   auto chroma_task = [&](const int p, const int i, const int by, const int bx, const Col16& cur) {
     const bool need = !I::RY || (i == 0 ? lv == 7 : (i == I::CBR - 1 ? lv == 0 : true));
     fast_col(cur, s_qs, lv, s_mid + lb * MS, qhi, qlo);
-    if constexpr (EX) {
-      // an all-zero block: the window samples this lane writes (its row, the
-      // ring column and the replicated edge columns below) are exact zeros
-      const bool zero = or8(col_nonzero(cur)) == 0;
-      if (zero && need) {
-        const int wc0 = bx * 8 - cwx0, wr = by * 8 + lv - cwy0;
-        int elo = 1 << 30, ehi = 0;  // replicated columns past the plane's right end
-        if constexpr (I::SX == 2) {
-          const int ke = g.wc - 1 - bx * 8;
-          if ((unsigned)ke < 8u) {
-            elo = wc0 + ke + 1;
-            ehi = I::CWC;
-          }
-        }
-        const int lo = (I::SX == 2 && bx == 0 && wc0 >= 1) ? wc0 - 1 : wc0;
-#pragma unroll
-        for (int w = 0; w < ZW; ++w) {
-          const uint32_t m = colbits(lo, wc0 + 8, w) | colbits(elo, ehi, w);
-          if (m) atomicOr(&s_zb[(p * I::CWR + wr) * ZW + w], m);
-        }
-      }
-    }
     if (need) {
       double c[8];
       fast_row<-128>(s_mid + lb * MS, lv, c);
       double* w = &s_cw[p][(by * 8 + lv - cwy0) * I::CWS];
       const int wc0 = bx * 8 - cwx0;
-#if JDS_INV_WIN_SEL
       // the ring blocks' columns outside the window go to a per-lane dummy
       // slot: a select per store instead of a branch per store
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         *((unsigned)(wc0 + k) < (unsigned)I::CWC ? w + wc0 + k : s_dummy + (tid & 63)) = c[k];
-#else
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if ((unsigned)(wc0 + k) < (unsigned)I::CWC) w[wc0 + k] = c[k];
-#endif
       if constexpr (I::SX == 2) {
         // cv2's clamped taps at the image's left / right edge pixels read the
         // edge column alone: replicate it into the ring (and past the
@@ -535,11 +417,11 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       }
     }
   };
-  // JDS_INV_MIX_PLANES (4:2:2): the two planes' 2 x NCB block tasks dealt over
+  // 4:2:2: the two planes' 2 x NCB block tasks dealt over
   // the workgroup's RB lane groups (one pass each, a second pass for the first
   // 2 NCB - RB groups) instead of NCB groups taking Cb then Cr while the other
   // waves wait at the barrier: the busiest SIMD runs 3 passes instead of 4
-  constexpr bool MIXP = JDS_INV_MIX_PLANES && MODE == M422 && 2 * I::NCB > I::RB && 2 * I::NCB <= 2 * I::RB;
+  constexpr bool MIXP = 1 && MODE == M422 && 2 * I::NCB > I::RB && 2 * I::NCB <= 2 * I::RB;
   if constexpr (MIXP) {
     constexpr int NTASK = 2 * I::NCB;
     auto tinfo = [&](int tt, int& pp, int& ii, int& by, int& bx, bool& ok) -> long long {
@@ -556,12 +438,8 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     bool ok;
     long long off = tinfo(lb, pp, ii, by, bx, ok);
     Col16 cq = load_col(cf + (pp ? g.off_cr : g.off_cb), off, lv, ok);
-#if JDS_INV_EARLY_LOADS
     table_setup();
-#endif
-#if JDS_INV_QMAX_FQ
     if (tid == 0) s_qmax = fq[frame].qmax;  // (used by this thread after the next barrier)
-#endif
 #pragma unroll 1
     for (int tt = lb; tt < NTASK; tt += I::RB) {  // (uniform per wave: RB lane groups, 8 per wave)
       const Col16 cur = cq;
@@ -580,14 +458,10 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     const bool cvalid = ctask && cby >= 0 && cbx >= 0 && cby < g.ncy && cbx < g.ncx;
     const long long cboff = ((long long)cby * g.ncx + cbx) * 64;
     Col16 cq = load_col(cf + g.off_cb, cboff, lv, cvalid);
-#if JDS_INV_EARLY_LOADS
     table_setup();
-#endif
-#if JDS_INV_QMAX_FQ
     if (tid == 0) s_qmax = fq[frame].qmax;  // (used by this thread after the next barrier)
-#endif
     if (ctask) {
-#pragma unroll JDS_INV_UNROLL_C
+#pragma unroll 1
       for (int p = 0; p < 2; ++p) {
         const Col16 cur = cq;
         if (p == 0) cq = load_col(cf + g.off_cr, cboff, lv, cvalid);
@@ -600,12 +474,11 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   // ---- 2. luma rounds: IDCT, upsample, colour, certify, store ----------------
   // the certificate: smallest / largest fraction word of the lane's outputs
   uint32_t lo_min = 0xffffffffu, lo_max = 0u;
-  double em = 1e300;  // EX: the smallest clip margin among the values taken as exact
   unsigned long long sse = 0ull;
   double ssy = 0.0;
   const uint8_t* in_f = XTRA ? rgb_in + (size_t)(frame / in_div) * g.H * g.W * 3 : nullptr;
   uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
-#pragma unroll JDS_INV_UNROLL_Y
+#pragma unroll 1
   for (int r = 0; r < I::NYB / I::RB; ++r) {
     int by, bx;
     const bool bvalid = luma_blk(r, by, bx);
@@ -619,22 +492,10 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       lq = load_col(cf, ((long long)by1 * g.nbx + bx1) * 64, lv, ok1);
     }
     if (bvalid) fast_col(cur, s_qs, lv, s_mid + lb * MS, qhi, qlo);
-    // EX: the luma block is all zeros (all 8 lanes of the block group take part)
-    const bool yzero = EX && or8(col_nonzero(cur)) == 0;
     const int y = by * 8 + lv, x0 = bx * 8;
     if (bvalid && y < g.H && x0 < g.W) {
       double Yv[8];
-      double ym[8];  // EX: how far beyond the clip range the fast luma lies (> 0: clipped)
-      if constexpr (EX) {
-        fast_row<-128, false>(s_mid + lb * MS, lv, Yv);  // Y - 128, unclipped
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          ym[k] = yzero ? 1e300 : fmax(-128.0 - Yv[k], Yv[k] - 127.0);
-          Yv[k] = fmin(fmax(Yv[k], -128.0), 127.0);  // (fast_row's clip)
-        }
-      } else {
-        fast_row<-128>(s_mid + lb * MS, lv, Yv);  // Y - 128
-      }
+      fast_row<-128>(s_mid + lb * MS, lv, Yv);  // Y - 128
       int wq, wt = 0;
       if constexpr (I::SY == 2) {
         // output row 2m: rows (m-1, m) weighted (1/4, 3/4); row 2m+1: (m+1, m)
@@ -648,56 +509,34 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
       uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
       const bool wide = nx == 8 && ((((uintptr_t)o) & 7u) == 0);
-      // EX: every window sample of plane p the lane's taps read (6 columns
-      // from c0, rows wq and wt) is an exact zero
-      bool zc[2] = {false, false};
-      if constexpr (EX) {
-        const int c0 = x0 / I::SX - 1 - cwx0, wi = c0 >> 5, sh = c0 & 31;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const uint32_t* zq = s_zb + (p * I::CWR + wq) * ZW + wi;
-          const uint32_t* zt = s_zb + (p * I::CWR + (I::SY == 2 ? wt : wq)) * ZW + wi;
-          const uint64_t bq = ((uint64_t)zq[1] << 32) | zq[0], bt = ((uint64_t)zt[1] << 32) | zt[0];
-          zc[p] = (((bq & bt) >> sh) & 63u) == 63u;
-        }
-      }
       uint32_t pk[6];
+      // the row's smallest / largest fraction word
+      uint32_t r_min = 0xffffffffu, r_max = 0u;
       {
-        // channel words (byte in bits 0-7) in output order R0 G0 B0 R1 ...
+        // channel high words (byte: clamp(low 16 bits)) in output order R0 G0 B0 R1 ...
         uint32_t cb[24];
         double C[8], Gt[8];
         chroma8_fast<MODE>(s_cw[0], x0, cwx0, wq, wt, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           Yv[k] = Yv[k] + (MAGIC + 128.0);  // Y on byte_cert_y's grid, shared by the three channels
-          const double B = col_b(Yv[k], C[k]);
-          Gt[k] = col_gt(Yv[k], C[k]);
-          if constexpr (EX) {
-            const bool ex = zc[0] && ym[k] > 0.0;
-            cb[3 * k + 2] = byte_cert_y(B, lo_min, lo_max, ex);
-            em = ex ? fmin(em, ym[k]) : em;
-          } else {
-            cb[3 * k + 2] = byte_cert_y(B, lo_min, lo_max);
-          }
+          const double B = col_b<MadDev, USH_>(Yv[k], C[k]);
+          Gt[k] = col_gt<MadDev, USH_>(Yv[k], C[k]);
+          cb[3 * k + 2] = cert_hi(B, r_min, r_max);
         }
         chroma8_fast<MODE>(s_cw[1], x0, cwx0, wq, wt, C);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const double R = col_r(Yv[k], C[k]);
-          const double G = col_g(Gt[k], C[k]);
-          if constexpr (EX) {
-            const bool exr = zc[1] && ym[k] > 0.0, exg = exr && zc[0];
-            cb[3 * k] = byte_cert_y(R, lo_min, lo_max, exr);
-            cb[3 * k + 1] = byte_cert_y(G, lo_min, lo_max, exg);
-            em = exr ? fmin(em, ym[k]) : em;
-          } else {
-            cb[3 * k] = byte_cert_y(R, lo_min, lo_max);
-            cb[3 * k + 1] = byte_cert_y(G, lo_min, lo_max);
-          }
+          const double R = col_r<MadDev, USH_>(Yv[k], C[k]);
+          const double G = col_g<MadDev, USH_>(Gt[k], C[k]);
+          cb[3 * k] = cert_hi(R, r_min, r_max);
+          cb[3 * k + 1] = cert_hi(G, r_min, r_max);
         }
 #pragma unroll
-        for (int w = 0; w < 6; ++w) pk[w] = pack4(cb[4 * w], cb[4 * w + 1], cb[4 * w + 2], cb[4 * w + 3]);
+        for (int w = 0; w < 6; ++w) pk[w] = pack4s(cb[4 * w], cb[4 * w + 1], cb[4 * w + 2], cb[4 * w + 3]);
       }
+      lo_min = lo_min < r_min ? lo_min : r_min;
+      lo_max = lo_max > r_max ? lo_max : r_max;
       if (wide) {
         uint2* o2 = reinterpret_cast<uint2*>(o);
         o2[0] = make_uint2(pk[0], pk[1]);
@@ -750,19 +589,7 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
 
   // ---- 3. certification: the tile's closest approach to an integer vs its bound
   int qm = max(qhi, -qlo);  // max |q| this lane read
-#if JDS_INV_CERT_DPP
-  // (EX: the margin as a float rounded down -- a smaller margin is conservative)
-  cert_to_lds<EX>(lo_min, lo_max, (uint32_t)qm, s_cert,
-                  EX ? __float_as_uint(__double2float_rd(fmin(em, 3.0e38))) : 0x7f800000u);
-#else
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t a = __shfl_xor(lo_min, o, 64), b = __shfl_xor(lo_max, o, 64);
-    lo_min = lo_min < a ? lo_min : a;
-    lo_max = lo_max > b ? lo_max : b;
-    qm = max(qm, __shfl_xor(qm, o, 64));
-  }
-#endif
+  cert_to_lds(lo_min, lo_max, (uint32_t)qm, s_cert);
   if constexpr (XTRA > 0) {
     unsigned long long s = sse;
 #pragma unroll
@@ -773,60 +600,15 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
     for (int o = 32; o > 0; o >>= 1) d = d + __shfl_xor(d, o, 64);  // (no products: nothing to fuse)
     if ((tid & 63) == 0) s_red[tid >> 6] = d;
   }
-#if !JDS_INV_CERT_DPP
-  if ((tid & 63) == 0) {
-    s_lmin[tid >> 6] = lo_min;
-    s_lmax[tid >> 6] = lo_max;
-    s_dq[tid >> 6] = (double)qm;
-  }
-#endif
   __syncthreads();
-#if JDS_INV_CERT_DPP && JDS_INV_ONE_BARRIER
-  {
-    // every thread decides from the three words (the same values for all: a
-    // uniform decision without thread 0's serial section and a second
-    // barrier; the exact fallback may overwrite the window at once, since
-    // every wave has passed the barrier above)
-    const uint32_t mn = s_cert[0], mx = s_cert[1];
-    const double q = (double)s_cert[2];
-    const double E = K_LIN * (q * s_qmax) + K_CONST + 0x1p-31;
-    const double T = ceil(E * 0x1p+32) + 1.0;
-    const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
-    const bool redo = uncertain || fix_all;
-    if (tid == 0) {
-      if (redo) {
-        atomicAdd(fixcount, 1u);  // tiles recomputed (jds_plan_fix_counts)
-        atomicAdd(cnt_now + frame, 1u);
-      } else if constexpr (XTRA > 0) {
-        double a = 0.0;
-        for (int i = 0; i < I::NT / 64; ++i) a = a + s_red[i];
-        sse_y_part[(size_t)frame * gridDim.x + tile] = a;
-        atomicAdd((unsigned long long*)&st[frame].sse_rgb, s_sse);
-      }
-      if (frame == 0 && tile == 0) *next_count = 0u;  // the next run counts from zero
-    }
-    return redo;
-  }
-#else
   if (tid == 0) {
-#if JDS_INV_CERT_DPP
     const uint32_t mn = s_cert[0], mx = s_cert[1];
     const double q = (double)s_cert[2];
-#else
-    uint32_t mn = 0xffffffffu, mx = 0u;
-    double q = 0.0;
-    for (int i = 0; i < I::NT / 64; ++i) {
-      mn = mn < s_lmin[i] ? mn : s_lmin[i];
-      mx = mx > s_lmax[i] ? mx : s_lmax[i];
-      q = fmax(q, s_dq[i]);
-    }
-#endif
     // |v_fast - v_ref| <= E, plus <= 3 roundings on the magic grid (2^-33 each:
     // byte_cert); T in units of 2^-32
     const double E = K_LIN * (q * s_qmax) + K_CONST + 0x1p-31;
     const double T = ceil(E * 0x1p+32) + 1.0;
-    const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T ||
-                           (EX && (double)__uint_as_float(s_cert[3]) <= E);
+    const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
     sh.redo = uncertain || fix_all;
     if (sh.redo) {
       atomicAdd(fixcount, 1u);  // tiles recomputed (jds_plan_fix_counts)
@@ -841,14 +623,12 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
   }
   __syncthreads();  // sh.redo is visible to the caller's uniform branch
   return sh.redo != 0;
-#endif
 }
 
 // XTRA: 0 = RGB only; 1 = + exact integer SSE and luma SSE partials (sweeps),
 // committed by the fast pass only for certified tiles (the exact tile code
-// commits the others).  EX: exact values leave the certificate (coarse tables;
-// inv_fast_tile).
-template <int MODE, int XTRA, bool EX = false>
+// commits the others).
+template <int MODE, int XTRA>
 __global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(Inv<MODE>::WPE)))
 k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
            const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
@@ -883,7 +663,7 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
     }
   } else {
     sh.redo = 0;
-    redo = inv_fast_tile<MODE, XTRA, EX>(sh, g, tiles_x, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part,
+    redo = inv_fast_tile<MODE, XTRA>(sh, g, tiles_x, frame, tile, coeffs, fq, rgb_in, rgb_out, st, sse_y_part,
                                          fixcount, next_count, cnt_now, in_div, fix_all);
   }
   // one call site of the exact tile code: items in exact mode, uncertain tiles
@@ -943,20 +723,9 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
     const double q = fq[frame].q[tid];
     s_qs[qs_index(tid >> 3, tid & 7)] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
     s_qi[tid] = (int)q;
-#if JDS_INV_QMAX_FQ
-#else
-    double m = q;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-    if (tid == 0) s_qmax = m;
-#endif
   }
   __syncthreads();
-#if JDS_INV_QMAX_FQ
   const double qmax = fq[frame].qmax;
-#else
-  const double qmax = s_qmax;
-#endif
   const int y = by * 8 + lv, x0 = bx * 8;
   const bool row_ok = bvalid && y < g.H;
   const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
@@ -1009,16 +778,11 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
   }
   // the block's Dmax over its three planes (its 8 lanes), then this lane's margin
   int qm = max(qhi, -qlo);
-#if JDS_INV_CERT_DPP
   // over the block's 8 lanes by DPP: quad_perm xor 1, xor 2, then row_half_mirror
   // (lane i of 8 with lane 7 - i, in the other quad)
   qm = max(qm, __builtin_amdgcn_update_dpp(0, qm, 0xb1, 0xf, 0xf, true));
   qm = max(qm, __builtin_amdgcn_update_dpp(0, qm, 0x4e, 0xf, 0xf, true));
   qm = max(qm, __builtin_amdgcn_update_dpp(0, qm, 0x141, 0xf, 0xf, true));
-#else
-#pragma unroll
-  for (int m = 1; m < 8; m <<= 1) qm = max(qm, __shfl_xor(qm, m, 64));
-#endif
   const double E = K_LIN * ((double)qm * qmax) + K_CONST + 0x1p-31;
   const double T = ceil(E * 0x1p+32) + 1.0;
   const bool unc = row_ok && ((double)lo_min <= T || (double)lo_max >= 0x1p+32 - 1.0 - T);
@@ -1149,8 +913,8 @@ __device__ __forceinline__ uint32_t byte_cert_m(double y, bool ok, uint32_t& lo_
 // (plan runs without SSE terms; BASELINE configs[4]).  k_inv16s's tile, window
 // and exchange layout (jds_inv16_exact.hpp: one chroma window at a time in
 // LDS, Cb then Cr), with k_inv_fast's arithmetic: the folded dequantisation
-// table, fidct16 lines, both planes clipped to [-128, 127], the difference
-// form upsample (fvblend / fhblend), the colour terms on the magic grid and
+// table, fidct16 lines, both planes clipped to [-128, 127], the unnormalised
+// upsample (fvsum / fhsum), the colour terms on the magic grid and
 // byte_cert_y's certificate, E = K_LIN16 * Dmax + K_CONST16 + 2^-31
 // (tools/inv_bound.py --b16; tests/test_inv_bound_cpu.py runs this chain on
 // the host against the oracle).  A tile with an uncertain value is recomputed
@@ -1168,7 +932,7 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
   __shared__ double s_qmax;
   __shared__ double s_dq[I::NT / 64];
   __shared__ uint32_t s_lmin[I::NT / 64], s_lmax[I::NT / 64];
-  __shared__ uint32_t s_cert[3];  // JDS_INV_CERT_DPP: min / max fraction word, max |q|
+  __shared__ uint32_t s_cert[3];  // min / max fraction word, max |q|
   __shared__ int s_redo;
   const int tid = threadIdx.x, grp = tid >> 4, line = tid & 15;
   const int frame = blockIdx.y, tile = blockIdx.x;
@@ -1181,12 +945,7 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
   if (tid < 64) {
     double m = fq[frame].q[tid];
     s_qi[tid] = (int)m;
-#if JDS_INV_QMAX_FQ
     m = fq[frame].qmax;
-#else
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-#endif
     if (tid == 0) {
       s_qmax = m;
       s_cert[0] = 0xffffffffu;
@@ -1240,26 +999,24 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
       }
     }
   };
-  // one plane's upsampled (C - 128) at pixels x0 .. x0 + 7 of row (wq, wt)
-  // (chroma8_fast's blends; cv2's clamped taps at the image's edge pixels
-  // take the edge sample, as in k_inv16s)
+  // one plane's upsampled (C - 128) at pixels x0 .. x0 + 7 of row (wq, wt),
+  // times 2^USH_ (chroma8_fast's sums; cv2's clamped taps at the image's edge
+  // pixels take the edge sample, as in k_inv16s: its vertical sum times 4)
+  constexpr int USH_ = USH<I::SY, 2>;
   auto upsample = [&](int x0, int wq, int wt, double (&C)[8]) {
     const int c0 = x0 / 2 - 1 - cwx0;
     double vb[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       if constexpr (I::SY == 2)
-        vb[j] = fvblend(s_cw[wq * I::CWC + c0 + j], s_cw[wt * I::CWC + c0 + j]);
+        vb[j] = fvsum(s_cw[wq * I::CWC + c0 + j], s_cw[wt * I::CWC + c0 + j]);
       else
         vb[j] = s_cw[wq * I::CWC + c0 + j];
     }
-    double d[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) d[j] = vb[j] - vb[j + 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      C[2 * i] = fhblend(d[i], 0.25, vb[i + 1]);
-      C[2 * i + 1] = fhblend(d[i + 1], -0.25, vb[i + 1]);
+      C[2 * i] = fhsum(vb[i], vb[i + 1]);
+      C[2 * i + 1] = fhsum(vb[i + 2], vb[i + 1]);
     }
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
@@ -1267,7 +1024,8 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
       if (kl >= 0) {
         const int e = (side == 0 ? 0 : g.wc - 1) - cwx0;
         double v = s_cw[wq * I::CWC + e];
-        if constexpr (I::SY == 2) v = fvblend(v, s_cw[wt * I::CWC + e]);
+        if constexpr (I::SY == 2) v = fvsum(v, s_cw[wt * I::CWC + e]);
+        v *= 4.0;  // (exact)
 #pragma unroll
         for (int k = 0; k < 8; ++k) C[k] = k == kl ? v : C[k];
       }
@@ -1309,8 +1067,8 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
         for (int k = 0; k < 8; ++k) {
           const double yv = Yv[8 * h + k] + (MAGIC + 128.0);
           Yv[8 * h + k] = yv;
-          cb[k] = byte_cert_m(col_b(yv, C[k]), x0 + k < g.W, lo_min, lo_max);
-          Gt[8 * h + k] = col_gt(yv, C[k]);
+          cb[k] = byte_cert_m(col_b<MadDev, USH_>(yv, C[k]), x0 + k < g.W, lo_min, lo_max);
+          Gt[8 * h + k] = col_gt<MadDev, USH_>(yv, C[k]);
         }
         bpk[2 * h] = pack4(cb[0], cb[1], cb[2], cb[3]);
         bpk[2 * h + 1] = pack4(cb[4], cb[5], cb[6], cb[7]);
@@ -1334,8 +1092,8 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const bool ok = k < nx;
-          ch[3 * k] = byte_cert_m(col_r(Yv[8 * h + k], C[k]), ok, lo_min, lo_max);
-          ch[3 * k + 1] = byte_cert_m(col_g(Gt[8 * h + k], C[k]), ok, lo_min, lo_max);
+          ch[3 * k] = byte_cert_m(col_r<MadDev, USH_>(Yv[8 * h + k], C[k]), ok, lo_min, lo_max);
+          ch[3 * k + 1] = byte_cert_m(col_g<MadDev, USH_>(Gt[8 * h + k], C[k]), ok, lo_min, lo_max);
           ch[3 * k + 2] = (bpk[2 * h + (k >> 2)] >> (8 * (k & 3))) & 255u;
         }
         uint32_t pk[6];
@@ -1358,36 +1116,11 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
 
   // ---- 3. certification: the tile's closest approach to an integer vs its bound
   int qm = max(qhi, -qlo);
-#if JDS_INV_CERT_DPP
   cert_to_lds(lo_min, lo_max, (uint32_t)qm, s_cert);
-#else
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t a = __shfl_xor(lo_min, o, 64), b = __shfl_xor(lo_max, o, 64);
-    lo_min = lo_min < a ? lo_min : a;
-    lo_max = lo_max > b ? lo_max : b;
-    qm = max(qm, __shfl_xor(qm, o, 64));
-  }
-  if ((tid & 63) == 0) {
-    s_lmin[tid >> 6] = lo_min;
-    s_lmax[tid >> 6] = lo_max;
-    s_dq[tid >> 6] = (double)qm;
-  }
-#endif
   __syncthreads();
   if (tid == 0) {
-#if JDS_INV_CERT_DPP
     const uint32_t mn = s_cert[0], mx = s_cert[1];
     const double q = (double)s_cert[2];
-#else
-    uint32_t mn = 0xffffffffu, mx = 0u;
-    double q = 0.0;
-    for (int i = 0; i < I::NT / 64; ++i) {
-      mn = mn < s_lmin[i] ? mn : s_lmin[i];
-      mx = mx > s_lmax[i] ? mx : s_lmax[i];
-      q = fmax(q, s_dq[i]);
-    }
-#endif
     const double E = K_LIN16 * (q * s_qmax) + K_CONST16 + 0x1p-31;
     const double T = ceil(E * 0x1p+32) + 1.0;
     const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
@@ -1431,13 +1164,9 @@ static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const F
   unsigned* cnt = fx.count + fx.parity;
   unsigned* nxt = fx.count + (fx.parity ^ 1);
   (void)rgb_in;  // SSE runs take the exact kernel (launch_codec)
-  if (fx.ex)
-    hipLaunchKernelGGL((k_inv_fast<MODE, 0, true>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part,
-                       cnt, nxt, fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
-  else
-    hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, cnt,
-                       nxt, fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
-  kmark(s, "k_inv_fast<%d,0%s>", MODE, fx.ex ? ",ex" : "");
+  hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, cnt, nxt,
+                     fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
+  kmark(s, "k_inv_fast<%d,0>", MODE);
   return hipGetLastError();
 }
 
@@ -1466,9 +1195,9 @@ hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs,
 //
 // k_inv_fast's (BS = 8) and k_inv16_fast's (BS = 16) arithmetic evaluated on
 // the host for a whole image, with the kernels' own helpers (aan8 / fidct16,
-// fvblend, fhblend, col_*): dequantisation with the folded table, the IDCT
-// along axis 0 then axis 1, clip to [-128, 127], the vertical then
-// difference-form horizontal chroma blends with cv2's clamped taps (the
+// fvsum, fhsum, col_*): dequantisation with the folded table, the IDCT
+// along axis 0 then axis 1, clip to [-128, 127], the unnormalised vertical
+// then horizontal chroma sums with cv2's clamped taps (the
 // kernels' replicated window ring or edge selects give the same operands), the
 // colour terms on the magic grid and byte_cert_y's byte.  fuse = 0: every
 // multiply-add rounded twice (MadDev on x86-64); 1: every one fused (MadFma).
@@ -1537,16 +1266,25 @@ static void inv_fast_host_t(int mode, const int16_t* cf, const double* Q, int H,
         auto vb = [&](int col) {
           if (sy == 2) {
             const int m = y >> 1, rq = (y & 1) ? m + 1 : m - 1;
-            return fvblend<M>(S(p, rq, col), S(p, m, col));
+            return fvsum<M>(S(p, rq, col), S(p, m, col));
           }
           return S(p, y, col);
         };
         const int m = x >> 1;
-        C[p] = (x & 1) == 0 ? fhblend<M>(vb(m - 1) - vb(m), 0.25, vb(m)) : fhblend<M>(vb(m) - vb(m + 1), -0.25, vb(m));
+        C[p] = (x & 1) == 0 ? fhsum<M>(vb(m - 1), vb(m)) : fhsum<M>(vb(m + 1), vb(m));
       }
       const double Yv = S(0, y, x) + (MAGIC + 128.0);
-      const double B = col_b<M>(Yv, C[1]), Gt = col_gt<M>(Yv, C[1]);
-      const double R = col_r<M>(Yv, C[2]), G = col_g<M>(Gt, C[2]);
+      double B, Gt, R, G;
+      if (sx == 1) {
+        B = col_b<M>(Yv, C[1]), Gt = col_gt<M>(Yv, C[1]);
+        R = col_r<M>(Yv, C[2]), G = col_g<M>(Gt, C[2]);
+      } else if (sy == 1) {
+        B = col_b<M, 2>(Yv, C[1]), Gt = col_gt<M, 2>(Yv, C[1]);
+        R = col_r<M, 2>(Yv, C[2]), G = col_g<M, 2>(Gt, C[2]);
+      } else {
+        B = col_b<M, 4>(Yv, C[1]), Gt = col_gt<M, 4>(Yv, C[1]);
+        R = col_r<M, 4>(Yv, C[2]), G = col_g<M, 4>(Gt, C[2]);
+      }
       const double o[3] = {R, G, B};
       for (int ch = 0; ch < 3; ++ch) {
         uint64_t bits;

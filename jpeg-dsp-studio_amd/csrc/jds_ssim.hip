@@ -1,16 +1,9 @@
-// jds_ssim.hip — K4: PSNR / SSIM of two uint8 RGB images on the GPU,
-// reproducing utils/metrics.py:9-28 (skimage.metrics + scipy.ndimage + NumPy)
-// bit for bit:
-//   * scipy.ndimage.uniform_filter(size=7, mode='reflect') = uniform_filter1d
-//     along axis 0 then axis 1; each line is a running sum of the raw values
-//     (s += new - old) divided by 7 at every output (scipy NI_UniformFilter1D);
-//   * skimage structural_similarity: sample covariance (49/48), K1=.01, K2=.03,
-//     data_range=255, mean over the 3-px-cropped map;
-//   * numpy mean over n elements: the C-order element stream is cut into
-//     8192-element buffers, each buffer is summed by NumPy's pairwise_sum
-//     (8 accumulators on leaves of <= 128), buffer sums accumulate left to
-//     right from 0.0, then / n.
-// The luma PSNR uses the same NumPy mean on (Y(orig) - Y(rec))^2.
+// jds_ssim.hip — the statistics kernels beside the SSIM pipeline
+// (jds_ssim_band.hip): the integer RGB squared-error sum behind PSNR-RGB
+// (utils/metrics.py:11) and the float32 magnitude-bits reduction
+// (utils/metrics.py:77-78).  (Rounds 1-4 also held the first SSIM kernels here,
+// one scipy line per lane; the batched pipeline replaced them and the tests
+// compare it with the oracle directly.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -19,251 +12,6 @@
 #pragma clang fp contract(off)
 
 namespace jds {
-
-constexpr int NP_BUF = 8192;   // NumPy ufunc buffer size (elements)
-constexpr int PW_BLOCK = 128;  // NumPy PW_BLOCKSIZE
-
-struct SsimConsts {
-  double c1, c2, cov_norm;
-};
-
-__device__ __forceinline__ int refl_sym(int i, int n) {  // scipy 'reflect' (edge repeated)
-  const int p = 2 * n;
-  i %= p;
-  if (i < 0) i += p;
-  return i >= n ? p - 1 - i : i;
-}
-
-__device__ __forceinline__ double chan_val(const uint8_t* img, size_t px, int c) {
-  if (c < 3) return (double)img[px * 3 + c];
-  const double R = img[px * 3], G = img[px * 3 + 1], B = img[px * 3 + 2];
-  return 0.299 * R + 0.587 * G + 0.114 * B;  // utils/metrics.py:17-18
-}
-
-// pass along axis 0 (columns): one running sum per thread -- column j,
-// quantity q (x, y, xx, yy, xy) and channel c from the grid -- so the four
-// channels' 5 quantities run in parallel (scipy NI_UniformFilter1D per line).
-// out: [c][q][H][W].  The loads of the next rows are issued ahead of the
-// recurrence (they do not depend on it).
-__device__ __forceinline__ double uf_term(const uint8_t* a, const uint8_t* b, size_t px, int c, int q) {
-  const double x = (q == 1 || q == 3) ? 0.0 : chan_val(a, px, c);
-  const double y = (q == 0 || q == 2) ? 0.0 : chan_val(b, px, c);
-  return q == 0 ? x : q == 1 ? y : q == 2 ? x * x : q == 3 ? y * y : x * y;
-}
-
-__global__ void __launch_bounds__(64) k_uf_axis0(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int H,
-                                                 int W, double* __restrict__ out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  const int q = blockIdx.y, c = blockIdx.z;
-  if (j >= W) return;
-  const size_t plane = (size_t)H * W;
-  double* o = out + ((size_t)c * 5 + q) * plane;
-  double s = 0.0;
-  for (int k = -3; k <= 3; ++k) s = s + uf_term(a, b, (size_t)refl_sym(k, H) * W + j, c, q);
-  o[j] = s / 7.0;
-  constexpr int U = 8;
-  int i = 1;
-  for (; i + U <= H; i += U) {
-    double d[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int ii = i + u;
-      // (xn - xo) etc.: scipy adds the difference of the new and old terms
-      const size_t pn = (size_t)refl_sym(ii + 3, H) * W + j, po = (size_t)refl_sym(ii - 4, H) * W + j;
-      d[u] = uf_term(a, b, pn, c, q) - uf_term(a, b, po, c, q);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      s = s + d[u];
-      o[(size_t)(i + u) * W + j] = s / 7.0;
-    }
-  }
-  for (; i < H; ++i) {
-    const size_t pn = (size_t)refl_sym(i + 3, H) * W + j, po = (size_t)refl_sym(i - 4, H) * W + j;
-    s = s + (uf_term(a, b, pn, c, q) - uf_term(a, b, po, c, q));
-    o[(size_t)i * W + j] = s / 7.0;
-  }
-}
-
-// pass along axis 1 (rows) over the 5 planes of channel blockIdx.y, then the
-// SSIM map on the cropped region (smap: [c][H-6][W-6])
-__global__ void __launch_bounds__(64) k_uf_axis1_ssim(const double* __restrict__ in, int H, int W, SsimConsts k,
-                                                      double* __restrict__ smap) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c = blockIdx.y;
-  if (i >= H) return;
-  const size_t plane = (size_t)H * W;
-  const int cw = W - 6;
-  smap += (size_t)c * (H - 6) * cw;
-  const double* r[5];
-  for (int q = 0; q < 5; ++q) r[q] = in + ((size_t)c * 5 + q) * plane + (size_t)i * W;
-  double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int t = -3; t <= 3; ++t) {
-    const int jj = refl_sym(t, W);
-    for (int q = 0; q < 5; ++q) s[q] = s[q] + r[q][jj];
-  }
-  const bool row_in = i >= 3 && i < H - 3;
-  auto emit = [&](int j) {
-    if (row_in && j >= 3 && j < W - 3) {
-      const double ux = s[0] / 7.0, uy = s[1] / 7.0, uxx = s[2] / 7.0, uyy = s[3] / 7.0, uxy = s[4] / 7.0;
-      // skimage structural_similarity (sample covariance)
-      const double vx = k.cov_norm * (uxx - ux * ux);
-      const double vy = k.cov_norm * (uyy - uy * uy);
-      const double vxy = k.cov_norm * (uxy - ux * uy);
-      const double a1 = 2 * ux * uy + k.c1, a2 = 2 * vxy + k.c2;
-      const double b1 = ux * ux + uy * uy + k.c1, b2 = vx + vy + k.c2;
-      const double d = b1 * b2;
-      smap[(size_t)(i - 3) * cw + (j - 3)] = (a1 * a2) / d;
-    }
-  };
-  emit(0);
-  constexpr int U = 4;
-  int j = 1;
-  for (; j + U <= W; j += U) {
-    double dn[U][5];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int jn = refl_sym(j + u + 3, W), jo = refl_sym(j + u - 4, W);
-#pragma unroll
-      for (int q = 0; q < 5; ++q) dn[u][q] = r[q][jn] - r[q][jo];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int q = 0; q < 5; ++q) s[q] = s[q] + dn[u][q];
-      emit(j + u);
-    }
-  }
-  for (; j < W; ++j) {
-    const int jn = refl_sym(j + 3, W), jo = refl_sym(j - 4, W);
-    for (int q = 0; q < 5; ++q) s[q] = s[q] + (r[q][jn] - r[q][jo]);
-    emit(j);
-  }
-}
-
-// ---- NumPy pairwise_sum over a <= 8192-element buffer, one workgroup ----
-
-struct LeafRange {
-  int off, n;
-};
-
-// in-order leaves of NumPy's pairwise recursion (leaf: n <= PW_BLOCK)
-__device__ int pw_leaves(int n, LeafRange* out) {
-  int so[24], sn[24], sp = 0, cnt = 0;
-  so[0] = 0; sn[0] = n; sp = 1;
-  while (sp > 0) {
-    --sp;
-    const int off = so[sp], m = sn[sp];
-    if (m <= PW_BLOCK) {
-      out[cnt++] = {off, m};
-    } else {
-      int m2 = m / 2;
-      m2 -= m2 % 8;
-      so[sp] = off + m2; sn[sp] = m - m2; ++sp;  // right, popped second
-      so[sp] = off;      sn[sp] = m2;     ++sp;  // left, popped first
-    }
-  }
-  return cnt;
-}
-
-template <typename Get>
-__device__ double pw_leaf_sum(Get get, int off, int n) {
-  if (n < 8) {
-    double r = 0.0;
-    for (int i = 0; i < n; ++i) r = r + get(off + i);
-    return r;
-  }
-  double r[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) r[k] = get(off + k);
-  int i = 8;
-  for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r[k] = r[k] + get(off + i + k);
-  }
-  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; ++i) res = res + get(off + i);
-  return res;
-}
-
-// combine leaf sums following the same recursion (post-order)
-__device__ double pw_combine(int n, const double* ls) {
-  int fn[24], fph[24];
-  double fl[24];
-  int sp = 0, li = 0;
-  double res = 0.0;
-  bool ret = false;
-  fn[0] = n; fph[0] = 0; sp = 1;
-  while (sp > 0) {
-    const int t = sp - 1;
-    if (ret) {
-      ret = false;
-      if (fph[t] == 1) {
-        fl[t] = res;
-        fph[t] = 2;
-        int m2 = fn[t] / 2;
-        m2 -= m2 % 8;
-        fn[sp] = fn[t] - m2; fph[sp] = 0; ++sp;
-      } else {
-        res = fl[t] + res;
-        --sp;
-        ret = true;
-      }
-      continue;
-    }
-    if (fn[t] <= PW_BLOCK) {
-      res = ls[li++];
-      --sp;
-      ret = true;
-      continue;
-    }
-    int m2 = fn[t] / 2;
-    m2 -= m2 % 8;
-    fph[t] = 1;
-    fn[sp] = m2; fph[sp] = 0; ++sp;
-  }
-  return res;
-}
-
-template <typename Get>
-__device__ void np_chunk_sum(Get get, long long n, double* chunk_out) {
-  __shared__ LeafRange s_leaf[NP_BUF / 64 + 2];
-  __shared__ double s_ls[NP_BUF / 64 + 2];
-  __shared__ int s_cnt;
-  const long long c0 = (long long)blockIdx.x * NP_BUF;
-  const int m = (int)((n - c0) < NP_BUF ? (n - c0) : NP_BUF);
-  if (threadIdx.x == 0) s_cnt = pw_leaves(m, s_leaf);
-  __syncthreads();
-  for (int l = threadIdx.x; l < s_cnt; l += blockDim.x) {
-    const LeafRange lr = s_leaf[l];
-    s_ls[l] = pw_leaf_sum([&](int i) { return get(c0 + i); }, lr.off, lr.n);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) chunk_out[blockIdx.x] = pw_combine(m, s_ls);
-}
-
-__global__ void k_chunks_smap(const double* __restrict__ smap, long long n, double* __restrict__ chunk_out,
-                              int nch) {
-  const double* m = smap + (size_t)blockIdx.y * n;  // channel blockIdx.y
-  np_chunk_sum([&](long long i) { return m[i]; }, n, chunk_out + (size_t)blockIdx.y * nch);
-}
-
-__global__ void k_chunks_ydiff(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, long long n,
-                               double* __restrict__ chunk_out) {
-  np_chunk_sum(
-      [&](long long i) {
-        const double d = chan_val(a, (size_t)i, 3) - chan_val(b, (size_t)i, 3);
-        return d * d;  // (image0 - image1) ** 2
-      },
-      n, chunk_out);
-}
-
-__global__ void k_chunks_final(const double* __restrict__ chunks, int nchunks, long long n, double* out) {
-  if (threadIdx.x != 0) return;
-  double acc = 0.0;
-  for (int k = 0; k < nchunks; ++k) acc = acc + chunks[k];
-  *out = acc / (double)n;
-}
 
 __global__ void k_sse_u8(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, long long n,
                          unsigned long long* out) {
@@ -405,28 +153,6 @@ hipError_t launch_mag_f32(const int16_t* coeffs, long long nblocks, unsigned* sc
   hipLaunchKernelGGL(k_mag_chunks, dim3(nwg), dim3(MAG_WG), 0, s, coeffs, nblocks, local_rank, wg_tot, chunk_sum,
                      max_chunks);
   hipLaunchKernelGGL(k_mag_final, dim3(1), dim3(64), 0, s, chunk_sum, wg_tot, nwg, wg_last, max_chunks, out);
-  return hipGetLastError();
-}
-
-// ssim_out[0..3] = SSIM of R, G, B, Y; ssim_out[4] = MSE of Y (for PSNR-Y)
-hipError_t launch_psnr_ssim(const uint8_t* a, const uint8_t* b, int H, int W, double c1, double c2,
-                            double* scratch_planes /*4*5*H*W*/, double* scratch_smap /*4*(H-6)*(W-6)*/,
-                            double* scratch_chunks /*>= 4*ceil(H*W/8192)*/, double* out /*5 doubles*/,
-                            hipStream_t s) {
-  SsimConsts k{c1, c2, 49.0 / 48.0};
-  const long long ns = (long long)(H - 6) * (W - 6);
-  const int nch_s = (int)((ns + NP_BUF - 1) / NP_BUF);
-  // all four channels at once: planes [c][q][H][W], maps [c][H-6][W-6]
-  hipLaunchKernelGGL(k_uf_axis0, dim3((W + 63) / 64, 5, 4), dim3(64), 0, s, a, b, H, W, scratch_planes);
-  hipLaunchKernelGGL(k_uf_axis1_ssim, dim3((H + 63) / 64, 4), dim3(64), 0, s, scratch_planes, H, W, k, scratch_smap);
-  hipLaunchKernelGGL(k_chunks_smap, dim3(nch_s, 4), dim3(128), 0, s, scratch_smap, ns, scratch_chunks, nch_s);
-  for (int c = 0; c < 4; ++c)
-    hipLaunchKernelGGL(k_chunks_final, dim3(1), dim3(64), 0, s, scratch_chunks + (size_t)c * nch_s, nch_s, ns,
-                       out + c);
-  const long long np_ = (long long)H * W;
-  const int nch_y = (int)((np_ + NP_BUF - 1) / NP_BUF);
-  hipLaunchKernelGGL(k_chunks_ydiff, dim3(nch_y), dim3(128), 0, s, a, b, np_, scratch_chunks);
-  hipLaunchKernelGGL(k_chunks_final, dim3(1), dim3(64), 0, s, scratch_chunks, nch_y, np_, out + 4);
   return hipGetLastError();
 }
 

@@ -2,8 +2,8 @@
 // bit-identical to utils/metrics.py:9-28 (skimage.metrics.structural_similarity
 // over scipy.ndimage.uniform_filter + NumPy means), laid out for the chip.
 //
-// The arithmetic contract is the one jds_ssim.hip's first kernels restate
-// (kept there as the legacy path the tests compare against):
+// The arithmetic contract (oracle/cpu_ref.py psnr_ssim_raw restates it; the
+// tests compare all six values bit for bit):
 //   * uniform_filter(size 7, mode 'reflect') = uniform_filter1d along axis 0,
 //     then along axis 1; per line a running sum s += (new - old) from
 //     s = sum of the reflected first window (left to right from 0.0), every
@@ -40,11 +40,11 @@
 //                 pairwise tree (a perfect binary tree over 64 leaves of 128
 //                 for a full buffer) is a shuffle butterfly -- fp64 addition
 //                 is commutative, only the association is fixed; the last,
-//                 partial buffer follows NumPy's recursion (np_chunk_sum);
+//                 partial buffer follows NumPy's recursion;
 //   k_ss_final    buffer sums left to right, / n.
 // Divisions by 7 use a quotient refined once by FMA (div7): correctly rounded
-// for every finite operand (pinned by tests against the
-// IEEE division of the legacy kernels).
+// for every finite operand (pinned by the tests against
+// the oracle's IEEE division).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -101,7 +101,6 @@ _SIGS = {
     'jds_magnitude_bits_f32_dev': (C.c_int, [_P, _P, C.c_int64, _P, _P]),
     'jds_magnitude_bits_f32_batch_dev': (C.c_int, [_P, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P]),
     'jds_psnr_ssim_batch_dev': (C.c_int, [_P, C.c_int32, _P, _P, C.c_int64, C.c_int64, _P, _P]),
-    'jds_selftest_psnr_ssim_legacy_dev': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, _P]),
     'jds_stage_rgb_to_ycbcr': (C.c_int, [_P, _P, _P, C.c_int64]),
     'jds_stage_ycbcr_to_rgb': (C.c_int, [_P, _P, _P, C.c_int64]),
     'jds_stage_subsample': (C.c_int, [_P, _P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P]),

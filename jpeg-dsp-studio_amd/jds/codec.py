@@ -123,15 +123,6 @@ def psnr_ssim_batch_dev(a_ptrs, b_ptrs, H: int, W: int, device: int = 0, after=N
     return out
 
 
-def psnr_ssim_legacy_dev(a_ptr: int, b_ptr: int, H: int, W: int, device: int = 0) -> np.ndarray:
-    """Test-only: psnr_ssim_dev through the round-1..3 kernels (jds_selftest_psnr_ssim_legacy_dev)."""
-    out = np.empty(6, np.float64)
-    with lease(device) as ctx:
-        check(lib().jds_selftest_psnr_ssim_legacy_dev(ctx.handle, int(a_ptr), int(b_ptr), int(H), int(W),
-                                                      out.ctypes.data))
-    return out
-
-
 def magnitude_bits_f32_dev(coeffs_ptr: int, n_coeffs: int, device: int = 0, after=None) -> float:
     """jds_magnitude_bits_f32_dev: NumPy's float32 np.sum of magnitude_bits
     (utils/metrics.py:77-78) over n_coeffs device-resident int16 coefficients."""

@@ -8,9 +8,9 @@ through the exact kernel (k_inv2_list).  Bar: bit-identical bytes, SSE and
 luma SSE with the default (fast), JDS_RUN_EXACT_INV (exact) and
 JDS_RUN_INV_FIXALL (fast, then every tile recomputed by the exact tile code).
 Plans take the wave-local k_inv_fast444 at 4:4:4 and, for 4:2:x plans with a
-coarse table, the variant that takes values exact in both orders out of the
-certificate (k_inv_fast<.., EX>); JDS_RUN_INV_FAST asks for the plain
-certificate there.  Both are checked against the exact kernel."""
+coarse table, the exact k_inv2 (most tiles of such frames would fall back);
+JDS_RUN_INV_FAST asks for the certified kernel there.  Both are checked
+against the exact kernel."""
 import numpy as np
 import pytest
 
@@ -146,12 +146,12 @@ def test_fast_inverse_arbitrary_int16_coefficients(scale):
         _same(fast, exact)
 
 
-@pytest.mark.parametrize('mode,q,fast', [('4:2:0', 50, True), ('4:2:2', 20, True), ('4:2:0', 10, True),
+@pytest.mark.parametrize('mode,q,fast', [('4:2:0', 50, True), ('4:2:2', 20, True), ('4:2:0', 10, False),
                                          ('4:4:4', 50, True), ('4:4:4', 10, True)])
 def test_default_inverse_route(mode, q, fast):
-    """The plan's own choice (the certified fast inverse everywhere: the
-    wave-local k_inv_fast444 at 4:4:4, the exact-value variant for coarse 4:2:x
-    tables) gives the exact kernel's bytes; the fix-up counter shows which
+    """The plan's own choice (the certified fast inverse, the wave-local
+    k_inv_fast444 at 4:4:4, k_inv2 for coarse 4:2:x tables) gives the exact
+    kernel's bytes; the fix-up counter shows which
     kernel ran (k_inv2 reports none, the fast kernels list the checkerboard's
     ties)."""
     from jds import _abi
@@ -180,16 +180,17 @@ def _coarse_frames(h, w, seed):
 
 @pytest.mark.parametrize('mode', ['4:2:0', '4:2:2'])
 @pytest.mark.parametrize('h,w', [(256, 384), (136, 200), (1080, 1920)])
-def test_coarse_tables_exact_value_tracking(mode, h, w):
-    """Coarse tables: the default route (k_inv_fast<.., EX>)
-    == the plain certificate (RUN_INV_FAST) == k_inv2 == EX with every tile
-    recomputed == the oracle, on random and saturated frames at Q 1 .. 13; and
-    on random frames the exact-value variant recomputes fewer tiles."""
+def test_coarse_tables(mode, h, w):
+    """Coarse tables: the default route (k_inv2) == the certified kernel
+    (RUN_INV_FAST) == k_inv2 asked for == the certified kernel with every tile
+    recomputed == the oracle, on random and saturated frames at Q 1 .. 13; on
+    random Q10 frames the certified kernel hands tiles to its fallback and the
+    default route reports none."""
     from jds import _abi
     qs = [1, 5, 10, 13, 10, 5] if h * w < 1e6 else [10, 5]
     fr = _coarse_frames(h, w, 40)
     frames = np.stack([fr[i % 3] for i in range(len(qs))])
-    ex, = _plan(frames, qs, mode, False, [0])              # a fresh plan: no adaptive state yet
+    ex, = _plan(frames, qs, mode, False, [0])
     plain, = _plan(frames, qs, mode, False, [_abi.RUN_INV_FAST])
     exact, fixall = _plan(frames, qs, mode, False, [_abi.RUN_EXACT_INV, _abi.RUN_INV_FIXALL])
     _same(ex, exact)
@@ -203,4 +204,5 @@ def test_coarse_tables_exact_value_tracking(mode, h, w):
     ex2, = _plan(rnd, [10, 10], mode, False, [0])
     plain2, = _plan(rnd, [10, 10], mode, False, [_abi.RUN_INV_FAST])
     _same(ex2, plain2)
-    assert ex2[3][1] < plain2[3][1] or plain2[3][1] == 0, (ex2[3], plain2[3])
+    assert ex2[3][1] == 0, ex2[3]
+    assert plain2[3][1] > 0 or h * w < 1e5, plain2[3]  # (a small frame may certify every tile)

@@ -62,19 +62,17 @@ def _golden_check(name, flags_list):
 
 
 def test_cfg3_4k_q10_420_plan_matches_reference_golden():
-    """configs[2]: the plan's default kernels (at this coarse table the fast
-    inverse's exact-value variant, k_inv_fast<2,0,EX>), that variant with every
-    tile recomputed, the plain certificate (RUN_INV_FAST) with and without
-    FIXALL, the exact inverse and the all-fp64 kernels."""
+    """configs[2]: the plan's default kernels (at this coarse table the exact
+    inverse k_inv2), the certified fast inverse (RUN_INV_FAST) with and without
+    FIXALL, the exact inverse asked for and the all-fp64 kernels."""
     from jds import _abi
-    _golden_check('cfg3_rand4k_s0_q10_420_nopf', [0, _abi.RUN_INV_FIXALL, _abi.RUN_INV_FAST,
-                                                  _abi.RUN_INV_FAST | _abi.RUN_INV_FIXALL, _abi.RUN_EXACT_INV,
-                                                  _abi.RUN_EXACT])
+    _golden_check('cfg3_rand4k_s0_q10_420_nopf', [0, _abi.RUN_INV_FAST, _abi.RUN_INV_FAST | _abi.RUN_INV_FIXALL,
+                                                  _abi.RUN_EXACT_INV, _abi.RUN_EXACT])
 
 
 def test_cfg5_4k_q50_422_plan_matches_reference_golden():
-    """configs[4], 8x8 blocks: 4:2:2 tiles (8-wave forward workgroups, barrier
-    statistics flush) and k_inv_fast<4:2:2>."""
+    """configs[4], 8x8 blocks: 4:2:2 tiles (8-wave forward workgroups, row-record
+    statistics) and k_inv_fast<4:2:2>."""
     from jds import _abi
     _golden_check('cfg5_rand4k_s0_q50_422_nopf', [0, _abi.RUN_INV_FIXALL, _abi.RUN_EXACT])
 

@@ -1,9 +1,9 @@
 """K4 v2 (csrc/jds_ssim_band.hip): the batched, band-swept SSIM pipeline against
-(a) the round-1..3 kernels (jds_selftest_psnr_ssim_legacy_dev: one scipy line
-per lane, IEEE divisions), bit for bit on all six values, over sizes that
-exercise every edge of the sweep (7-px images, partial bands, partial column
-chunks, partial NumPy buffers, odd map sizes), and (b) the oracle's NumPy /
-scipy restatement of utils/metrics.py:9-28."""
+the oracle's NumPy / scipy restatement of utils/metrics.py:9-28
+(oracle/cpu_ref.py psnr_ssim_raw), bit for bit on all six values, over sizes
+that exercise every edge of the sweep (7-px images, partial bands, partial
+column chunks, partial NumPy buffers, odd map sizes).  (Rounds 1-4 compared
+with the round-1..3 kernels instead; those left the product library in round 5.)"""
 import numpy as np
 import pytest
 
@@ -41,7 +41,7 @@ SIZES = [(7, 7), (7, 40), (40, 7), (8, 9), (13, 8), (14, 14), (15, 39), (23, 70)
 
 
 @pytest.mark.parametrize('h,w', SIZES)
-def test_batched_pipeline_equals_legacy_kernels_bitwise(h, w):
+def test_batched_pipeline_equals_oracle_bitwise(h, w):
     import torch
     from jds import codec
     kinds = ['noise', 'indep', 'flat', 'smooth'] if h * w <= 300000 else ['noise']
@@ -51,16 +51,17 @@ def test_batched_pipeline_equals_legacy_kernels_bitwise(h, w):
     tb = [torch.from_numpy(b).to(dev) for _, b in pairs]
     torch.cuda.synchronize()
     batch = codec.psnr_ssim_batch_dev([t.data_ptr() for t in ta], [t.data_ptr() for t in tb], h, w, 0, None)
-    for k in range(len(pairs)):
-        leg = codec.psnr_ssim_legacy_dev(ta[k].data_ptr(), tb[k].data_ptr(), h, w, 0)
+    for k, (a, b) in enumerate(pairs):
+        ref = cpu_ref.psnr_ssim_raw(a, b)
         one = codec.psnr_ssim_dev(ta[k].data_ptr(), tb[k].data_ptr(), h, w, 0)
-        assert np.array_equal(batch[k].view(np.uint64), leg.view(np.uint64)), (kinds[k], batch[k], leg)
-        assert np.array_equal(one.view(np.uint64), leg.view(np.uint64)), (kinds[k], one, leg)
+        assert np.array_equal(batch[k].view(np.uint64), ref.view(np.uint64)), (kinds[k], batch[k], ref)
+        assert np.array_equal(one.view(np.uint64), ref.view(np.uint64)), (kinds[k], one, ref)
 
 
 @pytest.mark.parametrize('h,w', [(7, 7), (31, 37), (100, 37), (257, 130)])
-def test_batched_pipeline_equals_oracle(h, w):
-    """Against the NumPy / scipy restatement (the golden fixtures pin that one to skimage)."""
+def test_metrics_api_equals_oracle(h, w):
+    """utils.metrics.compute_psnr_ssim (host arrays) against the restatement (the
+    golden fixtures pin that one to skimage)."""
     from utils.metrics import compute_psnr_ssim
     for i, k in enumerate(['noise', 'indep', 'smooth']):
         a, b = _pair(h, w, 5 + i, k)

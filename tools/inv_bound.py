@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Rigorous error bound for the certified fast inverse (csrc/jds_inv_fast.hip),
-modelling the operation order the kernel SHIPS (v24).
+modelling the operation order the kernel SHIPS (v25).
 
 The fast inverse computes every output value v of the reconstruction
 (reference engines/pipeline.py:68-95: dequantize, idctn, +128, clip, cv2
@@ -17,11 +17,14 @@ The kernel's chain (jds_inv_fast.hip), as modelled here:
   * AAN 8-point IDCT along axis 0, then axis 1 (aan8, the source's doubles
     F_SQ2 / F_A2C2 / F_K10 / F_K12), NO +128, clip to [-128, 127] in both
     planes (fast_row<-128>);
-  * chroma upsample (chroma8_fast): 4:2:0 vertical blend a * 0.25 + b * 0.75,
-    then the horizontal difference form near + (far - near) * (+-0.25);
+  * chroma upsample (chroma8_fast) unnormalised: 4:2:0 vertical a + b * 3
+    (4x the blend a * 0.25 + b * 0.75), then horizontal far + near * 3 (4x
+    again): the upsampled chroma is carried at scale S = 16 (4:2:0), 4 (4:2:2)
+    or 1 (4:4:4, no blend);
   * colour on the magic grid (byte_cert_y): Yv = Y' + (MAGIC + 128), then
-    B = Yv + Cb * 1.772, Gt = Yv + Cb * -0.344136, R = Yv + Cr * 1.402,
-    G = Gt + Cr * -0.714136.  Each of those results lies in [2^20, 2^21) where
+    B = Yv + Cb * (1.772 / S), Gt = Yv + Cb * (-0.344136 / S),
+    R = Yv + Cr * (1.402 / S), G = Gt + Cr * (-0.714136 / S) (the constants'
+    scaling by a power of two is exact).  Each of those results lies in [2^20, 2^21) where
     the fp64 spacing is 2^-32, so each of their roundings costs <= 2^-33
     ABSOLUTE, whatever the value; G has 3 of them, R and B 2.  The kernel adds
     2^-31 (= 4 * 2^-33) to E for them; everything else (the products C * k,
@@ -117,7 +120,7 @@ def kernel_constants():
     assert len(aan) == 8, aan
     klin = re.search(r'constexpr double K_LIN = ([0-9.e+-]+) \* ([0-9.]+);', src)
     kcon = re.search(r'constexpr double K_CONST = ([0-9.e+-]+) \* ([0-9.]+);', src)
-    colour = sorted(float(v) for v in re.findall(r'M::mad\(c[br], (-?\d\.\d+), ', src))
+    colour = sorted(float(v) for v in re.findall(r'M::mad\(c[br], (-?\d\.\d+) \* USC<SH>, ', src))
     return {'aan': aan, 'F_SQ2': c['F_SQ2'], 'F_A2C2': c['F_A2C2'], 'F_K10': c['F_K10'], 'F_K12': c['F_K12'],
             'MAGIC': c.get('MAGIC'), 'K_LIN': float(klin.group(1)) * float(klin.group(2)),
             'K_CONST': float(kcon.group(1)) * float(kcon.group(2)), 'colour': colour}
@@ -183,6 +186,7 @@ def fresh(cap, el, ec):
 
 F = Fraction
 QUARTER, THREEQ = F(1, 4), F(3, 4)
+UPSAMPLE_SCALE = {'4:4:4': 1, '4:2:2': 4, '4:2:0': 16}  # the fast chain's unnormalised chroma
 
 
 # ---- 8-point transforms on V ---------------------------------------------------
@@ -290,13 +294,13 @@ def upsample_bound(x, chain, mode):
     if mode == '4:4:4':
         return x
     if chain == 'fast':
+        # unnormalised sums (caps follow: 4x per blended axis): the colour
+        # constants carry the 1 / S (UPSAMPLE_SCALE)
         v = x
-        if mode == '4:2:0':  # a * 0.25 + b * 0.75 (two independent samples)
-            v = add(mul(x, QUARTER, exact_product=True), mul(x, THREEQ)); v.cap = x.cap
+        if mode == '4:2:0':  # a + b * 3 (two independent samples)
+            v = add(fresh(x.cap, x.el, x.ec), mul(x, F(3)))
         w = fresh(v.cap, v.el, v.ec)
-        dlt = add(v, w, -1)  # far - near
-        h = add(mul(dlt, QUARTER, exact_product=True), w); h.cap = x.cap  # near + (far - near) * (+-1/4)
-        return h
+        return add(w, mul(v, F(3)))  # far + near * 3
     # cv2 HResizeLinear then VResizeLinear: S0 * a0 + S1 * a1 (products rounded, sum rounded)
     h = add(mul(x, QUARTER), mul(x, THREEQ)); h.cap = x.cap
     if mode == '4:2:0':
@@ -312,8 +316,10 @@ def colour_bound(ey, ec_, chain, mode):
         Y = fresh(128.0, *ey)      # Y' = clip(AAN, -128, 127); +128 rides on the grid
         C = upsample_bound(fresh(128.0, *ec_), 'fast', mode)
 
-        def prod(k):  # C * kd, fused into the grid add or rounded on its own (counted)
-            return mul(C, k, float(k))
+        sc = UPSAMPLE_SCALE[mode]
+
+        def prod(k):  # C * (kd / S), fused into the grid add or rounded on its own (counted)
+            return mul(C, k / sc, float(k) / sc)
         R = V(np.zeros(64), 0, Y.el + prod(kr).el, Y.ec + prod(kr).ec)
         B = V(np.zeros(64), 0, Y.el + prod(kb).el, Y.ec + prod(kb).ec)
         G = V(np.zeros(64), 0, Y.el + prod(kgb).el + prod(kgr).el, Y.ec + prod(kgb).ec + prod(kgr).ec)

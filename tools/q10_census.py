@@ -103,6 +103,47 @@ def main():
     out['exact_int_luma_dc_only_chroma_zero'] = int(
         (unc & ex & czero[..., None] & (nz_b[0] & ~acnz_b[0])[yb, xb][..., None]).sum())
     out['not_exact'] = int((unc & ~ex).sum())
+    # the exact-value rule round 5 tried (k_inv_fast<.., EX>, retired): luma exactly known (all-zero block, or the
+    # fast value beyond the clip range by more than E) and every chroma tap of the channel's
+    # plane(s) from an all-zero block -- per pixel (PER_LANE=1: the lane's 8 pixels together)
+    if mode != '4:4:4':
+        hc, wc = pl[1]
+        m = yy // sy
+        if sy == 2:
+            rq = np.clip(np.where(yy & 1, m + 1, m - 1), 0, hc - 1)
+        else:
+            rq = np.clip(m, 0, hc - 1)
+        rt = np.clip(m, 0, hc - 1)
+        j = xx // 2
+        c_a = np.clip(np.where(xx & 1, j, j - 1), 0, wc - 1)
+        c_b = np.clip(np.where(xx & 1, j + 1, j), 0, wc - 1)
+        zpl = []
+        for p in (1, 2):
+            zb = ~nz_b[p]
+            z = np.ones((H, W), bool)
+            for r_ in (rq, rt):
+                for c_ in (c_a, c_b):
+                    z &= zb[r_ // 8, c_ // 8]
+            if os.environ.get('PER_LANE') == '1':
+                z = z.reshape(H, W // 8, 8).all(axis=2).repeat(8, axis=1)
+            zpl.append(z)
+        ny_, nx_ = -(-H // 8), -(-W // 8)
+        # fast luma before clip: approximated by the reference's unclipped luma (within E of it)
+        from scipy import fft as sfft
+        qb = cf[:ny_ * nx_ * 64].reshape(-1, 8, 8)
+        raw = cpu_ref.merge_blocks(sfft.idctn(cpu_ref.dequantize(qb, Q), type=2, norm='ortho', axes=(-2, -1)),
+                                   (ny_ * 8, nx_ * 8))[:H, :W]
+        margin = np.maximum(-128.0 - raw, raw - 127.0)
+        yex = (~nz_b[0])[yb, xb] | (margin > E[..., 0])
+        if os.environ.get('DC_ONLY') == '1':  # luma DC-only blocks replayed exactly
+            yex |= (~acnz_b[0])[yb, xb]
+        exv = np.stack([yex & zpl[1], yex & zpl[0] & zpl[1], yex & zpl[0]], axis=-1)
+        left = unc & ~exv
+        out['ex_rule_covers'] = int((unc & exv).sum())
+        out['ex_rule_left'] = int(left.sum())
+        tl = left.any(axis=2)
+        out['ex_rule_tiles_left'] = sum(bool(tl[t0:t0 + th, t1:t1 + tw].any())
+                                        for t0 in range(0, H, th) for t1 in range(0, W, tw))
     print(json.dumps(out))
 
 

@@ -21,8 +21,8 @@ if has tests; then
   rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/${TAG}_pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
 if has quick; then
-  timeout -k 10 900 python -u -m pytest tests/test_gpu_plan_4k.py tests/test_gpu_inv_fast.py tests/test_gpu_entropy.py \
-    tests/test_gpu_ssim.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest ${QUICK_TESTS:-tests/test_gpu_plan_4k.py tests/test_gpu_inv_fast.py tests/test_gpu_entropy.py \
+    tests/test_gpu_ssim.py tests/test_gpu_parity.py} -m gpu -x -q --timeout 300 --timeout-method thread \
     -p no:cacheprovider > gpurun_out/${TAG}_quick.log 2>&1
   rc=$?; echo "quick rc=$rc"; tail -4 gpurun_out/${TAG}_quick.log; [ $rc -eq 0 ] || exit $rc
 fi
@@ -47,7 +47,7 @@ if has cfg4k; then
   rc=$?; echo "cfg4k rc=$rc"; tail -3 gpurun_out/${TAG}_cfg4k.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc
 fi
 if has q10; then
-  # configs[2] (16 x 4K Q10 4:2:0): the exact-value fast inverse (default) vs the plain certificate vs k_inv2
+  # configs[2] (16 x 4K Q10 4:2:0): the plan default (k_inv2 at this table) vs the certified fast inverse vs k_inv2 asked for
   for v in default --inv-fast --exact-inv; do
     a=$v; [ "$v" = default ] && a=""
     timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --height 2160 --width 3840 --frames 16 --quality 10 \

@@ -145,7 +145,7 @@ def inv_budget():
     key = [ln for ln in asm.split('\n') if ln.startswith('_ZN3jds10k_inv_fastILi2ELi0E') and ln.split(';')[0].strip().endswith(':')][0]
     bbs = blocks(asm, key.split(';')[0].strip())
     src = os.path.join(CSRC, 'jds_inv_fast.hip')
-    fr = func_ranges(src, ['aan8', 'fast_col', 'fast_row', 'chroma8_fast', 'fvblend', 'fhblend', 'col_b', 'col_gt',
+    fr = func_ranges(src, ['aan8', 'fast_col', 'fast_row', 'chroma8_fast', 'fvsum', 'fhsum', 'col_b', 'col_gt',
                            'col_r', 'col_g', 'byte_cert_y', 'pack4', 'inv_fast_tile'])
     text = open(src).read().split('\n')
     mark = {k: next(i + 1 for i, l in enumerate(text) if k in l) for k in
@@ -169,7 +169,7 @@ def inv_budget():
             return 'dequantise + Dmax (fast_col)'
         if within(line, 'fast_row'):
             return 'IDCT row loads + clip (fast_row)'
-        if within(line, 'chroma8_fast') or within(line, 'fvblend') or within(line, 'fhblend'):
+        if within(line, 'chroma8_fast') or within(line, 'fvsum') or within(line, 'fhsum'):
             return 'upsample (chroma8_fast)'
         if any(within(line, n) for n in ('col_b', 'col_gt', 'col_r', 'col_g')):
             return 'colour on the magic grid'
