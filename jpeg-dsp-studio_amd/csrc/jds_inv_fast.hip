@@ -763,17 +763,17 @@ k_inv_fast444(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __r
     fast_col(qy, s_qs, lv, slot, qhi, qlo);
     __builtin_amdgcn_wave_barrier();
     fast_row<-128>(slot, lv, Yv);  // Y - 128
-    uint32_t cb[24];  // channel words (byte in bits 0-7), output order R0 G0 B0 R1 ...
+    uint32_t cb[24];  // channel high words (byte: clamp(low 16 bits)), output order R0 G0 B0 R1 ...
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const double y = Yv[k] + (MAGIC + 128.0);
-      cb[3 * k] = byte_cert_y(col_r(y, Cr[k]), lo_min, lo_max);
-      cb[3 * k + 1] = byte_cert_y(col_g(col_gt(y, Cb[k]), Cr[k]), lo_min, lo_max);
-      cb[3 * k + 2] = byte_cert_y(col_b(y, Cb[k]), lo_min, lo_max);
+      cb[3 * k] = cert_hi(col_r(y, Cr[k]), lo_min, lo_max);
+      cb[3 * k + 1] = cert_hi(col_g(col_gt(y, Cb[k]), Cr[k]), lo_min, lo_max);
+      cb[3 * k + 2] = cert_hi(col_b(y, Cb[k]), lo_min, lo_max);
     }
     uint32_t pk[6];
 #pragma unroll
-    for (int w = 0; w < 6; ++w) pk[w] = pack4(cb[4 * w], cb[4 * w + 1], cb[4 * w + 2], cb[4 * w + 3]);
+    for (int w = 0; w < 6; ++w) pk[w] = pack4s(cb[4 * w], cb[4 * w + 1], cb[4 * w + 2], cb[4 * w + 3]);
     store(pk);
   }
   // the block's Dmax over its three planes (its 8 lanes), then this lane's margin
