@@ -2,7 +2,7 @@
 # PMC passes over tools/ssim_probe.py (K4 kernels), one --pmc pass per group.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-ROOT=$(pwd); OUT=gpurun_out/${1:-ssimpmc}; mkdir -p $OUT; export TMPDIR=/tmp LEGACY=0 REPS=4
+ROOT=$(pwd); OUT=gpurun_out/${1:-ssimpmc}; mkdir -p $OUT; export TMPDIR=/tmp REPS=4
 cd /tmp
 i=0
 while read -r group; do

@@ -1,5 +1,5 @@
 """Time K4 (SSIM / PSNR) per 1080p frame: the batched band pipeline
-(jds_psnr_ssim_batch_dev) at batch 1 and 8, and the legacy kernels.  Prints
+(jds_psnr_ssim_batch_dev) at batch 1, 8 and 32 (BATCH env).  Prints
 one JSON line.  Run on the GPU box (optionally under rocprofv3 --kernel-trace
 --stats for per-kernel times)."""
 import json
@@ -21,7 +21,7 @@ def main():
     reps = int(os.environ.get('REPS', '10'))
     dev = torch.device('cuda', 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    n = 8
+    n = int(os.environ.get('BATCH', '8'))
     a = torch.randint(0, 256, (n, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
     noise = torch.randint(-8, 8, (n, H, W, 3), dtype=torch.int16, device=dev, generator=g)
     b = (a.to(torch.int16) + noise).clamp(0, 255).to(torch.uint8)
@@ -50,16 +50,8 @@ def main():
     def eight():
         nonlocal r8
         r8 = codec.psnr_ssim_batch_dev(pa, pb, H, W, 0, None)
-    res['batch8_ms_per_item'] = timeit(eight, max(2, reps // 4)) / n
-    if os.environ.get('LEGACY', '1') == '1':
-        leg = None
-
-        def legacy():
-            nonlocal leg
-            leg = codec.psnr_ssim_legacy_dev(pa[0], pb[0], H, W, 0)
-        res['legacy_ms'] = timeit(legacy, max(2, reps // 4))
-        res['bitwise_equal_legacy'] = bool(np.array_equal(leg.view(np.uint64), r1[0].view(np.uint64)))
-        res['bitwise_equal_batch'] = bool(np.array_equal(r8[0].view(np.uint64), r1[0].view(np.uint64)))
+    res[f'batch{n}_ms_per_item'] = timeit(eight, max(2, reps // 4)) / n
+    res['bitwise_equal_batch'] = bool(np.array_equal(r8[0].view(np.uint64), r1[0].view(np.uint64)))
     res['values'] = [float(x) for x in r1[0]]
     print(json.dumps(res))
 
