@@ -45,6 +45,25 @@ __device__ __forceinline__ void unpack(uint32_t v, double& R, double& G, double&
   B = (double)(v >> 16);
 }
 
+// 1/d for d > 0 to within 2^-60 relative: v_rcp_f64 and two Newton steps
+__device__ __forceinline__ double recip64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+  return __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+}
+
+// rint(x / d) of the IEEE quotient (np.round(c / Q): round half to even of
+// the correctly rounded fp64 quotient) with r = recip64(d): t = x * r is within
+// |t| 2^-52 of x / d, and fl(x / d) within |x / d| 2^-53, so when t lies
+// farther than |t| 2^-49 from its nearest half-integer both round to rint(t);
+// otherwise (rare) the division decides.
+__device__ __forceinline__ int rint_quot(double x, double d, double r) {
+  const double t = x * r, q = __builtin_rint(t);
+  const double m = fabs(fabs(t - q) - 0.5);  // distance to the nearest half-integer
+  if (__builtin_expect(m > fabs(t) * 0x1p-49, 1)) return (int)q;
+  return (int)__builtin_rint(x / d);
+}
+
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -833,11 +833,15 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
       long long dnz = 0, dmb = 0;
       jds_frame_stats* fs = st + frame;
       const double* q8 = fq[frame].q + (u >> 1) * 8;
+      double rq[8];  // 1 / (32 Q8[u/2][j]): each serves two coefficients
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rq[j] = recip64(32.0 * q8[j]);
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) {
         // quantizer.py:22-24: the true quotient of the reference's coefficient
-        // (v / 32, exact) by Q16 = Q8[u/2][cc/2]
-        const int qn = (int)__builtin_rint(v[cc] / (32.0 * q8[cc >> 1]));
+        // (v / 32, exact) by Q16 = Q8[u/2][cc/2] (rint_quot: the division only
+        // near a half-integer)
+        const int qn = rint_quot(v[cc], 32.0 * q8[cc >> 1], rq[cc >> 1]);
         const int qo = (int16_t)((ow[cc >> 1] >> ((cc & 1) * 16)) & 0xffffu);
         nw[cc >> 1] |= (uint32_t)(uint16_t)qn << ((cc & 1) * 16);
         if (qn != qo) {
