@@ -342,10 +342,16 @@ __device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uin
     const uint32_t cc = P.ccv[i] & 255u, col = min((uint32_t)lo + cc, (uint32_t)hi - 1u);
     const uint32_t px = P.row[i] + col;
     const bool im = (P.ccv[i] >> 8) & 1u;
+#ifdef JDS_SSIM_PROBE_NOSTAGE  // tools: timing probe without the staging loads (wrong values)
+    R.b[i] = px & 255u;
+    R.y[i] = (double)(px & 255u);
+    (void)im;
+#else
     if (c < 3)
       R.b[i] = (im ? b : a)[px * 3u + (uint32_t)c];
     else
       R.y[i] = (im ? Y : X)[px];
+#endif
   }
   if (c == 3 && t < 5 * SB_SC) {
     const int q = t / SB_SC, col = min(lo + t % SB_SC, hi - 1);
