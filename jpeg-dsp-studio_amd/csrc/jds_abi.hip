@@ -33,7 +33,8 @@ hipError_t stage_area_gen(const double* in, int H, int W, const AreaTap* ytab, c
                           int oh, int ow, hipStream_t s);
 hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const* b, int items, int H, int W,
                                   double c1, double c2, double* scratch, double* out, int out_stride,
-                                  unsigned long long* sse, hipStream_t s);
+                                  unsigned long long* sse, hipStream_t s, hipStream_t side, hipEvent_t fork,
+                                  hipEvent_t join);
 size_t ssim_batch_scratch_doubles(int H, int W);
 int ssim_batch_max_items();
 hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
@@ -136,6 +137,10 @@ struct jds_ctx {
   // the statistics kernels (SSIM, float32 magnitude bits) of the same call
   hipStream_t xfer = nullptr;
   hipEvent_t xfer_ev = nullptr;
+  // SSIM: the RGB channels' band kernel runs on a stream of its own beside the
+  // luma planes, chains and band (jds_ssim_band.hip)
+  hipStream_t ss_side = nullptr;
+  hipEvent_t ss_fork = nullptr, ss_join = nullptr;
   // host-path scratch
   DevBuf rgb, out, coeffs, stats, part, fq, gk, erry, errrgb, sel;
   DevBuf ss_planes, ss_out, img_a, img_b;  // ss_planes: k_ss_* scratch
@@ -158,12 +163,17 @@ static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const 
   int group = (int)std::max<size_t>(1, std::min<size_t>((size_t)per, ((size_t)2 << 30) / each));
   group = std::min(group, items);
   HIP_TRY(c->ss_planes.ensure(each * group));
+  if (!c->ss_side) {
+    HIP_TRY(hipStreamCreateWithFlags(&c->ss_side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->ss_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ss_join, hipEventDisableTiming));
+  }
   if (sse) HIP_TRY(hipMemsetAsync(sse, 0, sizeof(unsigned long long) * items, c->stream));
   for (int i0 = 0; i0 < items; i0 += group) {
     const int k = std::min(group, items - i0);
     HIP_TRY(launch_psnr_ssim_batch(a + i0, b + i0, k, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_planes.p,
                                    out + (size_t)i0 * out_stride, out_stride, sse ? sse + i0 : nullptr,
-                                   c->stream));
+                                   c->stream, c->ss_side, c->ss_fork, c->ss_join));
   }
   return JDS_OK;
 }
@@ -443,6 +453,12 @@ void jds_ctx_destroy(jds_ctx* c) {
     (void)hipStreamDestroy(c->xfer);
   }
   if (c->xfer_ev) (void)hipEventDestroy(c->xfer_ev);
+  if (c->ss_side) {
+    (void)hipStreamSynchronize(c->ss_side);
+    (void)hipStreamDestroy(c->ss_side);
+  }
+  if (c->ss_fork) (void)hipEventDestroy(c->ss_fork);
+  if (c->ss_join) (void)hipEventDestroy(c->ss_join);
   DevBuf* bufs[] = {&c->rgb,     &c->out,    &c->coeffs,    &c->stats,  &c->part,  &c->fq,   &c->gk,  &c->erry,
                     &c->errrgb,  &c->sel,    &c->ss_planes, &c->ss_out, &c->img_a, &c->img_b};
   for (DevBuf* b : bufs) b->release();

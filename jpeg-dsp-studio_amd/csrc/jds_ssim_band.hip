@@ -51,6 +51,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "jds_internal.hpp"
 
@@ -261,7 +262,10 @@ __global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
 
 constexpr int SB_SC = SB_CW + 4;  // staged columns per chunk (chunk 0 fills CW + 3)
 
-template <int BH>
+// LU: the luma channel's workgroups (fp64 inputs and chain checkpoints) and
+// the RGB channels' (bytes) are separate kernel instances, so the RGB ones --
+// three in four -- carry 34 KB of LDS instead of 51 and four fit a CU
+template <int BH, bool LU>
 struct BandLds {
   double ring[5][BH][SB_RP];  // axis-0 outputs, column c at slot c & (SB_RING - 1)
   double st[5][BH][SB_SP];    // axis-1 running sums of the current chunk
@@ -270,11 +274,14 @@ struct BandLds {
   // rows per word, consecutive columns in consecutive words (the fill's and
   // the staging's accesses of a wave hit distinct banks); luma: a column's
   // 2 (BH + 6) values at an odd stride in doubles (likewise)
-  union {
-    uint32_t b4[2][4][SB_SC];           // RGB: byte r & 3 of word [image][r >> 2][column]
+  struct InB {
+    uint32_t b4[2][4][SB_SC];  // RGB: byte r & 3 of word [image][r >> 2][column]
+  };
+  struct InY {
     double y[SB_SC][2 * (BH + 6) + 1];  // luma: [column][image * (BH + 6) + r]
-  } in[2];
-  double ck[2][5][SB_SC];              // luma: the axis-0 chains' states at row i0
+  };
+  typename std::conditional<LU, InY, InB>::type in[2];
+  double ck[LU ? 2 : 1][5][LU ? SB_SC : 1];  // luma: the axis-0 chains' states at row i0
 };
 
 // fill columns of chunk k: chunk 0 fills [0, CW + 3), chunk k > 0 the new
@@ -300,10 +307,10 @@ struct StagePlan {
   uint32_t row[StageCfg<BH>::SE];
   uint32_t ccv[StageCfg<BH>::SE];
 };
-template <int BH>
+template <int BH, bool LU>
 struct StageRegs {
-  uint32_t b[StageCfg<BH>::SE];
-  double y[StageCfg<BH>::SE];
+  uint32_t b[LU ? 1 : StageCfg<BH>::SE];
+  double y[LU ? StageCfg<BH>::SE : 1];
   double ck;
 };
 
@@ -327,10 +334,10 @@ __device__ __forceinline__ StagePlan<BH> stage_plan(int c, int H, int W, int i0)
   return P;
 }
 
-template <int BH>
+template <int BH, bool LU>
 __device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uint8_t* a, const uint8_t* b,
                                             const double* X, const double* Y, const double* ck, int band, int k,
-                                            int nchunks, const StagePlan<BH>& P, StageRegs<BH>& R) {
+                                            int nchunks, const StagePlan<BH>& P, StageRegs<BH, LU>& R) {
   constexpr int SE = StageCfg<BH>::SE;
   if (k >= nchunks) return;
   int lo, hi;
@@ -343,25 +350,27 @@ __device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uin
     const uint32_t px = P.row[i] + col;
     const bool im = (P.ccv[i] >> 8) & 1u;
 #ifdef JDS_SSIM_PROBE_NOSTAGE  // tools: timing probe without the staging loads (wrong values)
-    R.b[i] = px & 255u;
-    R.y[i] = (double)(px & 255u);
+    if constexpr (LU)
+      R.y[i] = (double)(px & 255u);
+    else
+      R.b[i] = px & 255u;
     (void)im;
 #else
-    if (c < 3)
-      R.b[i] = (im ? b : a)[px * 3u + (uint32_t)c];
-    else
+    if constexpr (LU)
       R.y[i] = (im ? Y : X)[px];
+    else
+      R.b[i] = (im ? b : a)[px * 3u + (uint32_t)c];
 #endif
   }
-  if (c == 3 && t < 5 * SB_SC) {
+  if (LU && t < 5 * SB_SC) {
     const int q = t / SB_SC, col = min(lo + t % SB_SC, hi - 1);
     R.ck = ck[((size_t)q * B.NB + band) * B.W + col];
   }
 }
 
-template <int BH>
+template <int BH, bool LU>
 __device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const StagePlan<BH>& P,
-                                             const StageRegs<BH>& R, BandLds<BH>& L) {
+                                             const StageRegs<BH, LU>& R, BandLds<BH, LU>& L) {
   constexpr int SE = StageCfg<BH>::SE;
   if (k >= nchunks) return;
   const int t = threadIdx.x, buf = k & 1;
@@ -370,20 +379,22 @@ __device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const St
   for (int i = 0; i < SE; ++i) {
     if ((P.ccv[i] >> 9) & 1u) {
       uint8_t* d = base + (P.ccv[i] >> 12);
-      if (c < 3)
-        *d = (uint8_t)R.b[i];
-      else
+      if constexpr (LU)
         *reinterpret_cast<double*>(d) = R.y[i];
+      else
+        *d = (uint8_t)R.b[i];
     }
   }
-  if (c == 3 && t < 5 * SB_SC) L.ck[buf][t / SB_SC][t % SB_SC] = R.ck;
+  if constexpr (LU)
+    if (t < 5 * SB_SC) L.ck[buf][t / SB_SC][t % SB_SC] = R.ck;
+  (void)c;
 }
 
 // the fill of chunk k from its staged inputs: lanes (q, column), the axis-0
 // outputs of the band's rows into the ring (RGB: exact window sums; luma: the
 // chain resumed from its checkpoint)
-template <int BH>
-__device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<BH>& L) {
+template <int BH, bool LU>
+__device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<BH, LU>& L) {
   constexpr int NR = BH + 6;
   int lo, hi;
   fill_cols(k, W, lo, hi);
@@ -391,7 +402,8 @@ __device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<
   if (t >= 5 * nc) return;
   const int q = t / nc, cc = t % nc, buf = k & 1;
   const int slot = (lo + cc) & (SB_RING - 1);
-  if (c < 3) {
+  (void)c;
+  if constexpr (!LU) {
     uint32_t xw[4], yw[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -483,10 +495,10 @@ __device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double
   (void)jj0;
 }
 
-template <int BH>
-__global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(3))) k_ss_band(SsimBatch B) {
-  __shared__ BandLds<BH> L;
-  const int band = blockIdx.x, c = blockIdx.y, item = blockIdx.z;
+template <int BH, bool LU>
+__global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(LU ? 3 : 4))) k_ss_band(SsimBatch B) {
+  __shared__ BandLds<BH, LU> L;
+  const int band = blockIdx.x, c = LU ? 3 : blockIdx.y, item = blockIdx.z;
   const int H = B.H, W = B.W;
   const int i0 = 3 + BH * band;
   const int nr = min(BH, H - 3 - i0);
@@ -505,14 +517,14 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   // chunk period -- the barrier interval that issued it and the next one --
   // before its value is needed
   const StagePlan<BH> P = stage_plan<BH>(c, H, W, i0);
-  StageRegs<BH> RA, RB;
-  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, 0, nchunks, P, RA);
-  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, 1, nchunks, P, RB);
-  stage_commit<BH>(c, 0, nchunks, P, RA, L);
-  stage_commit<BH>(c, 1, nchunks, P, RB, L);
+  StageRegs<BH, LU> RA, RB;
+  stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, 0, nchunks, P, RA);
+  stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, 1, nchunks, P, RB);
+  stage_commit<BH, LU>(c, 0, nchunks, P, RA, L);
+  stage_commit<BH, LU>(c, 1, nchunks, P, RB, L);
   __syncthreads();
-  stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, 2, nchunks, P, RA);
-  fill_chunk<BH>(c, nr, 0, W, L);
+  stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, 2, nchunks, P, RA);
+  fill_chunk<BH, LU>(c, nr, 0, W, L);
   __syncthreads();
 
   // chain lanes: (q, row)
@@ -521,7 +533,7 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   double s = 0.0;
   // one chunk: cur holds chunk k + 2's loaded inputs (committed here), nxt
   // receives chunk k + 3's
-  auto step = [&](int k, StageRegs<BH>& cur, StageRegs<BH>& nxt) {
+  auto step = [&](int k, StageRegs<BH, LU>& cur, StageRegs<BH, LU>& nxt) {
     const int jc = k * SB_CW;
 #ifndef JDS_SSIM_PROBE_NOCHAIN  // tools: timing probes only (wrong values)
     if (chain_lane) {
@@ -542,7 +554,7 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
     // chunk k + 1's fill (LDS buffer (k + 1) & 1), chunk k's map, chunk k + 2's
     // inputs into the buffer chunk k's fill has released, chunk k + 3's loads
 #ifndef JDS_SSIM_PROBE_NOFILL
-    if (k + 1 < nchunks) fill_chunk<BH>(c, nr, k + 1, W, L);
+    if (k + 1 < nchunks) fill_chunk<BH, LU>(c, nr, k + 1, W, L);
 #endif
 #ifdef JDS_SSIM_PROBE_NOMAP
     if (false)
@@ -563,8 +575,8 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
         smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = (a1 * a2) / d;
       }
     }
-    stage_commit<BH>(c, k + 2, nchunks, P, cur, L);
-    stage_issue<BH>(B, c, pr.a, pr.b, X, Y, ck, band, k + 3, nchunks, P, nxt);
+    stage_commit<BH, LU>(c, k + 2, nchunks, P, cur, L);
+    stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, k + 3, nchunks, P, nxt);
     __syncthreads();
   };
   for (int k = 0; k < nchunks; k += 2) {
@@ -788,7 +800,8 @@ size_t ssim_batch_scratch_doubles(int H, int W) {
 // items * ssim_batch_scratch_doubles(H, W).
 hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const* b, int items, int H, int W,
                                   double c1, double c2, double* scratch, double* out, int out_stride,
-                                  unsigned long long* sse, hipStream_t s) {
+                                  unsigned long long* sse, hipStream_t s, hipStream_t side, hipEvent_t fork,
+                                  hipEvent_t join) {
   if (items < 1 || items > SB_MAX_ITEMS || H < 7 || W < 7) return hipErrorInvalidValue;
   if ((unsigned long long)H * (unsigned long long)W * 3ull >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit staging offsets
   SsimBatch B{};
@@ -816,10 +829,18 @@ hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const*
   B.out = out;
   B.out_stride = out_stride;
   B.sse = sse;
+  // the RGB channels' bands need only the images: on the side stream from the
+  // start, beside the luma planes, chains and band on s (which holds the
+  // scratch's previous users in order); joined before the means
+  hipError_t e;
+  if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess) return e;
+  hipLaunchKernelGGL((k_ss_band<SB_BH, false>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
+  if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_ss_yplanes, dim3((unsigned)std::min<long long>((n + 255) / 256, SB_PLANE_BLOCKS), items),
                      dim3(256), 0, s, B);
   hipLaunchKernelGGL(k_ss_ychk<SB_BH>, dim3((W + 63) / 64, 5, items), dim3(64), 0, s, B);
-  hipLaunchKernelGGL(k_ss_band<SB_BH>, dim3(B.NB, 4, items), dim3(SB_THREADS), 0, s, B);
+  hipLaunchKernelGGL((k_ss_band<SB_BH, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
+  if ((e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 5, items), dim3(SB_THREADS), 0, s, B);
   hipLaunchKernelGGL(k_ss_final, dim3(5, items), dim3(256), 0, s, B);
   return hipGetLastError();
