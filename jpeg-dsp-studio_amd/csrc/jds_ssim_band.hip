@@ -61,9 +61,13 @@ namespace jds {
 
 constexpr int SB_NP_BUF = 8192;  // NumPy ufunc buffer (elements)
 constexpr int SB_CW = 32;        // output columns per chunk
-constexpr int SB_RING = 64;      // ring slots per row (power of two >= CW + 7)
-static_assert(SB_RING == 2 * SB_CW, "chain_chunk's ring phase is 0 or CW");
-constexpr int SB_RP = 65;        // ring row pitch in doubles (odd: lane = row reads hit distinct banks)
+// ring slots per row: >= CW + 7 (a chunk's chain reads columns jc - 4 .. jc +
+// CW + 2, and the next fill writes CW columns from jc + CW + 3 after it), 48
+// rather than 64 so an RGB workgroup fits 28.5 KB of LDS (five per CU);
+// chunk bases jc mod 48 cycle through 0, 32, 16
+constexpr int SB_RING = 48;
+static_assert(SB_RING >= SB_CW + 7 + 0 && (3 * SB_CW) % SB_RING == 0, "chain_chunk's ring phases");
+constexpr int SB_RP = 49;        // ring row pitch in doubles (odd: lane = row reads hit distinct banks)
 constexpr int SB_SP = SB_CW + 1; // chain output tile pitch
 constexpr int SB_THREADS = 256;
 constexpr int SB_MAX_ITEMS = 32; // image pairs per launch (kernel-argument array)
@@ -267,7 +271,7 @@ constexpr int SB_SC = SB_CW + 4;  // staged columns per chunk (chunk 0 fills CW 
 // three in four -- carry 34 KB of LDS instead of 51 and four fit a CU
 template <int BH, bool LU>
 struct BandLds {
-  double ring[5][BH][SB_RP];  // axis-0 outputs, column c at slot c & (SB_RING - 1)
+  double ring[5][BH][SB_RP];  // axis-0 outputs, column c at slot c mod SB_RING
   double st[5][BH][SB_SP];    // axis-1 running sums of the current chunk
   // inputs of the fill of one chunk, double-buffered (staged two chunks ahead):
   // per staged column, rows i0 - 3 .. i0 + BH + 2 of both images.  RGB: four
@@ -401,7 +405,7 @@ __device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<
   const int nc = hi - lo, t = threadIdx.x;
   if (t >= 5 * nc) return;
   const int q = t / nc, cc = t % nc, buf = k & 1;
-  const int slot = (lo + cc) & (SB_RING - 1);
+  const int slot = (lo + cc) % SB_RING;
   (void)c;
   if constexpr (!LU) {
     uint32_t xw[4], yw[4];
@@ -443,60 +447,67 @@ __device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<
   }
 }
 
-// One chunk of a chain lane's axis-1 running sum, steps j = jc + jj: every ring
-// read first (static LDS offsets: jc is a multiple of CW, so the ring phase
-// BASE = jc & (RING - 1) is 0 or CW), then the dependent adds.  FIRST: j = 0
-// starts scipy's reflected window; NJ: steps in this chunk (all CW but the last).
+// One chunk of a chain lane's axis-1 running sum, steps j = jc + jj, in two
+// halves of CW / 2 steps: each half's ring reads first (static LDS offsets: jc
+// is a multiple of CW, so the ring phase BASE = jc mod RING is 0, 32 or 16),
+// then its dependent adds (half the values in flight: fewer VGPRs for the
+// workgroups a CU holds).  FIRST: j = 0 starts scipy's reflected window; NJ:
+// steps in this chunk (all CW but the last).
+constexpr int rmod(int x) { return ((x % SB_RING) + SB_RING) % SB_RING; }
 template <int BASE, bool FIRST>
 __device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double* __restrict__ o, double& s, int nj) {
-  constexpr int M = SB_RING - 1;
-  double nv[SB_CW], ov[SB_CW];
+  constexpr int HC = SB_CW / 2;
 #pragma unroll
-  for (int jj = 0; jj < SB_CW; ++jj) {
-    nv[jj] = R[(BASE + jj + 3) & M];
-    ov[jj] = R[(BASE + jj - 4) & M];
-  }
-  int jj0 = 0;
-  if constexpr (FIRST) {
-    // scipy's first window: reflect(-3 .. 3) = 2, 1, 0, 0, 1, 2, 3; then j = 1..3
-    // take their old column from reflect(j - 4) = 2, 1, 0
-    const double r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3];
-    s = s + r2;
-    s = s + r1;
-    s = s + r0;
-    s = s + r0;
-    s = s + r1;
-    s = s + r2;
-    s = s + r3;
-    o[0] = s;
-    s = s + (nv[1] - r2);
-    o[1] = s;
-    s = s + (nv[2] - r1);
-    o[2] = s;
-    s = s + (nv[3] - r0);
-    o[3] = s;
-    jj0 = 4;
-  }
-  if (nj == SB_CW) {
+  for (int h = 0; h < 2; ++h) {
+    double nv[HC], ov[HC];
 #pragma unroll
-    for (int jj = FIRST ? 4 : 0; jj < SB_CW; ++jj) {
-      s = s + (nv[jj] - ov[jj]);
-      o[jj] = s;
+    for (int i = 0; i < HC; ++i) {
+      nv[i] = R[rmod(BASE + h * HC + i + 3)];
+      ov[i] = R[rmod(BASE + h * HC + i - 4)];
     }
-  } else {
+    int i0 = 0;
+    if (FIRST && h == 0) {
+      // scipy's first window: reflect(-3 .. 3) = 2, 1, 0, 0, 1, 2, 3; then j = 1..3
+      // take their old column from reflect(j - 4) = 2, 1, 0
+      const double r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3];
+      s = s + r2;
+      s = s + r1;
+      s = s + r0;
+      s = s + r0;
+      s = s + r1;
+      s = s + r2;
+      s = s + r3;
+      o[0] = s;
+      s = s + (nv[1] - r2);
+      o[1] = s;
+      s = s + (nv[2] - r1);
+      o[2] = s;
+      s = s + (nv[3] - r0);
+      o[3] = s;
+      i0 = 4;
+    }
+    if (nj == SB_CW) {
 #pragma unroll
-    for (int jj = FIRST ? 4 : 0; jj < SB_CW; ++jj) {
-      if (jj < nj) {
-        s = s + (nv[jj] - ov[jj]);
-        o[jj] = s;
+      for (int i = 0; i < HC; ++i) {
+        if (i >= i0) {
+          s = s + (nv[i] - ov[i]);
+          o[h * HC + i] = s;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < HC; ++i) {
+        if (i >= i0 && h * HC + i < nj) {
+          s = s + (nv[i] - ov[i]);
+          o[h * HC + i] = s;
+        }
       }
     }
   }
-  (void)jj0;
 }
 
 template <int BH, bool LU>
-__global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(LU ? 3 : 4))) k_ss_band(SsimBatch B) {
+__global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(LU ? 3 : 5))) k_ss_band(SsimBatch B) {
   __shared__ BandLds<BH, LU> L;
   const int band = blockIdx.x, c = LU ? 3 : blockIdx.y, item = blockIdx.z;
   const int H = B.H, W = B.W;
@@ -543,10 +554,13 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
       const double* Rg = L.ring[cq][crow];
       double* o = L.st[cq][crow];
       const int nj = min(SB_CW, jend - jc);
+      const int base = jc % SB_RING;
       if (k == 0)
         chain_chunk<0, true>(Rg, o, s, nj);
-      else if (jc & SB_CW)
-        chain_chunk<SB_CW, false>(Rg, o, s, nj);
+      else if (base == 32)
+        chain_chunk<32, false>(Rg, o, s, nj);
+      else if (base == 16)
+        chain_chunk<16, false>(Rg, o, s, nj);
       else
         chain_chunk<0, false>(Rg, o, s, nj);
     }
