@@ -605,14 +605,14 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
 // leaf: the per-leaf 16-B reads of a wave land on distinct banks)
 __device__ __forceinline__ int sb_pad(int e) { return e + 8 * (e >> 7); }
 
-// grid (nch, 5, items): y < 4 = the SSIM map of channel y, y = 4 the luma
+// grid (nch, channels, items) from channel ch0: ch < 4 = the SSIM map of channel ch, ch = 4 the luma
 // squared-difference stream (Y(a) - Y(b))^2 over H*W (utils/metrics.py:20 ->
 // skimage mean_squared_error)
-__global__ void __launch_bounds__(SB_THREADS) k_ss_chunks(SsimBatch B) {
+__global__ void __launch_bounds__(SB_THREADS) k_ss_chunks(SsimBatch B, const int ch0) {
   __shared__ double v[SB_NP_BUF + 8 * (SB_NP_BUF / 128)];
   __shared__ double wsum[4];
   __shared__ double lsum[2 * PW_MAXN];
-  const int ch = blockIdx.y, item = blockIdx.z, t = threadIdx.x;
+  const int ch = ch0 + (int)blockIdx.y, item = blockIdx.z, t = threadIdx.x;
   const long long n = ch < 4 ? B.ns : (long long)B.H * B.W;
   const long long c0 = (long long)blockIdx.x * SB_NP_BUF;
   if (c0 >= n) return;
@@ -849,13 +849,15 @@ hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const*
   hipError_t e;
   if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL((k_ss_band<SB_BH, false>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
+  // their maps' buffer sums there too, beside the luma work
+  hipLaunchKernelGGL(k_ss_chunks, dim3(B.nch_s, 3, items), dim3(SB_THREADS), 0, side, B, 0);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_ss_yplanes, dim3((unsigned)std::min<long long>((n + 255) / 256, SB_PLANE_BLOCKS), items),
                      dim3(256), 0, s, B);
   hipLaunchKernelGGL(k_ss_ychk<SB_BH>, dim3((W + 63) / 64, 5, items), dim3(64), 0, s, B);
   hipLaunchKernelGGL((k_ss_band<SB_BH, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
+  hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 2, items), dim3(SB_THREADS), 0, s, B, 3);  // luma map, luma MSE
   if ((e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 5, items), dim3(SB_THREADS), 0, s, B);
   hipLaunchKernelGGL(k_ss_final, dim3(5, items), dim3(256), 0, s, B);
   return hipGetLastError();
 }
