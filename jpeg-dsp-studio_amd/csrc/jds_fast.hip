@@ -1286,9 +1286,17 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
       uint32_t nw[4] = {0u, 0u, 0u, 0u};
       long long dnz = 0, dmb = 0;
       jds_frame_stats* fs = st + frame;
+      double qd[8], rq[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const int qn = (int)__builtin_rint(v[c] / fq[frame].q16[u * 8 + c]);
+        qd[c] = fq[frame].q16[u * 8 + c];
+        rq[c] = recip64(qd[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        // rint(v / Q) without an fp64 division (rint_quot: the division only
+        // when the product lies within |t| 2^-49 of a half-integer)
+        const int qn = rint_quot(v[c], qd[c], rq[c]);
         const int qo = (int16_t)((ow[c >> 1] >> ((c & 1) * 16)) & 0xffffu);
         nw[c >> 1] |= (uint32_t)(uint16_t)qn << ((c & 1) * 16);
         if (qn != qo) {
