@@ -876,7 +876,7 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
 // ------------------------------------------------------------ launchers --
 
 hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s);
-constexpr int FIX16_GRID = 4096;  // k_fix_fwd16 workgroups (x 4 blocks in flight)
+constexpr int FIX16_GRID = 8192;  // k_fix_fwd16 workgroups (x 4 blocks in flight; 4096: 87 -> 73 us at configs[4] 16x16)
 
 template <int MODE, bool PF>
 static hipError_t fast16_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coeffs, const FrameQ* fq,
