@@ -979,31 +979,34 @@ k_fwd444w(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
 // the frame's rare-bin row for the next run.
 constexpr int RROWS_TILES = 64;  // tiles per k_fwd_reduce_rows workgroup
 // FMT 0: k_fwd32i's 4-word records (8-bit fields); FMT 1: k_fwd444w's 8-word
-// records (16-bit fields, 24 coefficients per valid lane).  ptiles = slots per frame.
-template <int NREC, int FMT = 0>
-__global__ void __launch_bounds__(256)
-k_fwd_reduce_rows(const Geo g, jds_frame_stats* __restrict__ st, uint32_t* __restrict__ part, const int ptiles) {
-  constexpr int RT = RROWS_TILES;
+// records (16-bit fields, 24 coefficients per valid lane).  ptiles = slots per
+// frame.  One workgroup of NT threads reduces tiles [RT * slice, RT * slice +
+// RT) of frame f (k_fwd_reduce_rows: NT = 256, RT = 64; k_fix_fwd's reduction
+// workgroups: NT = 64, RT = 16).
+template <int NREC, int FMT, int NT, int RT>
+__device__ __forceinline__ void reduce_rows_wg(jds_frame_stats* __restrict__ st, uint32_t* __restrict__ part,
+                                               const int ptiles, const int nframes, const int f, const int slice,
+                                               unsigned (*s_acc)[11]) {
   constexpr int RW = FMT ? 8 : 4;  // words per record
-  __shared__ unsigned s_acc[4][11];
-  const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int t0 = blockIdx.x * RT, t1 = min(ptiles, t0 + RT);
+  constexpr int NW = NT / 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t0 = slice * RT, t1 = min(ptiles, t0 + RT);
   unsigned acc[11] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // bins 22..29, nz, mb, zeros
   const int nr = (t1 - t0) * NREC;
   // a fixed trip count with compile-time record arithmetic: every load issued before the first use
-  static_assert((RT * NREC) % 256 == 0, "whole record passes");
+  static_assert((RT * NREC) % NT == 0, "whole record passes");
   static_assert(RW * NREC <= PSLOT, "records fit the slot");
-  uint4 xs[RT * NREC / 256], ys[FMT ? RT * NREC / 256 : 1];
+  uint4 xs[RT * NREC / NT], ys[FMT ? RT * NREC / NT : 1];
 #pragma unroll
-  for (int it = 0; it < RT * NREC / 256; ++it) {
-    const int i = t + 256 * it;
+  for (int it = 0; it < RT * NREC / NT; ++it) {
+    const int i = t + NT * it;
     const int tile = t0 + i / NREC, r = i % NREC;
     const uint32_t* rec = part + ((size_t)f * ptiles + tile) * PSLOT + RW * r;
     xs[it] = i < nr ? *reinterpret_cast<const uint4*>(rec) : make_uint4(0u, 0u, 0u, 0u);
     if constexpr (FMT) ys[it] = i < nr ? *reinterpret_cast<const uint4*>(rec + 4) : make_uint4(0u, 0u, 0u, 0u);
   }
 #pragma unroll
-  for (int it = 0; it < RT * NREC / 256; ++it) {
+  for (int it = 0; it < RT * NREC / NT; ++it) {
     const uint4 x = xs[it];
     if constexpr (FMT == 0) {
 #pragma unroll
@@ -1036,30 +1039,45 @@ k_fwd_reduce_rows(const Geo g, jds_frame_stats* __restrict__ st, uint32_t* __res
     if (lane == 0) s_acc[w][k] = v;
   }
   __syncthreads();
+  auto wsum = [&](int k) {
+    unsigned long long v = 0ull;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) v += s_acc[q][k];
+    return v;
+  };
   jds_frame_stats* sf = st + f;
   if (t < 11) {
-    const unsigned long long v = (unsigned long long)s_acc[0][t] + s_acc[1][t] + s_acc[2][t] + s_acc[3][t];
+    const unsigned long long v = wsum(t);
     if (t < 8) {
       // bin 22 + t; zeros fall in bin 25 (k_finalize adds them back)
-      const unsigned long long z = t == 3 ? (unsigned long long)s_acc[0][10] + s_acc[1][10] + s_acc[2][10] + s_acc[3][10]
-                                          : 0ull;
+      const unsigned long long z = t == 3 ? wsum(10) : 0ull;
       if (v - z) atomicAdd((unsigned long long*)&sf->hist[22 + t], v - z);
     } else if (t == 8) {
       if (v) atomicAdd((unsigned long long*)&sf->nonzero, v);
     } else if (t == 9) {
-      const unsigned long long nz = (unsigned long long)s_acc[0][8] + s_acc[1][8] + s_acc[2][8] + s_acc[3][8];
+      const unsigned long long nz = wsum(8);
       if (v + nz) atomicAdd((unsigned long long*)&sf->magnitude_bits, v + nz);  // bit length + 1 per nonzero
     }
   }
-  if (blockIdx.x == 0 && t >= 64 && t < 64 + 50) {
-    unsigned* rr = part + (size_t)gridDim.y * ptiles * PSLOT + (size_t)f * 64;  // the frame's rare row
-    const int b = t - 64;
+  // slice 0 also adds the frame's rare-bin row and re-zeroes it for the next run
+  const int b = NT > 64 ? t - 64 : t - 14;
+  if (slice == 0 && b >= 0 && b < 50) {
+    unsigned* rr = part + (size_t)nframes * ptiles * PSLOT + (size_t)f * 64;  // the frame's rare row
     const unsigned v = rr[2 + b];
     if (v) {
       atomicAdd((unsigned long long*)&sf->hist[b], (unsigned long long)v);
       rr[2 + b] = 0u;
     }
   }
+}
+
+template <int NREC, int FMT = 0>
+__global__ void __launch_bounds__(256)
+k_fwd_reduce_rows(const Geo g, jds_frame_stats* __restrict__ st, uint32_t* __restrict__ part, const int ptiles) {
+  __shared__ unsigned s_acc[4][11];
+  (void)g;
+  reduce_rows_wg<NREC, FMT, 256, RROWS_TILES>(st, part, ptiles, (int)gridDim.y, (int)blockIdx.y, (int)blockIdx.x,
+                                              s_acc);
 }
 
 // words of the statistics partials a single-quality 8x8 plan needs (tile slots
@@ -1130,12 +1148,28 @@ k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ 
 //   many workgroups as it has entries.  Each workgroup prefix-sums the n list
 //   lengths in LDS (dynamic, 4 (n + 1) bytes) and maps its entry index to
 //   (item, slot) by binary search.
-template <int MODE, bool PF>
+// NRED > 0 (single-quality plans): the last nred workgroups of each item's row
+// are the statistics reduction instead (k_fwd_reduce_rows' work, 16 tiles of
+// NRED row records each, 64 threads): both roles only add into the frame
+// statistics, and the latency-bound reduction runs beside the latency-bound
+// fix-up instead of after it, one launch fewer.
+constexpr int FIX_RED_TILES = 16;
+template <int MODE, bool PF, int NRED = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
           const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq, const int n_flat,
-          unsigned* __restrict__ rearm) {
+          unsigned* __restrict__ rearm, uint32_t* __restrict__ part = nullptr, const int ptiles = 0,
+          const int nred = 0) {
+  const int gfix = (int)gridDim.x - nred;  // the fix-up role's workgroups per item
+  if constexpr (NRED > 0) {
+    if ((int)blockIdx.x >= gfix) {  // (uniform) the reduction role
+      __shared__ unsigned s_acc[1][11];
+      reduce_rows_wg<NRED, 0, 64, FIX_RED_TILES>(st, part, ptiles, (int)gridDim.y, (int)blockIdx.y,
+                                                  (int)blockIdx.x - gfix, s_acc);
+      return;
+    }
+  }
   constexpr bool CPLANE = (MODE != M444) && PF;
   constexpr int SY = Cfg<MODE>::SY;
   constexpr int WRR = 8 * SY + 2, WCC = 18;  // prefilter source window of one chroma block
@@ -1182,7 +1216,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
     if (rearm != nullptr && blockIdx.x == 0 && t == 0) rearm[blockIdx.y] = 0u;
   }
   const double k[3] = {gk[0], gk[1], gk[2]};
-  for (unsigned e = blockIdx.x; e < count; e += gridDim.x) {
+  for (unsigned e = blockIdx.x; e < count; e += (unsigned)gfix) {
     uint2 ent;
     if (n_flat) {  // entry e of the concatenated lists: item = last start <= e
       int lo = 0, hi = n_flat - 1;
@@ -1193,7 +1227,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
       ent = list[(size_t)lo * cap + (e - s_off[lo])];
     } else {
       ent = next;
-      if (e + gridDim.x < count) next = list[e + gridDim.x];
+      if (e + gfix < count) next = list[e + gfix];
     }
     const int frame = (int)ent.x;
     const int plane = (int)(ent.y >> 24);
@@ -1555,20 +1589,19 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
   }
   const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
   if (!mq) {
-    // single quality: the statistics partials into the frame stats (reset by
-    // the front-end launch above); k_fix_fwd reads the live counter bank `par`
-    // the front end appended to and re-arms the other bank.  (Reducing the
-    // partials inside k_fix_fwd instead of this launch measured slower: 49.4
-    // vs 29.1 + 5.4 us per 64 x 1080p; the reduction on a side stream beside
-    // the fix-up, 0.627 vs 0.617 ms per step: the fork / join costs more than
-    // the overlap returns.)
+    // single quality: one launch fixes the listed blocks and reduces the
+    // statistics partials into the frame stats (reset by the front-end launch
+    // above) in workgroups of their own (k_fix_fwd's NRED role); it reads the
+    // live counter bank `par` the front end appended to and re-arms the other
+    // bank.  Per 64 x 1080p: 31.4-32.1 us against 28.1 + 11.5 us as two
+    // launches (same box, interleaved).  (Earlier forms: the reduction done by
+    // the fix-up workgroups themselves, 49.4 vs 29.1 + 5.4 us; on a side
+    // stream beside the fix-up, 0.627 vs 0.617 ms per step: the fork / join
+    // costs more than the overlap returns.)
     static_assert(C::TF <= 64 * NW_MAX, "row records fit the tile slot");
-    hipLaunchKernelGGL(k_fwd_reduce_rows<4 * (C::TF / 64)>, dim3((ptiles + RROWS_TILES - 1) / RROWS_TILES, n),
-                       dim3(256), 0, s, g, st, part, ptiles);
-    kmark(s, "k_fwd_reduce_rows<%d>", 4 * (C::TF / 64));
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
-                       fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
+    const int nred = (ptiles + FIX_RED_TILES - 1) / FIX_RED_TILES;
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF, 4 * (C::TF / 64)>), dim3(gx + nred, n), dim3(64), 0, s, g, rgb, coeffs,
+                       fq, gk, st, fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ptiles, nred);
     kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;
