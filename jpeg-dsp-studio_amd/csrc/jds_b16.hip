@@ -737,7 +737,7 @@ int tile_dims16(int mode, int* MY, int* MX) {
 }
 
 hipError_t launch_inv16_fast(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
-                             uint8_t* rgb_out, const InvFix& fx, hipStream_t s);
+                             uint8_t* rgb_out, const InvFix& fx, hipStream_t s, jds_frame_stats* st, int fin);
 
 template <int MODE>
 static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coeffs,
@@ -747,6 +747,9 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
   using C = Cfg16<MODE>;
   const dim3 grid(g.tiles_y * g.tiles_x, n);
   hipError_t e = hipSuccess;
+  // the certified fast inverse (RGB only) finalizes the frame statistics
+  // itself: no k_fwd_finish / k_finalize launches around it
+  const bool fast_inv = (phases & 2) && MODE != M444 && fx && !(want_sse || err_y);
   if (phases & 1) {
     if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
     if (ff)  // certified fp32 forward + exact fix-up of the listed blocks (jds_fast16.hip)
@@ -758,7 +761,7 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
       hipLaunchKernelGGL((k_fwd16<MODE, false>), grid, dim3(C::TF), 0, s, g, rgb, coeffs, fq, gk, st);
     if (!ff) kmark(s, "k_fwd16<%d,%d>", MODE, (int)(MODE != M444 && pf));
     if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_fwd_finish(g, n, st, nullptr, 0, s)) != hipSuccess) return e;
+    if (!fast_inv && (e = launch_fwd_finish(g, n, st, nullptr, 0, s)) != hipSuccess) return e;
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
   }
   if (phases & 2) {
@@ -769,8 +772,8 @@ static hipError_t launch16_t(bool pf, const Geo& g, int n, const uint8_t* rgb, u
       const int tx = (g.W + I::TW - 1) / I::TW;
       tiles = ((g.H + I::TH - 1) / I::TH) * tx;
       const dim3 gi(tiles, n), bi(I::NT);
-      if (fx && !rin) {  // RGB only: the certified fast inverse (jds_inv_fast.hip)
-        if ((e = launch_inv16_fast(MODE, g, n, coeffs, fq, rgb_out, *fx, s)) != hipSuccess) return e;
+      if (fast_inv) {  // RGB only: the certified fast inverse (jds_inv_fast.hip), zero bin if this run's forward deferred it
+        return launch_inv16_fast(MODE, g, n, coeffs, fq, rgb_out, *fx, s, st, (phases & 1) ? 1 : 0);
       } else {
 #define K_INV16 k_inv16s
       if (err_y)

@@ -1154,7 +1154,7 @@ k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ 
 // statistics, and the latency-bound reduction runs beside the latency-bound
 // fix-up instead of after it, one launch fewer.
 constexpr int FIX_RED_TILES = 16;
-template <int MODE, bool PF, int NRED = 0>
+template <int MODE, bool PF, int NRED = 0, int RFMT = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
@@ -1165,7 +1165,7 @@ k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ co
   if constexpr (NRED > 0) {
     if ((int)blockIdx.x >= gfix) {  // (uniform) the reduction role
       __shared__ unsigned s_acc[1][11];
-      reduce_rows_wg<NRED, 0, 64, FIX_RED_TILES>(st, part, ptiles, (int)gridDim.y, (int)blockIdx.y,
+      reduce_rows_wg<NRED, RFMT, 64, FIX_RED_TILES>(st, part, ptiles, (int)gridDim.y, (int)blockIdx.y,
                                                   (int)blockIdx.x - gfix, s_acc);
       return;
     }
@@ -1532,12 +1532,10 @@ static hipError_t fast_fwd_t(const Geo& g, int n, int nq, const uint8_t* rgb, in
     if (e != hipSuccess) return e;
     const int gx = FIX_GRID / n > 1 ? FIX_GRID / n : 1;
     static_assert(F444_WAVES * 4 == 16, "16 row records per k_fwd444w workgroup");
-    hipLaunchKernelGGL((k_fwd_reduce_rows<16, 1>), dim3((ng + RROWS_TILES - 1) / RROWS_TILES, n), dim3(256), 0, s, g,
-                       st, part, ng);
-    kmark(s, "k_fwd_reduce_rows<16,1>");
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_fix_fwd<MODE, PF>), dim3(gx, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
-                       fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n);
+    // the fix-up and the statistics reduction in one launch (k_fix_fwd's NRED role)
+    const int nred = (ng + FIX_RED_TILES - 1) / FIX_RED_TILES;
+    hipLaunchKernelGGL((k_fix_fwd<MODE, PF, 16, 1>), dim3(gx + nred, n), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st,
+                       fixlist, fixcount + par * n, nq, 0, fixcount + (par ^ 1) * n, part, ng, nred);
     kmark(s, "k_fix_fwd<%d,%d>", MODE, (int)PF);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return finish ? launch_fwd_finish(g, n, st, nullptr, 0, s) : hipSuccess;

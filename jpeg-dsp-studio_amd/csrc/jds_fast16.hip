@@ -784,19 +784,43 @@ __device__ __forceinline__ void fix_column(const uint8_t* __restrict__ img, cons
   }
 }
 
+// Workgroups past the first gfix (gridDim.x - n * per) are the statistics
+// reduction instead (k_fwd_reduce's work, one launch fewer): workgroup r sums
+// tiles [64 s, 64 s + 64) of frame r / per (s = r % per) of k_fwd16f's per-tile
+// partials, lane j < 52 statistic j, one u64 atomic per statistic; both roles
+// only add into the frame statistics.
+constexpr int FIX16_RED_TILES = 64;
 template <int MODE, bool PF>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
             const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
             const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, unsigned* __restrict__ fixlen,
-            const unsigned cap) {
+            const unsigned cap, const uint32_t* __restrict__ part, const int ptiles, const int nframes) {
+  const int per = (ptiles + FIX16_RED_TILES - 1) / FIX16_RED_TILES;
+  const int gfix = (int)gridDim.x - nframes * per;
+  if ((int)blockIdx.x >= gfix) {  // (uniform) the reduction role
+    const int r = (int)blockIdx.x - gfix, f = r / per, t0 = (r - f * per) * FIX16_RED_TILES;
+    const int j = threadIdx.x, nt = min(FIX16_RED_TILES, ptiles - t0);
+    if (j < 52) {
+      const uint32_t* src = part + ((size_t)f * ptiles + t0) * 52 + j;
+      unsigned long long a = 0ull;
+#pragma unroll 16
+      for (int i = 0; i < nt; ++i) a += src[(size_t)i * 52];
+      jds_frame_stats* sf = st + f;
+      unsigned long long* dst = j == 0 ? (unsigned long long*)&sf->nonzero
+                                : j == 1 ? (unsigned long long*)&sf->magnitude_bits
+                                         : (unsigned long long*)&sf->hist[j - 2];
+      if (a) atomicAdd(dst, a);
+    }
+    return;
+  }
   __shared__ double s_b[4 * 272];  // four blocks, rows of 17 (jds_b16.hip's BS16 layout)
   const int lane = threadIdx.x, grp = lane >> 4, line = lane & 15;
   const unsigned c = *fixcount;
   const unsigned count = c < cap ? c : cap;
   const double k[3] = {gk[0], gk[1], gk[2]};
   double* const sb = s_b + grp * 272;
-  for (unsigned e0 = blockIdx.x * 4u; e0 < count; e0 += gridDim.x * 4u) {
+  for (unsigned e0 = blockIdx.x * 4u; e0 < count; e0 += (unsigned)gfix * 4u) {
     const unsigned e = e0 + (unsigned)grp;
     const bool act = e < count;  // uniform per 16-lane group
     int frame = 0, plane = 0, bidx = 0, gy = 0, gx = 0;
@@ -875,7 +899,6 @@ k_fix_fwd16(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ 
 
 // ------------------------------------------------------------ launchers --
 
-hipError_t launch_fwd_reduce(int n, jds_frame_stats* st, const uint32_t* part, int ptiles, hipStream_t s);
 constexpr int FIX16_GRID = 8192;  // k_fix_fwd16 workgroups (x 4 blocks in flight; 4096: 87 -> 73 us at configs[4] 16x16)
 
 template <int MODE, bool PF>
@@ -891,11 +914,12 @@ static hipError_t fast16_t(const Geo& g, int n, const uint8_t* rgb, int16_t* coe
   kmark(s, "k_fwd16f<%d,%d>", MODE, (int)PF);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_fix_fwd16<MODE, PF>), dim3(FIX16_GRID), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st, fixlist,
-                     counters + parity, counters + 2, cap);
+  // the fix-up and the per-tile partials' reduction (order-free: u64 atomics) in one launch
+  const int nred = n * ((tiles + FIX16_RED_TILES - 1) / FIX16_RED_TILES);
+  hipLaunchKernelGGL((k_fix_fwd16<MODE, PF>), dim3(FIX16_GRID + nred), dim3(64), 0, s, g, rgb, coeffs, fq, gk, st,
+                     fixlist, counters + parity, counters + 2, cap, part, tiles, n);
   kmark(s, "k_fix_fwd16<%d,%d>", MODE, (int)PF);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_fwd_reduce(n, st, part, tiles, s);  // the per-tile partials (order-free: u64 atomics)
+  return hipGetLastError();
 }
 
 // counters: [0..1] list lengths (this run appends to [parity]), [2] the run's length

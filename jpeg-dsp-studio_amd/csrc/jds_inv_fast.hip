@@ -923,7 +923,8 @@ template <int MODE>
 __global__ void __launch_bounds__(Inv16<MODE>::NT)
 k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
              uint8_t* __restrict__ rgb_out, unsigned* __restrict__ fixcount, unsigned* __restrict__ next_count,
-             unsigned* __restrict__ item_cnt, const int rot, const int fix_all) {
+             unsigned* __restrict__ item_cnt, const int rot, const int fix_all, jds_frame_stats* __restrict__ st,
+             const int fin) {
   using I = Inv16<MODE>;
   static_assert(I::NT == 256, "one table entry per thread");
   __shared__ __attribute__((aligned(16))) double s_b[I::NG * BS16];
@@ -936,6 +937,9 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
   __shared__ int s_redo;
   const int tid = threadIdx.x, grp = tid >> 4, line = tid & 15;
   const int frame = blockIdx.y, tile = blockIdx.x;
+  // k_finalize's per-frame work (fin >= 0: the run's forward phase completed
+  // before this launch; fin = 1 also adds the histogram's zero bin)
+  if (fin >= 0 && tile == 0 && tid == 0) finalize_frame(g, st + frame, fin);
   const unsigned n_items = gridDim.y;
   unsigned* cnt_now = item_cnt + rot * n_items;
   if (tile == 0 && tid == 0) {
@@ -1139,11 +1143,11 @@ k_inv16_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs,
 }
 
 hipError_t launch_inv16_fast(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
-                             uint8_t* rgb_out, const InvFix& fx, hipStream_t s) {
+                             uint8_t* rgb_out, const InvFix& fx, hipStream_t s, jds_frame_stats* st, int fin) {
   auto go = [&](auto kern, int TH, int TW) {
     const int tx = (g.W + TW - 1) / TW, ty = (g.H + TH - 1) / TH;
     hipLaunchKernelGGL(kern, dim3(ty * tx, n), dim3(256), 0, s, g, tx, coeffs, fq, rgb_out, fx.count + fx.parity,
-                       fx.count + (fx.parity ^ 1), fx.item, fx.rot, fx.fix_all);
+                       fx.count + (fx.parity ^ 1), fx.item, fx.rot, fx.fix_all, st, fin);
     kmark(s, "k_inv16_fast<%d>", mode);
     return hipGetLastError();
   };
