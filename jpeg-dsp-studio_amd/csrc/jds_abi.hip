@@ -33,9 +33,12 @@ hipError_t stage_area_gen(const double* in, int H, int W, const AreaTap* ytab, c
                           int oh, int ow, hipStream_t s);
 hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const* b, int items, int H, int W,
                                   double c1, double c2, double* scratch, double* out, int out_stride,
-                                  unsigned long long* sse, hipStream_t s, hipStream_t side, hipEvent_t fork,
-                                  hipEvent_t join);
+                                  unsigned long long* sse, hipStream_t s, bool rgb, hipStream_t side,
+                                  hipEvent_t fork, hipEvent_t join);
+hipError_t launch_ssim_rgb(const void* pairs_dev, int items, int H, int W, double c1, double c2, double* scratch,
+                           double* out, int out_stride, hipStream_t s);
 size_t ssim_batch_scratch_doubles(int H, int W);
+size_t ssim_rgb_scratch_doubles(int H, int W);
 int ssim_batch_max_items();
 hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
 size_t mag_scratch_bytes(long long nblocks, int max_chunks);
@@ -137,19 +140,26 @@ struct jds_ctx {
   // the statistics kernels (SSIM, float32 magnitude bits) of the same call
   hipStream_t xfer = nullptr;
   hipEvent_t xfer_ev = nullptr;
-  // SSIM: the RGB channels' band kernel runs on a stream of its own beside the
-  // luma planes, chains and band (jds_ssim_band.hip)
+  // SSIM: the R, G, B rows kernels run on a stream of its own beside the luma
+  // planes, chains and band (jds_ssim_band.hip); ss_pairs: the batch's image
+  // pointers (pinned host staging, device copy)
   hipStream_t ss_side = nullptr;
   hipEvent_t ss_fork = nullptr, ss_join = nullptr;
+  void* ss_pairs_host = nullptr;
+  size_t ss_pairs_cap = 0;
   // host-path scratch
   DevBuf rgb, out, coeffs, stats, part, fq, gk, erry, errrgb, sel;
   DevBuf ss_planes, ss_out, img_a, img_b;  // ss_planes: k_ss_* scratch
+  DevBuf ss_rgb, ss_pairs;                 // k_ss_rows / k_ss_rgbsum scratch, device pair array
   DevBuf st[5];  // per-stage API staging
   DevBuf chunks;
   DevBuf planes;  // 16x16 path: reconstructed chroma planes
   DevBuf ent[8], ent_hdr, ent_tab, ent_cf, ent_out, ent_meta;  // entropy coder (jds_encode_jfif)
   DevBuf gen_tab, gen_sub, gen_rec;  // general-geometry path (jds_gen.hip)
 };
+
+// batches from this size take the R, G, B rows kernel (jds_ssim_band.hip)
+constexpr int SSIM_ROWS_MIN = 32;
 
 // SSIM of `items` image pairs (K4, jds_ssim_band.hip) on the context's stream:
 // out[i * out_stride + 0..4] = SSIM R, G, B, Y, MSE of Y (device doubles);
@@ -159,7 +169,8 @@ static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const 
                           double* out, int out_stride, unsigned long long* sse) {
   const int per = ssim_batch_max_items();
   const size_t each = ssim_batch_scratch_doubles(H, W) * sizeof(double);
-  // scratch for up to `per` items, at most ~2 GB (1080p: ~110 MB per item)
+  // luma (and small batches' RGB) scratch for up to `per` items, at most ~2 GB
+  // (1080p: ~110 MB per item)
   int group = (int)std::max<size_t>(1, std::min<size_t>((size_t)per, ((size_t)2 << 30) / each));
   group = std::min(group, items);
   HIP_TRY(c->ss_planes.ensure(each * group));
@@ -169,12 +180,50 @@ static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const 
     HIP_TRY(hipEventCreateWithFlags(&c->ss_join, hipEventDisableTiming));
   }
   if (sse) HIP_TRY(hipMemsetAsync(sse, 0, sizeof(unsigned long long) * items, c->stream));
+  // R, G, B: batches of SSIM_ROWS_MIN items or more take the rows kernel (one
+  // lane per map row, every item in one launch: its grid fills the chip only
+  // with many items); smaller ones the band kernel beside each luma group
+  const bool rows = items >= SSIM_ROWS_MIN;
+  if (rows) {
+    // as many items per launch as ~4 GB of scratch holds (1080p: ~4 MB per item)
+    const size_t each_rgb = ssim_rgb_scratch_doubles(H, W) * sizeof(double);
+    const int group_rgb = (int)std::min<size_t>((size_t)items, std::max<size_t>(1, ((size_t)4 << 30) / each_rgb));
+    HIP_TRY(c->ss_rgb.ensure(each_rgb * group_rgb));
+    // the pair array: pinned staging (reused only after the previous call's
+    // final synchronisation) -> device, on the context's stream
+    const size_t pbytes = sizeof(const void*) * 2 * (size_t)items;
+    if (c->ss_pairs_cap < pbytes) {
+      if (c->ss_pairs_host) HIP_TRY(hipHostFree(c->ss_pairs_host));
+      c->ss_pairs_host = nullptr;
+      c->ss_pairs_cap = 0;
+      HIP_TRY(hipHostMalloc(&c->ss_pairs_host, pbytes, hipHostMallocDefault));
+      c->ss_pairs_cap = pbytes;
+    }
+    const void** ph = (const void**)c->ss_pairs_host;
+    for (int i = 0; i < items; ++i) {
+      ph[2 * i] = a[i];
+      ph[2 * i + 1] = b[i];
+    }
+    HIP_TRY(c->ss_pairs.ensure(pbytes));
+    HIP_TRY(hipMemcpyAsync(c->ss_pairs.p, ph, pbytes, hipMemcpyHostToDevice, c->stream));
+    // on the side stream (after the copy and the stream's earlier work), beside
+    // the luma groups on the context's stream; joined at the end
+    HIP_TRY(hipEventRecord(c->ss_fork, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->ss_side, c->ss_fork, 0));
+    for (int i0 = 0; i0 < items; i0 += group_rgb) {
+      const int k = std::min(group_rgb, items - i0);
+      HIP_TRY(launch_ssim_rgb((const char*)c->ss_pairs.p + sizeof(const void*) * 2 * (size_t)i0, k, H, W, SSIM_C1,
+                              SSIM_C2, (double*)c->ss_rgb.p, out + (size_t)i0 * out_stride, out_stride, c->ss_side));
+    }
+    HIP_TRY(hipEventRecord(c->ss_join, c->ss_side));
+  }
   for (int i0 = 0; i0 < items; i0 += group) {
     const int k = std::min(group, items - i0);
     HIP_TRY(launch_psnr_ssim_batch(a + i0, b + i0, k, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_planes.p,
-                                   out + (size_t)i0 * out_stride, out_stride, sse ? sse + i0 : nullptr,
-                                   c->stream, c->ss_side, c->ss_fork, c->ss_join));
+                                   out + (size_t)i0 * out_stride, out_stride, sse ? sse + i0 : nullptr, c->stream,
+                                   !rows, c->ss_side, c->ss_fork, c->ss_join));
   }
+  if (rows) HIP_TRY(hipStreamWaitEvent(c->stream, c->ss_join, 0));
   return JDS_OK;
 }
 
@@ -459,6 +508,9 @@ void jds_ctx_destroy(jds_ctx* c) {
   }
   if (c->ss_fork) (void)hipEventDestroy(c->ss_fork);
   if (c->ss_join) (void)hipEventDestroy(c->ss_join);
+  if (c->ss_pairs_host) (void)hipHostFree(c->ss_pairs_host);
+  c->ss_rgb.release();
+  c->ss_pairs.release();
   DevBuf* bufs[] = {&c->rgb,     &c->out,    &c->coeffs,    &c->stats,  &c->part,  &c->fq,   &c->gk,  &c->erry,
                     &c->errrgb,  &c->sel,    &c->ss_planes, &c->ss_out, &c->img_a, &c->img_b};
   for (DevBuf* b : bufs) b->release();

@@ -599,6 +599,317 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   }
 }
 
+// --------------------------------------------------- RGB rows (k_ss_rows) --
+//
+// The R, G, B channels' SSIM maps, one lane per map row: every axis-0 window
+// sum is an exact integer (order-free), so a lane forms its row's axis-0
+// outputs A_q(j) = RN(S_q(j) / 7) column by column from the 7 input rows
+// around it, carries scipy's axis-1 running sums s_q(j) = s_q(j - 1) +
+// (A_q(j + 3) - A_q(j - 4)) itself (the last 8 columns' integer window sums in
+// a register ring, 4 words per column: A(j - 4) is recomputed, exactly, rather
+// than held as 5 doubles) and evaluates the map at once.  No exchange between
+// lanes, one barrier per 16-column chunk (the staging of both images' 70
+// input rows through LDS).  A workgroup is 64 map rows x 3 channels (a wave per
+// channel); one launch covers every item of the batch (device pair array), so
+// the grid holds ~50 waves per 1080p item instead of the band kernel's
+// latency-bound chain phases.
+//
+// The NumPy mean is folded in: the map stream (C order over the cropped map)
+// is summed in 8192-element buffers by pairwise_sum, whose leaves are the
+// 128-element aligned runs; a lane sums the leaves that lie inside its row
+// (eight accumulators by element index mod 8, NumPy's leaf order) and writes
+// one double per leaf; the elements of leaves that cross a row boundary, and
+// the last partial buffer, are written raw (k_ss_rgbsum sums them).
+constexpr int SR_ROWS = 64;                                    // map rows per workgroup (a lane each)
+constexpr int SR_IN = SR_ROWS + 6;                             // input rows staged
+constexpr int SR_CW = 16;                                      // columns per staged chunk
+constexpr int SR_RW = 13;                                      // dwords per staged row (48 B + <= 3 misaligned)
+constexpr int SR_THREADS = 192;                                // three channels
+constexpr int SR_NE = 2 * SR_IN * SR_RW;                       // dwords per chunk (both images)
+constexpr int SR_SE = (SR_NE + SR_THREADS - 1) / SR_THREADS;   // per thread
+
+struct RgbBatch {
+  const SsimPair* pairs;  // [items] (device)
+  int H, W, cw;           // cw = W - 6
+  int nfull, mpart;       // full 8192-element buffers of a map stream; elements of the last, partial one
+  long long ns, efull;    // ns = (H - 6) * cw; efull = 8192 * nfull
+  double c1, c2, cov_norm;
+  double* lsum;           // [item][3][lsum_pitch]: sums of the leaves inside one map row
+  double* raws;           // [item][3][raws_pitch]: elements of row-crossing leaves, 128 per slot
+  double* rawp;           // [item][3][8192]: the partial buffer's elements
+  double* chunks;         // [item][3][nfull + 1]: buffer sums
+  double* out;            // [item][out_stride]: ssim R, G, B
+  int out_stride;
+  long long lsum_pitch, raws_pitch;
+  PwTree tree;            // the partial buffer's pairwise tree
+};
+
+// slot of a row-crossing leaf starting at element e0: rows of >= 128 elements
+// are crossed by one leaf per row boundary (slot = the row it ends in); narrow
+// maps take a slot per leaf
+__host__ __device__ __forceinline__ long long rs_slot(long long e0, int cw) { return cw >= 128 ? (e0 + 127) / cw : e0 >> 7; }
+
+// the map value of one pixel from its five axis-1 running sums (skimage
+// structural_similarity with the sample covariance; k_ss_band's order)
+__device__ __forceinline__ double ssim_px(const double (&s)[5], double c1, double c2, double cov_norm) {
+  const double ux = div7(s[0]), uy = div7(s[1]);
+  const double uxx = div7(s[2]), uyy = div7(s[3]);
+  const double uxy = div7(s[4]);
+  const double vx = cov_norm * (uxx - ux * ux);
+  const double vy = cov_norm * (uyy - uy * uy);
+  const double vxy = cov_norm * (uxy - ux * uy);
+  const double a1 = 2 * ux * uy + c1, a2 = 2 * vxy + c2;
+  const double b1 = ux * ux + uy * uy + c1, b2 = vx + vy + c2;
+  const double d = b1 * b2;
+  return (a1 * a2) / d;
+}
+
+__global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu(3))) k_ss_rows(RgbBatch B) {
+  __shared__ uint32_t L[2][2][SR_IN][SR_RW];  // [buffer][image][input row][dword]
+  __shared__ double LF[8][SR_THREADS];          // the current leaf's eight accumulators, per lane
+  const int rb = blockIdx.x, item = blockIdx.y, t = threadIdx.x;
+  const int ch = t >> 6, lane = t & 63;
+  const int H = B.H, W = B.W, cw = B.cw;
+  const int R0 = rb * SR_ROWS;  // map row R0 + lane reads input rows R0 + lane .. + 6
+  const int r = R0 + lane;
+  const bool rowok = r < H - 6;
+  const SsimPair pr = B.pairs[item];
+  const long long nbytes = (long long)H * W * 3;
+  const size_t ic = (size_t)item * 3 + ch;
+  double* lsum = B.lsum + ic * B.lsum_pitch;
+  double* raws = B.raws + ic * B.raws_pitch;
+  double* rawp = B.rawp + ic * SB_NP_BUF;
+  const int nchunks = (W + SR_CW - 1) / SR_CW;
+
+  // staging: element e = (image, input row, dword) of a chunk.  Every load is
+  // an unconditional global dword load (addresses past the image's last whole
+  // dword are clamped to it: those bytes belong to columns >= W, never used),
+  // all in flight together; the image's last, partial dword (H W 3 not a
+  // multiple of 4) is patched from bytes afterwards
+  typedef const uint32_t __attribute__((address_space(1)))* gdw;
+  const long long alast = (nbytes & ~3LL) - 4;  // the last whole dword (H W 3 >= 147)
+  uint32_t v[SR_SE];
+  auto issue = [&](int k) {
+    const long long j0 = (long long)k * SR_CW;
+    unsigned partial = 0u;
+#pragma unroll
+    for (int i = 0; i < SR_SE; ++i) {
+      const int e = t + i * SR_THREADS;
+      const int im = e >= SR_IN * SR_RW ? 1 : 0, rem = e - im * SR_IN * SR_RW;
+      const int rr = rem / SR_RW, d = rem - rr * SR_RW;
+      const long long grow = min(R0 + rr, H - 1);
+      const long long a = ((grow * W + j0) * 3 & ~3LL) + 4 * d;
+      const uint8_t* img = im ? pr.b : pr.a;
+      v[i] = *(gdw)(img + (a < alast ? a : alast));
+      if (e < SR_NE && a > alast && a < nbytes) partial |= 1u << i;
+    }
+    if (partial) {  // (rare: the last row's last chunk)
+#pragma unroll
+      for (int i = 0; i < SR_SE; ++i) {
+        if (partial & (1u << i)) {
+          const int e = t + i * SR_THREADS;
+          const int im = e >= SR_IN * SR_RW ? 1 : 0, rem = e - im * SR_IN * SR_RW;
+          const int rr = rem / SR_RW, d = rem - rr * SR_RW;
+          const long long grow = min(R0 + rr, H - 1);
+          const long long a = ((grow * W + j0) * 3 & ~3LL) + 4 * d;
+          const uint8_t* img = im ? pr.b : pr.a;
+          uint32_t x = 0u;
+          for (int q = 0; q < 4; ++q)
+            if (a + q < nbytes) x |= (uint32_t)img[a + q] << (8 * q);
+          v[i] = x;
+        }
+      }
+    }
+  };
+  auto commit = [&](int k) {
+    uint32_t* dst = &L[k & 1][0][0][0];
+#pragma unroll
+    for (int i = 0; i < SR_SE; ++i) {
+      const int e = t + i * SR_THREADS;
+      if (e < SR_NE) dst[e] = v[i];
+    }
+  };
+  // byte offset of this lane's 7 rows within their staged dwords (a chunk
+  // starts 96 k bytes further: the same offset mod 4)
+  int mis[7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) mis[q] = (int)(((long long)min(r + q, H - 1) * W * 3) & 3) + ch;
+
+  // this map row's stream elements [rs, re); whole leaves in [hs, te)
+  const long long rs = (long long)r * cw, re = rs + cw;
+  const long long hs = (rs + 127) & ~127LL, te = re & ~127LL;
+
+  issue(0);
+  commit(0);
+  __syncthreads();
+  // the window sums of the last 7 columns (a shift register, oldest first):
+  // x | y << 16, xx, yy, xy
+  int rw[4][7];
+  double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  auto a_of = [](int v) { return div7((double)v); };
+  auto a_q = [&](int q, int u) {  // the axis-0 output of quantity q, ring entry u
+    return a_of(q == 0 ? (rw[0][u] & 0xffff) : q == 1 ? (rw[0][u] >> 16) : rw[q - 1][u]);
+  };
+  // the window sums of column jj of the staged chunk (buffer kb)
+  auto wsum = [&](int kb, int jj, int (&n)[4]) {
+    const uint8_t* ra = reinterpret_cast<const uint8_t*>(&L[kb][0][lane][0]) + 3 * jj;
+    const uint8_t* rbp = reinterpret_cast<const uint8_t*>(&L[kb][1][lane][0]) + 3 * jj;
+    int sx = 0, sy = 0, sxx = 0, syy = 0, sxy = 0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int x = ra[q * (SR_RW * 4) + mis[q]], y = rbp[q * (SR_RW * 4) + mis[q]];
+      sx += x;
+      sy += y;
+      sxx += x * x;
+      syy += y * y;
+      sxy += x * y;
+    }
+    n[0] = sx | (sy << 16);
+    n[1] = sxx;
+    n[2] = syy;
+    n[3] = sxy;
+  };
+  // the map value of column jn - 3 (stream element rs + jn - 6) into its leaf,
+  // or raw (leaves that cross a row boundary: slot r for the head of this row,
+  // r + 1 for its tail; narrow maps a slot per leaf)
+  auto emit = [&](int jn) {
+    if (!rowok) return;
+    const double m = ssim_px(s, B.c1, B.c2, B.cov_norm);
+    const long long e = rs + (jn - 6);
+    if (e >= B.efull) {
+      rawp[e - B.efull] = m;
+    } else if (e < hs || e >= te) {
+      const long long slot = cw >= 128 ? (e < hs ? r : r + 1) : (e >> 7);
+      raws[slot * 128 + (e & 127)] = m;
+    } else {
+      // NumPy's leaf: accumulator e mod 8 starts at the leaf's first 8
+      // elements and adds every 8th after them; the sum once the leaf is full
+      const int p = (int)(e & 127), kq = p & 7;
+      const double a = p < 8 ? m : LF[kq][t] + m;
+      LF[kq][t] = a;
+      if (p == 127) {
+        double rk[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) rk[kk] = kk == 7 ? a : LF[kk][t];
+        lsum[e >> 7] = ((rk[0] + rk[1]) + (rk[2] + rk[3])) + ((rk[4] + rk[5]) + (rk[6] + rk[7]));
+      }
+    }
+  };
+
+  // chunk 0, columns 0 .. 6: scipy's first window (W >= 7): reflect(-3 .. 3) =
+  // 2, 1, 0, 0, 1, 2, 3, then outputs 1 .. 3 take their old column from
+  // reflect(-3 .. -1) = 2, 1, 0
+  if (1 < nchunks) issue(1);
+#pragma unroll
+  for (int u = 0; u < 7; ++u) {
+    int n[4];
+    wsum(0, u, n);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) rw[w][u] = n[w];
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    double x = 0.0;
+    x = x + a_q(q, 2);
+    x = x + a_q(q, 1);
+    x = x + a_q(q, 0);
+    x = x + a_q(q, 0);
+    x = x + a_q(q, 1);
+    x = x + a_q(q, 2);
+    x = x + a_q(q, 3);
+    x = x + (a_q(q, 4) - a_q(q, 2));
+    x = x + (a_q(q, 5) - a_q(q, 1));
+    x = x + (a_q(q, 6) - a_q(q, 0));
+    s[q] = x;
+    __builtin_amdgcn_sched_barrier(0);  // one quantity's window at a time (registers)
+  }
+  emit(6);
+  // then column jn enters, column jn - 7 (the register's oldest) leaves
+  for (int k = 0; k < nchunks; ++k) {
+    if (k > 0 && k + 1 < nchunks) issue(k + 1);
+#pragma unroll 1
+    for (int jj = k == 0 ? 7 : 0; jj < SR_CW; ++jj) {
+      const int jn = k * SR_CW + jj;  // (uniform)
+      if (jn >= W) break;
+      int n[4];
+      wsum(k & 1, jj, n);
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const int nv = q == 0 ? (n[0] & 0xffff) : q == 1 ? (n[0] >> 16) : n[q - 1];
+        s[q] = s[q] + (a_of(nv) - a_q(q, 0));
+      }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+#pragma unroll
+        for (int u = 0; u < 6; ++u) rw[w][u] = rw[w][u + 1];
+        rw[w][6] = n[w];
+      }
+      emit(jn);
+    }
+    if (k + 1 < nchunks) commit(k + 1);
+    __syncthreads();
+  }
+}
+
+// The R, G, B maps' buffer sums: grid (nfull + 1, 3, items), 64 lanes.  A full
+// buffer's 64 leaves: a lane's leaf from lsum, or, if it crosses a row
+// boundary, summed here from its raw elements (NumPy's leaf order); then the
+// perfect binary tree by a shuffle butterfly.  The partial buffer: the host's
+// pairwise tree (pw_tree) over its raw elements.
+__global__ void __launch_bounds__(64) k_ss_rgbsum(RgbBatch B) {
+  __shared__ double lsh[2 * PW_MAXN];
+  const int b = blockIdx.x, ch = blockIdx.y, item = blockIdx.z, t = threadIdx.x;
+  const size_t ic = (size_t)item * 3 + ch;
+  double* out = B.chunks + ic * (B.nfull + 1) + b;
+  auto leaf = [](const double* v, int n) {  // pairwise_sum of n <= 128 elements
+    if (n < 8) {
+      double a = 0.0;
+      for (int i = 0; i < n; ++i) a = a + v[i];
+      return a;
+    }
+    double r8[8];
+    for (int k = 0; k < 8; ++k) r8[k] = v[k];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int k = 0; k < 8; ++k) r8[k] = r8[k] + v[i + k];
+    double a = ((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7]));
+    for (; i < n; ++i) a = a + v[i];
+    return a;
+  };
+  if (b < B.nfull) {
+    const long long Lf = (long long)b * 64 + t, e0 = Lf * 128;
+    double p;
+    if (e0 / B.cw != (e0 + 127) / B.cw)
+      p = leaf(B.raws + ic * B.raws_pitch + rs_slot(e0, B.cw) * 128, 128);
+    else
+      p = B.lsum[ic * B.lsum_pitch + Lf];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) p = p + __shfl_xor(p, o, 64);
+    if (t == 0) *out = p;
+  } else if (B.mpart > 0) {
+    const PwTree& T = B.tree;
+    const double* v = B.rawp + ic * SB_NP_BUF;
+    for (int l = t; l < T.nl; l += 64) lsh[l] = leaf(v + T.off[l], T.n[l]);
+    __syncthreads();
+    for (int h = 0; h < T.nh; ++h) {
+      for (int i = T.hs[h] + t; i < T.hs[h + 1]; i += 64) lsh[T.nl + i] = lsh[T.l[i]] + lsh[T.r[i]];
+      __syncthreads();
+    }
+    if (t == 0) *out = lsh[T.ni ? T.nl + T.ni - 1 : 0];
+  }
+}
+
+// buffer sums left to right from 0.0, / ns: grid (3, items)
+__global__ void __launch_bounds__(64) k_ss_rgbfinal(RgbBatch B) {
+  const int ch = blockIdx.x, item = blockIdx.y;
+  if (threadIdx.x != 0) return;
+  const int nb = B.nfull + (B.mpart > 0 ? 1 : 0);
+  const double* cs = B.chunks + ((size_t)item * 3 + ch) * (B.nfull + 1);
+  double acc = 0.0;
+  for (int k = 0; k < nb; ++k) acc = acc + cs[k];
+  B.out[(size_t)item * B.out_stride + ch] = acc / (double)B.ns;
+}
+
 // ---------------------------------------------------------- NumPy means --
 
 // LDS image of one buffer: element e at e + 8 * (e >> 7) (8-double pad per
@@ -708,9 +1019,9 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_chunks(SsimBatch B, const int
 // buffer sums left to right from 0.0, then / n: one workgroup per (item,
 // quantity); the sums are loaded 256 at a time into LDS (in parallel), one
 // lane adds them in order
-__global__ void __launch_bounds__(256) k_ss_final(SsimBatch B) {
+__global__ void __launch_bounds__(256) k_ss_final(SsimBatch B, const int ch0) {
   __shared__ double part[256];
-  const int ch = blockIdx.x, item = blockIdx.y;
+  const int ch = ch0 + blockIdx.x, item = blockIdx.y;  // (ch0 = 3: the luma SSIM and MSE; k_ss_rgbfinal took R, G, B)
   const long long n = ch < 4 ? B.ns : (long long)B.H * B.W;
   const int nb = (int)((n + SB_NP_BUF - 1) / SB_NP_BUF);
   const int nch = max(B.nch_s, B.nch_y);
@@ -808,14 +1119,64 @@ size_t ssim_batch_scratch_doubles(int H, int W) {
   return 2 * (size_t)n_pitch_of(H, W) + (size_t)ck_pitch_of(H, W) + 4 * (size_t)ns_pitch_of(H, W) + 5 * nch;
 }
 
-// SSIM R, G, B, Y and the luma MSE of `items` (<= SB_MAX_ITEMS) pairs (device
-// image pointers a[i], b[i]) into out[item * out_stride + 0..4], and the RGB
+// k_ss_rows' raw slots per (item, channel), 128 doubles each
+static long long rgb_raws_pitch(int H, int W) {
+  const int cw = W - 6;
+  const long long ns = (long long)(H - 6) * cw;
+  return (cw >= 128 ? (long long)(H - 5) : (ns + 127) / 128 + 1) * 128;
+}
+
+// scratch doubles per item of the R, G, B path (k_ss_rows, k_ss_rgbsum)
+size_t ssim_rgb_scratch_doubles(int H, int W) {
+  const long long ns = (long long)(H - 6) * (W - 6);
+  const long long nfull = ns / SB_NP_BUF;
+  return 3 * (size_t)(nfull * 64 + rgb_raws_pitch(H, W) + SB_NP_BUF + nfull + 1);
+}
+
+// SSIM R, G, B of `items` pairs (pairs_dev: items x {a, b} device image
+// pointers, in device memory) into out[item * out_stride + 0..2]; scratch:
+// items * ssim_rgb_scratch_doubles(H, W).  One launch of each kernel for the
+// whole batch.
+hipError_t launch_ssim_rgb(const void* pairs_dev, int items, int H, int W, double c1, double c2, double* scratch,
+                           double* out, int out_stride, hipStream_t s) {
+  if (items < 1 || H < 7 || W < 7) return hipErrorInvalidValue;
+  if ((unsigned long long)H * (unsigned long long)W * 3ull >= (1ull << 32)) return hipErrorInvalidValue;
+  RgbBatch R{};
+  R.pairs = (const SsimPair*)pairs_dev;
+  R.H = H;
+  R.W = W;
+  R.cw = W - 6;
+  R.ns = (long long)(H - 6) * R.cw;
+  R.nfull = (int)(R.ns / SB_NP_BUF);
+  R.efull = (long long)R.nfull * SB_NP_BUF;
+  R.mpart = (int)(R.ns - R.efull);
+  R.c1 = c1;
+  R.c2 = c2;
+  R.cov_norm = 49.0 / 48.0;
+  R.lsum_pitch = (long long)R.nfull * 64;
+  R.raws_pitch = rgb_raws_pitch(H, W);
+  R.lsum = scratch;
+  R.raws = R.lsum + (size_t)items * 3 * R.lsum_pitch;
+  R.rawp = R.raws + (size_t)items * 3 * R.raws_pitch;
+  R.chunks = R.rawp + (size_t)items * 3 * SB_NP_BUF;
+  R.out = out;
+  R.out_stride = out_stride;
+  pw_tree(R.mpart, &R.tree);
+  hipLaunchKernelGGL(k_ss_rows, dim3((H - 6 + SR_ROWS - 1) / SR_ROWS, items), dim3(SR_THREADS), 0, s, R);
+  hipLaunchKernelGGL(k_ss_rgbsum, dim3(R.nfull + 1, 3, items), dim3(64), 0, s, R);
+  hipLaunchKernelGGL(k_ss_rgbfinal, dim3(3, items), dim3(64), 0, s, R);
+  return hipGetLastError();
+}
+
+// SSIM Y and the luma MSE of `items` (<= SB_MAX_ITEMS) pairs (device image
+// pointers a[i], b[i]) into out[item * out_stride + 3..4], and the RGB
 // squared-error sums into sse[item] (nullable; the caller zeroes it); scratch:
-// items * ssim_batch_scratch_doubles(H, W).
+// items * ssim_batch_scratch_doubles(H, W).  rgb: also SSIM R, G, B (out[.. 0..2])
+// by the band kernel on `side` (small batches; large ones take launch_ssim_rgb).
 hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const* b, int items, int H, int W,
                                   double c1, double c2, double* scratch, double* out, int out_stride,
-                                  unsigned long long* sse, hipStream_t s, hipStream_t side, hipEvent_t fork,
-                                  hipEvent_t join) {
+                                  unsigned long long* sse, hipStream_t s, bool rgb, hipStream_t side,
+                                  hipEvent_t fork, hipEvent_t join) {
   if (items < 1 || items > SB_MAX_ITEMS || H < 7 || W < 7) return hipErrorInvalidValue;
   if ((unsigned long long)H * (unsigned long long)W * 3ull >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit staging offsets
   SsimBatch B{};
@@ -843,22 +1204,24 @@ hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const*
   B.out = out;
   B.out_stride = out_stride;
   B.sse = sse;
-  // the RGB channels' bands need only the images: on the side stream from the
-  // start, beside the luma planes, chains and band on s (which holds the
-  // scratch's previous users in order); joined before the means
   hipError_t e;
-  if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess) return e;
-  hipLaunchKernelGGL((k_ss_band<SB_BH, false>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
-  // their maps' buffer sums there too, beside the luma work
-  hipLaunchKernelGGL(k_ss_chunks, dim3(B.nch_s, 3, items), dim3(SB_THREADS), 0, side, B, 0);
-  if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
+  if (rgb) {
+    // the RGB channels' bands need only the images: on the side stream from
+    // the start, beside the luma planes, chains and band on s; joined before
+    // the means
+    if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL((k_ss_band<SB_BH, false>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
+    hipLaunchKernelGGL(k_ss_chunks, dim3(B.nch_s, 3, items), dim3(SB_THREADS), 0, side, B, 0);
+    if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_ss_yplanes, dim3((unsigned)std::min<long long>((n + 255) / 256, SB_PLANE_BLOCKS), items),
                      dim3(256), 0, s, B);
   hipLaunchKernelGGL(k_ss_ychk<SB_BH>, dim3((W + 63) / 64, 5, items), dim3(64), 0, s, B);
   hipLaunchKernelGGL((k_ss_band<SB_BH, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 2, items), dim3(SB_THREADS), 0, s, B, 3);  // luma map, luma MSE
-  if ((e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_ss_final, dim3(5, items), dim3(256), 0, s, B);
+  if (rgb && (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_ss_final, dim3(rgb ? 5 : 2, items), dim3(256), 0, s, B, rgb ? 0 : 3);
   return hipGetLastError();
 }
 

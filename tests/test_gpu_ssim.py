@@ -69,7 +69,8 @@ def test_metrics_api_equals_oracle(h, w):
 
 
 def test_batch_larger_than_one_launch():
-    """More pairs than one launch carries (32): consecutive launches, same values."""
+    """More pairs than one luma launch carries (32): consecutive launches, same
+    values (R, G, B by the rows kernel: 37 >= 32 pairs)."""
     import torch
     from jds import codec
     h, w = 21, 29
@@ -82,6 +83,31 @@ def test_batch_larger_than_one_launch():
     for k, (a, b) in enumerate(pairs):
         ref = codec.psnr_ssim_raw(a, b)
         assert np.array_equal(r[k], ref)
+
+
+ROWS_SIZES = [(7, 7), (8, 9), (15, 39), (23, 70), (100, 37), (129, 131), (135, 131), (255, 257), (518, 931)]
+
+
+@pytest.mark.parametrize('h,w', ROWS_SIZES)
+def test_rows_path_equals_oracle_bitwise(h, w):
+    """Batches of 32 pairs or more take the R, G, B rows kernel (k_ss_rows: leaf
+    sums in-lane, row-crossing leaves and the partial buffer raw, k_ss_rgbsum):
+    every item bit-exact against the oracle, over narrow maps (a leaf per slot),
+    wide ones (a slot per row boundary), partial buffers and images whose byte
+    count is not a multiple of 4 (the staging's patched last dword)."""
+    import torch
+    from jds import codec
+    kinds = ['noise', 'indep', 'flat', 'smooth']
+    pairs = [_pair(h, w, 41 + i, k) for i, k in enumerate(kinds)]
+    refs = [cpu_ref.psnr_ssim_raw(a, b) for a, b in pairs]
+    dev = torch.device('cuda', 0)
+    ta = [torch.from_numpy(a).to(dev) for a, _ in pairs]
+    tb = [torch.from_numpy(b).to(dev) for _, b in pairs]
+    torch.cuda.synchronize()
+    order = [(7 * i + 3) % 4 for i in range(34)]  # 34 items, every pair several times, mixed order
+    r = codec.psnr_ssim_batch_dev([ta[k].data_ptr() for k in order], [tb[k].data_ptr() for k in order], h, w, 0, None)
+    for i, k in enumerate(order):
+        assert np.array_equal(r[i].view(np.uint64), refs[k].view(np.uint64)), (h, w, i, kinds[k], r[i], refs[k])
 
 
 def test_batch_rejects_small_images():
