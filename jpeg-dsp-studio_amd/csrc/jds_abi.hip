@@ -31,13 +31,12 @@ size_t gen_rec_doubles(const Geo& g);
 int gen_px_tiles(const Geo& g);
 hipError_t stage_area_gen(const double* in, int H, int W, const AreaTap* ytab, const AreaTap* xtab, double* out,
                           int oh, int ow, hipStream_t s);
-hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const* b, int items, int H, int W,
-                                  double c1, double c2, double* scratch, double* out, int out_stride,
-                                  unsigned long long* sse, hipStream_t s, bool rgb, hipStream_t side,
-                                  hipEvent_t fork, hipEvent_t join);
+hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W, double c1, double c2,
+                                  double* scratch, double* out, int out_stride, unsigned long long* sse,
+                                  hipStream_t s, bool rgb, hipStream_t side, hipEvent_t fork, hipEvent_t join);
 hipError_t launch_ssim_rgb(const void* pairs_dev, int items, int H, int W, double c1, double c2, double* scratch,
                            double* out, int out_stride, hipStream_t s);
-size_t ssim_batch_scratch_doubles(int H, int W);
+size_t ssim_batch_scratch_doubles(int H, int W, bool rgb);
 size_t ssim_rgb_scratch_doubles(int H, int W);
 int ssim_batch_max_items();
 hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
@@ -160,6 +159,8 @@ struct jds_ctx {
 
 // batches from this size take the R, G, B rows kernel (jds_ssim_band.hip)
 constexpr int SSIM_ROWS_MIN = 32;
+// SSIM scratch (luma planes, chain checkpoints, maps) per launch group
+constexpr size_t SSIM_SCRATCH = (size_t)16 << 30;
 
 // SSIM of `items` image pairs (K4, jds_ssim_band.hip) on the context's stream:
 // out[i * out_stride + 0..4] = SSIM R, G, B, Y, MSE of Y (device doubles);
@@ -167,11 +168,17 @@ constexpr int SSIM_ROWS_MIN = 32;
 // Batches beyond the kernel's per-launch limit run as consecutive launches.
 static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const uint8_t* const* b, int H, int W,
                           double* out, int out_stride, unsigned long long* sse) {
+  // R, G, B: batches of SSIM_ROWS_MIN items or more take the rows kernel (one
+  // lane per map row, every item in one launch: its grid fills the chip only
+  // with many items); smaller ones the band kernel beside each luma group
+  const bool rows = items >= SSIM_ROWS_MIN;
   const int per = ssim_batch_max_items();
-  const size_t each = ssim_batch_scratch_doubles(H, W) * sizeof(double);
-  // luma (and small batches' RGB) scratch for up to `per` items, at most ~2 GB
-  // (1080p: ~110 MB per item)
-  int group = (int)std::max<size_t>(1, std::min<size_t>((size_t)per, ((size_t)2 << 30) / each));
+  const size_t each = ssim_batch_scratch_doubles(H, W, !rows) * sizeof(double);
+  // luma (and small batches' RGB) scratch: as many items per launch as
+  // SSIM_SCRATCH bytes hold (1080p: ~60 MB per item, ~110 MB with RGB maps) --
+  // the luma chains, like the rows, are latency-bound per lane and need many
+  // items in flight
+  int group = (int)std::max<size_t>(1, std::min<size_t>((size_t)per, SSIM_SCRATCH / each));
   group = std::min(group, items);
   HIP_TRY(c->ss_planes.ensure(each * group));
   if (!c->ss_side) {
@@ -179,47 +186,44 @@ static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const 
     HIP_TRY(hipEventCreateWithFlags(&c->ss_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ss_join, hipEventDisableTiming));
   }
+  // the pair array: pinned staging (reused only after the previous call's
+  // final synchronisation) -> device, on the context's stream
+  const size_t pbytes = sizeof(const void*) * 2 * (size_t)items;
+  if (c->ss_pairs_cap < pbytes) {
+    if (c->ss_pairs_host) HIP_TRY(hipHostFree(c->ss_pairs_host));
+    c->ss_pairs_host = nullptr;
+    c->ss_pairs_cap = 0;
+    HIP_TRY(hipHostMalloc(&c->ss_pairs_host, pbytes, hipHostMallocDefault));
+    c->ss_pairs_cap = pbytes;
+  }
+  const void** ph = (const void**)c->ss_pairs_host;
+  for (int i = 0; i < items; ++i) {
+    ph[2 * i] = a[i];
+    ph[2 * i + 1] = b[i];
+  }
+  HIP_TRY(c->ss_pairs.ensure(pbytes));
+  HIP_TRY(hipMemcpyAsync(c->ss_pairs.p, ph, pbytes, hipMemcpyHostToDevice, c->stream));
+  auto pairs_at = [&](int i0) { return (const void*)((const char*)c->ss_pairs.p + sizeof(const void*) * 2 * (size_t)i0); };
   if (sse) HIP_TRY(hipMemsetAsync(sse, 0, sizeof(unsigned long long) * items, c->stream));
-  // R, G, B: batches of SSIM_ROWS_MIN items or more take the rows kernel (one
-  // lane per map row, every item in one launch: its grid fills the chip only
-  // with many items); smaller ones the band kernel beside each luma group
-  const bool rows = items >= SSIM_ROWS_MIN;
   if (rows) {
     // as many items per launch as ~4 GB of scratch holds (1080p: ~4 MB per item)
     const size_t each_rgb = ssim_rgb_scratch_doubles(H, W) * sizeof(double);
     const int group_rgb = (int)std::min<size_t>((size_t)items, std::max<size_t>(1, ((size_t)4 << 30) / each_rgb));
     HIP_TRY(c->ss_rgb.ensure(each_rgb * group_rgb));
-    // the pair array: pinned staging (reused only after the previous call's
-    // final synchronisation) -> device, on the context's stream
-    const size_t pbytes = sizeof(const void*) * 2 * (size_t)items;
-    if (c->ss_pairs_cap < pbytes) {
-      if (c->ss_pairs_host) HIP_TRY(hipHostFree(c->ss_pairs_host));
-      c->ss_pairs_host = nullptr;
-      c->ss_pairs_cap = 0;
-      HIP_TRY(hipHostMalloc(&c->ss_pairs_host, pbytes, hipHostMallocDefault));
-      c->ss_pairs_cap = pbytes;
-    }
-    const void** ph = (const void**)c->ss_pairs_host;
-    for (int i = 0; i < items; ++i) {
-      ph[2 * i] = a[i];
-      ph[2 * i + 1] = b[i];
-    }
-    HIP_TRY(c->ss_pairs.ensure(pbytes));
-    HIP_TRY(hipMemcpyAsync(c->ss_pairs.p, ph, pbytes, hipMemcpyHostToDevice, c->stream));
     // on the side stream (after the copy and the stream's earlier work), beside
     // the luma groups on the context's stream; joined at the end
     HIP_TRY(hipEventRecord(c->ss_fork, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->ss_side, c->ss_fork, 0));
     for (int i0 = 0; i0 < items; i0 += group_rgb) {
       const int k = std::min(group_rgb, items - i0);
-      HIP_TRY(launch_ssim_rgb((const char*)c->ss_pairs.p + sizeof(const void*) * 2 * (size_t)i0, k, H, W, SSIM_C1,
-                              SSIM_C2, (double*)c->ss_rgb.p, out + (size_t)i0 * out_stride, out_stride, c->ss_side));
+      HIP_TRY(launch_ssim_rgb(pairs_at(i0), k, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_rgb.p,
+                              out + (size_t)i0 * out_stride, out_stride, c->ss_side));
     }
     HIP_TRY(hipEventRecord(c->ss_join, c->ss_side));
   }
   for (int i0 = 0; i0 < items; i0 += group) {
     const int k = std::min(group, items - i0);
-    HIP_TRY(launch_psnr_ssim_batch(a + i0, b + i0, k, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_planes.p,
+    HIP_TRY(launch_psnr_ssim_batch(pairs_at(i0), k, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_planes.p,
                                    out + (size_t)i0 * out_stride, out_stride, sse ? sse + i0 : nullptr, c->stream,
                                    !rows, c->ss_side, c->ss_fork, c->ss_join));
   }

@@ -70,7 +70,7 @@ static_assert(SB_RING >= SB_CW + 7 + 0 && (3 * SB_CW) % SB_RING == 0, "chain_chu
 constexpr int SB_RP = 49;        // ring row pitch in doubles (odd: lane = row reads hit distinct banks)
 constexpr int SB_SP = SB_CW + 1; // chain output tile pitch
 constexpr int SB_THREADS = 256;
-constexpr int SB_MAX_ITEMS = 32; // image pairs per launch (kernel-argument array)
+constexpr int SB_MAX_ITEMS = 4096;  // image pairs per launch (scratch bounds it first)
 
 struct SsimPair {
   const uint8_t* a;
@@ -91,7 +91,8 @@ struct PwTree {
 };
 
 struct SsimBatch {
-  SsimPair pairs[SB_MAX_ITEMS];  // by value: nothing to stage or keep alive on the host
+  const SsimPair* pairs;  // [items] (device)
+  int smap_ch;            // maps per item in smap: 4 (R, G, B, Y) or 1 (Y only: k_ss_rows takes R, G, B)
   int H, W;
   int NB;                 // bands of BH output rows: ceil((H - 6) / BH)
   long long ns;           // cropped map size (H - 6) * (W - 6)
@@ -518,7 +519,7 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   const double* X = B.yplanes + (size_t)item * 2 * B.n_pitch;
   const double* Y = X + B.n_pitch;
   const double* ck = B.ck + (size_t)item * B.ck_pitch;
-  double* smap = B.smap + ((size_t)item * 4 + c) * B.ns_pitch;
+  double* smap = B.smap + ((size_t)item * B.smap_ch + (B.smap_ch == 4 ? c : 0)) * B.ns_pitch;
   const int jend = W - 3;  // axis-1 steps j = 0 .. W - 4 (outputs 3 .. W - 4)
   const int nchunks = (jend + SB_CW - 1) / SB_CW;
   const int cw = W - 6;
@@ -932,7 +933,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_chunks(SsimBatch B, const int
   double* out = B.chunks + ((size_t)item * 5 + ch) * nch + blockIdx.x;
   // stage the buffer (element e of the buffer at LDS sb_pad(e))
   if (ch < 4) {
-    const double* src = B.smap + ((size_t)item * 4 + ch) * B.ns_pitch + c0;
+    const double* src = B.smap + ((size_t)item * B.smap_ch + (B.smap_ch == 4 ? ch : 0)) * B.ns_pitch + c0;
     if (m == SB_NP_BUF) {
 #pragma unroll
       for (int k = 0; k < SB_NP_BUF / (2 * SB_THREADS); ++k) {
@@ -1112,11 +1113,13 @@ static long long ck_pitch_of(int H, int W) { return (5LL * ssim_bands(H) * W + 6
 
 int ssim_batch_max_items() { return SB_MAX_ITEMS; }
 
-// scratch doubles per item for H x W (H, W >= 7)
-size_t ssim_batch_scratch_doubles(int H, int W) {
+// scratch doubles per item for H x W (H, W >= 7); rgb: with the band
+// kernel's R, G, B maps
+size_t ssim_batch_scratch_doubles(int H, int W, bool rgb) {
   const size_t n = (size_t)H * W;
   const size_t nch = (n + SB_NP_BUF - 1) / SB_NP_BUF;  // n > ns
-  return 2 * (size_t)n_pitch_of(H, W) + (size_t)ck_pitch_of(H, W) + 4 * (size_t)ns_pitch_of(H, W) + 5 * nch;
+  return 2 * (size_t)n_pitch_of(H, W) + (size_t)ck_pitch_of(H, W) + (rgb ? 4 : 1) * (size_t)ns_pitch_of(H, W) +
+         5 * nch;
 }
 
 // k_ss_rows' raw slots per (item, channel), 128 doubles each
@@ -1168,19 +1171,20 @@ hipError_t launch_ssim_rgb(const void* pairs_dev, int items, int H, int W, doubl
   return hipGetLastError();
 }
 
-// SSIM Y and the luma MSE of `items` (<= SB_MAX_ITEMS) pairs (device image
-// pointers a[i], b[i]) into out[item * out_stride + 3..4], and the RGB
-// squared-error sums into sse[item] (nullable; the caller zeroes it); scratch:
-// items * ssim_batch_scratch_doubles(H, W).  rgb: also SSIM R, G, B (out[.. 0..2])
-// by the band kernel on `side` (small batches; large ones take launch_ssim_rgb).
-hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const* b, int items, int H, int W,
-                                  double c1, double c2, double* scratch, double* out, int out_stride,
-                                  unsigned long long* sse, hipStream_t s, bool rgb, hipStream_t side,
-                                  hipEvent_t fork, hipEvent_t join) {
+// SSIM Y and the luma MSE of `items` (<= SB_MAX_ITEMS) pairs (pairs_dev:
+// items x {a, b} device image pointers, in device memory) into out[item *
+// out_stride + 3..4], and the RGB squared-error sums into sse[item] (nullable;
+// the caller zeroes it); scratch: items * ssim_batch_scratch_doubles(H, W, rgb).
+// rgb: also SSIM R, G, B (out[.. 0..2]) by the band kernel on `side` (small
+// batches; large ones take launch_ssim_rgb).
+hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W, double c1, double c2,
+                                  double* scratch, double* out, int out_stride, unsigned long long* sse,
+                                  hipStream_t s, bool rgb, hipStream_t side, hipEvent_t fork, hipEvent_t join) {
   if (items < 1 || items > SB_MAX_ITEMS || H < 7 || W < 7) return hipErrorInvalidValue;
   if ((unsigned long long)H * (unsigned long long)W * 3ull >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit staging offsets
   SsimBatch B{};
-  for (int i = 0; i < items; ++i) B.pairs[i] = {a[i], b[i]};
+  B.pairs = (const SsimPair*)pairs_dev;
+  B.smap_ch = rgb ? 4 : 1;
   B.H = H;
   B.W = W;
   B.NB = ssim_bands(H);
@@ -1200,7 +1204,7 @@ hipError_t launch_psnr_ssim_batch(const uint8_t* const* a, const uint8_t* const*
   B.ck = B.yplanes + (size_t)items * 2 * B.n_pitch;
   B.ck_pitch = ck_pitch_of(H, W);
   B.smap = B.ck + (size_t)items * B.ck_pitch;
-  B.chunks = B.smap + (size_t)items * 4 * B.ns_pitch;
+  B.chunks = B.smap + (size_t)items * B.smap_ch * B.ns_pitch;
   B.out = out;
   B.out_stride = out_stride;
   B.sse = sse;
