@@ -216,6 +216,9 @@ static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const 
     HIP_TRY(hipStreamWaitEvent(c->ss_side, c->ss_fork, 0));
     for (int i0 = 0; i0 < items; i0 += group_rgb) {
       const int k = std::min(group_rgb, items - i0);
+#ifdef JDS_SSIM_PROBE_NORGB  // tools: timing probes only (wrong values)
+      continue;
+#endif
       HIP_TRY(launch_ssim_rgb(pairs_at(i0), k, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_rgb.p,
                               out + (size_t)i0 * out_stride, out_stride, c->ss_side));
     }
@@ -223,6 +226,9 @@ static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const 
   }
   for (int i0 = 0; i0 < items; i0 += group) {
     const int k = std::min(group, items - i0);
+#ifdef JDS_SSIM_PROBE_NOLUMA  // tools: timing probes only (wrong values)
+    if (rows) continue;
+#endif
     HIP_TRY(launch_psnr_ssim_batch(pairs_at(i0), k, H, W, SSIM_C1, SSIM_C2, (double*)c->ss_planes.p,
                                    out + (size_t)i0 * out_stride, out_stride, sse ? sse + i0 : nullptr, c->stream,
                                    !rows, c->ss_side, c->ss_fork, c->ss_join));
