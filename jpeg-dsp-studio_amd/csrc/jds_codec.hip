@@ -635,7 +635,7 @@ hipError_t launch_inv_fast(int mode, const Geo& g, int n, const int16_t* coeffs,
                            const InvFix& fx, hipStream_t s, int in_div, int fin);
 hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
                        const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y,
-                       double* err_rgb, hipStream_t s, int in_div);
+                       double* err_rgb, hipStream_t s, int in_div, int fin);
 hipError_t launch_sel_recon(const int16_t* coeffs, const FrameQ* fq, jds_selected_block* sel, int sel_blk,
                             hipStream_t s);
 
@@ -703,8 +703,12 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
         fused_fin = !sel;
         e = launch_inv_fast(mode, g, n, coeffs, fq, rin, rgb_out, st, part, *fx, s, in_div,
                             fused_fin ? ((phases & 8) ? 1 : 0) : -1);
-      } else
-        e = launch_inv2(mode, g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, s, in_div);
+      } else {
+        // without SSE terms, maps or a selected block k_inv2 finalizes too
+        fused_fin = !err_y && !rin && !sel;
+        e = launch_inv2(mode, g, n, coeffs, fq, rin, rgb_out, st, part, err_y, err_rgb, s, in_div,
+                        fused_fin ? ((phases & 8) ? 1 : 0) : -1);
+      }
       tiles = inv_tiles(mode, g.H, g.W);
     } else switch (mode) {
       case M420:

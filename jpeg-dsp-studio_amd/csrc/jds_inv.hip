@@ -39,8 +39,12 @@ template <int MODE, int XTRA>
 __global__ void __launch_bounds__(Inv<MODE>::NT) __attribute__((amdgpu_waves_per_eu(XTRA > 1 ? 2 : Inv<MODE>::WPE)))
 k_inv2(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
        const uint8_t* __restrict__ rgb_in, uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st,
-       double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb, const int in_div) {
+       double* __restrict__ sse_y_part, double* __restrict__ err_y, double* __restrict__ err_rgb, const int in_div,
+       const int fin) {
   __shared__ __attribute__((aligned(16))) InvShared<MODE, XTRA> sh;
+  // k_finalize's per-frame work for runs without SSE terms (fin >= 0; 1 also
+  // adds the zero bin the forward deferred): one launch fewer
+  if (XTRA == 0 && fin >= 0 && blockIdx.x == 0 && threadIdx.x == 0) finalize_frame(g, st + blockIdx.y, fin);
   inv2_tile<MODE, XTRA>(sh, g, tiles_x, gridDim.x, blockIdx.y, blockIdx.x, coeffs, fq, rgb_in, rgb_out, st,
                         sse_y_part, err_y, err_rgb, in_div);
 }
@@ -84,30 +88,30 @@ int inv_tiles(int mode, int H, int W) {
 template <int MODE>
 static hipError_t inv2_t(const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq, const uint8_t* rgb_in,
                          uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y, double* err_rgb,
-                         hipStream_t s, int in_div) {
+                         hipStream_t s, int in_div, int fin) {
   int tx;
   const int tiles = inv_tiles_t<MODE>(g.H, g.W, &tx);
   const dim3 grid(tiles, n), blk(Inv<MODE>::NT);
   if (err_y)
     hipLaunchKernelGGL((k_inv2<MODE, 2>), grid, blk, 0, s, g, tx, coeffs, fq, rgb_in, rgb_out, st, part, err_y,
-                       err_rgb, in_div);
+                       err_rgb, in_div, -1);
   else if (rgb_in)
     hipLaunchKernelGGL((k_inv2<MODE, 1>), grid, blk, 0, s, g, tx, coeffs, fq, rgb_in, rgb_out, st, part, nullptr,
-                       nullptr, in_div);
+                       nullptr, in_div, -1);
   else
     hipLaunchKernelGGL((k_inv2<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, nullptr,
-                       nullptr, in_div);
+                       nullptr, in_div, fin);
   kmark(s, "k_inv2<%d,%d>", MODE, err_y ? 2 : rgb_in ? 1 : 0);
   return hipGetLastError();
 }
 
 hipError_t launch_inv2(int mode, const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq,
                        const uint8_t* rgb_in, uint8_t* rgb_out, jds_frame_stats* st, double* part, double* err_y,
-                       double* err_rgb, hipStream_t s, int in_div) {
+                       double* err_rgb, hipStream_t s, int in_div, int fin) {
   switch (mode) {
-    case M420: return inv2_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div);
-    case M422: return inv2_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div);
-    default: return inv2_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div);
+    case M420: return inv2_t<M420>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div, fin);
+    case M422: return inv2_t<M422>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div, fin);
+    default: return inv2_t<M444>(g, n, coeffs, fq, rgb_in, rgb_out, st, part, err_y, err_rgb, s, in_div, fin);
   }
 }
 
