@@ -201,8 +201,9 @@ int jds_psnr_ssim_dev_after(jds_ctx* ctx, const uint8_t* a_dev, const uint8_t* b
 
 /* The same for n device-resident image pairs of one size (the batch sweep's
  * items, gui/worker.py:62-68): pair i = (a_dev[i], b_dev[i]) (host arrays of
- * device pointers); out[6 i + 0..5] as above.  The pairs run together
- * (up to 32 per launch), so a sweep's SSIM fills the chip.  `after` as above. */
+ * device pointers); out[6 i + 0..5] as above.  The pairs run together (from
+ * 32 pairs, R, G, B in one launch for all of them; the luma in groups sized by
+ * a 16 GB scratch budget), so a sweep's SSIM fills the chip.  `after` as above. */
 int jds_psnr_ssim_batch_dev(jds_ctx* ctx, int32_t n, const uint8_t* const* a_dev, const uint8_t* const* b_dev,
                             int64_t H, int64_t W, double* out, void* after);
 
