@@ -606,11 +606,12 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
 // sum is an exact integer (order-free), so a lane forms its row's axis-0
 // outputs A_q(j) = RN(S_q(j) / 7) column by column from the 7 input rows
 // around it, carries scipy's axis-1 running sums s_q(j) = s_q(j - 1) +
-// (A_q(j + 3) - A_q(j - 4)) itself (the last 8 columns' integer window sums in
-// a register ring, 4 words per column: A(j - 4) is recomputed, exactly, rather
-// than held as 5 doubles) and evaluates the map at once.  No exchange between
-// lanes, one barrier per 16-column chunk (the staging of both images' 70
-// input rows through LDS).  A workgroup is 64 map rows x 3 channels (a wave per
+// (A_q(j + 3) - A_q(j - 4)) itself (the last 7 columns' integer window sums in
+// a register ring, 4 words per column, slot column mod 7 -- static in a loop
+// unrolled by 7: A(j - 4) is recomputed, exactly, rather than held as 5
+// doubles) and evaluates the map at once.  No exchange between lanes, one
+// barrier per 14-column chunk (the staging of both images' 70 input rows
+// through LDS).  A workgroup is 64 map rows x 3 channels (a wave per
 // channel); one launch covers every item of the batch (device pair array), so
 // the grid holds ~50 waves per 1080p item instead of the band kernel's
 // latency-bound chain phases.
@@ -623,8 +624,8 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
 // the last partial buffer, are written raw (k_ss_rgbsum sums them).
 constexpr int SR_ROWS = 64;                                    // map rows per workgroup (a lane each)
 constexpr int SR_IN = SR_ROWS + 6;                             // input rows staged
-constexpr int SR_CW = 16;                                      // columns per staged chunk
-constexpr int SR_RW = 13;                                      // dwords per staged row (48 B + <= 3 misaligned)
+constexpr int SR_CW = 14;                                      // columns per staged chunk (2 x 7: static ring slots)
+constexpr int SR_RW = 12;                                      // dwords per staged row (42 B + <= 3 misaligned)
 constexpr int SR_THREADS = 192;                                // three channels
 constexpr int SR_NE = 2 * SR_IN * SR_RW;                       // dwords per chunk (both images)
 constexpr int SR_SE = (SR_NE + SR_THREADS - 1) / SR_THREADS;   // per thread
@@ -730,11 +731,18 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
       if (e < SR_NE) dst[e] = v[i];
     }
   };
-  // byte offset of this lane's 7 rows within their staged dwords (a chunk
-  // starts 96 k bytes further: the same offset mod 4)
-  int mis[7];
+  // byte offset of this lane's 7 rows within their staged dwords: chunk k
+  // starts 42 k bytes further, i.e. 2 k mod 4 (mis: chunk 0's, + the channel)
+  int mis0[7], mis[7];
 #pragma unroll
-  for (int q = 0; q < 7; ++q) mis[q] = (int)(((long long)min(r + q, H - 1) * W * 3) & 3) + ch;
+  for (int q = 0; q < 7; ++q) {
+    mis0[q] = (int)(((long long)min(r + q, H - 1) * W * 3) & 3);
+    mis[q] = mis0[q] + ch;
+  }
+  auto set_mis = [&](int k) {
+#pragma unroll
+    for (int q = 0; q < 7; ++q) mis[q] = ((mis0[q] + 2 * k) & 3) + ch;
+  };
 
   // this map row's stream elements [rs, re); whole leaves in [hs, te)
   const long long rs = (long long)r * cw, re = rs + cw;
@@ -743,12 +751,12 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
   issue(0);
   commit(0);
   __syncthreads();
-  // the window sums of the last 7 columns (a shift register, oldest first):
-  // x | y << 16, xx, yy, xy
+  // the window sums of the last 7 columns, slot column mod 7: x | y << 16, xx,
+  // yy, xy
   int rw[4][7];
   double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   auto a_of = [](int v) { return div7((double)v); };
-  auto a_q = [&](int q, int u) {  // the axis-0 output of quantity q, ring entry u
+  auto a_q = [&](int q, int u) {  // the axis-0 output of quantity q, ring slot u
     return a_of(q == 0 ? (rw[0][u] & 0xffff) : q == 1 ? (rw[0][u] >> 16) : rw[q - 1][u]);
   };
   // the window sums of column jj of the staged chunk (buffer kb)
@@ -797,6 +805,20 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
     }
   };
 
+  // column jn enters (ring slot u = jn mod 7), column jn - 7 (the same slot) leaves
+  auto step = [&](int kb, int jj, int jn, int u) {
+    int n[4];
+    wsum(kb, jj, n);
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const int nv = q == 0 ? (n[0] & 0xffff) : q == 1 ? (n[0] >> 16) : n[q - 1];
+      s[q] = s[q] + (a_of(nv) - a_q(q, u));
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) rw[w][u] = n[w];
+    emit(jn);
+  };
+
   // chunk 0, columns 0 .. 6: scipy's first window (W >= 7): reflect(-3 .. 3) =
   // 2, 1, 0, 0, 1, 2, 3, then outputs 1 .. 3 take their old column from
   // reflect(-3 .. -1) = 2, 1, 0
@@ -825,27 +847,16 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
     __builtin_amdgcn_sched_barrier(0);  // one quantity's window at a time (registers)
   }
   emit(6);
-  // then column jn enters, column jn - 7 (the register's oldest) leaves
   for (int k = 0; k < nchunks; ++k) {
     if (k > 0 && k + 1 < nchunks) issue(k + 1);
+    set_mis(k);
 #pragma unroll 1
-    for (int jj = k == 0 ? 7 : 0; jj < SR_CW; ++jj) {
-      const int jn = k * SR_CW + jj;  // (uniform)
-      if (jn >= W) break;
-      int n[4];
-      wsum(k & 1, jj, n);
+    for (int g7 = k == 0 ? 7 : 0; g7 < SR_CW; g7 += 7) {
 #pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        const int nv = q == 0 ? (n[0] & 0xffff) : q == 1 ? (n[0] >> 16) : n[q - 1];
-        s[q] = s[q] + (a_of(nv) - a_q(q, 0));
+      for (int j7 = 0; j7 < 7; ++j7) {
+        const int jj = g7 + j7, jn = k * SR_CW + jj;  // (jn mod 7 = j7: SR_CW and g7 are multiples of 7)
+        if (jn < W) step(k & 1, jj, jn, j7);
       }
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-#pragma unroll
-        for (int u = 0; u < 6; ++u) rw[w][u] = rw[w][u + 1];
-        rw[w][6] = n[w];
-      }
-      emit(jn);
     }
     if (k + 1 < nchunks) commit(k + 1);
     __syncthreads();
