@@ -21,7 +21,7 @@
 // fp64 chains (Y = .299R + .587G + .114B is not an integer).  Every axis-1
 // running sum is a chain.  So:
 //   k_ss_yplanes  Y of both images as fp64 planes (NumPy order, no FMA);
-//   k_ss_ychk     the luma axis-0 chains, one lane per (column, quantity), run
+//   k_ss_ychk     the luma axis-0 chains, one lane per column (all five), run
 //                 down the whole column keeping only the chain state at each
 //                 band's first row (checkpoints; no per-row output);
 //   k_ss_band     one workgroup per (band of BH output rows, channel, item):
@@ -121,6 +121,22 @@ __device__ __forceinline__ double div7(double x) {
   return __builtin_fma(r, r7, q0);
 }
 
+// n / d correctly rounded for the SSIM map's operands (d = b1 b2 >= C1 C2 ~ 380,
+// both far from overflow and underflow): the compiler's fp64 division without
+// its range scaling (v_div_scale: a factor of 1 here) and special-case fixup
+// (v_div_fixup: finite, nonzero operands) -- reciprocal, two Newton steps, the
+// quotient and its one fma correction, the same operations and roundings.
+__device__ __forceinline__ double div_map(double n, double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-d, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  const double q = n * y;
+  const double r = __builtin_fma(-d, q, n);
+  return __builtin_fma(r, y, q);
+}
+
 __device__ __forceinline__ double luma_u8(const uint8_t* img, size_t px) {
   const double R = img[px * 3], G = img[px * 3 + 1], B = img[px * 3 + 2];
   return 0.299 * R + 0.587 * G + 0.114 * B;  // utils/metrics.py:17-18, NumPy order
@@ -171,6 +187,128 @@ __global__ void __launch_bounds__(256) k_ss_yplanes(SsimBatch B) {
 
 // ----------------------------------------------------------- luma chains --
 
+// Lane = column j, all five quantities: the axis-0 running sums of column j
+// from row 0 (scipy's reflected first window, then s_q += T_q(i+3) - T_q(i-4),
+// T_q recomputed from the row's x and y -- the same product, the same value),
+// storing s_q at each band's first row 3 + BH*b.  The lane visits every pixel
+// of its column once, so it also forms the luma of both images from the bytes
+// (k_ss_yplanes' expression), writes the planes the band kernel and the luma
+// MSE read, and sums the column's RGB squared error.  x and y of the last 8
+// rows live in a register ring indexed by row & 7; the next block of U rows'
+// bytes are loaded one block ahead.
+template <int BH>
+__global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
+  constexpr int U = 8;  // steps per block; BH divides U, so a block's checkpoints sit at fixed steps
+  static_assert(U % BH == 0, "band height must divide the block");
+  const int H = B.H, W = B.W, NB = B.NB, item = blockIdx.y;
+  const int j0 = blockIdx.x * 64 + threadIdx.x;
+  const bool ok = j0 < W;
+  const int j = ok ? j0 : W - 1;  // (lanes past W load column W - 1 and store nothing)
+  const SsimPair pr = B.pairs[item];
+  double* X = B.yplanes + (size_t)item * 2 * B.n_pitch;
+  double* Y = X + B.n_pitch;
+  double* ck = B.ck + (size_t)item * B.ck_pitch + j;  // [q][band][column]
+  const size_t qs = (size_t)NB * W;
+  unsigned long long sse = 0;
+  // a row's six bytes; loads are never predicated (rows clamped to the image:
+  // a clamped row is only loaded past the last step and never stored)
+  struct Px {
+    int a[3], b[3];
+  };
+  auto ldp = [&](int r, Px& p) {
+    const size_t o = ((size_t)min(r, H - 1) * W + j) * 3;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      p.a[k] = pr.a[o + k];
+      p.b[k] = pr.b[o + k];
+    }
+  };
+  auto cvt = [&](int r, const Px& p, double& x, double& y) {
+    x = 0.299 * (double)p.a[0] + 0.587 * (double)p.a[1] + 0.114 * (double)p.a[2];  // utils/metrics.py:17-18
+    y = 0.299 * (double)p.b[0] + 0.587 * (double)p.b[1] + 0.114 * (double)p.b[2];
+    if (r < H) {
+      if (ok) {
+        X[(size_t)r * W + j] = x;
+        Y[(size_t)r * W + j] = y;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sse += (unsigned)((p.a[k] - p.b[k]) * (p.a[k] - p.b[k]));
+      }
+    }
+  };
+  double rx[8], ry[8];
+  {
+    Px p0[7];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) ldp(r, p0[r]);  // H >= 7
+#pragma unroll
+    for (int r = 0; r < 7; ++r) cvt(r, p0[r], rx[r], ry[r]);
+  }
+  double s[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    auto T = [&](int r) { return qterm<double>(q, rx[r], ry[r]); };
+    double v = 0.0;
+    v = v + T(2);
+    v = v + T(1);
+    v = v + T(0);
+    v = v + T(0);
+    v = v + T(1);
+    v = v + T(2);
+    v = v + T(3);
+    v = v + (T(4) - T(2));  // i = 1: old row reflect(-3) = 2
+    v = v + (T(5) - T(1));  // i = 2
+    v = v + (T(6) - T(0));  // i = 3
+    s[q] = v;
+    if (ok) ck[q * qs] = v;  // band 0 starts at row 3
+  }
+  const int ilast = 3 + BH * (NB - 1);
+  // step i (>= 4): new row i + 3 into slot (i + 3) & 7, old row i - 4 from slot (i - 4) & 7
+  double nx[U], ny[U];
+  auto row_step = [&](int ii, int u) {  // ii = 4 mod 8
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+      s[q] = s[q] + (qterm<double>(q, nx[u], ny[u]) - qterm<double>(q, rx[u & 7], ry[u & 7]));
+    rx[(u + 7) & 7] = nx[u];
+    ry[(u + 7) & 7] = ny[u];
+    if ((u + 1) % BH == 0 && ok) {  // ii = 3 mod BH
+#pragma unroll
+      for (int q = 0; q < 5; ++q) ck[q * qs + (size_t)((ii - 3) / BH) * W] = s[q];
+    }
+  };
+  Px pb[U];  // the bytes of the current block's rows i + 3 .. i + U + 2
+#pragma unroll
+  for (int u = 0; u < U; ++u) ldp(7 + u, pb[u]);
+  int i = 4;
+  for (; i + U - 1 <= ilast; i += U) {
+    Px pn[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ldp(i + U + 3 + u, pn[u]);  // the next block, in flight while this one runs
+#pragma unroll
+    for (int u = 0; u < U; ++u) cvt(i + 3 + u, pb[u], nx[u], ny[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) row_step(i + u, u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) pb[u] = pn[u];
+  }
+  // the last, partial block; then the rows below the last step's window
+#pragma unroll
+  for (int u = 0; u < U; ++u) cvt(i + 3 + u, pb[u], nx[u], ny[u]);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (i + u <= ilast) row_step(i + u, u);
+  for (int r = i + U + 3; r < H; ++r) {
+    Px p;
+    double x, y;
+    ldp(r, p);
+    cvt(r, p, x, y);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sse += __shfl_xor(sse, off, 64);
+  if (threadIdx.x == 0 && B.sse && sse) atomicAdd(&B.sse[item], sse);
+}
+
+// Small batches (k_ss_ychkq): lane = (column j, quantity Q), five times the
+// lanes of k_ss_ychk for the latency of one item's 1,080-step columns.
 // Lane (column j, quantity Q): the axis-0 running sum of column j from row 0
 // (scipy's reflected first window, then s += T(i+3) - T(i-4)), storing s at
 // each band's first row 3 + BH*b.  Terms of the last 8 rows live in a
@@ -247,7 +385,7 @@ __device__ __forceinline__ void ychk_lane(const double* __restrict__ X, const do
 }
 
 template <int BH>
-__global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
+__global__ void __launch_bounds__(64) k_ss_ychkq(SsimBatch B) {
   const int j = blockIdx.x * 64 + threadIdx.x;
   if (j >= B.W) return;
   const int item = blockIdx.z;
@@ -587,7 +725,7 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
         const double a1 = 2 * ux * uy + B.c1, a2 = 2 * vxy + B.c2;
         const double b1 = ux * ux + uy * uy + B.c1, b2 = vx + vy + B.c2;
         const double d = b1 * b2;
-        smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = (a1 * a2) / d;
+        smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
       }
     }
     stage_commit<BH, LU>(c, k + 2, nchunks, P, cur, L);
@@ -663,7 +801,7 @@ __device__ __forceinline__ double ssim_px(const double (&s)[5], double c1, doubl
   const double a1 = 2 * ux * uy + c1, a2 = 2 * vxy + c2;
   const double b1 = ux * ux + uy * uy + c1, b2 = vx + vy + c2;
   const double d = b1 * b2;
-  return (a1 * a2) / d;
+  return div_map(a1 * a2, d);
 }
 
 __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu(3))) k_ss_rows(RgbBatch B) {
@@ -1057,6 +1195,7 @@ __global__ void __launch_bounds__(256) k_ss_final(SsimBatch B, const int ch0) {
 // (b4[2][4][...]: four rows per word), i.e. the band plus its 6-row window
 // (BH = 16 measured 0.40 against 0.34 ms per pair, and does not fit it)
 constexpr int SB_BH = 8;
+constexpr int SB_YCHK_COL_ITEMS = 8;  // from this many items a lane per column (k_ss_ychk) fills the CUs
 static_assert(SB_BH + 6 <= 16, "k_ss_band's RGB staging holds 16 rows per image");
 
 int ssim_bands(int H) { return (H - 6 + SB_BH - 1) / SB_BH; }
@@ -1230,9 +1369,13 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
     hipLaunchKernelGGL(k_ss_chunks, dim3(B.nch_s, 3, items), dim3(SB_THREADS), 0, side, B, 0);
     if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_ss_yplanes, dim3((unsigned)std::min<long long>((n + 255) / 256, SB_PLANE_BLOCKS), items),
-                     dim3(256), 0, s, B);
-  hipLaunchKernelGGL(k_ss_ychk<SB_BH>, dim3((W + 63) / 64, 5, items), dim3(64), 0, s, B);
+  if (items >= SB_YCHK_COL_ITEMS) {  // planes, SSE and chains in one pass over the bytes
+    hipLaunchKernelGGL(k_ss_ychk<SB_BH>, dim3((W + 63) / 64, items), dim3(64), 0, s, B);
+  } else {
+    hipLaunchKernelGGL(k_ss_yplanes, dim3((unsigned)std::min<long long>((n + 255) / 256, SB_PLANE_BLOCKS), items),
+                       dim3(256), 0, s, B);
+    hipLaunchKernelGGL(k_ss_ychkq<SB_BH>, dim3((W + 63) / 64, 5, items), dim3(64), 0, s, B);
+  }
   hipLaunchKernelGGL((k_ss_band<SB_BH, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 2, items), dim3(SB_THREADS), 0, s, B, 3);  // luma map, luma MSE
   if (rgb && (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
