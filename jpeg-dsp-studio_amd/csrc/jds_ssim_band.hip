@@ -423,8 +423,8 @@ struct BandLds {
   struct InY {
     double y[SB_SC][2 * (BH + 6) + 1];  // luma: [column][image * (BH + 6) + r]
   };
-  typename std::conditional<LU, InY, InB>::type in[2];
-  double ck[LU ? 2 : 1][5][LU ? SB_SC : 1];  // luma: the axis-0 chains' states at row i0
+  typename std::conditional<LU, InY, InB>::type in[1];  // (one buffer: committed in the chain phase)
+  double ck[1][5][LU ? SB_SC : 1];  // luma: the axis-0 chains' states at row i0
 };
 
 // fill columns of chunk k: chunk 0 fills [0, CW + 3), chunk k > 0 the new
@@ -516,7 +516,7 @@ __device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const St
                                              const StageRegs<BH, LU>& R, BandLds<BH, LU>& L) {
   constexpr int SE = StageCfg<BH>::SE;
   if (k >= nchunks) return;
-  const int t = threadIdx.x, buf = k & 1;
+  const int t = threadIdx.x, buf = 0;
   uint8_t* base = reinterpret_cast<uint8_t*>(&L.in[buf]);
 #pragma unroll
   for (int i = 0; i < SE; ++i) {
@@ -543,7 +543,7 @@ __device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<
   fill_cols(k, W, lo, hi);
   const int nc = hi - lo, t = threadIdx.x;
   if (t >= 5 * nc) return;
-  const int q = t / nc, cc = t % nc, buf = k & 1;
+  const int q = t / nc, cc = t % nc, buf = 0;
   const int slot = (lo + cc) % SB_RING;
   (void)c;
   if constexpr (!LU) {
@@ -646,7 +646,7 @@ __device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double
 }
 
 template <int BH, bool LU>
-__global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(LU ? 3 : 5))) k_ss_band(SsimBatch B) {
+__global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(LU ? 4 : 5))) k_ss_band(SsimBatch B) {
   __shared__ BandLds<BH, LU> L;
   const int band = blockIdx.x, c = LU ? 3 : blockIdx.y, item = blockIdx.z;
   const int H = B.H, W = B.W;
@@ -662,16 +662,15 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   const int nchunks = (jend + SB_CW - 1) / SB_CW;
   const int cw = W - 6;
 
-  // chunk k's fill inputs are loaded three chunks ahead (two register sets),
-  // stored into LDS two chunks ahead (two buffers): each load has a whole
-  // chunk period -- the barrier interval that issued it and the next one --
-  // before its value is needed
+  // chunk k's fill inputs are loaded three chunks ahead (two register sets)
+  // and stored into the one LDS input buffer in the chain phase before its
+  // fill: each load has a barrier interval and a half before its value is
+  // needed
   const StagePlan<BH> P = stage_plan<BH>(c, H, W, i0);
   StageRegs<BH, LU> RA, RB;
   stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, 0, nchunks, P, RA);
   stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, 1, nchunks, P, RB);
   stage_commit<BH, LU>(c, 0, nchunks, P, RA, L);
-  stage_commit<BH, LU>(c, 1, nchunks, P, RB, L);
   __syncthreads();
   stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, 2, nchunks, P, RA);
   fill_chunk<BH, LU>(c, nr, 0, W, L);
@@ -681,9 +680,9 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   const int cq = t / BH, crow = t % BH;
   const bool chain_lane = t < 5 * BH && crow < nr;
   double s = 0.0;
-  // one chunk: cur holds chunk k + 2's loaded inputs (committed here), nxt
-  // receives chunk k + 3's
-  auto step = [&](int k, StageRegs<BH, LU>& cur, StageRegs<BH, LU>& nxt) {
+  // one chunk: cur holds chunk k + 1's loaded inputs (committed beside the
+  // chain), then receives chunk k + 3's
+  auto step = [&](int k, StageRegs<BH, LU>& cur) {
     const int jc = k * SB_CW;
 #ifndef JDS_SSIM_PROBE_NOCHAIN  // tools: timing probes only (wrong values)
     if (chain_lane) {
@@ -703,9 +702,9 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
       else
         chain_chunk<0, false>(Rg, o, s, nj);
     }
+    stage_commit<BH, LU>(c, k + 1, nchunks, P, cur, L);  // chunk k's fill has read the buffer
     __syncthreads();
-    // chunk k + 1's fill (LDS buffer (k + 1) & 1), chunk k's map, chunk k + 2's
-    // inputs into the buffer chunk k's fill has released, chunk k + 3's loads
+    // chunk k + 1's fill, chunk k's map, chunk k + 3's loads
 #ifndef JDS_SSIM_PROBE_NOFILL
     if (k + 1 < nchunks) fill_chunk<BH, LU>(c, nr, k + 1, W, L);
 #endif
@@ -728,13 +727,12 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
         smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
       }
     }
-    stage_commit<BH, LU>(c, k + 2, nchunks, P, cur, L);
-    stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, k + 3, nchunks, P, nxt);
+    stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, k + 3, nchunks, P, cur);
     __syncthreads();
   };
   for (int k = 0; k < nchunks; k += 2) {
-    step(k, RA, RB);
-    if (k + 1 < nchunks) step(k + 1, RB, RA);
+    step(k, RB);
+    if (k + 1 < nchunks) step(k + 1, RA);
   }
 }
 
