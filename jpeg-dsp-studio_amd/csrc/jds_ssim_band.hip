@@ -1093,22 +1093,43 @@ __global__ void __launch_bounds__(SB_THREADS) k_ss_chunks(SsimBatch B, const int
       for (int e = t; e < m; e += SB_THREADS) v[sb_pad(e)] = src[e];
     }
   } else {
-    // (image0 - image1) ** 2 of the luma planes k_ss_yplanes wrote
-    const double* ya = B.yplanes + (size_t)item * 2 * B.n_pitch + c0;
-    const double* yb = ya + B.n_pitch;
+    // (Y(image0) - Y(image1)) ** 2, the lumas formed from the bytes as
+    // k_ss_yplanes / k_ss_ychk form them (6 B per element read instead of the
+    // planes' 16)
+    const SsimPair pr = B.pairs[item];
+    auto lum = [](unsigned r, unsigned g, unsigned b) {
+      return 0.299 * (double)r + 0.587 * (double)g + 0.114 * (double)b;  // utils/metrics.py:17-18
+    };
     if (m == SB_NP_BUF) {
+      typedef const uint32_t __attribute__((address_space(1)))* gdw;
+      const uint8_t* pa = pr.a + 3 * c0;  // 4-B aligned: c0 is a multiple of 8192
+      const uint8_t* pb = pr.b + 3 * c0;
 #pragma unroll
-      for (int k = 0; k < SB_NP_BUF / (2 * SB_THREADS); ++k) {
-        const int e = 2 * t + 2 * SB_THREADS * k;
-        const double2 wa = *reinterpret_cast<const double2*>(ya + e);  // 16-B aligned (n_pitch, c0, e even)
-        const double2 wb = *reinterpret_cast<const double2*>(yb + e);
-        const double d0 = wa.x - wb.x, d1 = wa.y - wb.y;
-        v[sb_pad(e)] = d0 * d0;
-        v[sb_pad(e + 1)] = d1 * d1;
+      for (int k = 0; k < SB_NP_BUF / (4 * SB_THREADS); ++k) {
+        const int e = 4 * t + 4 * SB_THREADS * k;  // four pixels = three dwords
+        uint32_t wa[3], wb[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          wa[q] = *(gdw)(pa + 3 * e + 4 * q);
+          wb[q] = *(gdw)(pb + 3 * e + 4 * q);
+        }
+#pragma unroll
+        for (int px = 0; px < 4; ++px) {
+          unsigned ca[3], cb[3];
+#pragma unroll
+          for (int k3 = 0; k3 < 3; ++k3) {
+            const int byte = 3 * px + k3;
+            ca[k3] = (wa[byte >> 2] >> (8 * (byte & 3))) & 255u;
+            cb[k3] = (wb[byte >> 2] >> (8 * (byte & 3))) & 255u;
+          }
+          const double d = lum(ca[0], ca[1], ca[2]) - lum(cb[0], cb[1], cb[2]);
+          v[sb_pad(e + px)] = d * d;
+        }
       }
     } else {
       for (int e = t; e < m; e += SB_THREADS) {
-        const double d = ya[e] - yb[e];
+        const size_t o = 3 * (size_t)(c0 + e);
+        const double d = lum(pr.a[o], pr.a[o + 1], pr.a[o + 2]) - lum(pr.b[o], pr.b[o + 1], pr.b[o + 2]);
         v[sb_pad(e)] = d * d;
       }
     }
