@@ -36,7 +36,8 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
                                   hipStream_t s, bool rgb, hipStream_t side, hipEvent_t fork, hipEvent_t join);
 hipError_t launch_ssim_rgb(const void* pairs_dev, int items, int H, int W, double c1, double c2, double* scratch,
                            double* out, int out_stride, hipStream_t s);
-size_t ssim_batch_scratch_doubles(int H, int W, bool rgb);
+size_t ssim_batch_scratch_doubles(int H, int W, bool rgb, bool planes);
+bool ssim_batch_planes(int items);
 size_t ssim_rgb_scratch_doubles(int H, int W);
 int ssim_batch_max_items();
 hipError_t launch_sse_u8(const uint8_t* a, const uint8_t* b, long long n, unsigned long long* out, hipStream_t s);
@@ -173,14 +174,18 @@ static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const 
   // with many items); smaller ones the band kernel beside each luma group
   const bool rows = items >= SSIM_ROWS_MIN;
   const int per = ssim_batch_max_items();
-  const size_t each = ssim_batch_scratch_doubles(H, W, !rows) * sizeof(double);
+  const size_t each = ssim_batch_scratch_doubles(H, W, !rows, ssim_batch_planes(items)) * sizeof(double);
   // luma (and small batches' RGB) scratch: as many items per launch as
-  // SSIM_SCRATCH bytes hold (1080p: ~60 MB per item, ~110 MB with RGB maps) --
-  // the luma chains, like the rows, are latency-bound per lane and need many
-  // items in flight
+  // SSIM_SCRATCH bytes hold (1080p: ~27 MB per item; small launches ~60 MB,
+  // ~110 MB with RGB maps) -- the luma chains, like the rows, are
+  // latency-bound per lane and need many items in flight
   int group = (int)std::max<size_t>(1, std::min<size_t>((size_t)per, SSIM_SCRATCH / each));
   group = std::min(group, items);
-  HIP_TRY(c->ss_planes.ensure(each * group));
+  size_t need = each * group;
+  const int last = items % group;  // a last, small group may keep planes
+  if (last && ssim_batch_planes(last))
+    need = std::max(need, ssim_batch_scratch_doubles(H, W, !rows, true) * sizeof(double) * last);
+  HIP_TRY(c->ss_planes.ensure(need));
   if (!c->ss_side) {
     HIP_TRY(hipStreamCreateWithFlags(&c->ss_side, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->ss_fork, hipEventDisableTiming));

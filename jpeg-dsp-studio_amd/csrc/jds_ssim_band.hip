@@ -190,12 +190,12 @@ __global__ void __launch_bounds__(256) k_ss_yplanes(SsimBatch B) {
 // Lane = column j, all five quantities: the axis-0 running sums of column j
 // from row 0 (scipy's reflected first window, then s_q += T_q(i+3) - T_q(i-4),
 // T_q recomputed from the row's x and y -- the same product, the same value),
-// storing s_q at each band's first row 3 + BH*b.  The lane visits every pixel
-// of its column once, so it also forms the luma of both images from the bytes
-// (k_ss_yplanes' expression), writes the planes the band kernel and the luma
-// MSE read, and sums the column's RGB squared error.  x and y of the last 8
-// rows live in a register ring indexed by row & 7; the next block of U rows'
-// bytes are loaded one block ahead.
+// storing s_q at each band's first row 3 + BH*b.  The lane forms the luma of
+// both images from the bytes (k_ss_yplanes' expression; no planes: the band
+// kernel and the luma MSE form it from the bytes too) and sums its column's
+// RGB squared error.  x and y of the last 8 rows live in a register ring
+// indexed by row & 7; the next block of U rows' bytes are loaded one block
+// ahead.
 template <int BH>
 __global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
   constexpr int U = 8;  // steps per block; BH divides U, so a block's checkpoints sit at fixed steps
@@ -203,15 +203,13 @@ __global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
   const int H = B.H, W = B.W, NB = B.NB, item = blockIdx.y;
   const int j0 = blockIdx.x * 64 + threadIdx.x;
   const bool ok = j0 < W;
-  const int j = ok ? j0 : W - 1;  // (lanes past W load column W - 1 and store nothing)
+  const int j = ok ? j0 : W - 1;  // (lanes past W load column W - 1, store and count nothing)
   const SsimPair pr = B.pairs[item];
-  double* X = B.yplanes + (size_t)item * 2 * B.n_pitch;
-  double* Y = X + B.n_pitch;
   double* ck = B.ck + (size_t)item * B.ck_pitch + j;  // [q][band][column]
   const size_t qs = (size_t)NB * W;
   unsigned long long sse = 0;
   // a row's six bytes; loads are never predicated (rows clamped to the image:
-  // a clamped row is only loaded past the last step and never stored)
+  // a clamped row is only loaded past the last step and never counted)
   struct Px {
     int a[3], b[3];
   };
@@ -228,8 +226,6 @@ __global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
     y = 0.299 * (double)p.b[0] + 0.587 * (double)p.b[1] + 0.114 * (double)p.b[2];
     if (r < H) {
       if (ok) {
-        X[(size_t)r * W + j] = x;
-        Y[(size_t)r * W + j] = y;
 #pragma unroll
         for (int k = 0; k < 3; ++k) sse += (unsigned)((p.a[k] - p.b[k]) * (p.a[k] - p.b[k]));
       }
@@ -450,10 +446,13 @@ struct StagePlan {
   uint32_t row[StageCfg<BH>::SE];
   uint32_t ccv[StageCfg<BH>::SE];
 };
-template <int BH, bool LU>
+// YP: the luma from k_ss_yplanes' planes (small batches, which run it for
+// k_ss_ychkq) instead of the bytes
+template <int BH, bool LU, bool YP = false>
 struct StageRegs {
   uint32_t b[LU ? 1 : StageCfg<BH>::SE];
-  double y[LU ? StageCfg<BH>::SE : 1];
+  uint32_t y[LU && !YP ? StageCfg<BH>::SE : 1][3];  // luma: the pixel's three bytes (converted when committed)
+  double yp[LU && YP ? StageCfg<BH>::SE : 1];
   double ck;
 };
 
@@ -477,10 +476,10 @@ __device__ __forceinline__ StagePlan<BH> stage_plan(int c, int H, int W, int i0)
   return P;
 }
 
-template <int BH, bool LU>
+template <int BH, bool LU, bool YP>
 __device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uint8_t* a, const uint8_t* b,
-                                            const double* X, const double* Y, const double* ck, int band, int k,
-                                            int nchunks, const StagePlan<BH>& P, StageRegs<BH, LU>& R) {
+                                            const double* Xp, const double* ck, int band, int k,
+                                            int nchunks, const StagePlan<BH>& P, StageRegs<BH, LU, YP>& R) {
   constexpr int SE = StageCfg<BH>::SE;
   if (k >= nchunks) return;
   int lo, hi;
@@ -494,15 +493,20 @@ __device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uin
     const bool im = (P.ccv[i] >> 8) & 1u;
 #ifdef JDS_SSIM_PROBE_NOSTAGE  // tools: timing probe without the staging loads (wrong values)
     if constexpr (LU)
-      R.y[i] = (double)(px & 255u);
+      R.y[i][0] = R.y[i][1] = R.y[i][2] = px & 255u;
     else
       R.b[i] = px & 255u;
     (void)im;
 #else
-    if constexpr (LU)
-      R.y[i] = (im ? Y : X)[px];
-    else
+    if constexpr (LU && YP) {
+      R.yp[i] = Xp[(im ? B.n_pitch : 0) + px];
+    } else if constexpr (LU) {
+      const uint8_t* img = im ? b : a;
+#pragma unroll
+      for (int k3 = 0; k3 < 3; ++k3) R.y[i][k3] = img[px * 3u + (uint32_t)k3];
+    } else {
       R.b[i] = (im ? b : a)[px * 3u + (uint32_t)c];
+    }
 #endif
   }
   if (LU && t < 5 * SB_SC) {
@@ -511,9 +515,9 @@ __device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uin
   }
 }
 
-template <int BH, bool LU>
+template <int BH, bool LU, bool YP>
 __device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const StagePlan<BH>& P,
-                                             const StageRegs<BH, LU>& R, BandLds<BH, LU>& L) {
+                                             const StageRegs<BH, LU, YP>& R, BandLds<BH, LU>& L) {
   constexpr int SE = StageCfg<BH>::SE;
   if (k >= nchunks) return;
   const int t = threadIdx.x, buf = 0;
@@ -523,7 +527,8 @@ __device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const St
     if ((P.ccv[i] >> 9) & 1u) {
       uint8_t* d = base + (P.ccv[i] >> 12);
       if constexpr (LU)
-        *reinterpret_cast<double*>(d) = R.y[i];
+        *reinterpret_cast<double*>(d) =  // utils/metrics.py:17-18, k_ss_yplanes' expression
+            YP ? R.yp[i] : 0.299 * (double)R.y[i][0] + 0.587 * (double)R.y[i][1] + 0.114 * (double)R.y[i][2];
       else
         *d = (uint8_t)R.b[i];
     }
@@ -645,7 +650,7 @@ __device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double
   }
 }
 
-template <int BH, bool LU>
+template <int BH, bool LU, bool YP = false>
 __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(LU ? 4 : 5))) k_ss_band(SsimBatch B) {
   __shared__ BandLds<BH, LU> L;
   const int band = blockIdx.x, c = LU ? 3 : blockIdx.y, item = blockIdx.z;
@@ -654,9 +659,8 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   const int nr = min(BH, H - 3 - i0);
   const int t = threadIdx.x;
   const SsimPair pr = B.pairs[item];
-  const double* X = B.yplanes + (size_t)item * 2 * B.n_pitch;
-  const double* Y = X + B.n_pitch;
   const double* ck = B.ck + (size_t)item * B.ck_pitch;
+  const double* Xp = YP ? B.yplanes + (size_t)item * 2 * B.n_pitch : nullptr;
   double* smap = B.smap + ((size_t)item * B.smap_ch + (B.smap_ch == 4 ? c : 0)) * B.ns_pitch;
   const int jend = W - 3;  // axis-1 steps j = 0 .. W - 4 (outputs 3 .. W - 4)
   const int nchunks = (jend + SB_CW - 1) / SB_CW;
@@ -667,12 +671,12 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   // fill: each load has a barrier interval and a half before its value is
   // needed
   const StagePlan<BH> P = stage_plan<BH>(c, H, W, i0);
-  StageRegs<BH, LU> RA, RB;
-  stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, 0, nchunks, P, RA);
-  stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, 1, nchunks, P, RB);
-  stage_commit<BH, LU>(c, 0, nchunks, P, RA, L);
+  StageRegs<BH, LU, YP> RA, RB;
+  stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 0, nchunks, P, RA);
+  stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 1, nchunks, P, RB);
+  stage_commit<BH, LU, YP>(c, 0, nchunks, P, RA, L);
   __syncthreads();
-  stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, 2, nchunks, P, RA);
+  stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 2, nchunks, P, RA);
   fill_chunk<BH, LU>(c, nr, 0, W, L);
   __syncthreads();
 
@@ -682,7 +686,7 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   double s = 0.0;
   // one chunk: cur holds chunk k + 1's loaded inputs (committed beside the
   // chain), then receives chunk k + 3's
-  auto step = [&](int k, StageRegs<BH, LU>& cur) {
+  auto step = [&](int k, StageRegs<BH, LU, YP>& cur) {
     const int jc = k * SB_CW;
 #ifndef JDS_SSIM_PROBE_NOCHAIN  // tools: timing probes only (wrong values)
     if (chain_lane) {
@@ -702,7 +706,7 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
       else
         chain_chunk<0, false>(Rg, o, s, nj);
     }
-    stage_commit<BH, LU>(c, k + 1, nchunks, P, cur, L);  // chunk k's fill has read the buffer
+    stage_commit<BH, LU, YP>(c, k + 1, nchunks, P, cur, L);  // chunk k's fill has read the buffer
     __syncthreads();
     // chunk k + 1's fill, chunk k's map, chunk k + 3's loads
 #ifndef JDS_SSIM_PROBE_NOFILL
@@ -727,7 +731,7 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
         smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
       }
     }
-    stage_issue<BH, LU>(B, c, pr.a, pr.b, X, Y, ck, band, k + 3, nchunks, P, cur);
+    stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, k + 3, nchunks, P, cur);
     __syncthreads();
   };
   for (int k = 0; k < nchunks; k += 2) {
@@ -1282,13 +1286,18 @@ static long long ck_pitch_of(int H, int W) { return (5LL * ssim_bands(H) * W + 6
 
 int ssim_batch_max_items() { return SB_MAX_ITEMS; }
 
+// whether a launch of `items` pairs keeps fp64 luma planes (small launches:
+// k_ss_yplanes for the per-quantity chains; larger ones form the luma from
+// the bytes wherever they need it)
+bool ssim_batch_planes(int items) { return items < SB_YCHK_COL_ITEMS; }
+
 // scratch doubles per item for H x W (H, W >= 7); rgb: with the band
-// kernel's R, G, B maps
-size_t ssim_batch_scratch_doubles(int H, int W, bool rgb) {
+// kernel's R, G, B maps; planes: ssim_batch_planes(items) of the launch
+size_t ssim_batch_scratch_doubles(int H, int W, bool rgb, bool planes) {
   const size_t n = (size_t)H * W;
   const size_t nch = (n + SB_NP_BUF - 1) / SB_NP_BUF;  // n > ns
-  return 2 * (size_t)n_pitch_of(H, W) + (size_t)ck_pitch_of(H, W) + (rgb ? 4 : 1) * (size_t)ns_pitch_of(H, W) +
-         5 * nch;
+  return (planes ? 2 * (size_t)n_pitch_of(H, W) : 0) + (size_t)ck_pitch_of(H, W) +
+         (rgb ? 4 : 1) * (size_t)ns_pitch_of(H, W) + 5 * nch;
 }
 
 // k_ss_rows' raw slots per (item, channel), 128 doubles each
@@ -1343,7 +1352,8 @@ hipError_t launch_ssim_rgb(const void* pairs_dev, int items, int H, int W, doubl
 // SSIM Y and the luma MSE of `items` (<= SB_MAX_ITEMS) pairs (pairs_dev:
 // items x {a, b} device image pointers, in device memory) into out[item *
 // out_stride + 3..4], and the RGB squared-error sums into sse[item] (nullable;
-// the caller zeroes it); scratch: items * ssim_batch_scratch_doubles(H, W, rgb).
+// the caller zeroes it); scratch: items * ssim_batch_scratch_doubles(H, W, rgb,
+// ssim_batch_planes(items)).
 // rgb: also SSIM R, G, B (out[.. 0..2]) by the band kernel on `side` (small
 // batches; large ones take launch_ssim_rgb).
 hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W, double c1, double c2,
@@ -1369,8 +1379,9 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
   B.c1 = c1;
   B.c2 = c2;
   B.cov_norm = 49.0 / 48.0;
-  B.yplanes = scratch;
-  B.ck = B.yplanes + (size_t)items * 2 * B.n_pitch;
+  const bool planes = ssim_batch_planes(items);
+  B.yplanes = planes ? scratch : nullptr;
+  B.ck = scratch + (planes ? (size_t)items * 2 * B.n_pitch : 0);
   B.ck_pitch = ck_pitch_of(H, W);
   B.smap = B.ck + (size_t)items * B.ck_pitch;
   B.chunks = B.smap + (size_t)items * B.smap_ch * B.ns_pitch;
@@ -1388,14 +1399,17 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
     hipLaunchKernelGGL(k_ss_chunks, dim3(B.nch_s, 3, items), dim3(SB_THREADS), 0, side, B, 0);
     if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   }
-  if (items >= SB_YCHK_COL_ITEMS) {  // planes, SSE and chains in one pass over the bytes
+  if (!planes) {  // SSE and chains in one pass over the bytes
     hipLaunchKernelGGL(k_ss_ychk<SB_BH>, dim3((W + 63) / 64, items), dim3(64), 0, s, B);
   } else {
     hipLaunchKernelGGL(k_ss_yplanes, dim3((unsigned)std::min<long long>((n + 255) / 256, SB_PLANE_BLOCKS), items),
                        dim3(256), 0, s, B);
     hipLaunchKernelGGL(k_ss_ychkq<SB_BH>, dim3((W + 63) / 64, 5, items), dim3(64), 0, s, B);
   }
-  hipLaunchKernelGGL((k_ss_band<SB_BH, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
+  if (!planes)
+    hipLaunchKernelGGL((k_ss_band<SB_BH, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
+  else
+    hipLaunchKernelGGL((k_ss_band<SB_BH, true, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 2, items), dim3(SB_THREADS), 0, s, B, 3);  // luma map, luma MSE
   if (rgb && (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_ss_final, dim3(rgb ? 5 : 2, items), dim3(256), 0, s, B, rgb ? 0 : 3);

@@ -110,6 +110,27 @@ def test_rows_path_equals_oracle_bitwise(h, w):
         assert np.array_equal(r[i].view(np.uint64), refs[k].view(np.uint64)), (h, w, i, kinds[k], r[i], refs[k])
 
 
+@pytest.mark.parametrize('h,w', [(7, 7), (8, 9), (15, 39), (135, 131), (255, 257)])
+def test_column_chain_path_equals_oracle_bitwise(h, w):
+    """Launches of 8 pairs or more run the luma chains a lane per column (all
+    five quantities, SSE from the bytes) and form the luma from the bytes in
+    the band kernel and the luma MSE, with no fp64 planes; 12 pairs keep the R,
+    G, B band kernel (under 32): every item bit-exact against the oracle."""
+    import torch
+    from jds import codec
+    kinds = ['noise', 'indep', 'flat', 'smooth']
+    pairs = [_pair(h, w, 71 + i, k) for i, k in enumerate(kinds)]
+    refs = [cpu_ref.psnr_ssim_raw(a, b) for a, b in pairs]
+    dev = torch.device('cuda', 0)
+    ta = [torch.from_numpy(a).to(dev) for a, _ in pairs]
+    tb = [torch.from_numpy(b).to(dev) for _, b in pairs]
+    torch.cuda.synchronize()
+    order = [(5 * i + 1) % 4 for i in range(12)]
+    r = codec.psnr_ssim_batch_dev([ta[k].data_ptr() for k in order], [tb[k].data_ptr() for k in order], h, w, 0, None)
+    for i, k in enumerate(order):
+        assert np.array_equal(r[i].view(np.uint64), refs[k].view(np.uint64)), (h, w, i, kinds[k], r[i], refs[k])
+
+
 def test_batch_rejects_small_images():
     import torch
     from jds import codec
