@@ -884,9 +884,14 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
     for (int q = 0; q < 7; ++q) mis[q] = ((mis0[q] + 2 * k) & 3) + ch;
   };
 
-  // this map row's stream elements [rs, re); whole leaves in [hs, te)
+  // this map row's stream elements [rs, re); whole leaves in [hs, te).  Column
+  // jn emits element rs + jn - 6: the in-leaf columns are [jh, jt) (32-bit
+  // lane constants, so the common path does no 64-bit index work)
   const long long rs = (long long)r * cw, re = rs + cw;
   const long long hs = (rs + 127) & ~127LL, te = re & ~127LL;
+  const int jh = (int)(hs - rs) + 6;
+  const int jt = (int)max(min(min(te, B.efull) - rs, (long long)cw), (long long)(jh - 6)) + 6;
+  const long long hleaf = hs >> 7;
 
   issue(0);
   commit(0);
@@ -924,23 +929,25 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
   auto emit = [&](int jn) {
     if (!rowok) return;
     const double m = ssim_px(s, B.c1, B.c2, B.cov_norm);
-    const long long e = rs + (jn - 6);
-    if (e >= B.efull) {
-      rawp[e - B.efull] = m;
-    } else if (e < hs || e >= te) {
-      const long long slot = cw >= 128 ? (e < hs ? r : r + 1) : (e >> 7);
-      raws[slot * 128 + (e & 127)] = m;
-    } else {
+    if (jn >= jh && jn < jt) {
       // NumPy's leaf: accumulator e mod 8 starts at the leaf's first 8
       // elements and adds every 8th after them; the sum once the leaf is full
-      const int p = (int)(e & 127), kq = p & 7;
+      const int d = jn - jh, p = d & 127, kq = p & 7;
       const double a = p < 8 ? m : LF[kq][t] + m;
       LF[kq][t] = a;
       if (p == 127) {
         double rk[8];
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) rk[kk] = kk == 7 ? a : LF[kk][t];
-        lsum[e >> 7] = ((rk[0] + rk[1]) + (rk[2] + rk[3])) + ((rk[4] + rk[5]) + (rk[6] + rk[7]));
+        lsum[hleaf + (d >> 7)] = ((rk[0] + rk[1]) + (rk[2] + rk[3])) + ((rk[4] + rk[5]) + (rk[6] + rk[7]));
+      }
+    } else {
+      const long long e = rs + (jn - 6);
+      if (e >= B.efull) {
+        rawp[e - B.efull] = m;
+      } else {  // e < hs or e >= te: a row-crossing leaf
+        const long long slot = cw >= 128 ? (e < hs ? r : r + 1) : (e >> 7);
+        raws[slot * 128 + (e & 127)] = m;
       }
     }
   };
