@@ -172,7 +172,7 @@ static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const 
   // R, G, B: batches of SSIM_ROWS_MIN items or more take the rows kernel (one
   // lane per map row, every item in one launch: its grid fills the chip only
   // with many items); smaller ones the band kernel beside each luma group
-  const bool rows = items >= SSIM_ROWS_MIN;
+  const bool rows = items >= SSIM_ROWS_MIN && (unsigned long long)H * W * 3ull < (1ull << 31);  // (32-bit staging)
   const int per = ssim_batch_max_items();
   const size_t each = ssim_batch_scratch_doubles(H, W, !rows, ssim_batch_planes(items)) * sizeof(double);
   // luma (and small batches' RGB) scratch: as many items per launch as

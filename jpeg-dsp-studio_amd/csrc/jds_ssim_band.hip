@@ -121,6 +121,10 @@ __device__ __forceinline__ double div7(double x) {
   return __builtin_fma(r, r7, q0);
 }
 
+// map2: skimage's 2 * ux * uy + C1 and 2 * vxy + C2 as fma(2, ux * uy, C1) and
+// fma(2, vxy, C2): doubling is exact (2 ux uy = 2 (ux uy) bit for bit), so
+// the fma's one rounding is the sum's.
+//
 // n / d correctly rounded for the SSIM map's operands (d = b1 b2 >= C1 C2 ~ 380,
 // both far from overflow and underflow): the compiler's fp64 division without
 // its range scaling (v_div_scale: a factor of 1 here) and special-case fixup
@@ -724,8 +728,9 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
         // skimage structural_similarity (sample covariance)
         const double vx = B.cov_norm * (uxx - ux * ux);
         const double vy = B.cov_norm * (uyy - uy * uy);
-        const double vxy = B.cov_norm * (uxy - ux * uy);
-        const double a1 = 2 * ux * uy + B.c1, a2 = 2 * vxy + B.c2;
+        const double pxy = ux * uy;
+        const double vxy = B.cov_norm * (uxy - pxy);
+        const double a1 = __builtin_fma(2.0, pxy, B.c1), a2 = __builtin_fma(2.0, vxy, B.c2);  // (map2: exact doubling)
         const double b1 = ux * ux + uy * uy + B.c1, b2 = vx + vy + B.c2;
         const double d = b1 * b2;
         smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
@@ -765,10 +770,10 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
 constexpr int SR_ROWS = 64;                                    // map rows per workgroup (a lane each)
 constexpr int SR_IN = SR_ROWS + 6;                             // input rows staged
 constexpr int SR_CW = 14;                                      // columns per staged chunk (2 x 7: static ring slots)
-constexpr int SR_RW = 12;                                      // dwords per staged row (42 B + <= 3 misaligned)
+constexpr int SR_RG = (SR_IN + 3) / 4;                         // staged row groups (four rows' bytes per word)
+constexpr int SR_PG = (SR_CW + 3) / 4;                         // 4-pixel groups per chunk row
 constexpr int SR_THREADS = 192;                                // three channels
-constexpr int SR_NE = 2 * SR_IN * SR_RW;                       // dwords per chunk (both images)
-constexpr int SR_SE = (SR_NE + SR_THREADS - 1) / SR_THREADS;   // per thread
+static_assert(2 * SR_RG * SR_PG <= SR_THREADS, "one staging item (image, row group, pixel group) per thread");
 
 struct RgbBatch {
   const SsimPair* pairs;  // [items] (device)
@@ -799,16 +804,21 @@ __device__ __forceinline__ double ssim_px(const double (&s)[5], double c1, doubl
   const double uxy = div7(s[4]);
   const double vx = cov_norm * (uxx - ux * ux);
   const double vy = cov_norm * (uyy - uy * uy);
-  const double vxy = cov_norm * (uxy - ux * uy);
-  const double a1 = 2 * ux * uy + c1, a2 = 2 * vxy + c2;
+  const double pxy = ux * uy;
+  const double vxy = cov_norm * (uxy - pxy);
+  const double a1 = __builtin_fma(2.0, pxy, c1), a2 = __builtin_fma(2.0, vxy, c2);  // (map2: exact doubling)
   const double b1 = ux * ux + uy * uy + c1, b2 = vx + vy + c2;
   const double d = b1 * b2;
   return div_map(a1 * a2, d);
 }
 
 __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu(3))) k_ss_rows(RgbBatch B) {
-  __shared__ uint32_t L[2][2][SR_IN][SR_RW];  // [buffer][image][input row][dword]
-  __shared__ double LF[8][SR_THREADS];          // the current leaf's eight accumulators, per lane
+  // [buffer][image][channel][column][row group]: a word holds one channel's
+  // bytes of one column for four consecutive input rows (the staging
+  // transposes), so a lane's 7-row window of a column is two words shifted by
+  // its row mod 4, summed by dot4 (v_dot4_u32_u8)
+  __shared__ uint32_t L[2][2][3][SR_CW][SR_RG];
+  __shared__ double LF[8][SR_THREADS];  // the current leaf's eight accumulators, per lane
   const int rb = blockIdx.x, item = blockIdx.y, t = threadIdx.x;
   const int ch = t >> 6, lane = t & 63;
   const int H = B.H, W = B.W, cw = B.cw;
@@ -816,72 +826,76 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
   const int r = R0 + lane;
   const bool rowok = r < H - 6;
   const SsimPair pr = B.pairs[item];
-  const long long nbytes = (long long)H * W * 3;
+  const uint32_t nbytes = (uint32_t)H * (uint32_t)W * 3u;  // < 2^32 (launch_ssim_rgb)
   const size_t ic = (size_t)item * 3 + ch;
   double* lsum = B.lsum + ic * B.lsum_pitch;
   double* raws = B.raws + ic * B.raws_pitch;
   double* rawp = B.rawp + ic * SB_NP_BUF;
   const int nchunks = (W + SR_CW - 1) / SR_CW;
 
-  // staging: element e = (image, input row, dword) of a chunk.  Every load is
-  // an unconditional global dword load (addresses past the image's last whole
-  // dword are clamped to it: those bytes belong to columns >= W, never used),
-  // all in flight together; the image's last, partial dword (H W 3 not a
-  // multiple of 4) is patched from bytes afterwards
+  // staging item of thread t (t < 2 SR_RG SR_PG): image si, row group sg
+  // (input rows R0 + 4 sg .. + 3), pixel group sp (chunk pixels 4 sp .. + 3).
+  // Per row: the 12 bytes of its four pixels from four unconditional global
+  // dword loads (addresses past the image's last whole dword clamped to it:
+  // those bytes belong to columns >= W or rows never used; the image's last,
+  // partial dword patched from bytes, rarely), aligned by the row's byte
+  // offset mod 4 when committed
   typedef const uint32_t __attribute__((address_space(1)))* gdw;
-  const long long alast = (nbytes & ~3LL) - 4;  // the last whole dword (H W 3 >= 147)
-  uint32_t v[SR_SE];
+  const bool stager = t < 2 * SR_RG * SR_PG;
+  const int sg = t % SR_RG, sp = (t / SR_RG) % SR_PG, si = t / (SR_RG * SR_PG);
+  const uint8_t* simg = si ? pr.b : pr.a;
+  const uint32_t alast = (nbytes & ~3u) - 4u;  // the last whole dword (H W 3 >= 147)
+  uint32_t rowoff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) rowoff[q] = (uint32_t)min(R0 + 4 * sg + q, H - 1) * (uint32_t)W * 3u + 12u * (uint32_t)sp;
+  uint32_t v[4][4];
   auto issue = [&](int k) {
-    const long long j0 = (long long)k * SR_CW;
+    if (!stager) return;
     unsigned partial = 0u;
 #pragma unroll
-    for (int i = 0; i < SR_SE; ++i) {
-      const int e = t + i * SR_THREADS;
-      const int im = e >= SR_IN * SR_RW ? 1 : 0, rem = e - im * SR_IN * SR_RW;
-      const int rr = rem / SR_RW, d = rem - rr * SR_RW;
-      const long long grow = min(R0 + rr, H - 1);
-      const long long a = ((grow * W + j0) * 3 & ~3LL) + 4 * d;
-      const uint8_t* img = im ? pr.b : pr.a;
-      v[i] = *(gdw)(img + (a < alast ? a : alast));
-      if (e < SR_NE && a > alast && a < nbytes) partial |= 1u << i;
-    }
-    if (partial) {  // (rare: the last row's last chunk)
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t o = rowoff[q] + 42u * (uint32_t)k, a0 = o & ~3u;
 #pragma unroll
-      for (int i = 0; i < SR_SE; ++i) {
-        if (partial & (1u << i)) {
-          const int e = t + i * SR_THREADS;
-          const int im = e >= SR_IN * SR_RW ? 1 : 0, rem = e - im * SR_IN * SR_RW;
-          const int rr = rem / SR_RW, d = rem - rr * SR_RW;
-          const long long grow = min(R0 + rr, H - 1);
-          const long long a = ((grow * W + j0) * 3 & ~3LL) + 4 * d;
-          const uint8_t* img = im ? pr.b : pr.a;
-          uint32_t x = 0u;
-          for (int q = 0; q < 4; ++q)
-            if (a + q < nbytes) x |= (uint32_t)img[a + q] << (8 * q);
-          v[i] = x;
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t a = a0 + 4u * d;
+        v[q][d] = *(gdw)(simg + (a < alast ? a : alast));
+        if (a > alast && a < nbytes) partial |= 1u << (4 * q + d);
+      }
+    }
+    if (partial) {  // (rare: the image's last dword)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (partial & (1u << (4 * q + d))) {
+            const uint32_t a = ((rowoff[q] + 42u * (uint32_t)k) & ~3u) + 4u * d;
+            uint32_t x = 0u;
+            for (uint32_t b = 0; b < 4; ++b)
+              if (a + b < nbytes) x |= (uint32_t)simg[a + b] << (8 * b);
+            v[q][d] = x;
+          }
         }
       }
     }
   };
+  // transpose: word (channel c, pixel i) = byte 3 i + c of the four rows
   auto commit = [&](int k) {
-    uint32_t* dst = &L[k & 1][0][0][0];
+    if (!stager) return;
+    uint32_t w[4][3];
 #pragma unroll
-    for (int i = 0; i < SR_SE; ++i) {
-      const int e = t + i * SR_THREADS;
-      if (e < SR_NE) dst[e] = v[i];
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t sh = (rowoff[q] + 42u * (uint32_t)k) & 3u;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) w[q][d] = __builtin_amdgcn_alignbyte(v[q][d + 1], v[q][d], sh);
     }
-  };
-  // byte offset of this lane's 7 rows within their staged dwords: chunk k
-  // starts 42 k bytes further, i.e. 2 k mod 4 (mis: chunk 0's, + the channel)
-  int mis0[7], mis[7];
+    uint32_t(*dst)[3][SR_CW][SR_RG] = L[k & 1];
 #pragma unroll
-  for (int q = 0; q < 7; ++q) {
-    mis0[q] = (int)(((long long)min(r + q, H - 1) * W * 3) & 3);
-    mis[q] = mis0[q] + ch;
-  }
-  auto set_mis = [&](int k) {
-#pragma unroll
-    for (int q = 0; q < 7; ++q) mis[q] = ((mis0[q] + 2 * k) & 3) + ch;
+    for (int kk = 0; kk < 12; ++kk) {
+      const int d = kk >> 2, b = kk & 3, i = kk / 3, c = kk % 3;
+      const uint32_t lo = __builtin_amdgcn_perm(w[1][d], w[0][d], 0x0c0c0000u | ((4u + b) << 8) | (uint32_t)b);
+      const uint32_t hi = __builtin_amdgcn_perm(w[3][d], w[2][d], 0x00000c0cu | ((4u + b) << 24) | ((uint32_t)b << 16));
+      if (4 * sp + i < SR_CW) dst[si][c][4 * sp + i][sg] = lo | hi;
+    }
   };
 
   // this map row's stream elements [rs, re); whole leaves in [hs, te).  Column
@@ -904,24 +918,24 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
   auto a_q = [&](int q, int u) {  // the axis-0 output of quantity q, ring slot u
     return a_of(q == 0 ? (rw[0][u] & 0xffff) : q == 1 ? (rw[0][u] >> 16) : rw[q - 1][u]);
   };
-  // the window sums of column jj of the staged chunk (buffer kb)
+  // the window sums of column jj of the staged chunk (buffer kb): input rows
+  // lane .. lane + 3 and lane + 4 .. lane + 6 as two words, summed by dot4
+  const int g0 = lane >> 2;
+  const uint32_t gsh = (uint32_t)lane & 3u;
   auto wsum = [&](int kb, int jj, int (&n)[4]) {
-    const uint8_t* ra = reinterpret_cast<const uint8_t*>(&L[kb][0][lane][0]) + 3 * jj;
-    const uint8_t* rbp = reinterpret_cast<const uint8_t*>(&L[kb][1][lane][0]) + 3 * jj;
-    int sx = 0, sy = 0, sxx = 0, syy = 0, sxy = 0;
-#pragma unroll
-    for (int q = 0; q < 7; ++q) {
-      const int x = ra[q * (SR_RW * 4) + mis[q]], y = rbp[q * (SR_RW * 4) + mis[q]];
-      sx += x;
-      sy += y;
-      sxx += x * x;
-      syy += y * y;
-      sxy += x * y;
-    }
-    n[0] = sx | (sy << 16);
-    n[1] = sxx;
-    n[2] = syy;
-    n[3] = sxy;
+    const uint32_t* ta = &L[kb][0][ch][jj][g0];
+    const uint32_t* tb = &L[kb][1][ch][jj][g0];
+    const uint32_t xl = __builtin_amdgcn_alignbyte(ta[1], ta[0], gsh);
+    const uint32_t xh = __builtin_amdgcn_alignbyte(ta[2], ta[1], gsh) & 0x00ffffffu;
+    const uint32_t yl = __builtin_amdgcn_alignbyte(tb[1], tb[0], gsh);
+    const uint32_t yh = __builtin_amdgcn_alignbyte(tb[2], tb[1], gsh) & 0x00ffffffu;
+    constexpr uint32_t ones = 0x01010101u;
+    const uint32_t sx = __builtin_amdgcn_udot4(xh, ones, __builtin_amdgcn_udot4(xl, ones, 0u, false), false);
+    const uint32_t sy = __builtin_amdgcn_udot4(yh, ones, __builtin_amdgcn_udot4(yl, ones, 0u, false), false);
+    n[0] = (int)(sx | (sy << 16));
+    n[1] = (int)__builtin_amdgcn_udot4(xh, xh, __builtin_amdgcn_udot4(xl, xl, 0u, false), false);
+    n[2] = (int)__builtin_amdgcn_udot4(yh, yh, __builtin_amdgcn_udot4(yl, yl, 0u, false), false);
+    n[3] = (int)__builtin_amdgcn_udot4(xh, yh, __builtin_amdgcn_udot4(xl, yl, 0u, false), false);
   };
   // the map value of column jn - 3 (stream element rs + jn - 6) into its leaf,
   // or raw (leaves that cross a row boundary: slot r for the head of this row,
@@ -996,7 +1010,6 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
   emit(6);
   for (int k = 0; k < nchunks; ++k) {
     if (k > 0 && k + 1 < nchunks) issue(k + 1);
-    set_mis(k);
 #pragma unroll 1
     for (int g7 = k == 0 ? 7 : 0; g7 < SR_CW; g7 += 7) {
 #pragma unroll
@@ -1328,7 +1341,7 @@ size_t ssim_rgb_scratch_doubles(int H, int W) {
 hipError_t launch_ssim_rgb(const void* pairs_dev, int items, int H, int W, double c1, double c2, double* scratch,
                            double* out, int out_stride, hipStream_t s) {
   if (items < 1 || H < 7 || W < 7) return hipErrorInvalidValue;
-  if ((unsigned long long)H * (unsigned long long)W * 3ull >= (1ull << 32)) return hipErrorInvalidValue;
+  if ((unsigned long long)H * (unsigned long long)W * 3ull >= (1ull << 31)) return hipErrorInvalidValue;  // 32-bit staging offsets
   RgbBatch R{};
   R.pairs = (const SsimPair*)pairs_dev;
   R.H = H;
