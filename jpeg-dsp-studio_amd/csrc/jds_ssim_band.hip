@@ -812,7 +812,7 @@ __device__ __forceinline__ double ssim_px(const double (&s)[5], double c1, doubl
   return div_map(a1 * a2, d);
 }
 
-__global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu(3))) k_ss_rows(RgbBatch B) {
+__global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu(4))) k_ss_rows(RgbBatch B) {
   // [buffer][image][channel][column][row group]: a word holds one channel's
   // bytes of one column for four consecutive input rows (the staging
   // transposes), so a lane's 7-row window of a column is two words shifted by
