@@ -199,7 +199,10 @@ __global__ void __launch_bounds__(256) k_ss_yplanes(SsimBatch B) {
 // kernel and the luma MSE form it from the bytes too) and sums its column's
 // RGB squared error.  x and y of the last 8 rows live in a register ring
 // indexed by row & 7; the next block of U rows' bytes are loaded one block
-// ahead.
+// ahead, a dword per lane per image: the wave's 64 pixels of a row are 192
+// contiguous bytes, and each lane takes its pixel's three bytes from the two
+// dwords holding them by ds_bpermute (two loads per row instead of six byte
+// loads: the byte loads kept the address units busy).
 template <int BH>
 __global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
   constexpr int U = 8;  // steps per block; BH divides U, so a block's checkpoints sit at fixed steps
@@ -212,26 +215,54 @@ __global__ void __launch_bounds__(64) k_ss_ychk(SsimBatch B) {
   double* ck = B.ck + (size_t)item * B.ck_pitch + j;  // [q][band][column]
   const size_t qs = (size_t)NB * W;
   unsigned long long sse = 0;
-  // a row's six bytes; loads are never predicated (rows clamped to the image:
-  // a clamped row is only loaded past the last step and never counted)
+  // lane l's dword of a row: bytes [a0 + 4 l, + 4) of the wave's segment
+  // (a0: the segment's first byte rounded down to a dword).  Loads are never
+  // predicated: rows clamped to the image (a clamped row is only loaded past
+  // the last step and never counted), addresses past the image's last whole
+  // dword clamped to it, the partial last dword patched from bytes (last row
+  // only).
+  typedef const uint32_t __attribute__((address_space(1)))* gdw;
+  const int lane = threadIdx.x;
+  const uint32_t nbytes = (uint32_t)H * (uint32_t)W * 3u;  // < 2^32 (launch_psnr_ssim_batch)
+  const uint32_t alast = (nbytes & ~3u) - 4u;
+  const uint32_t jw0 = blockIdx.x * 64u;
   struct Px {
-    int a[3], b[3];
+    uint32_t a, b;
   };
+  auto seg = [&](int r) { return ((uint32_t)min(r, H - 1) * (uint32_t)W + jw0) * 3u; };
   auto ldp = [&](int r, Px& p) {
-    const size_t o = ((size_t)min(r, H - 1) * W + j) * 3;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      p.a[k] = pr.a[o + k];
-      p.b[k] = pr.b[o + k];
+    const uint32_t a = (seg(r) & ~3u) + 4u * (uint32_t)lane;
+    const uint32_t ac = a < alast ? a : alast;
+    p.a = *(gdw)(pr.a + ac);
+    p.b = *(gdw)(pr.b + ac);
+    if (r >= H - 1 && a > alast && a < nbytes) {  // (rare: the image's last dword)
+      uint32_t xa = 0u, xb = 0u;
+      for (uint32_t k = 0; a + k < nbytes && k < 4; ++k) {
+        xa |= (uint32_t)pr.a[a + k] << (8 * k);
+        xb |= (uint32_t)pr.b[a + k] << (8 * k);
+      }
+      p.a = xa;
+      p.b = xb;
     }
   };
   auto cvt = [&](int r, const Px& p, double& x, double& y) {
-    x = 0.299 * (double)p.a[0] + 0.587 * (double)p.a[1] + 0.114 * (double)p.a[2];  // utils/metrics.py:17-18
-    y = 0.299 * (double)p.b[0] + 0.587 * (double)p.b[1] + 0.114 * (double)p.b[2];
+    const uint32_t o = (seg(r) & 3u) + 3u * (uint32_t)lane, d4 = (o >> 2) * 4u, sh = o & 3u;
+    const uint32_t wa = __builtin_amdgcn_alignbyte((uint32_t)__builtin_amdgcn_ds_bpermute((int)d4 + 4, (int)p.a),
+                                                   (uint32_t)__builtin_amdgcn_ds_bpermute((int)d4, (int)p.a), sh);
+    const uint32_t wb = __builtin_amdgcn_alignbyte((uint32_t)__builtin_amdgcn_ds_bpermute((int)d4 + 4, (int)p.b),
+                                                   (uint32_t)__builtin_amdgcn_ds_bpermute((int)d4, (int)p.b), sh);
+    int ca[3], cb[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      ca[k] = (int)((wa >> (8 * k)) & 255u);
+      cb[k] = (int)((wb >> (8 * k)) & 255u);
+    }
+    x = 0.299 * (double)ca[0] + 0.587 * (double)ca[1] + 0.114 * (double)ca[2];  // utils/metrics.py:17-18
+    y = 0.299 * (double)cb[0] + 0.587 * (double)cb[1] + 0.114 * (double)cb[2];
     if (r < H) {
       if (ok) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) sse += (unsigned)((p.a[k] - p.b[k]) * (p.a[k] - p.b[k]));
+        for (int k = 0; k < 3; ++k) sse += (unsigned)((ca[k] - cb[k]) * (ca[k] - cb[k]));
       }
     }
   };
