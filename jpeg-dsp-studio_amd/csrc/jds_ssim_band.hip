@@ -61,13 +61,16 @@ namespace jds {
 
 constexpr int SB_NP_BUF = 8192;  // NumPy ufunc buffer (elements)
 constexpr int SB_CW = 32;        // output columns per chunk
-// ring slots per row: >= CW + 7 (a chunk's chain reads columns jc - 4 .. jc +
-// CW + 2, and the next fill writes CW columns from jc + CW + 3 after it), 48
-// rather than 64 so an RGB workgroup fits 28.5 KB of LDS (five per CU);
-// chunk bases jc mod 48 cycle through 0, 32, 16
-constexpr int SB_RING = 48;
-static_assert(SB_RING >= SB_CW + 7 + 0 && (3 * SB_CW) % SB_RING == 0, "chain_chunk's ring phases");
-constexpr int SB_RP = 49;        // ring row pitch in doubles (odd: lane = row reads hit distinct banks)
+// ring slots per row (k_ss_band's two schedules): a chunk's chain reads
+// columns jc - 4 .. jc + CW + 2; the serial schedule fills the next chunk
+// (CW columns from jc + CW + 3) after it: >= CW + 7, 48 (bases jc mod 48: 0,
+// 32, 16); the overlapped one (OV) fills it in the same barrier interval: >= 2
+// CW + 7, 80 (bases 0, 32, 64, 16, 48).  Row pitch RING + 1 doubles (odd:
+// lane = row reads hit distinct banks).
+template <bool OV>
+constexpr int sb_ring() { return OV ? 80 : 48; }
+static_assert(sb_ring<false>() >= SB_CW + 7 && (3 * SB_CW) % sb_ring<false>() == 0, "chain_chunk's ring phases");
+static_assert(sb_ring<true>() >= 2 * SB_CW + 7 && (5 * SB_CW) % sb_ring<true>() == 0, "chain_chunk's ring phases");
 constexpr int SB_SP = SB_CW + 1; // chain output tile pitch
 constexpr int SB_THREADS = 256;
 constexpr int SB_MAX_ITEMS = 4096;  // image pairs per launch (scratch bounds it first)
@@ -439,9 +442,9 @@ constexpr int SB_SC = SB_CW + 4;  // staged columns per chunk (chunk 0 fills CW 
 // LU: the luma channel's workgroups (fp64 inputs and chain checkpoints) and
 // the RGB channels' (bytes) are separate kernel instances, so the RGB ones --
 // three in four -- carry 34 KB of LDS instead of 51 and four fit a CU
-template <int BH, bool LU>
+template <int BH, bool LU, bool OV>
 struct BandLds {
-  double ring[5][BH][SB_RP];  // axis-0 outputs, column c at slot c mod SB_RING
+  double ring[5][BH][sb_ring<OV>() + 1];  // axis-0 outputs, column c at slot c mod sb_ring<OV>()
   double st[5][BH][SB_SP];    // axis-1 running sums of the current chunk
   // inputs of the fill of one chunk, double-buffered (staged two chunks ahead):
   // per staged column, rows i0 - 3 .. i0 + BH + 2 of both images.  RGB: four
@@ -550,9 +553,9 @@ __device__ __forceinline__ void stage_issue(const SsimBatch& B, int c, const uin
   }
 }
 
-template <int BH, bool LU, bool YP>
+template <int BH, bool LU, bool YP, class LDS>
 __device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const StagePlan<BH>& P,
-                                             const StageRegs<BH, LU, YP>& R, BandLds<BH, LU>& L) {
+                                             const StageRegs<BH, LU, YP>& R, LDS& L) {
   constexpr int SE = StageCfg<BH>::SE;
   if (k >= nchunks) return;
   const int t = threadIdx.x, buf = 0;
@@ -576,15 +579,15 @@ __device__ __forceinline__ void stage_commit(int c, int k, int nchunks, const St
 // the fill of chunk k from its staged inputs: lanes (q, column), the axis-0
 // outputs of the band's rows into the ring (RGB: exact window sums; luma: the
 // chain resumed from its checkpoint)
-template <int BH, bool LU>
-__device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<BH, LU>& L) {
+template <int BH, bool LU, int RING, class LDS>
+__device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, LDS& L, int t) {
   constexpr int NR = BH + 6;
   int lo, hi;
   fill_cols(k, W, lo, hi);
-  const int nc = hi - lo, t = threadIdx.x;
-  if (t >= 5 * nc) return;
+  const int nc = hi - lo;
+  if (t < 0 || t >= 5 * nc) return;
   const int q = t / nc, cc = t % nc, buf = 0;
-  const int slot = (lo + cc) % SB_RING;
+  const int slot = (lo + cc) % RING;
   (void)c;
   if constexpr (!LU) {
     uint32_t xw[4], yw[4];
@@ -632,8 +635,9 @@ __device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, BandLds<
 // then its dependent adds (half the values in flight: fewer VGPRs for the
 // workgroups a CU holds).  FIRST: j = 0 starts scipy's reflected window; NJ:
 // steps in this chunk (all CW but the last).
-constexpr int rmod(int x) { return ((x % SB_RING) + SB_RING) % SB_RING; }
-template <int BASE, bool FIRST>
+template <int RING>
+constexpr int rmod(int x) { return ((x % RING) + RING) % RING; }
+template <int BASE, bool FIRST, int RING>
 __device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double* __restrict__ o, double& s, int nj) {
   constexpr int HC = SB_CW / 2;
 #pragma unroll
@@ -641,8 +645,8 @@ __device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double
     double nv[HC], ov[HC];
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
-      nv[i] = R[rmod(BASE + h * HC + i + 3)];
-      ov[i] = R[rmod(BASE + h * HC + i - 4)];
+      nv[i] = R[rmod<RING>(BASE + h * HC + i + 3)];
+      ov[i] = R[rmod<RING>(BASE + h * HC + i - 4)];
     }
     int i0 = 0;
     if (FIRST && h == 0) {
@@ -685,9 +689,14 @@ __device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double
   }
 }
 
-template <int BH, bool LU, bool YP = false>
-__global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(LU ? 4 : 5))) k_ss_band(SsimBatch B) {
-  __shared__ BandLds<BH, LU> L;
+// OV: the overlapped schedule (chain beside the next chunk's fill; a larger
+// ring, 46 KB for luma): shorter per-chunk latency, for small launches whose
+// few workgroups are latency-bound; big launches keep the serial one (36 KB,
+// four workgroups per CU).
+template <int BH, bool LU, bool YP = false, bool OV = false>
+__global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(LU && !OV ? 4 : (LU ? 3 : 5)))) k_ss_band(SsimBatch B) {
+  constexpr int RING = sb_ring<OV>();
+  __shared__ BandLds<BH, LU, OV> L;
   const int band = blockIdx.x, c = LU ? 3 : blockIdx.y, item = blockIdx.z;
   const int H = B.H, W = B.W;
   const int i0 = 3 + BH * band;
@@ -701,78 +710,164 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
   const int nchunks = (jend + SB_CW - 1) / SB_CW;
   const int cw = W - 6;
 
-  // chunk k's fill inputs are loaded three chunks ahead (two register sets)
-  // and stored into the one LDS input buffer in the chain phase before its
-  // fill: each load has a barrier interval and a half before its value is
-  // needed
-  const StagePlan<BH> P = stage_plan<BH>(c, H, W, i0);
-  StageRegs<BH, LU, YP> RA, RB;
-  stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 0, nchunks, P, RA);
-  stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 1, nchunks, P, RB);
-  stage_commit<BH, LU, YP>(c, 0, nchunks, P, RA, L);
-  __syncthreads();
-  stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 2, nchunks, P, RA);
-  fill_chunk<BH, LU>(c, nr, 0, W, L);
-  __syncthreads();
+  if constexpr (OV) {
+    // Per chunk k, two barrier intervals: (A) wave 0 runs chunk k's chains
+    // while waves 1-3 fill chunk k + 1 (the ring holds both column ranges);
+    // (B) every lane maps chunk k, then chunk k + 2's inputs go into the one LDS
+    // input buffer (chunk k + 1's fill has read it) and chunk k + 4's loads are
+    // issued (two register sets: each load has two chunk periods)
+    static_assert(5 * BH <= 64 && 5 * (SB_CW + 3) <= SB_THREADS - 64, "chain lanes in wave 0, fill lanes in waves 1-3");
+    const int ft = t - 64;  // fill lane
+    const StagePlan<BH> P = stage_plan<BH>(c, H, W, i0);
+    StageRegs<BH, LU, YP> RA, RB;
+    stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 0, nchunks, P, RA);
+    stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 1, nchunks, P, RB);
+    stage_commit<BH, LU, YP>(c, 0, nchunks, P, RA, L);
+    __syncthreads();
+    stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 2, nchunks, P, RA);
+    fill_chunk<BH, LU, RING>(c, nr, 0, W, L, ft);
+    __syncthreads();
+    stage_commit<BH, LU, YP>(c, 1, nchunks, P, RB, L);
+    stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 3, nchunks, P, RB);
+    __syncthreads();
 
-  // chain lanes: (q, row)
-  const int cq = t / BH, crow = t % BH;
-  const bool chain_lane = t < 5 * BH && crow < nr;
-  double s = 0.0;
-  // one chunk: cur holds chunk k + 1's loaded inputs (committed beside the
-  // chain), then receives chunk k + 3's
-  auto step = [&](int k, StageRegs<BH, LU, YP>& cur) {
-    const int jc = k * SB_CW;
-#ifndef JDS_SSIM_PROBE_NOCHAIN  // tools: timing probes only (wrong values)
-    if (chain_lane) {
-#else
-    if (false) {
-#endif
-      const double* Rg = L.ring[cq][crow];
-      double* o = L.st[cq][crow];
-      const int nj = min(SB_CW, jend - jc);
-      const int base = jc % SB_RING;
-      if (k == 0)
-        chain_chunk<0, true>(Rg, o, s, nj);
-      else if (base == 32)
-        chain_chunk<32, false>(Rg, o, s, nj);
-      else if (base == 16)
-        chain_chunk<16, false>(Rg, o, s, nj);
-      else
-        chain_chunk<0, false>(Rg, o, s, nj);
-    }
-    stage_commit<BH, LU, YP>(c, k + 1, nchunks, P, cur, L);  // chunk k's fill has read the buffer
-    __syncthreads();
-    // chunk k + 1's fill, chunk k's map, chunk k + 3's loads
-#ifndef JDS_SSIM_PROBE_NOFILL
-    if (k + 1 < nchunks) fill_chunk<BH, LU>(c, nr, k + 1, W, L);
-#endif
-#ifdef JDS_SSIM_PROBE_NOMAP
-    if (false)
-#endif
-    for (int p = t; p < BH * SB_CW; p += SB_THREADS) {
-      const int row = p / SB_CW, jj = p % SB_CW, j = jc + jj;
-      if (row < nr && j >= 3 && j < jend) {
-        const double ux = div7(L.st[0][row][jj]), uy = div7(L.st[1][row][jj]);
-        const double uxx = div7(L.st[2][row][jj]), uyy = div7(L.st[3][row][jj]);
-        const double uxy = div7(L.st[4][row][jj]);
-        // skimage structural_similarity (sample covariance)
-        const double vx = B.cov_norm * (uxx - ux * ux);
-        const double vy = B.cov_norm * (uyy - uy * uy);
-        const double pxy = ux * uy;
-        const double vxy = B.cov_norm * (uxy - pxy);
-        const double a1 = __builtin_fma(2.0, pxy, B.c1), a2 = __builtin_fma(2.0, vxy, B.c2);  // (map2: exact doubling)
-        const double b1 = ux * ux + uy * uy + B.c1, b2 = vx + vy + B.c2;
-        const double d = b1 * b2;
-        smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
+    // chain lanes: (q, row)
+    const int cq = t / BH, crow = t % BH;
+    const bool chain_lane = t < 5 * BH && crow < nr;
+    double s = 0.0;
+    // one chunk: cur holds chunk k + 2's loaded inputs (committed after the
+    // map), then receives chunk k + 4's
+    auto step = [&](int k, StageRegs<BH, LU, YP>& cur) {
+      const int jc = k * SB_CW;
+  #ifndef JDS_SSIM_PROBE_NOCHAIN  // tools: timing probes only (wrong values)
+      if (chain_lane) {
+  #else
+      if (false) {
+  #endif
+        const double* Rg = L.ring[cq][crow];
+        double* o = L.st[cq][crow];
+        const int nj = min(SB_CW, jend - jc);
+        const int base = jc % RING;
+        if (k == 0)
+          chain_chunk<0, true, RING>(Rg, o, s, nj);
+        else if (base == 32)
+          chain_chunk<32, false, RING>(Rg, o, s, nj);
+        else if (base == 64)
+          chain_chunk<64, false, RING>(Rg, o, s, nj);
+        else if (base == 16)
+          chain_chunk<16, false, RING>(Rg, o, s, nj);
+        else if (base == 48)
+          chain_chunk<48, false, RING>(Rg, o, s, nj);
+        else
+          chain_chunk<0, false, RING>(Rg, o, s, nj);
       }
+  #ifndef JDS_SSIM_PROBE_NOFILL
+      if (k + 1 < nchunks) fill_chunk<BH, LU, RING>(c, nr, k + 1, W, L, ft);
+  #endif
+      __syncthreads();
+      // chunk k's map, chunk k + 2's inputs, chunk k + 4's loads
+  #ifdef JDS_SSIM_PROBE_NOMAP
+      if (false)
+  #endif
+      for (int p = t; p < BH * SB_CW; p += SB_THREADS) {
+        const int row = p / SB_CW, jj = p % SB_CW, j = jc + jj;
+        if (row < nr && j >= 3 && j < jend) {
+          const double ux = div7(L.st[0][row][jj]), uy = div7(L.st[1][row][jj]);
+          const double uxx = div7(L.st[2][row][jj]), uyy = div7(L.st[3][row][jj]);
+          const double uxy = div7(L.st[4][row][jj]);
+          // skimage structural_similarity (sample covariance)
+          const double vx = B.cov_norm * (uxx - ux * ux);
+          const double vy = B.cov_norm * (uyy - uy * uy);
+          const double pxy = ux * uy;
+          const double vxy = B.cov_norm * (uxy - pxy);
+          const double a1 = __builtin_fma(2.0, pxy, B.c1), a2 = __builtin_fma(2.0, vxy, B.c2);  // (map2: exact doubling)
+          const double b1 = ux * ux + uy * uy + B.c1, b2 = vx + vy + B.c2;
+          const double d = b1 * b2;
+          smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
+        }
+      }
+      stage_commit<BH, LU, YP>(c, k + 2, nchunks, P, cur, L);
+      stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, k + 4, nchunks, P, cur);
+      __syncthreads();
+    };
+    for (int k = 0; k < nchunks; k += 2) {
+      step(k, RA);
+      if (k + 1 < nchunks) step(k + 1, RB);
     }
-    stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, k + 3, nchunks, P, cur);
+  } else {
+    // chunk k's fill inputs are loaded three chunks ahead (two register sets)
+    // and stored into the one LDS input buffer in the chain phase before its
+    // fill: each load has a barrier interval and a half before its value is
+    // needed
+    const StagePlan<BH> P = stage_plan<BH>(c, H, W, i0);
+    StageRegs<BH, LU, YP> RA, RB;
+    stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 0, nchunks, P, RA);
+    stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 1, nchunks, P, RB);
+    stage_commit<BH, LU, YP>(c, 0, nchunks, P, RA, L);
     __syncthreads();
-  };
-  for (int k = 0; k < nchunks; k += 2) {
-    step(k, RB);
-    if (k + 1 < nchunks) step(k + 1, RA);
+    stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, 2, nchunks, P, RA);
+    fill_chunk<BH, LU, RING>(c, nr, 0, W, L, t);
+    __syncthreads();
+
+    // chain lanes: (q, row)
+    const int cq = t / BH, crow = t % BH;
+    const bool chain_lane = t < 5 * BH && crow < nr;
+    double s = 0.0;
+    // one chunk: cur holds chunk k + 1's loaded inputs (committed beside the
+    // chain), then receives chunk k + 3's
+    auto step = [&](int k, StageRegs<BH, LU, YP>& cur) {
+      const int jc = k * SB_CW;
+  #ifndef JDS_SSIM_PROBE_NOCHAIN  // tools: timing probes only (wrong values)
+      if (chain_lane) {
+  #else
+      if (false) {
+  #endif
+        const double* Rg = L.ring[cq][crow];
+        double* o = L.st[cq][crow];
+        const int nj = min(SB_CW, jend - jc);
+        const int base = jc % RING;
+        if (k == 0)
+          chain_chunk<0, true, RING>(Rg, o, s, nj);
+        else if (base == 32)
+          chain_chunk<32, false, RING>(Rg, o, s, nj);
+        else if (base == 16)
+          chain_chunk<16, false, RING>(Rg, o, s, nj);
+        else
+          chain_chunk<0, false, RING>(Rg, o, s, nj);
+      }
+      stage_commit<BH, LU, YP>(c, k + 1, nchunks, P, cur, L);  // chunk k's fill has read the buffer
+      __syncthreads();
+      // chunk k + 1's fill, chunk k's map, chunk k + 3's loads
+  #ifndef JDS_SSIM_PROBE_NOFILL
+      if (k + 1 < nchunks) fill_chunk<BH, LU, RING>(c, nr, k + 1, W, L, t);
+  #endif
+  #ifdef JDS_SSIM_PROBE_NOMAP
+      if (false)
+  #endif
+      for (int p = t; p < BH * SB_CW; p += SB_THREADS) {
+        const int row = p / SB_CW, jj = p % SB_CW, j = jc + jj;
+        if (row < nr && j >= 3 && j < jend) {
+          const double ux = div7(L.st[0][row][jj]), uy = div7(L.st[1][row][jj]);
+          const double uxx = div7(L.st[2][row][jj]), uyy = div7(L.st[3][row][jj]);
+          const double uxy = div7(L.st[4][row][jj]);
+          // skimage structural_similarity (sample covariance)
+          const double vx = B.cov_norm * (uxx - ux * ux);
+          const double vy = B.cov_norm * (uyy - uy * uy);
+          const double pxy = ux * uy;
+          const double vxy = B.cov_norm * (uxy - pxy);
+          const double a1 = __builtin_fma(2.0, pxy, B.c1), a2 = __builtin_fma(2.0, vxy, B.c2);  // (map2: exact doubling)
+          const double b1 = ux * ux + uy * uy + B.c1, b2 = vx + vy + B.c2;
+          const double d = b1 * b2;
+          smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
+        }
+      }
+      stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, k + 3, nchunks, P, cur);
+      __syncthreads();
+    };
+    for (int k = 0; k < nchunks; k += 2) {
+      step(k, RB);
+      if (k + 1 < nchunks) step(k + 1, RA);
+    }
   }
 }
 
@@ -1446,7 +1541,10 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
     // the means
     if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL((k_ss_band<SB_BH, false>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
+    if (planes)  // (small launches: the overlapped schedule)
+      hipLaunchKernelGGL((k_ss_band<SB_BH, false, false, true>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
+    else
+      hipLaunchKernelGGL((k_ss_band<SB_BH, false>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
     hipLaunchKernelGGL(k_ss_chunks, dim3(B.nch_s, 3, items), dim3(SB_THREADS), 0, side, B, 0);
     if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   }
@@ -1460,7 +1558,7 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
   if (!planes)
     hipLaunchKernelGGL((k_ss_band<SB_BH, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   else
-    hipLaunchKernelGGL((k_ss_band<SB_BH, true, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
+    hipLaunchKernelGGL((k_ss_band<SB_BH, true, true, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 2, items), dim3(SB_THREADS), 0, s, B, 3);  // luma map, luma MSE
   if (rgb && (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_ss_final, dim3(rgb ? 5 : 2, items), dim3(256), 0, s, B, rgb ? 0 : 3);
