@@ -1541,10 +1541,7 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
     // the means
     if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess)
       return e;
-    if (planes)  // (small launches: the overlapped schedule)
-      hipLaunchKernelGGL((k_ss_band<SB_BH, false, false, true>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
-    else
-      hipLaunchKernelGGL((k_ss_band<SB_BH, false>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
+    hipLaunchKernelGGL((k_ss_band<SB_BH, false, false, true>), dim3(B.NB, 3, items), dim3(SB_THREADS), 0, side, B);
     hipLaunchKernelGGL(k_ss_chunks, dim3(B.nch_s, 3, items), dim3(SB_THREADS), 0, side, B, 0);
     if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   }
@@ -1555,8 +1552,10 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
                        dim3(256), 0, s, B);
     hipLaunchKernelGGL(k_ss_ychkq<SB_BH>, dim3((W + 63) / 64, 5, items), dim3(64), 0, s, B);
   }
-  if (!planes)
+  if (!planes && !rgb)
     hipLaunchKernelGGL((k_ss_band<SB_BH, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
+  else if (!planes)
+    hipLaunchKernelGGL((k_ss_band<SB_BH, true, false, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   else
     hipLaunchKernelGGL((k_ss_band<SB_BH, true, true, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 2, items), dim3(SB_THREADS), 0, s, B, 3);  // luma map, luma MSE
