@@ -163,6 +163,7 @@ def dry_run_main(args):
 
 
 PREWARM_S = 0.3
+PROFILE_CHUNK = 500  # profiled steps per jds_plan_profile_read (event pool: 8192 marks)
 
 
 def init_dist(world, local):
@@ -593,9 +594,17 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
     if NS == 1:
         plans[0].profile(True)
         torch.cuda.synchronize(dev)
+        # the plan's event pool holds 8192 marks (~7 per step): read every
+        # PROFILE_CHUNK steps and sum (a read past the pool fails loudly)
+        kt, span = {}, 0.0
         for k in range(args.steps):
             run_step(nwarm + args.steps + k)
-        kt, span = plans[0].profile_read()
+            if (k + 1) % PROFILE_CHUNK == 0 or k + 1 == args.steps:
+                part, sp = plans[0].profile_read()
+                span += sp
+                for name, (tot, cnt) in part.items():
+                    t0_, c0_ = kt.get(name, (0.0, 0))
+                    kt[name] = (t0_ + tot, c0_ + cnt)
         plans[0].profile(False)
         kernels = {name: {'ms_per_step': tot / args.steps, 'launches_per_step': cnt / args.steps,
                           'avg_launch_ms': tot / cnt} for name, (tot, cnt) in kt.items()}

@@ -119,6 +119,10 @@ int jds_geometry_of(const jds_params* p, int64_t H, int64_t W, jds_geometry* out
 int jds_ctx_create(int device, jds_ctx** out);
 void jds_ctx_destroy(jds_ctx* ctx);
 void* jds_ctx_stream(jds_ctx* ctx);  /* the context's own hipStream_t */
+/* SSIM scratch budget per luma launch group of jds_psnr_ssim_batch_dev (bytes;
+ * <= 0: the default 16 GB).  The group size follows from it; the scratch is
+ * sized for the groups that run (a single pair beyond the budget still runs). */
+int jds_ctx_set_ssim_scratch(jds_ctx* ctx, int64_t bytes);
 
 /* Device-resident batch path (bench, batch sweep).  n_frames frames of the same
  * HxW share one subsampling/prefilter setting; params[i] gives frame i's table.
@@ -155,7 +159,9 @@ void jds_plan_destroy(jds_plan* plan);
  * mark, and the number of launches.  "(between runs)" is the time from one run's
  * last mark to the next run's first (host gaps).  The intervals tile the span
  * from the first mark to the last, so their sum equals *span_ms.  Reading resets
- * the record; jds_plan_profile(plan, 0) stops marking. */
+ * the record; jds_plan_profile(plan, 0) stops marking.  The event pool holds
+ * 8192 marks (~7 per run): a read after more marks than that fails with
+ * JDS_EINVAL ("profile overflow") and returns no totals. */
 typedef struct {
   char name[64];
   double total_ms;

@@ -156,6 +156,7 @@ struct jds_ctx {
   DevBuf planes;  // 16x16 path: reconstructed chroma planes
   DevBuf ent[8], ent_hdr, ent_tab, ent_cf, ent_out, ent_meta;  // entropy coder (jds_encode_jfif)
   DevBuf gen_tab, gen_sub, gen_rec;  // general-geometry path (jds_gen.hip)
+  size_t ss_budget = 0;  // SSIM scratch budget per launch group (0: SSIM_SCRATCH; jds_ctx_set_ssim_scratch)
 };
 
 // batches from this size take the R, G, B rows kernel (jds_ssim_band.hip)
@@ -174,17 +175,29 @@ static int run_ssim_batch(jds_ctx* c, int items, const uint8_t* const* a, const 
   // with many items); smaller ones the band kernel beside each luma group
   const bool rows = items >= SSIM_ROWS_MIN && (unsigned long long)H * W * 3ull < (1ull << 31);  // (32-bit staging)
   const int per = ssim_batch_max_items();
-  const size_t each = ssim_batch_scratch_doubles(H, W, !rows, ssim_batch_planes(items)) * sizeof(double);
-  // luma (and small batches' RGB) scratch: as many items per launch as
-  // SSIM_SCRATCH bytes hold (1080p: ~27 MB per item; small launches ~60 MB,
-  // ~110 MB with RGB maps) -- the luma chains, like the rows, are
-  // latency-bound per lane and need many items in flight
-  int group = (int)std::max<size_t>(1, std::min<size_t>((size_t)per, SSIM_SCRATCH / each));
-  group = std::min(group, items);
-  size_t need = each * group;
-  const int last = items % group;  // a last, small group may keep planes
-  if (last && ssim_batch_planes(last))
-    need = std::max(need, ssim_batch_scratch_doubles(H, W, !rows, true) * sizeof(double) * last);
+  // luma (and small batches' RGB) scratch: as many items per launch as the
+  // budget holds (1080p: ~27 MB per item; launches under 8 pairs keep fp64
+  // luma planes, ~60 MB, ~110 MB with RGB maps) -- the luma chains, like the
+  // rows, are latency-bound per lane and need many items in flight.  A
+  // launch's layout (planes or not) follows its own size, so the group size
+  // is settled first and the scratch sized for the groups that actually run:
+  // the full groups and the remainder.
+  const size_t budget = c->ss_budget ? c->ss_budget : SSIM_SCRATCH;
+  auto bytes_of = [&](int k) {  // scratch of one launch of k pairs
+    return ssim_batch_scratch_doubles(H, W, !rows, ssim_batch_planes(k)) * sizeof(double) * (size_t)k;
+  };
+  int group = std::min(per, items);
+  if (bytes_of(group) > budget) {
+    const size_t each_np = ssim_batch_scratch_doubles(H, W, !rows, false) * sizeof(double);
+    group = (int)std::max<size_t>(1, std::min<size_t>((size_t)group, budget / each_np));
+    if (ssim_batch_planes(group) && bytes_of(group) > budget) {  // the planes layout: larger per item
+      const size_t each_p = ssim_batch_scratch_doubles(H, W, !rows, true) * sizeof(double);
+      group = (int)std::max<size_t>(1, std::min<size_t>((size_t)group, budget / each_p));
+    }
+  }
+  size_t need = bytes_of(group);
+  const int last = items % group;
+  if (last) need = std::max(need, bytes_of(last));
   HIP_TRY(c->ss_planes.ensure(need));
   if (!c->ss_side) {
     HIP_TRY(hipStreamCreateWithFlags(&c->ss_side, hipStreamNonBlocking));
@@ -291,7 +304,11 @@ thread_local KMarks* t_kmarks = nullptr;
 
 void kmark(hipStream_t s, const char* fmt, ...) {
   KMarks* m = t_kmarks;
-  if (!m || m->n >= m->cap) return;
+  if (!m) return;
+  if (m->n >= m->cap) {  // reported by jds_plan_profile_read (the totals would be short)
+    m->dropped++;
+    return;
+  }
   if (hipEventRecord(m->ev[m->n], s) != hipSuccess) return;
   va_list ap;
   va_start(ap, fmt);
@@ -473,6 +490,12 @@ int jds_device_count(int* n) {
 }
 
 void* jds_ctx_stream(jds_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int jds_ctx_set_ssim_scratch(jds_ctx* c, int64_t bytes) {
+  if (!c) return fail(JDS_EINVAL, "null argument");
+  c->ss_budget = bytes > 0 ? (size_t)bytes : 0;
+  return JDS_OK;
+}
 
 int jds_geometry_of(const jds_params* p, int64_t H, int64_t W, jds_geometry* out) {
   Geo g;
@@ -845,6 +868,7 @@ int jds_plan_profile(jds_plan* p, int enable) {
   }
   p->prof_on = enable != 0;
   p->marks.n = 0;
+  p->marks.dropped = 0;
   return JDS_OK;
 }
 
@@ -853,6 +877,14 @@ int jds_plan_profile_read(jds_plan* p, jds_kernel_time* out, int max, int* n_out
   KMarks& m = p->marks;
   *n_out = 0;
   if (span_ms) *span_ms = 0.0;
+  if (m.dropped) {  // the pool filled up: partial totals would under-report, so none are returned
+    const long long d = m.dropped;
+    if (m.n) (void)hipEventSynchronize(m.ev[m.n - 1]);
+    m.n = 0;
+    m.dropped = 0;
+    return fail(JDS_EINVAL, "profile overflow: %lld launch marks dropped (pool of %d); read every <= %d runs",
+                d, m.cap, m.cap / 8);
+  }
   if (m.n < 2) {
     m.n = 0;
     return JDS_OK;

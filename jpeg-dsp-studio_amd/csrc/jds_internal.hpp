@@ -142,6 +142,7 @@ struct KMarks {
   hipEvent_t* ev = nullptr;
   char (*name)[64] = nullptr;
   int n = 0, cap = 0;
+  long long dropped = 0;  // marks not taken since the last read (pool full)
 };
 extern thread_local KMarks* t_kmarks;
 void kmark(hipStream_t s, const char* fmt, ...) __attribute__((format(printf, 2, 3)));

@@ -83,6 +83,7 @@ _SIGS = {
     'jds_ctx_create': (C.c_int, [C.c_int, C.POINTER(_P)]),
     'jds_ctx_destroy': (None, [_P]),
     'jds_ctx_stream': (_P, [_P]),
+    'jds_ctx_set_ssim_scratch': (C.c_int, [_P, C.c_int64]),
     'jds_plan_create': (C.c_int, [_P, C.POINTER(Params), C.c_int, C.c_int64, C.c_int64, C.POINTER(_P)]),
     'jds_plan_create_q': (C.c_int, [_P, C.POINTER(Params), C.c_int, C.c_int, C.c_int64, C.c_int64, C.POINTER(_P)]),
     'jds_plan_run': (C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, _P]),
@@ -192,6 +193,10 @@ class Context:
         check(lib().jds_ctx_create(device, C.byref(h)))
         self.handle = h
         self.device = device
+
+    def set_ssim_scratch(self, nbytes: int = 0):
+        """SSIM luma scratch budget per launch group (jds_ctx_set_ssim_scratch; 0 = default)."""
+        check(lib().jds_ctx_set_ssim_scratch(self.handle, int(nbytes)))
 
     def close(self):
         if self.handle:

@@ -105,11 +105,12 @@ def psnr_ssim_dev(a_ptr: int, b_ptr: int, H: int, W: int, device: int = 0, after
     return out
 
 
-def psnr_ssim_batch_dev(a_ptrs, b_ptrs, H: int, W: int, device: int = 0, after=None) -> np.ndarray:
+def psnr_ssim_batch_dev(a_ptrs, b_ptrs, H: int, W: int, device: int = 0, after=None, ctx=None) -> np.ndarray:
     """jds_psnr_ssim_batch_dev: [n, 6] (psnr_ssim_raw's six values) for n
     device-resident image pairs (a_ptrs[i], b_ptrs[i]) of one size, run together
     on the GPU (the batch sweep's per-item SSIM).  after as in psnr_ssim_dev
-    (None: the caller has synchronised)."""
+    (None: the caller has synchronised).  ctx: a caller-owned Context of that
+    device (e.g. with its own SSIM scratch budget) instead of a pooled one."""
     n = len(a_ptrs)
     if len(b_ptrs) != n:
         raise ValueError('a_ptrs and b_ptrs differ in length')
@@ -118,8 +119,11 @@ def psnr_ssim_batch_dev(a_ptrs, b_ptrs, H: int, W: int, device: int = 0, after=N
         return out
     pa = (C.c_void_p * n)(*[int(p) for p in a_ptrs])
     pb = (C.c_void_p * n)(*[int(p) for p in b_ptrs])
-    with lease(device) as ctx:
+    if ctx is not None:
         check(lib().jds_psnr_ssim_batch_dev(ctx.handle, n, pa, pb, int(H), int(W), out.ctypes.data, _after(after)))
+        return out
+    with lease(device) as c:
+        check(lib().jds_psnr_ssim_batch_dev(c.handle, n, pa, pb, int(H), int(W), out.ctypes.data, _after(after)))
     return out
 
 

@@ -149,6 +149,46 @@ def test_gpu_plan_entropy_64_frame_1080p_batch_matches_oracle():
         assert bits_h[i].tolist() == bits, i
 
 
+def test_gpu_plan_entropy_4k_long_scans_match_oracle():
+    """Scans of more than 512 segments (4K 4:2:0 luma: 129,600 blocks = 2,025
+    segments of 64) take k_entropy's long-scan placement: a k_ent_fscan<false>
+    prefix launch, then pre = segoff[g] - segoff[g - q.seg] in k_ent_place
+    (ADVICE r05); the 1080p tests stay on the self-summing branch.  Two frames
+    at different qualities, bytes and scan bits against the oracle encoder."""
+    import multiprocessing as mp
+    import torch
+    from jds import _abi, codec, entropy
+    H, W, mode, qs = 2160, 3840, '4:2:0', [50, 90]
+    tabs = [cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q) for q in qs]
+    params = [_abi.make_params(q, t, mode, True, codec.gaussian_kernel3()) for q, t in zip(qs, tabs)]
+    plan = _abi.Plan(_abi.context(0), params, H, W)
+    ent = entropy.PlanEntropy(plan)
+    dev = torch.device('cuda:0')
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(4242)
+    rgb = torch.randint(0, 256, (len(qs), H, W, 3), dtype=torch.uint8, device=dev, generator=gen)
+    out = torch.empty_like(rgb)
+    cf = torch.empty((len(qs), plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+    st = torch.zeros((len(qs), _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    files = torch.empty((len(qs), ent.capacity), dtype=torch.uint8, device=dev)
+    lengths = torch.zeros(len(qs), dtype=torch.int64, device=dev)
+    sbits = torch.zeros((len(qs), 3), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(), 0, s)
+    ent.run(cf.data_ptr(), files.data_ptr(), ent.capacity, lengths.data_ptr(), sbits.data_ptr(), s)
+    torch.cuda.synchronize()
+    ny, nc = counts(H, W, mode)
+    assert ny // 64 > 512  # the long-scan branch is the one under test
+    cfh, n_h, bits_h, files_h = cf.cpu().numpy(), lengths.cpu().numpy(), sbits.cpu().numpy(), files.cpu().numpy()
+    plan.close()
+    with mp.get_context('spawn').Pool(len(qs)) as pool:  # (no GPU in the workers; ~20 s of Python per frame)
+        refs = pool.starmap(je.encode_jfif, [(cfh[i], H, W, mode, tabs[i], ny, nc) for i in range(len(qs))])
+    for i, (data, bits) in enumerate(refs):
+        assert int(n_h[i]) == len(data), i
+        assert files_h[i, :len(data)].tobytes() == data, i
+        assert bits_h[i].tolist() == bits, i
+
+
 @pytest.mark.parametrize('nblk,rows,seed', [(65, 1, 1), (129, 1, 2), (65, 2, 3), (66, 1, 6), (193, 1, 5)])
 def test_gpu_jfif_short_last_segment(nblk, rows, seed):
     """Scans whose last segment (nblk mod 64 blocks) is short and mostly zero

@@ -68,9 +68,10 @@ def test_metrics_api_equals_oracle(h, w):
         assert compute_psnr_ssim(a, b) == cpu_ref.compute_psnr_ssim(a, b)
 
 
-def test_batch_larger_than_one_launch():
-    """More pairs than one luma launch carries (32): consecutive launches, same
-    values (R, G, B by the rows kernel: 37 >= 32 pairs)."""
+def test_batch_of_37_small_pairs():
+    """37 small pairs: R, G, B by the rows kernel (>= 32 pairs), the luma in one
+    launch (the 16 GB scratch budget holds them all; the multi-group case is
+    test_scratch_budget_groups_equal_oracle)."""
     import torch
     from jds import codec
     h, w = 21, 29
@@ -138,3 +139,67 @@ def test_batch_rejects_small_images():
     torch.cuda.synchronize()
     with pytest.raises(ValueError, match='win_size exceeds image extent'):
         codec.psnr_ssim_batch_dev([t.data_ptr()], [t.data_ptr()], 6, 9, 0, None)
+
+
+@pytest.mark.parametrize('n', [12, 32])
+def test_full_hd_batch_routes_equal_oracle_bitwise(n):
+    """The batched routes the 384-item sweep runs, at the sweep's own size
+    (1080p: a map row spans 1,914 columns, a leaf/row-crossing layout the
+    smaller ROWS_SIZES do not reach): 12 pairs take the overlapped R, G, B band
+    kernel and the byte-formed luma; 32 pairs the rows kernel (k_ss_rows +
+    k_ss_rgbsum).  Items first, middle and last checked bit for bit against
+    the oracle."""
+    import torch
+    from jds import codec
+    h, w = 1080, 1920
+    kinds = ['noise', 'indep', 'smooth']
+    pairs = [_pair(h, w, 900 + i, k) for i, k in enumerate(kinds)]
+    dev = torch.device('cuda', 0)
+    ta = [torch.from_numpy(a).to(dev) for a, _ in pairs]
+    tb = [torch.from_numpy(b).to(dev) for _, b in pairs]
+    torch.cuda.synchronize()
+    # item i uses pair order[i]; the checked items 0, n // 2, n - 1 hold three distinct pairs
+    order = [(i * 7 + 1) % 3 for i in range(n)]
+    checks = [0, n // 2, n - 1]
+    order[checks[0]], order[checks[1]], order[checks[2]] = 0, 1, 2
+    r = codec.psnr_ssim_batch_dev([ta[k].data_ptr() for k in order], [tb[k].data_ptr() for k in order], h, w, 0, None)
+    for i in checks:
+        a, b = pairs[order[i]]
+        ref = cpu_ref.psnr_ssim_raw(a, b)
+        assert np.array_equal(r[i].view(np.uint64), ref.view(np.uint64)), (n, i, kinds[order[i]], r[i], ref)
+    # every other item equals the checked item of its pair (same inputs, same launch)
+    for i in range(n):
+        assert np.array_equal(r[i].view(np.uint64), r[checks[order[i]]].view(np.uint64)), (n, i)
+
+
+@pytest.mark.parametrize('n', [12, 34])
+def test_scratch_budget_groups_equal_oracle(n):
+    """A small SSIM scratch budget (jds_ctx_set_ssim_scratch) splits the luma into
+    several launch groups, each laid out by its own size: groups under 8 pairs
+    keep fp64 planes and need more scratch per item than the others; the scratch
+    is sized for the groups that run, full ones and the remainder (ADVICE r05:
+    sized by the batch's layout, a planes group wrote past the buffer).  Every
+    budget gives the oracle's values bit for bit."""
+    import torch
+    from jds import _abi, codec
+    h, w = 135, 131
+    kinds = ['noise', 'indep', 'flat', 'smooth']
+    pairs = [_pair(h, w, 500 + i, k) for i, k in enumerate(kinds)]
+    refs = [cpu_ref.psnr_ssim_raw(a, b) for a, b in pairs]
+    dev = torch.device('cuda', 0)
+    ta = [torch.from_numpy(a).to(dev) for a, _ in pairs]
+    tb = [torch.from_numpy(b).to(dev) for _, b in pairs]
+    torch.cuda.synchronize()
+    order = [(3 * i + 2) % 4 for i in range(n)]
+    ctx = _abi.Context(0)
+    try:
+        # ~0.6 MB per item without planes, ~0.9 MB with them at 135 x 131: budgets for
+        # groups of 1 (planes), 2 (planes), 10 (+ a planes remainder) and the default
+        for budget in (1, 2_500_000, 6_000_000, 0):
+            ctx.set_ssim_scratch(budget)
+            r = codec.psnr_ssim_batch_dev([ta[k].data_ptr() for k in order], [tb[k].data_ptr() for k in order],
+                                          h, w, 0, None, ctx=ctx)
+            for i, k in enumerate(order):
+                assert np.array_equal(r[i].view(np.uint64), refs[k].view(np.uint64)), (budget, i, kinds[k])
+    finally:
+        ctx.close()

@@ -74,5 +74,4 @@ def test_two_ranks_real_compute_equal_one_process(tmp_path):
         ref = cpu_ref.compress_reconstruct(f0, q, 8, '4:2:0', True, metrics=True)
         it = one[qi]
         assert it[2] == ref['bitrate']['nonzero_count']
-        assert it[6] == pytest.approx(ref['metrics']['ssim_rgb'], rel=1e-12)
-        assert it[7] == pytest.approx(ref['metrics']['ssim_y'], rel=1e-12)
+        assert it[6] == ref['metrics']['ssim_rgb'] and it[7] == ref['metrics']['ssim_y']  # bitwise
