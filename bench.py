@@ -643,40 +643,48 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
     dom = 'k_inv' if kname.startswith(INV_PREFIXES) or kname == 'inverse phase' else 'k_fwd'
     dom_bytes = bytes_inv if dom == 'k_inv' else bytes_fwd
     achieved = dom_bytes / (t_dom * 1e-3) / 1e9
-    traffic, traffic_src = None, None
-    tf = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
-    if os.path.exists(tf):
-        try:
-            rec = json.load(open(tf))
-            base = (f'{W}x{H}_q{quality}_{mode}_pf{int(bool(pf))}' + ('_B16' if block == 16 else '') + '_b')
-            for kk, vv in rec.items():  # bytes scale with frames per launch (recorded for some launch size)
-                if kk.startswith(base) and kname in vv.get('kernels', {}):
-                    traffic = int(vv['kernels'][kname] * B / int(kk[len(base):]))
-                    traffic_src = vv.get('source')
-                    break
-        except Exception:
-            traffic = None
+    # PMC records of the same configuration (profiles/pmc_valu.json,
+    # profiles/pmc_traffic.json: tools/r6_pmc.sh + tools/r6_valu.py), per kernel;
+    # recorded for some frames-per-launch count B0, scaled to this B
+    base = f'{W}x{H}_q{quality}_{mode}_pf{int(bool(pf))}' + ('_B16' if block == 16 else '') + '_b'
 
-    # VALU issue roofline of the same phase (profiles/pmc_valu.json, tools/r4_pmc.sh):
-    # PMC-counted VALU instructions per launch by class x their measured issue
-    # cost, over what 1024 SIMDs at 2.4 GHz issue in this run's launch time
-    valu = None
-    vf = os.path.join(ROOT, 'profiles', 'pmc_valu.json')
-    if os.path.exists(vf):
+    def pmc_entry(fname):
+        f = os.path.join(ROOT, 'profiles', fname)
+        if not os.path.exists(f):
+            return None, None, None
         try:
-            vrec = json.load(open(vf))
-            vkey = (f'{W}x{H}_q{quality}_{mode}_pf{int(bool(pf))}' + ('_B16' if block == 16 else '') + f'_b{B}')
-            ph = vrec.get(vkey, {}).get(dom)
-            if ph and not (args.exact or args.exact_inv or args.inv_fast):
-                cap = 1024 * 2.4e9 * t_dom * 1e-3
-                lo, hi = ph['issue_cycles_lo'] / cap, ph['issue_cycles_hi'] / cap
-                valu = {'frac_lo': round(lo, 4), 'frac_hi': round(hi, 4), 'frac': round((lo + hi) / 2, 4),
-                        'peak': '1024 SIMDs x 2.4 GHz, one VALU wave instruction at its measured issue cost',
-                        'valu_insts_per_launch': sum(k['valu_insts'] for k in ph['kernels']),
-                        'kernels': [k['kernel'] for k in ph['kernels']],
-                        'source': f'profiles/pmc_valu.json[{vkey}] ({vrec[vkey].get("source", "")})'}
-        except Exception:
-            valu = None
+            rec = json.load(open(f))
+        except ValueError:
+            return None, None, None
+        want = kname.split('<')[0]
+        for kk, vv in rec.items():
+            if not kk.startswith(base) or not isinstance(vv, dict) or 'kernels' not in vv:
+                continue
+            cands = {k: v for k, v in vv['kernels'].items() if k.replace('jds::', '').split('<')[0] == want}
+            if cands:
+                pick = max(cands, key=lambda k: cands[k]['valu_insts'] if isinstance(cands[k], dict) else cands[k])
+                return cands[pick], int(kk[len(base):]), f'profiles/{fname}[{kk}] ({vv.get("source", "")})'
+        return None, None, None
+
+    traffic, traffic_src = None, None
+    tb, tb0, tsrc = pmc_entry('pmc_traffic.json')
+    if tb is not None:
+        traffic, traffic_src = int(tb * B / tb0), tsrc
+
+    # VALU issue of the dominant kernel from its own PMC counts: every class at
+    # its minimum (peak-rate) issue cost over the SIMD-cycles of the profiled
+    # launches -- a lower bound on VALU-busy, <= 1 by construction
+    # (tools/r6_valu.py); frac_upper prices int32 / unclassified at the slow class
+    valu = None
+    vr, _, vsrc = pmc_entry('pmc_valu.json')
+    if vr is not None and not (args.exact or args.exact_inv or args.inv_fast):
+        valu = {'frac': round(vr['valu_frac'], 4), 'frac_upper': round(vr['valu_frac_upper'], 4),
+                'valu_insts_per_wave': round(vr['valu_per_wave'], 1),
+                'wave_split': {k: round(v, 3) for k, v in vr['wave_split'].items()},
+                'lds_conflict_share': round(vr['lds_conflict_share'], 3),
+                'peak': 'SIMD-cycles of the profiled launches (1024 x GRBM_GUI_ACTIVE / 8); each VALU class at its '
+                        'minimum wave64 issue cost (fp64 4, fp32 / int32 / moves 2, cvt 4, transcendental 8 cycles)',
+                'source': vsrc}
     bound = 'valu' if valu and valu['frac'] > achieved / HBM_PEAK_GBS else 'hbm'
 
     result = {
@@ -713,7 +721,9 @@ def run_point(args, dev, world, backend, rank, B, H, W, quality, mode, pf, block
                      'valu': valu,
                      'note': ('kernel: the longest single launch of the step; achieved / peak / frac: the HBM '
                               'roofline by its algorithmic bytes; bound: the resource with the larger fraction '
-                              '(valu.frac: issue cycles / SIMD cycles, DESIGN.md section 4 floor table)')},
+                              '(valu.frac: a lower bound on the VALU-busy fraction from the kernel\'s own PMC counts, '
+                              'DESIGN.md section 4); traffic: HBM bytes per launch from calibrated FETCH / WRITE '
+                              'counters')},
         'kernels_ms': {k: round(v['ms_per_step'], 4) for k, v in kernels.items()},
         'kernels_profile': kprof and {**{k: round(v, 4) if isinstance(v, float) else v for k, v in kprof.items()},
                                       'avg_launch_ms': {k: round(v['avg_launch_ms'], 4) for k, v in kernels.items()},

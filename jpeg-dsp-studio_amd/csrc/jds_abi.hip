@@ -271,6 +271,7 @@ struct jds_plan {
   // fast path: fp32 tables, fix-up lists and counters
   DevBuf fq32, gk32, fixbits, fixlist, counters, part32;  // per-item fix-up bitmaps and lists; per-tile statistics
   DevBuf invfix;  // certified fast inverse: run and per-item counters (InvFix, jds_inv_fast.hip)
+  DevBuf invlist;  // k_inv_fast6 (4:2:0): the tiles a run hands to the exact kernel (InvFix::list)
   unsigned inv_runs = 0;  // fast-inverse runs so far: picks the list counter (InvFix::parity)
   bool last_inv_fast = false;  // the last run's inverse was the certified fast one
   // Where the certified fast inverse pays (measured, 1 MI355X): 4:2:x plans
@@ -287,7 +288,7 @@ struct jds_plan {
   int last_fwd8_bank = -1;       // bank of the last such run (jds_plan_fix_counts), -1: none
   InvFix inv_fix() const {
     return {(unsigned*)invfix.p, (unsigned*)invfix.p + 16, 0, (int)(inv_runs & 1u), (int)(inv_runs % 3u),
-            (int)(inv_runs % 16u == 15u)};
+            (int)(inv_runs % 16u == 15u), (uint2*)invlist.p};
   }
   DevBuf planes;  // 16x16 path: reconstructed chroma planes (n x 2 x hc x wc f64)
   double* qt = nullptr;  // host copy of the per-frame 8x8 tables (entropy headers)
@@ -706,6 +707,7 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
         (e = hipMemset(p->part32.p, 0, p->part32.n)) != hipSuccess ||
         (e = p->invfix.ensure(64 + 12 * (size_t)n)) != hipSuccess ||
         (e = hipMemset(p->invfix.p, 0, 64 + 12 * (size_t)n)) != hipSuccess ||
+        (mode == JDS_SS_420 && (e = p->invlist.ensure(8 * (size_t)n * inv_tiles(mode, (int)H, (int)W))) != hipSuccess) ||
         (n_q > 1 && (e = p->dct32.ensure(sizeof(float) * (size_t)n_frames * g.cpf)) != hipSuccess) ||
         (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess ||
@@ -858,7 +860,10 @@ int jds_plan_profile(jds_plan* p, int enable) {
       return fail(JDS_ENOMEM, "host allocation failed");
     }
     for (; m.cap < cap; ++m.cap) {
-      hipError_t e = hipEventCreate(&m.ev[m.cap]);
+      // timing-only marks: no system-scope fence (cache write-back and
+      // invalidate) per mark, which otherwise lands inside the next launch's
+      // interval and perturbs the profiled step (r06: +5 % over the timed one)
+      hipError_t e = hipEventCreateWithFlags(&m.ev[m.cap], hipEventDisableSystemFence);
       if (e != hipSuccess) {
         marks_release(m);
         return fail(JDS_EHIP, "hipEventCreate: %s", hipGetErrorString(e));
@@ -930,6 +935,7 @@ void jds_plan_destroy(jds_plan* p) {
   p->fixbits.release();
   p->part32.release();
   p->invfix.release();
+  p->invlist.release();
   p->planes.release();
   p->dct32.release();
   p->gen_tab.release();

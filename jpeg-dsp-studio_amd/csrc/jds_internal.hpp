@@ -94,6 +94,9 @@ struct Fwd16Fast {
 //   runs the exact tile code directly; every 16th run (`probe`) tries the fast
 //   path again.
 // All zeroed at plan creation.
+// * list (k_inv_fast6, 4:2:0): the (frame, tile) of every tile the run hands
+//   to the exact kernel, count[parity] entries (n x tiles capacity), walked by
+//   k_inv6_fix right after.
 struct InvFix {
   unsigned* count;
   unsigned* item;
@@ -101,6 +104,7 @@ struct InvFix {
   int parity;
   int rot;
   int probe;
+  uint2* list;
 };
 
 // Per-frame quantiser: q16 = 16*Q (pocketfft's first-axis fct = 1/16 folded in), q = Q.

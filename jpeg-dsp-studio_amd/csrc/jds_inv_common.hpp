@@ -60,4 +60,92 @@ __device__ __forceinline__ Col16 load_col(const int16_t* __restrict__ plane, lon
   for (int r = 0; r < 8; ++r) c.q[r] = blk[r * 8 + v];
   return c;
 }
+
+// A column held two coefficients per VGPR (k_inv_fast6: the prefetched column
+// lives across a whole luma round, 4 VGPRs instead of 8): element r in the
+// low / high half of w[r / 2], loaded by d16 / d16_hi loads.
+typedef short jds_short2 __attribute__((ext_vector_type(2)));
+struct Col16p {
+  jds_short2 w[4];
+  __device__ __forceinline__ int q(int r) const { return (int)((r & 1) ? w[r >> 1].y : w[r >> 1].x); }
+};
+__device__ __forceinline__ Col16p load_colp(const int16_t* __restrict__ plane, long long boff, int v, bool ok) {
+  const int16_t* blk = plane + (ok ? boff : 0ll);
+  Col16p c;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    c.w[i].x = blk[(2 * i) * 8 + v];
+    c.w[i].y = blk[(2 * i + 1) * 8 + v];
+  }
+  return c;
+}
+
+// ---- the transpose-free 4:2:0 tile (k_inv_fast6, round 6) ------------------
+//
+// k_inv_fast's 64 x 128 tile with its chroma window widened to whole ring
+// blocks, so that every chroma block's 8 x 8 samples have a place in it: a
+// block's column pass writes its outputs there and its row pass reads the rows
+// back and overwrites them (the window is the transpose medium), and the luma
+// transposes run in registers (xpose8).  Window column 0 is chroma column
+// X0/2 - 8: block j of the tile's 10 chroma block columns (ring included)
+// starts at window column 8 j (16-B aligned: the row pass's ds_read_b128 /
+// ds_write_b128), and the upsample's six samples at 4 bj + 7 are read as the
+// aligned pairs from 4 bj + 6.  Row r of the window is chroma row Y0/2 - 1 + r
+// as in k_inv_fast (the top / bottom ring blocks contribute one row each).
+// Rows 82 doubles apart differ by 36 dword banks (4 mod 8): with the in-block
+// index's bit 0 on lane bit 3 (xpose8) the two output rows of a 16-lane group
+// read adjacent window rows on disjoint bank halves (tools/lds_bank_model.py).
+struct W6 {
+  static constexpr int TH = 64, TW = 128, NT = 512, SY = 2, SX = 2;
+  static constexpr int RB = 64, NYB = 128, YBC = 16;   // luma blocks per round / per tile / per block row
+  static constexpr int CBR = 6, CBC = 10, NCB = 60;    // chroma blocks per plane incl. the ring
+  static constexpr int CWR = 34, CX = 8, CWC = 80, CWS = 82;
+};
+
+// 8 x 8 transpose of doubles across the 8 lanes of a block with no LDS.  The
+// lanes of block b in a wave are b, b + 8, .., b + 56 (in-block index k =
+// lane >> 3 & 7).  In: lane k holds c[i] = A[i][k] (column k); out: lane k
+// holds c[j] = A[k][j] (row k).  One butterfly stage per bit of k, each
+// exchanging the register halves whose index bit differs from the lane's:
+// k bit 2 = lane bit 5 by v_permlane32_swap and k bit 1 = lane bit 4 by
+// v_permlane16_swap (the swap of the upper lanes of one register with the
+// lower lanes of the other is exactly a stage: one instruction per dword pair),
+// k bit 0 = lane bit 3 by a DPP row rotation by 8 (lane ^ 8 in a 16-lane row)
+// and selects.  Every lane of the wave must be active.
+__device__ __forceinline__ void xswap32(double& x, double& y) {
+  const auto a = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(x), (unsigned)__double2loint(y), false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(y), false, false);
+  x = __hiloint2double((int)h[0], (int)a[0]);
+  y = __hiloint2double((int)h[1], (int)a[1]);
+}
+__device__ __forceinline__ void xswap16(double& x, double& y) {
+  const auto a = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(x), (unsigned)__double2loint(y), false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(y), false, false);
+  x = __hiloint2double((int)h[0], (int)a[0]);
+  y = __hiloint2double((int)h[1], (int)a[1]);
+}
+__device__ __forceinline__ double dpp_ror8(double v) {  // the value of lane ^ 8 (every lane has a source)
+  const int l = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x128, 0xf, 0xf, true);
+  const int h = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x128, 0xf, 0xf, true);
+  return __hiloint2double(h, l);
+}
+__device__ __forceinline__ void xswap8(double& x, double& y, bool odd) {
+  const double px = dpp_ror8(x), py = dpp_ror8(y);
+  const double nx = odd ? py : x, ny = odd ? y : px;
+  x = nx;
+  y = ny;
+}
+__device__ __forceinline__ void xpose8(double (&c)[8]) {
+  const bool odd = (threadIdx.x >> 3) & 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) xswap32(c[i], c[i + 4]);
+  xswap16(c[0], c[2]);
+  xswap16(c[1], c[3]);
+  xswap16(c[4], c[6]);
+  xswap16(c[5], c[7]);
+  xswap8(c[0], c[1], odd);
+  xswap8(c[2], c[3], odd);
+  xswap8(c[4], c[5], odd);
+  xswap8(c[6], c[7], odd);
+}
 }  // namespace jds

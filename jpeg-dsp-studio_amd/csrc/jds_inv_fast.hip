@@ -45,6 +45,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -674,6 +675,323 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
 #endif
 }
 
+// ------------------------------------- 4:2:0 without a transpose buffer --
+//
+// k_inv_fast6 (round 6): k_inv_fast<4:2:0, 0>'s tile (64 x 128 px, 512
+// threads), operations and certificate, without the 37 KB transpose buffer
+// that held k_inv_fast to two workgroups (four waves) per SIMD-quad: 45 KB of
+// LDS, so three workgroups fit a CU when the registers allow it (<= 80).
+//  * chroma: each block's column pass writes its outputs into the chroma
+//    window at the block's own place (W6: the window widened to whole ring
+//    blocks) and its row pass reads the row back, transforms, clips and
+//    overwrites it -- the window is the transpose medium (the 8 lanes of a
+//    block are one wave's, whose LDS operations keep their order: no barrier);
+//  * luma: the column-to-row transpose in registers (xpose8), lanes b + 8 k of
+//    a wave holding block b's column / row k.
+// Every value goes through k_inv_fast's operations in k_inv_fast's order
+// (aan8 on the folded table, the clips, the unnormalised upsample, the colour
+// terms on the magic grid), so tools/inv_bound.py's bound and the certificate
+// carry over unchanged; only the data movement differs.  An uncertain tile
+// (and every tile of an item in exact mode) is appended to a list that
+// k_inv6_fix recomputes right after with inv2_tile (the reference's order).
+// a volatile 2-double LDS access: emitted as exactly one ds_read_b128 /
+// ds_write_b128 (plain ones get narrowed to the used halves and re-paired as
+// 8-cycle ds_read2_b64; MI355X_MICROARCH.md §LDS)
+typedef double dv2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) volatile dv2 lds_dv2;
+
+__device__ __forceinline__ void chroma8_fast_w6(const double* __restrict__ cw, int c0, int wq, int wt,
+                                                double (&C)[8]) {
+  double vb[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) vb[j] = fvsum(cw[wq * W6::CWS + c0 + j], cw[wt * W6::CWS + c0 + j]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    C[2 * i] = fhsum(vb[i], vb[i + 1]);          // (1/4, 3/4) on (m-1, m)
+    C[2 * i + 1] = fhsum(vb[i + 2], vb[i + 1]);  // (3/4, 1/4) on (m, m+1)
+  }
+}
+
+// the folded table's column k (fast_col's four ds_read_b128) times the
+// column's coefficients; qhi / qlo track the coefficient range when `track`
+// (the column's LDS offset is laundered per call: otherwise the compiler keeps
+// the loop-invariant table column live across the luma rounds, 16 VGPRs)
+__device__ __forceinline__ void deq_col(const Col16p& in, const double* __restrict__ qs, int k, bool track,
+                                        double (&c)[8], int& qhi, int& qlo) {
+  double t[8];
+  int off = k * QS_STRIDE;
+  asm volatile("" : "+v"(off));
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const double2 d = *reinterpret_cast<const double2*>(qs + off + 2 * p);
+    t[2 * p] = d.x;
+    t[2 * p + 1] = d.y;
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int q = in.q(r);
+    qhi = track ? max(qhi, q) : qhi;
+    qlo = track ? min(qlo, q) : qlo;
+    c[r] = (double)q * t[r];
+  }
+}
+
+#ifndef JDS_K6_WPE
+#define JDS_K6_WPE 6
+#endif
+__global__ void __launch_bounds__(W6::NT) __attribute__((amdgpu_waves_per_eu(JDS_K6_WPE)))
+k_inv_fast6(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+            uint8_t* __restrict__ rgb_out, jds_frame_stats* __restrict__ st, unsigned* __restrict__ fixcount,
+            unsigned* __restrict__ next_count, unsigned* __restrict__ item_cnt, uint2* __restrict__ fixlist,
+            const int rot, const int probe, const int fix_all, const int fin) {
+  __shared__ __attribute__((aligned(16))) double s_cw[2][W6::CWR * W6::CWS];
+  __shared__ __attribute__((aligned(16))) double s_qs[QS_WORDS];  // Q[u][v] * a_u * a_v / 8 at qs_index(u, v)
+  __shared__ uint32_t s_cert[3];                                   // min / max fraction word, max |q|
+  __shared__ double s_qmax;
+  const int tid = threadIdx.x;
+  const int frame = blockIdx.y, tile = blockIdx.x;
+  if (fin >= 0 && tile == 0 && tid == 0) finalize_frame(g, st + frame, fin);
+  // per-item adaptivity (InvFix), as k_inv_fast
+  const unsigned n_items = gridDim.y, ntile = gridDim.x;
+  unsigned* cnt_prev = item_cnt + ((rot + 2) % 3) * n_items;
+  unsigned* cnt_now = item_cnt + rot * n_items;
+  const unsigned prev = cnt_prev[frame];
+  if (tid == 0) {
+    if (tile == 0) item_cnt[((rot + 1) % 3) * n_items + frame] = 0u;  // the next run's
+    if (frame == 0 && tile == 0) *next_count = 0u;                     // the next run counts from zero
+  }
+#ifndef JDS_K6_PROBE
+#define JDS_K6_PROBE 0  // tools: timing probes (wrong values): 1 no luma transpose, 2 no chroma row pass, 4 no chroma column writes
+#endif
+  const bool item_exact = !JDS_K6_PROBE && !probe && !fix_all && prev * 8u > ntile;
+  if (item_exact) {  // (uniform) every tile of the item to the exact kernel; the item keeps its count
+    if (tid == 0) {
+      if (tile == 0) cnt_now[frame] = prev;
+      fixlist[atomicAdd(fixcount, 1u)] = make_uint2((unsigned)frame, (unsigned)tile);
+    }
+    return;
+  }
+
+  // lane (block slot lb, in-block index k): the 8 lanes of a block are b, b + 8, .. of one wave
+  const int k = (tid >> 3) & 7, lb = ((tid >> 6) << 3) | (tid & 7);
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int Y0 = ty * W6::TH, X0 = tx * W6::TW;
+  const int16_t* cf = coeffs + (size_t)frame * g.cpf;
+  const int cwy0 = Y0 / 2 - 1;
+  auto luma_blk = [&](int r, int& by, int& bx) {
+    const int blk = r * W6::RB + lb;
+    by = Y0 / 8 + (blk >> 4);
+    bx = X0 / 8 + (blk & 15);
+    return by < g.nby && bx < g.nbx;
+  };
+  int qhi = 0, qlo = 0;  // max / min q this lane read
+  // the first coefficient loads (luma round 0, this lane group's Cb block) before the table set-up
+  Col16p lq;
+  {
+    int by, bx;
+    const bool ok = luma_blk(0, by, bx);
+    lq = load_colp(cf, ((long long)by * g.nbx + bx) * 64, k, ok);
+  }
+  const int ci = lb / W6::CBC, cj = lb - ci * W6::CBC;
+  const int cby = Y0 / 16 - 1 + ci, cbx = X0 / 16 - 1 + cj;
+  const bool cvalid = lb < W6::NCB && cby >= 0 && cbx >= 0 && cby < g.ncy && cbx < g.ncx;
+  const long long cboff = ((long long)cby * g.ncx + cbx) * 64;
+  Col16p cq = load_colp(cf + g.off_cb, cboff, k, cvalid);
+  if (tid < 64) {
+    const double q = fq[frame].q[tid];
+    s_qs[qs_index(tid >> 3, tid & 7)] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
+    if (tid == 0) {
+      s_cert[0] = 0xffffffffu;
+      s_cert[1] = 0u;
+      s_cert[2] = 0u;
+      s_qmax = fq[frame].qmax;
+    }
+  }
+  __syncthreads();
+
+  // ---- 1. chroma window: column pass into the block's place, row pass in place
+  const int r0 = 8 * ci - 7, c0 = 8 * cj;  // the block's first window row / column
+#pragma unroll 1
+  for (int p = 0; p < 2; ++p) {
+    const Col16p cur = cq;
+    if (p == 0) cq = load_colp(cf + g.off_cr, cboff, k, cvalid);
+    if (cvalid) {
+      double* w = s_cw[p];
+      double c[8];
+      deq_col(cur, s_qs, k, true, c, qhi, qlo);
+      aan8(c);
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (!(JDS_K6_PROBE & 4) && (unsigned)(r0 + r) < (unsigned)W6::CWR) w[(r0 + r) * W6::CWS + c0 + k] = c[r];
+      __builtin_amdgcn_wave_barrier();  // the block's other lanes' columns (a wave's LDS operations keep their order)
+      const int wr = r0 + k;
+      if (!(JDS_K6_PROBE & 2) && (unsigned)wr < (unsigned)W6::CWR) {  // the rows the window holds (a ring block: one)
+        double* row = w + wr * W6::CWS + c0;  // (16-B aligned: four b128 each way)
+        lds_dv2* row2 = (lds_dv2*)row;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const dv2 d = row2[j];
+          c[2 * j] = d.x;
+          c[2 * j + 1] = d.y;
+        }
+        aan8(c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c[j] = fmin(fmax(c[j], -128.0), 127.0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dv2 d;
+          d.x = c[2 * j];
+          d.y = c[2 * j + 1];
+          row2[j] = d;
+        }
+        // cv2's clamped taps at the image's left / right edge pixels read the
+        // edge column alone: replicated into the ring (and past the plane's end)
+        if (cbx == 0) row[-1] = c[0];
+        const int ke = g.wc - 1 - cbx * 8;
+        if ((unsigned)ke < 8u) {
+          const double e = (ke == 0 ? c[0] : ke == 1 ? c[1] : ke == 2 ? c[2] : ke == 3 ? c[3]
+                            : ke == 4 ? c[4] : ke == 5 ? c[5] : ke == 6 ? c[6] : c[7]);
+          for (int col = c0 + ke + 1; col < W6::CWC; ++col) w[wr * W6::CWS + col] = e;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. luma rounds: IDCT (transpose in registers), upsample, colour, certify, store
+  uint32_t lo_min = 0xffffffffu, lo_max = 0u;
+  uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
+#pragma unroll 1
+  for (int r = 0; r < W6::NYB / W6::RB; ++r) {
+    int by, bx;
+    const bool bvalid = luma_blk(r, by, bx);
+#ifdef JDS_K6_NOPREFETCH
+    if (r > 0) lq = load_colp(cf, ((long long)by * g.nbx + bx) * 64, k, bvalid);
+    const Col16p cur = lq;
+#else
+    const Col16p cur = lq;
+    if (r + 1 < W6::NYB / W6::RB) {
+      int by1, bx1;
+      const bool ok1 = luma_blk(r + 1, by1, bx1);
+      lq = load_colp(cf, ((long long)by1 * g.nbx + bx1) * 64, k, ok1);
+    }
+#endif
+    // every lane transforms (xpose8 needs the whole wave); blocks outside the
+    // grid neither count towards Dmax nor store
+    double Yv[8];
+    deq_col(cur, s_qs, k, bvalid, Yv, qhi, qlo);
+    aan8(Yv);
+    if (!(JDS_K6_PROBE & 1)) xpose8(Yv);
+    aan8(Yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Yv[j] = fmin(fmax(Yv[j], -128.0), 127.0);  // Y - 128
+    const int y = by * 8 + k, x0 = bx * 8;
+    if (bvalid && y < g.H && x0 < g.W) {
+      // output row 2m: chroma rows (m-1, m) weighted (1/4, 3/4); row 2m+1: (m+1, m)
+      const int m = y >> 1;
+      const int rq = (y & 1) ? m + 1 : m - 1;
+      const int wq = clampi(clampi(rq, 0, g.hc - 1) - cwy0, 0, W6::CWR - 1);
+      const int wt = clampi(clampi(m, 0, g.hc - 1) - cwy0, 0, W6::CWR - 1);
+      const int cc0 = (x0 - X0) / 2 + 7;  // window column of chroma column x0/2 - 1
+      const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
+      uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
+      const bool wide = nx == 8 && ((((uintptr_t)o) & 7u) == 0);
+      uint32_t pk[6];
+      uint32_t r_min = 0xffffffffu, r_max = 0u;
+      // four pixels at a time, both planes per pixel (register economy: the
+      // vertical sums of the 4 chroma columns a half reads, 12 channel words
+      // before packing); chroma8_fast's operations, column by column
+      // (the six samples from cc0 = 4 bj + 7 as halves of the aligned pairs from cc0 - 1)
+      // (volatile: exactly these b128 accesses -- the compiler otherwise narrows
+      // them to the used halves and re-pairs those as 8-cycle ds_read2_b64)
+      const lds_dv2* q0 = (const lds_dv2*)(s_cw[0] + wq * W6::CWS + cc0 - 1);
+      const lds_dv2* t0 = (const lds_dv2*)(s_cw[0] + wt * W6::CWS + cc0 - 1);
+      const lds_dv2* q1 = (const lds_dv2*)(s_cw[1] + wq * W6::CWS + cc0 - 1);
+      const lds_dv2* t1 = (const lds_dv2*)(s_cw[1] + wt * W6::CWS + cc0 - 1);
+      double vB[6], vR[6];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        // pairs 0..2 (samples cc0 - 1 .. cc0 + 4) for the first half, pair 3 (cc0 + 5, + 6) for the second
+#pragma unroll
+        for (int pr = (h ? 3 : 0); pr < (h ? 4 : 3); ++pr) {
+          const dv2 a = q0[pr], b = t0[pr], c = q1[pr], d = t1[pr];  // (volatile LDS reads)
+          if (pr > 0) {
+            vB[2 * pr - 1] = fvsum(a.x, b.x);
+            vR[2 * pr - 1] = fvsum(c.x, d.x);
+          }
+          if (pr < 3) {
+            vB[2 * pr] = fvsum(a.y, b.y);
+            vR[2 * pr] = fvsum(c.y, d.y);
+          }
+        }
+        uint32_t ch[12];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int px = 4 * h + e, i = px >> 1;
+          const double Cb = (px & 1) ? fhsum(vB[i + 2], vB[i + 1]) : fhsum(vB[i], vB[i + 1]);
+          const double Cr = (px & 1) ? fhsum(vR[i + 2], vR[i + 1]) : fhsum(vR[i], vR[i + 1]);
+          const double Y = Yv[px] + (MAGIC + 128.0);  // Y on byte_cert_y's grid, shared by the three channels
+          const double B = col_b<MadDev, 4>(Y, Cb);
+          const double Gt = col_gt<MadDev, 4>(Y, Cb);
+          const double R = col_r<MadDev, 4>(Y, Cr);
+          const double G = col_g<MadDev, 4>(Gt, Cr);
+          ch[3 * e] = cert_hi(R, r_min, r_max);
+          ch[3 * e + 1] = cert_hi(G, r_min, r_max);
+          ch[3 * e + 2] = cert_hi(B, r_min, r_max);
+        }
+#pragma unroll
+        for (int w = 0; w < 3; ++w) pk[3 * h + w] = pack4s(ch[4 * w], ch[4 * w + 1], ch[4 * w + 2], ch[4 * w + 3]);
+      }
+      lo_min = lo_min < r_min ? lo_min : r_min;
+      lo_max = lo_max > r_max ? lo_max : r_max;
+      if (wide) {
+        uint2* o2 = reinterpret_cast<uint2*>(o);
+        o2[0] = make_uint2(pk[0], pk[1]);
+        o2[1] = make_uint2(pk[2], pk[3]);
+        o2[2] = make_uint2(pk[4], pk[5]);
+      } else {
+#pragma unroll
+        for (int bb = 0; bb < 24; ++bb)
+          if (bb < 3 * nx) o[bb] = (uint8_t)(pk[bb >> 2] >> (8 * (bb & 3)));
+      }
+    }
+  }
+
+  // ---- 3. certification (k_inv_fast's); an uncertain tile goes to the exact kernel's list
+  cert_to_lds(lo_min, lo_max, (uint32_t)max(qhi, -qlo), s_cert);
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t mn = s_cert[0], mx = s_cert[1];
+    const double q = (double)s_cert[2];
+    const double E = K_LIN * (q * s_qmax) + K_CONST + 0x1p-31;
+    const double T = ceil(E * 0x1p+32) + 1.0;
+    const bool uncertain = (double)mn <= T || (double)mx >= 0x1p+32 - 1.0 - T;
+    if (uncertain || fix_all) {
+      fixlist[atomicAdd(fixcount, 1u)] = make_uint2((unsigned)frame, (unsigned)tile);  // (jds_plan_fix_counts)
+      atomicAdd(cnt_now + frame, 1u);
+    }
+  }
+}
+
+// The exact recomputation of the tiles k_inv_fast6 listed (inv2_tile: the
+// reference's operation order, k_inv2's layout), right after it on the same
+// stream: a few hundred workgroups walk the list (typically a handful of tiles
+// per 64 x 1080p run; every tile of an item in exact mode, all of them under
+// JDS_RUN_INV_FIXALL).  Separate from k_inv_fast6 so that the fallback's
+// registers and LDS do not hold the fast kernel's occupancy down.
+__global__ void __launch_bounds__(Inv<M420>::NT) __attribute__((amdgpu_waves_per_eu(Inv<M420>::WPE)))
+k_inv6_fix(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, const FrameQ* __restrict__ fq,
+           uint8_t* __restrict__ rgb_out, const unsigned* __restrict__ fixcount, const uint2* __restrict__ fixlist) {
+  __shared__ __attribute__((aligned(16))) InvShared<M420, 0> sh;
+  const unsigned n = *fixcount;
+  for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {  // (uniform)
+    const uint2 e = fixlist[i];
+    inv2_tile<M420, 0>(sh, g, tiles_x, 0, (int)e.x, (int)e.y, coeffs, fq, nullptr, rgb_out, nullptr, nullptr,
+                       nullptr, nullptr, 1);
+    __syncthreads();  // the next tile reuses the shared arrays
+  }
+}
+
 // ------------------------------------------------- 4:4:4, wave-local --
 //
 // k_inv_fast444: without chroma subsampling every output sample reads only the
@@ -1158,6 +1476,10 @@ hipError_t launch_inv16_fast(int mode, const Geo& g, int n, const int16_t* coeff
 
 // ------------------------------------------------------------ launchers --
 
+// k_inv6_fix's workgroups (grid-stride over the list): typically a handful of
+// tiles per run; an item in exact mode lists all of its tiles
+constexpr int INV6_FIX_GRID = 256;
+
 template <int MODE>
 static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const FrameQ* fq, const uint8_t* rgb_in,
                              uint8_t* rgb_out, jds_frame_stats* st, double* part, const InvFix& fx, hipStream_t s,
@@ -1168,6 +1490,20 @@ static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const F
   unsigned* cnt = fx.count + fx.parity;
   unsigned* nxt = fx.count + (fx.parity ^ 1);
   (void)rgb_in;  // SSE runs take the exact kernel (launch_codec)
+#ifdef JDS_INV6  // (A/B: tools/build_variant.py -DJDS_INV6 routes 4:2:0 to the transpose-free kernel)
+  if (MODE == M420 && fx.list) {
+    // the transpose-free kernel, then the exact recomputation of the tiles it listed
+    hipLaunchKernelGGL(k_inv_fast6, grid, dim3(W6::NT), 0, s, g, tx, coeffs, fq, rgb_out, st, cnt, nxt, fx.item,
+                       fx.list, fx.rot, fx.probe, fx.fix_all, fin);
+    kmark(s, "k_inv_fast6");
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int nfix = std::min(ty * tx * n, INV6_FIX_GRID);
+    hipLaunchKernelGGL(k_inv6_fix, dim3(nfix), dim3(Inv<M420>::NT), 0, s, g, tx, coeffs, fq, rgb_out, cnt, fx.list);
+    kmark(s, "k_inv6_fix");
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, cnt, nxt,
                      fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
   kmark(s, "k_inv_fast<%d,0>", MODE);
