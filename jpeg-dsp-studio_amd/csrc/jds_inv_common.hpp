@@ -80,6 +80,53 @@ __device__ __forceinline__ Col16p load_colp(const int16_t* __restrict__ plane, l
   return c;
 }
 
+// Row k of a block as one 16-B load (k_inv_fast6: lane b + 8 k of a wave,
+// block b), and the int16 8 x 8 transpose that turns the 8 lanes' rows into
+// their columns (Col16p) in registers: xpose8's three butterfly stages on
+// packed coefficients -- k bit 2 / bit 1 swap dword pairs (0,2),(1,3) /
+// (0,1),(2,3) by v_permlane32 / v_permlane16_swap, k bit 0 exchanges the
+// 16-bit halves with lane ^ 8 (DPP row rotation by 8, one v_perm_b32 whose
+// per-lane selector keeps the lane's own half): 12 instructions instead of
+// eight 2-byte loads per lane, whose 16-lane address groups spanned eight
+// blocks (measured: the column loads of the b + 8 k layout cost 44 us of
+// k_inv_fast6 at four waves per SIMD, 127 us at six).
+__device__ __forceinline__ uint4 load_rowq(const int16_t* __restrict__ plane, long long boff, int k, bool ok) {
+  return *reinterpret_cast<const uint4*>(plane + (ok ? boff : 0ll) + 8 * k);
+}
+// the same through a buffer resource of the frame's coefficients (boff and
+// the row in coefficients; the 32-bit byte offset: frames < 2 GB)
+__device__ __forceinline__ uint4 load_rowq_b(__amdgpu_buffer_rsrc_t r, long long boff, int k, bool ok) {
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(((ok ? boff : 0ll) + 8 * k) * 2), 0, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ Col16p xpose_q16(uint4 v) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // k bit 2: dwords (0,2), (1,3)
+    const auto a = __builtin_amdgcn_permlane32_swap(w[i], w[i + 2], false, false);
+    w[i] = a[0];
+    w[i + 2] = a[1];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i += 2) {  // k bit 1: dwords (0,1), (2,3)
+    const auto a = __builtin_amdgcn_permlane16_swap(w[i], w[i + 1], false, false);
+    w[i] = a[0];
+    w[i + 1] = a[1];
+  }
+  const bool odd = (threadIdx.x >> 3) & 1;  // k bit 0: the 16-bit halves with lane ^ 8
+  const uint32_t sel = odd ? 0x03020706u : 0x05040100u;  // odd: partner.hi | own.hi << 16; even: own.lo | partner.lo << 16
+  Col16p c;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t p = (uint32_t)__builtin_amdgcn_mov_dpp((int)w[i], 0x128, 0xf, 0xf, true);
+    const uint32_t r = __builtin_amdgcn_perm(p, w[i], sel);
+    c.w[i].x = (short)(r & 0xffffu);
+    c.w[i].y = (short)(r >> 16);
+  }
+  return c;
+}
+
 // ---- the transpose-free 4:2:0 tile (k_inv_fast6, round 6) ------------------
 //
 // k_inv_fast's 64 x 128 tile with its chroma window widened to whole ring

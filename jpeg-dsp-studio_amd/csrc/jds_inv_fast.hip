@@ -776,7 +776,10 @@ k_inv_fast6(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, 
   const int k = (tid >> 3) & 7, lb = ((tid >> 6) << 3) | (tid & 7);
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int Y0 = ty * W6::TH, X0 = tx * W6::TW;
-  const int16_t* cf = coeffs + (size_t)frame * g.cpf;
+  // the frame's coefficients and output through buffer resources (uniform
+  // bases in SGPRs, 32-bit lane offsets: fewer VGPRs than 64-bit addresses)
+  const __amdgpu_buffer_rsrc_t cf = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(coeffs + (size_t)frame * g.cpf), 0, (int)(g.cpf * 2), 0x00020000);
   const int cwy0 = Y0 / 2 - 1;
   auto luma_blk = [&](int r, int& by, int& bx) {
     const int blk = r * W6::RB + lb;
@@ -784,19 +787,25 @@ k_inv_fast6(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, 
     bx = X0 / 8 + (blk & 15);
     return by < g.nby && bx < g.nbx;
   };
+  auto luma_off = [&](int r, bool& ok) {
+    const int blk = r * W6::RB + lb;
+    const int by = Y0 / 8 + (blk >> 4), bx = X0 / 8 + (blk & 15);
+    ok = by < g.nby && bx < g.nbx;
+    return ((long long)by * g.nbx + bx) * 64;
+  };
   int qhi = 0, qlo = 0;  // max / min q this lane read
-  // the first coefficient loads (luma round 0, this lane group's Cb block) before the table set-up
-  Col16p lq;
+  // the first coefficient rows (luma round 0, this lane group's Cb block) before the table set-up
+  uint4 lq;
   {
-    int by, bx;
-    const bool ok = luma_blk(0, by, bx);
-    lq = load_colp(cf, ((long long)by * g.nbx + bx) * 64, k, ok);
+    bool ok;
+    const long long off = luma_off(0, ok);
+    lq = load_rowq_b(cf, off, k, ok);
   }
   const int ci = lb / W6::CBC, cj = lb - ci * W6::CBC;
   const int cby = Y0 / 16 - 1 + ci, cbx = X0 / 16 - 1 + cj;
   const bool cvalid = lb < W6::NCB && cby >= 0 && cbx >= 0 && cby < g.ncy && cbx < g.ncx;
   const long long cboff = ((long long)cby * g.ncx + cbx) * 64;
-  Col16p cq = load_colp(cf + g.off_cb, cboff, k, cvalid);
+  uint4 cq = load_rowq_b(cf, g.off_cb + cboff, k, cvalid);
   if (tid < 64) {
     const double q = fq[frame].q[tid];
     s_qs[qs_index(tid >> 3, tid & 7)] = q * c_aan[tid >> 3] * c_aan[tid & 7] * 0.125;
@@ -813,8 +822,8 @@ k_inv_fast6(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, 
   const int r0 = 8 * ci - 7, c0 = 8 * cj;  // the block's first window row / column
 #pragma unroll 1
   for (int p = 0; p < 2; ++p) {
-    const Col16p cur = cq;
-    if (p == 0) cq = load_colp(cf + g.off_cr, cboff, k, cvalid);
+    const Col16p cur = xpose_q16(cq);  // (uniform: the whole wave)
+    if (p == 0) cq = load_rowq_b(cf, g.off_cr + cboff, k, cvalid);
     if (cvalid) {
       double* w = s_cw[p];
       double c[8];
@@ -860,20 +869,25 @@ k_inv_fast6(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, 
 
   // ---- 2. luma rounds: IDCT (transpose in registers), upsample, colour, certify, store
   uint32_t lo_min = 0xffffffffu, lo_max = 0u;
-  uint8_t* out_f = rgb_out + (size_t)frame * g.H * g.W * 3;
+  const __amdgpu_buffer_rsrc_t out_f = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(rgb_out + (size_t)frame * g.H * g.W * 3), 0, g.H * g.W * 3, 0x00020000);
 #pragma unroll 1
   for (int r = 0; r < W6::NYB / W6::RB; ++r) {
     int by, bx;
     const bool bvalid = luma_blk(r, by, bx);
 #ifdef JDS_K6_NOPREFETCH
-    if (r > 0) lq = load_colp(cf, ((long long)by * g.nbx + bx) * 64, k, bvalid);
-    const Col16p cur = lq;
+    if (r > 0) {
+      bool ok;
+      const long long off = luma_off(r, ok);
+      lq = load_rowq_b(cf, off, k, ok);
+    }
+    const Col16p cur = xpose_q16(lq);
 #else
-    const Col16p cur = lq;
+    const Col16p cur = xpose_q16(lq);
     if (r + 1 < W6::NYB / W6::RB) {
-      int by1, bx1;
-      const bool ok1 = luma_blk(r + 1, by1, bx1);
-      lq = load_colp(cf, ((long long)by1 * g.nbx + bx1) * 64, k, ok1);
+      bool ok1;
+      const long long off1 = luma_off(r + 1, ok1);
+      lq = load_rowq_b(cf, off1, k, ok1);
     }
 #endif
     // every lane transforms (xpose8 needs the whole wave); blocks outside the
@@ -894,8 +908,7 @@ k_inv_fast6(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, 
       const int wt = clampi(clampi(m, 0, g.hc - 1) - cwy0, 0, W6::CWR - 1);
       const int cc0 = (x0 - X0) / 2 + 7;  // window column of chroma column x0/2 - 1
       const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
-      uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
-      const bool wide = nx == 8 && ((((uintptr_t)o) & 7u) == 0);
+      const int o = (y * g.W + x0) * 3;  // byte offset in the frame (8-B aligned when nx == 8)
       uint32_t pk[6];
       uint32_t r_min = 0xffffffffu, r_max = 0u;
       // four pixels at a time, both planes per pixel (register economy: the
@@ -944,15 +957,19 @@ k_inv_fast6(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, 
       }
       lo_min = lo_min < r_min ? lo_min : r_min;
       lo_max = lo_max > r_max ? lo_max : r_max;
-      if (wide) {
-        uint2* o2 = reinterpret_cast<uint2*>(o);
-        o2[0] = make_uint2(pk[0], pk[1]);
-        o2[1] = make_uint2(pk[2], pk[3]);
-        o2[2] = make_uint2(pk[4], pk[5]);
+      if (nx == 8) {
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int w = 0; w < 3; ++w) {
+          u2 v;
+          v.x = pk[2 * w];
+          v.y = pk[2 * w + 1];
+          __builtin_amdgcn_raw_buffer_store_b64(v, out_f, o + 8 * w, 0, 0);
+        }
       } else {
 #pragma unroll
         for (int bb = 0; bb < 24; ++bb)
-          if (bb < 3 * nx) o[bb] = (uint8_t)(pk[bb >> 2] >> (8 * (bb & 3)));
+          if (bb < 3 * nx) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pk[bb >> 2] >> (8 * (bb & 3))), out_f, o + bb, 0, 0);
       }
     }
   }
