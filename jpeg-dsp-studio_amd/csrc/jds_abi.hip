@@ -18,6 +18,12 @@
 #include "jds_dct8.hpp"
 #include "jds_internal.hpp"
 
+#ifdef JDS_INV6
+#define JDS_INV6_LIST 1  // the transpose-free variant's tile list (A/B builds: tools/build_variant.py)
+#else
+#define JDS_INV6_LIST 0
+#endif
+
 namespace jds {
 hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* rgb, uint8_t* rgb_out,
                         int16_t* coeffs, const FrameQ* fq, const double* gk, jds_frame_stats* st,
@@ -271,7 +277,7 @@ struct jds_plan {
   // fast path: fp32 tables, fix-up lists and counters
   DevBuf fq32, gk32, fixbits, fixlist, counters, part32;  // per-item fix-up bitmaps and lists; per-tile statistics
   DevBuf invfix;  // certified fast inverse: run and per-item counters (InvFix, jds_inv_fast.hip)
-  DevBuf invlist;  // k_inv_fast6 (4:2:0): the tiles a run hands to the exact kernel (InvFix::list)
+  DevBuf invlist;  // k_inv_fast6 (4:2:0, -DJDS_INV6 builds): the tiles a run hands to the exact kernel (InvFix::list)
   unsigned inv_runs = 0;  // fast-inverse runs so far: picks the list counter (InvFix::parity)
   bool last_inv_fast = false;  // the last run's inverse was the certified fast one
   // Where the certified fast inverse pays (measured, 1 MI355X): 4:2:x plans
@@ -707,7 +713,7 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
         (e = hipMemset(p->part32.p, 0, p->part32.n)) != hipSuccess ||
         (e = p->invfix.ensure(64 + 12 * (size_t)n)) != hipSuccess ||
         (e = hipMemset(p->invfix.p, 0, 64 + 12 * (size_t)n)) != hipSuccess ||
-        (mode == JDS_SS_420 && (e = p->invlist.ensure(8 * (size_t)n * inv_tiles(mode, (int)H, (int)W))) != hipSuccess) ||
+        (JDS_INV6_LIST && mode == JDS_SS_420 && (e = p->invlist.ensure(8 * (size_t)n * inv_tiles(mode, (int)H, (int)W))) != hipSuccess) ||
         (n_q > 1 && (e = p->dct32.ensure(sizeof(float) * (size_t)n_frames * g.cpf)) != hipSuccess) ||
         (e = hipMemcpy(p->fq32.p, h32, fqs * n, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(p->gk32.p, gk32, sizeof gk32, hipMemcpyHostToDevice)) != hipSuccess ||

@@ -61,6 +61,7 @@ __device__ __forceinline__ Col16 load_col(const int16_t* __restrict__ plane, lon
   return c;
 }
 
+#ifdef JDS_INV6  // k_inv_fast6's helpers (jds_inv_fast.hip, A/B builds only)
 // A column held two coefficients per VGPR (k_inv_fast6: the prefetched column
 // lives across a whole luma round, 4 VGPRs instead of 8): element r in the
 // low / high half of w[r / 2], loaded by d16 / d16_hi loads.
@@ -195,4 +196,5 @@ __device__ __forceinline__ void xpose8(double (&c)[8]) {
   xswap8(c[4], c[5], odd);
   xswap8(c[6], c[7], odd);
 }
+#endif  // JDS_INV6
 }  // namespace jds

@@ -675,6 +675,7 @@ k_inv_fast(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
 #endif
 }
 
+#ifdef JDS_INV6  // the transpose-free variant, built for A/B only (tools/build_variant.py -DJDS_INV6; tests/test_variants_cpu.py compiles it)
 // ------------------------------------- 4:2:0 without a transpose buffer --
 //
 // k_inv_fast6 (round 6): k_inv_fast<4:2:0, 0>'s tile (64 x 128 px, 512
@@ -1008,6 +1009,7 @@ k_inv6_fix(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, c
     __syncthreads();  // the next tile reuses the shared arrays
   }
 }
+#endif  // JDS_INV6
 
 // ------------------------------------------------- 4:4:4, wave-local --
 //
