@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 #include <mutex>
 #include <new>
 
@@ -288,6 +289,10 @@ struct jds_plan {
   // 4:4:4 the wave-local k_inv_fast444 is faster at every quality (512x512 x
   // 256: 167.5 vs k_inv2's 331.8 us).
   bool inv_fast_ok = true;
+  // some item's table is not coarse: mixed plans (quality sweeps) run the
+  // certified inverse too, their coarse items seeded into its per-item exact
+  // mode (InvFix), so every item takes the faster kernel for its table
+  bool inv_fast_any = true;
   bool last_fwd16_fast = false;  // 16x16: the last forward was the certified fp32 one
   unsigned fwd16_runs = 0;       // 16x16 certified forward runs so far: picks the list counter
   unsigned fwd8_runs = 0;        // 8x8 single-quality certified forward runs: picks the counter bank
@@ -631,8 +636,12 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
   // 4:2:0 Q10: 358 vs 410 us; an exact-value certificate variant, 425 us, did
   // not pay either -- DESIGN.md): such plans run k_inv2 unless JDS_RUN_INV_FAST
   p->inv_fast_ok = true;
+  p->inv_fast_any = mode == JDS_SS_444;
   if (mode != JDS_SS_444)
-    for (int i = 0; i < n; ++i) p->inv_fast_ok = p->inv_fast_ok && params[i].qtable[0] <= 60.0;
+    for (int i = 0; i < n; ++i) {
+      p->inv_fast_ok = p->inv_fast_ok && params[i].qtable[0] <= 60.0;
+      p->inv_fast_any = p->inv_fast_any || params[i].qtable[0] <= 60.0;
+    }
   p->mode = mode;
   p->pf = pf;
   p->g = g;
@@ -725,6 +734,20 @@ int jds_plan_create_q(jds_ctx* ctx, const jds_params* params, int n_frames, int 
       return fail(e == hipErrorOutOfMemory ? JDS_ENOMEM : JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
     }
     free(h32);
+    if (p->inv_fast_any && !p->inv_fast_ok) {
+      // mixed tables: the coarse items start in the certified inverse's exact
+      // mode (every rotation slot of their "tiles recomputed last run" counter
+      // holds all of their tiles); the probe run every 16th re-measures them
+      std::vector<unsigned> seed(3 * (size_t)n, 0u);
+      const unsigned nt = (unsigned)inv_tiles(mode, (int)H, (int)W);
+      for (int i = 0; i < n; ++i)
+        if (params[i].qtable[0] > 60.0) seed[i] = seed[n + i] = seed[2 * (size_t)n + i] = nt;
+      if ((e = hipMemcpy((unsigned*)p->invfix.p + 16, seed.data(), sizeof(unsigned) * seed.size(),
+                         hipMemcpyHostToDevice)) != hipSuccess) {
+        jds_plan_destroy(p);
+        return fail(JDS_EHIP, "plan upload: %s", hipGetErrorString(e));
+      }
+    }
   }
   *out = p;
   return JDS_OK;
@@ -839,7 +862,7 @@ int jds_plan_run(jds_plan* p, const uint8_t* rgb, uint8_t* rgb_out, int16_t* coe
   }
   InvFix fx = p->inv_fix();
   fx.fix_all = (flags & JDS_RUN_INV_FIXALL) ? 1 : 0;
-  const bool exact_inv = exact || (flags & JDS_RUN_EXACT_INV) != 0 || (!p->inv_fast_ok && !(flags & JDS_RUN_INV_FAST));
+  const bool exact_inv = exact || (flags & JDS_RUN_EXACT_INV) != 0 || (!p->inv_fast_any && !(flags & JDS_RUN_INV_FAST));
   if (phases & 2)
     HIP_TRY(launch_codec(p->mode, p->pf, p->g, p->n, rgb, rgb_out, coeffs, (const FrameQ*)p->fq.p,
                          (const double*)p->gk.p, stats, (double*)p->part.p, (flags & JDS_RUN_SSE) != 0, nullptr,

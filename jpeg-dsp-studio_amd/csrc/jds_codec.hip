@@ -695,12 +695,13 @@ hipError_t launch_codec(int mode, bool pf, const Geo& g, int n, const uint8_t* r
     bool fused_fin = false;
     if (!(phases & 4)) {  // jds_inv.hip (default); bit 2 selects the original k_inv
       // certified fast inverse (jds_inv_fast.hip) unless the caller wants the
-      // exact kernels, the IntermediateData maps or the SSE: with the SSE terms
-      // (sweeps) the fast kernel measured slower than k_inv2<MODE, 1> (register
-      // pressure of both paths in one kernel), so those runs stay exact
-      if (fx && !err_y && !rin) {
+      // exact kernels or the IntermediateData maps; 4:2:x SSE runs (sweeps)
+      // take k_inv_fast<MODE, 1> (round 6: 4.15 against 4.21-4.23 ms per
+      // 384-item sweep step with k_inv2<MODE, 1>, sse_y bit for bit), 4:4:4
+      // SSE runs the exact kernel
+      if (fx && !err_y && (!rin || mode != M444)) {
         // no SSE terms: the fast kernel does k_finalize's per-frame work itself
-        fused_fin = !sel;
+        fused_fin = !sel && !rin;
         e = launch_inv_fast(mode, g, n, coeffs, fq, rin, rgb_out, st, part, *fx, s, in_div,
                             fused_fin ? ((phases & 8) ? 1 : 0) : -1);
       } else {

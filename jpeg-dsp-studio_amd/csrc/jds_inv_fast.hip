@@ -1508,7 +1508,6 @@ static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const F
   // count[parity] was zeroed by the previous run; this run zeroes the other
   unsigned* cnt = fx.count + fx.parity;
   unsigned* nxt = fx.count + (fx.parity ^ 1);
-  (void)rgb_in;  // SSE runs take the exact kernel (launch_codec)
 #ifdef JDS_INV6  // (A/B: tools/build_variant.py -DJDS_INV6 routes 4:2:0 to the transpose-free kernel)
   if (MODE == M420 && fx.list) {
     // the transpose-free kernel, then the exact recomputation of the tiles it listed
@@ -1523,6 +1522,14 @@ static hipError_t inv_fast_t(const Geo& g, int n, const int16_t* coeffs, const F
     return hipGetLastError();
   }
 #endif
+  if (rgb_in != nullptr) {
+    // SSE runs (sweeps): the exact integer SSE and the luma SSE partials, per
+    // certified tile by the fast pass, per uncertain tile by the exact tile code
+    hipLaunchKernelGGL((k_inv_fast<MODE, 1>), grid, blk, 0, s, g, tx, coeffs, fq, rgb_in, rgb_out, st, part, cnt,
+                       nxt, fx.item, fx.rot, fx.probe, in_div, fx.fix_all, -1);
+    kmark(s, "k_inv_fast<%d,1>", MODE);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((k_inv_fast<MODE, 0>), grid, blk, 0, s, g, tx, coeffs, fq, nullptr, rgb_out, st, part, cnt, nxt,
                      fx.item, fx.rot, fx.probe, in_div, fx.fix_all, fin);
   kmark(s, "k_inv_fast<%d,0>", MODE);

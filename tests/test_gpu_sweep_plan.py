@@ -154,3 +154,43 @@ def test_sweep_plan_rejects_bad_shapes():
         _abi.Plan(_abi.context(0), [p] * 18, 64, 64, nq=9)  # more than 8 tables per frame
     with pytest.raises(ValueError):
         _abi.Plan(_abi.context(0), [p] * 5, 64, 64, nq=2)   # not a whole number of frames
+
+
+@pytest.mark.parametrize('h,w,mode', [(200, 328, '4:2:0'), (136, 264, '4:2:2'), (1080, 1920, '4:2:0')])
+def test_sweep_plan_sse_through_fast_inverse(h, w, mode):
+    """RUN_SSE | RUN_INV_FAST on a sweep plan: the certified inverse with the SSE
+    terms (k_inv_fast<MODE, 1>) where the library routes them there, coarse
+    items through its per-item exact mode from the second run on.  Two runs of
+    one plan, both bit-identical to the exact kernels, SSE fields included."""
+    import torch
+    from jds import _abi, codec
+    qs = [5, 10, 20, 50, 80, 95] if h < 1000 else [10, 50]
+    F = 2
+    frames = np.stack([cpu_ref.random_image(h, w, 810 + i) for i in range(F)])
+    o_x, c_x, s_x, _ = run_plan(frames, qs, mode, True, _abi.RUN_SSE | _abi.RUN_EXACT, len(qs))
+    # sse_y is an fp64 sum in the inverse kernel's own tile order (not part of the
+    # reference contract; NumPy's mean comes from the SSIM path): compared with
+    # the default SSE route's (k_inv2<MODE, 1>, the fast kernel's fallback code)
+    _, _, s_2, _ = run_plan(frames, qs, mode, True, _abi.RUN_SSE, len(qs))
+    params = [_abi.make_params(q, cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q), mode, True,
+                               codec.gaussian_kernel3()) for _ in range(F) for q in qs]
+    plan = _abi.Plan(_abi.context(0), params, h, w, nq=len(qs))
+    dev = torch.device('cuda:0')
+    rgb = torch.from_numpy(np.ascontiguousarray(frames)).to(dev)
+    out = torch.empty((len(params), h, w, 3), dtype=torch.uint8, device=dev)
+    cf = torch.empty((len(params), plan.geometry.coeffs_per_frame), dtype=torch.int16, device=dev)
+    st = torch.zeros((len(params), _abi.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    try:
+        for run in range(2):
+            out.zero_()
+            plan.run(rgb.data_ptr(), out.data_ptr(), cf.data_ptr(), st.data_ptr(),
+                     _abi.RUN_SSE | _abi.RUN_INV_FAST, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            s_f = st.cpu().numpy().view(_abi.STATS_DTYPE).reshape(-1)
+            assert np.array_equal(cf.cpu().numpy(), c_x), run
+            assert np.array_equal(out.cpu().numpy(), o_x), run
+            for fld in ('sse_rgb', 'nonzero', 'magnitude_bits', 'hist', 'pixels'):
+                assert np.array_equal(s_f[fld], s_x[fld]), (run, fld)
+            assert np.array_equal(s_f['sse_y'].view(np.uint64), s_2['sse_y'].view(np.uint64)), run
+    finally:
+        plan.close()
