@@ -72,7 +72,8 @@ typedef struct {
   double gauss[3];     /* cv2.getGaussianKernel(3, 0.75) taps (engines/color_space.py:39-40) */
 } jds_params;
 
-/* Per-frame statistics, all exact integers except sse_y.
+/* Per-frame statistics, all exact integers; sse_y is an exact integer sum
+ * converted to double and divided by 1e6.
  * estimate_bitrate_no_entropy (utils/metrics.py:51-92), histogram
  * (engines/pipeline.py:123-124) and the PSNR sums (utils/metrics.py:11,20). */
 typedef struct {
@@ -82,7 +83,8 @@ typedef struct {
   uint64_t block_overhead_bits; /* 2 * ceil(H/B) * ceil(W/B) (luma grid only) */
   uint64_t hist[50];            /* np.histogram(q, bins=50, range=(-100, 100))[0] */
   uint64_t sse_rgb;             /* sum (orig - rec)^2 over H*W*3 uint8 samples (JDS_RUN_SSE) */
-  double sse_y;                 /* sum (Y(orig) - Y(rec))^2, Y = .299R+.587G+.114B (JDS_RUN_SSE) */
+  double sse_y;                 /* sum (Y(orig) - Y(rec))^2, Y = .299R+.587G+.114B (JDS_RUN_SSE):
+                                   sum of (299dR+587dG+114dB)^2 in 64-bit integers / 1e6 */
   uint64_t pixels;              /* H * W */
   double fwd_ms, inv_ms;        /* host path only: forward / inverse kernel time (hipEvents) */
   double ssim[4];               /* host path only: SSIM of R, G, B and of Y (utils/metrics.py:12-21) */

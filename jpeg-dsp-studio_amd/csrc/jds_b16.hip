@@ -416,9 +416,7 @@ k_inv16(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __restric
         sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
         const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
         const double yo = luma(R0, G0, B0);
-        const double yr = luma((double)ur, (double)ug, (double)ub);
-        const double dy = yo - yr;
-        ssy = ssy + dy * dy;
+        ssy = ssy + luma_sse_e6(d0, d1, d2);
         ey[k] = fabs(yo - Y);                                          // pipeline.py:120
         er[k] = ((fabs(R0 - R) + fabs(G0 - G)) + fabs(B0 - B)) / 3.0;  // pipeline.py:121
       }
@@ -653,9 +651,7 @@ k_inv16f(const Geo g, const int tiles_x, const int16_t* __restrict__ coeffs, con
               sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
               const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
               const double yo = luma(R0, G0, B0);
-              const double yr = luma((double)ur, (double)ug, (double)ub);
-              const double dy = yo - yr;
-              ssy = ssy + dy * dy;
+              ssy = ssy + luma_sse_e6(d0, d1, d2);
               if constexpr (XTRA > 1) {
                 const size_t pix = (size_t)y * g.W + x0 + k;
                 err_y[pix] = fabs(yo - Yv[8 * h + k]);  // pipeline.py:120

@@ -482,9 +482,7 @@ k_inv(const Geo g, const int16_t* __restrict__ coeffs, const FrameQ* __restrict_
         sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
         const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
         const double yo = luma(R0, G0, B0);
-        const double yr = luma((double)ur, (double)ug, (double)ub);
-        const double dy = yo - yr;
-        ssy = ssy + dy * dy;
+        ssy = ssy + luma_sse_e6(d0, d1, d2);
         ey[k] = fabs(yo - Y);                                                   // pipeline.py:120
         er[k] = ((fabs(R0 - R) + fabs(G0 - G)) + fabs(B0 - B)) / 3.0;           // pipeline.py:121
       }
@@ -591,9 +589,11 @@ __global__ void k_finalize(const Geo g, jds_frame_stats* st, const double* __res
   jds_frame_stats* s = st + f;
   finalize_frame(g, s, zero_bin);
   if (with_sse) {
-    double a = 0.0;
-    for (int t = 0; t < tiles; ++t) a = a + sse_y_part[(size_t)f * tiles + t];
-    s->sse_y = a;
+    // the tiles' exact integer partials (luma_sse_e6) summed exactly in 64 bits,
+    // then converted to double and scaled by 1e-6 (round-to-nearest at each step)
+    unsigned long long e = 0ull;
+    for (int t = 0; t < tiles; ++t) e += (unsigned long long)sse_y_part[(size_t)f * tiles + t];
+    s->sse_y = (double)e / 1e6;
   }
 }
 

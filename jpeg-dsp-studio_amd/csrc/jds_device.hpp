@@ -32,6 +32,18 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 __device__ __forceinline__ double luma(double R, double G, double B) {
   return 0.299 * R + 0.587 * G + 0.114 * B;
 }
+// The luma SSE term of one pixel pair, 1e6 (Y(a) - Y(b))^2 with Y = .299 R +
+// .587 G + .114 B in exact decimal arithmetic, from the byte differences
+// d = a - b: D = 299 d0 + 587 d1 + 114 d2 is an integer (|D| <= 255,000), D^2 <
+// 2^36 is exact in a double, and so is any sum of up to 2^17 of them, in any
+// order.  Every inverse kernel sums these per tile (exact, order-free) and
+// k_finalize divides the frame total by 1e6 once (round 6: two fp64 lumas per
+// pixel, ~19 fp64 operations, became 3 integer and 2 fp64 ones; the total is
+// the exact sum correctly rounded, not NumPy's pairwise fp64 one: jds.h).
+__device__ __forceinline__ double luma_sse_e6(int d0, int d1, int d2) {
+  const double x = (double)(299 * d0 + 587 * d1 + 114 * d2);
+  return x * x;
+}
 __device__ __forceinline__ double chroma_b(double R, double G, double B) {
   return -0.168736 * R - 0.331264 * G + 0.5 * B + 128.0;
 }

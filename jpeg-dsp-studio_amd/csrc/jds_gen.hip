@@ -346,8 +346,7 @@ k_gen_px(const Geo g, const double* __restrict__ rec, const uint8_t* __restrict_
       sse = (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
       const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
       const double yo = luma(R0, G0, B0);
-      const double dy = yo - luma((double)ur, (double)ug, (double)ub);
-      ssy = dy * dy;
+      ssy = luma_sse_e6(d0, d1, d2);
       if constexpr (XTRA > 1) {
         err_y[i] = fabs(yo - Y);                                             // pipeline.py:119-120
         err_rgb[i] = ((fabs(R0 - R) + fabs(G0 - G)) + fabs(B0 - B)) / 3.0;  // pipeline.py:121

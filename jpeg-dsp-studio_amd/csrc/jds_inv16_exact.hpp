@@ -312,9 +312,7 @@ __device__ __forceinline__ void inv16s_tile(double* __restrict__ s_b, double* __
             sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
             const double R0 = (double)o0, G0 = (double)o1, B0 = (double)o2;
             const double yo = luma(R0, G0, B0);
-            const double yr = luma((double)ur, (double)ug, (double)ub);
-            const double dy = yo - yr;
-            ssy = ssy + dy * dy;
+            ssy = ssy + luma_sse_e6(d0, d1, d2);
             if constexpr (XTRA > 1) {
               const size_t pix = (size_t)y * g.W + x0 + k;
               err_y[pix] = fabs(yo - Yv[8 * h + k]);  // pipeline.py:120

@@ -367,10 +367,7 @@ __device__ __forceinline__ void inv2_tile(InvShared<MODE, XTRA>& sh, const Geo& 
             const int ur = byte_of(pk, b), ug = byte_of(pk, b + 1), ub = byte_of(pk, b + 2);
             const int d0 = o0 - ur, d1 = o1 - ug, d2 = o2 - ub;
             r_sse += (unsigned long long)(d0 * d0 + d1 * d1 + d2 * d2);
-            const double yo = luma((double)o0, (double)o1, (double)o2);
-            const double yr = luma((double)ur, (double)ug, (double)ub);
-            const double dy = yo - yr;
-            r_ssy = r_ssy + dy * dy;
+            r_ssy = r_ssy + luma_sse_e6(d0, d1, d2);
           }
         }
       }

@@ -156,6 +156,14 @@ def test_sweep_plan_rejects_bad_shapes():
         _abi.Plan(_abi.context(0), [p] * 5, 64, 64, nq=2)   # not a whole number of frames
 
 
+def exact_sse_y(orig, rec):
+    """sum over pixels of (Y(orig) - Y(rec))^2 with Y = .299R + .587G + .114B,
+    as the library states it: the integer sum of (299dR + 587dG + 114dB)^2 / 1e6"""
+    d = orig.astype(np.int64) - rec.astype(np.int64)
+    D = 299 * d[..., 0] + 587 * d[..., 1] + 114 * d[..., 2]
+    return int((D * D).sum()) / 1e6
+
+
 @pytest.mark.parametrize('h,w,mode', [(200, 328, '4:2:0'), (136, 264, '4:2:2'), (1080, 1920, '4:2:0')])
 def test_sweep_plan_sse_through_fast_inverse(h, w, mode):
     """RUN_SSE | RUN_INV_FAST on a sweep plan: the certified inverse with the SSE
@@ -168,10 +176,12 @@ def test_sweep_plan_sse_through_fast_inverse(h, w, mode):
     F = 2
     frames = np.stack([cpu_ref.random_image(h, w, 810 + i) for i in range(F)])
     o_x, c_x, s_x, _ = run_plan(frames, qs, mode, True, _abi.RUN_SSE | _abi.RUN_EXACT, len(qs))
-    # sse_y is an fp64 sum in the inverse kernel's own tile order (not part of the
-    # reference contract; NumPy's mean comes from the SSIM path): compared with
-    # the default SSE route's (k_inv2<MODE, 1>, the fast kernel's fallback code)
+    # sse_y is an exact integer sum of (299dR + 587dG + 114dB)^2 scaled by 1e-6
+    # (the same two roundings as Python's int / float): the same bits from every inverse route, and from NumPy
     _, _, s_2, _ = run_plan(frames, qs, mode, True, _abi.RUN_SSE, len(qs))
+    want = np.array([exact_sse_y(frames[i // len(qs)], o_x[i]) for i in range(F * len(qs))])
+    assert np.array_equal(s_x['sse_y'].view(np.uint64), want.view(np.uint64))
+    assert np.array_equal(s_2['sse_y'].view(np.uint64), want.view(np.uint64))
     params = [_abi.make_params(q, cpu_ref.scale_quant_matrix(cpu_ref.JPEG_LUMA_Q50, q), mode, True,
                                codec.gaussian_kernel3()) for _ in range(F) for q in qs]
     plan = _abi.Plan(_abi.context(0), params, h, w, nq=len(qs))
