@@ -858,7 +858,12 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
           const double a1 = __builtin_fma(2.0, pxy, B.c1), a2 = __builtin_fma(2.0, vxy, B.c2);  // (map2: exact doubling)
           const double b1 = ux * ux + uy * uy + B.c1, b2 = vx + vy + B.c2;
           const double d = b1 * b2;
+#ifdef JDS_SSIM_PROBE_NOSMAP  // tools: timing probe only (wrong values): the map computed, not stored
+          const double mv = div_map(a1 * a2, d);
+          if (mv == -7.25) smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = mv;
+#else
           smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
+#endif
         }
       }
       stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, k + 3, nchunks, P, cur);
@@ -1563,7 +1568,11 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
     hipLaunchKernelGGL((k_ss_band<SB_BH, true, false, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   else
     hipLaunchKernelGGL((k_ss_band<SB_BH, true, true, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
+#ifdef JDS_SSIM_PROBE_NOSMAP
+  hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 1, items), dim3(SB_THREADS), 0, s, B, 4);
+#else
   hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 2, items), dim3(SB_THREADS), 0, s, B, 3);  // luma map, luma MSE
+#endif
   if (rgb && (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_ss_final, dim3(rgb ? 5 : 2, items), dim3(256), 0, s, B, rgb ? 0 : 3);
   return hipGetLastError();
