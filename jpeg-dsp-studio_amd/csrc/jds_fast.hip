@@ -1155,7 +1155,10 @@ k_fwd_reduce_fix(const Geo g, jds_frame_stats* st, const uint32_t* __restrict__ 
 // fix-up instead of after it, one launch fewer.
 constexpr int FIX_RED_TILES = 16;
 template <int MODE, bool PF, int NRED = 0, int RFMT = 0>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
+#ifndef JDS_FIX_WPE  // tools: A/B builds of the fix-up's register budget
+#define JDS_FIX_WPE 5
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(JDS_FIX_WPE)))
 k_fix_fwd(const Geo g, const uint8_t* __restrict__ rgb, int16_t* __restrict__ coeffs,
           const FrameQ* __restrict__ fq, const double* __restrict__ gk, jds_frame_stats* __restrict__ st,
           const uint2* __restrict__ fixlist, const unsigned* __restrict__ fixcount, const int nq, const int n_flat,
