@@ -113,7 +113,7 @@ def sweep_device(frames, qualities: Sequence[int], mode: str = '4:2:0', prefilte
             br = bitrate_from_counts(int(s['nonzero']), float(magf[f, qi]), int(s['total_coeffs']), (H, W), 8)
             mse = float(s['sse_rgb']) / (H * W * 3)
             # mse_y: with ssim, the bit-exact NumPy mean (jds_psnr_ssim_dev); otherwise the
-            # fp64 luma SSE summed in tile order -- NumPy's pairwise mean to ~1e-15 relative
+            # luma SSE (an exact integer sum / 1e6) over H W -- NumPy's pairwise mean to ~1e-15 relative
             mse_y = float(ssims[f, qi, 2]) if ssim else float(s['sse_y']) / (H * W)
             items.append({'frame': f, 'quality': q, 'nonzero': int(s['nonzero']),
                           'magnitude_bits': int(s['magnitude_bits']), 'magnitude_bits_f32': float(magf[f, qi]),
