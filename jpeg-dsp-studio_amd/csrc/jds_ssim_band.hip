@@ -585,11 +585,47 @@ __device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, LDS& L, 
   int lo, hi;
   fill_cols(k, W, lo, hi);
   const int nc = hi - lo;
-  if (t < 0 || t >= 5 * nc) return;
-  const int q = t / nc, cc = t % nc, buf = 0;
-  const int slot = (lo + cc) % RING;
-  (void)c;
-  if constexpr (!LU) {
+  // luma: lanes (quantity group, column) -- x, x^2 | y, y^2 | x y -- so each
+  // staged row is read once per group instead of once per quantity (the
+  // fill's LDS reads -60 %: luma half 40.3 -> 38.5-39.3 us per 1080p item in a
+  // 384-pair batch)
+  if constexpr (LU) {
+    if (t < 0 || t >= 3 * nc) return;
+    const int g = t / nc, cc = t % nc, buf = 0;
+    const int slot = (lo + cc) % RING;
+    const double* tx = &L.in[buf].y[cc][0];
+    const double* ty = &L.in[buf].y[cc][NR];
+    if (g < 2) {  // q = g (the mean) and q = g + 2 (the square), from one image's rows
+      const double* tv = g == 0 ? tx : ty;
+      double s1 = L.ck[buf][g][cc], s2 = L.ck[buf][g + 2][cc];
+      L.ring[g][0][slot] = div7(s1);
+      L.ring[g + 2][0][slot] = div7(s2);
+#pragma unroll
+      for (int rr = 1; rr < BH; ++rr) {
+        if (rr < nr) {
+          const double vn = tv[rr + 6], vo = tv[rr - 1];
+          s1 = s1 + (vn - vo);
+          s2 = s2 + (vn * vn - vo * vo);
+          L.ring[g][rr][slot] = div7(s1);
+          L.ring[g + 2][rr][slot] = div7(s2);
+        }
+      }
+    } else {
+      double s = L.ck[buf][4][cc];
+      L.ring[4][0][slot] = div7(s);
+#pragma unroll
+      for (int rr = 1; rr < BH; ++rr) {
+        if (rr < nr) {
+          s = s + (tx[rr + 6] * ty[rr + 6] - tx[rr - 1] * ty[rr - 1]);
+          L.ring[4][rr][slot] = div7(s);
+        }
+      }
+    }
+  } else {  // R, G, B: lanes (quantity, column), exact integer window sums
+    if (t < 0 || t >= 5 * nc) return;
+    const int q = t / nc, cc = t % nc, buf = 0;
+    const int slot = (lo + cc) % RING;
+    (void)c;
     uint32_t xw[4], yw[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -609,21 +645,6 @@ __device__ __forceinline__ void fill_chunk(int c, int nr, int k, int W, LDS& L, 
       if (rr < nr) {
         S += tt[rr + 6] - tt[rr - 1];
         L.ring[q][rr][slot] = div7((double)S);
-      }
-    }
-  } else {
-    const double* tx = &L.in[buf].y[cc][0];
-    const double* ty = &L.in[buf].y[cc][NR];
-    double s = L.ck[buf][q][cc];
-    L.ring[q][0][slot] = div7(s);
-#pragma unroll
-    for (int rr = 1; rr < BH; ++rr) {
-      if (rr < nr) {
-        // row i = i0 + rr: new row i + 3 (index rr + 6), old row i - 4 (rr - 1)
-        const double tn = qterm<double>(q, tx[rr + 6], ty[rr + 6]);
-        const double to = qterm<double>(q, tx[rr - 1], ty[rr - 1]);
-        s = s + (tn - to);
-        L.ring[q][rr][slot] = div7(s);
       }
     }
   }
