@@ -284,6 +284,7 @@ constexpr int ES_DENSE = 32;  // zigzag positions coded by the unrolled walk; th
 // ms per 64 x 1080p (LDS -> 5 workgroups per CU)
 constexpr int ES_SW = 8;
 constexpr int ES_HI = 64 - ES_DENSE;     // positions of the nonzero loop
+static_assert(ES_HI <= 32, "es_hi_stash's nonzero mask is one 32-bit word (ES_DENSE = 24 dropped positions 56-63)");
 constexpr int ES_MAXW = 53;              // words per block at most (1660 bits + the partial word): the spill area
 constexpr int ES_WAVES = 4;
 
