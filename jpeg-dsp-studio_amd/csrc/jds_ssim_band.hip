@@ -74,6 +74,11 @@ static_assert(sb_ring<true>() >= 2 * SB_CW + 7 && (5 * SB_CW) % sb_ring<true>() 
 constexpr int SB_SP = SB_CW + 1; // chain output tile pitch
 constexpr int SB_THREADS = 256;
 constexpr int SB_MAX_ITEMS = 4096;  // image pairs per launch (scratch bounds it first)
+#ifdef JDS_SSIM_NO_LF  // tools: A/B builds only -- big luma launches store the map (k_ss_chunks sums it)
+constexpr bool SB_LEAF_FOLD = false;
+#else
+constexpr bool SB_LEAF_FOLD = true;  // big luma launches fold the map into leaf sums in k_ss_band
+#endif
 
 struct SsimPair {
   const uint8_t* a;
@@ -112,6 +117,13 @@ struct SsimBatch {
   int out_stride;
   unsigned long long* sse;  // [item]: sum of (a - b)^2 over the H*W*3 bytes (zeroed by the caller)
   PwTree tree_s, tree_y;    // the partial buffers of the map stream and of the luma MSE stream
+  // leaf-folded luma map (k_ss_band<.., LF>, big launches without the R, G, B
+  // bands): per item at lf + item * lf_pitch, the sums of the leaves inside one
+  // map row [nfull * 64], the row-crossing leaves' elements at lf_raws (128 per
+  // slot) and the partial buffer's at lf_rawp (k_ss_rows' layout; k_ss_rgbsum
+  // finishes them)
+  double* lf;
+  long long lf_pitch, lf_raws, lf_rawp, efull;
 };
 
 // x / 7 correctly rounded: q0 = RN(x * RN(1/7)) is within an ulp of x/7, the
@@ -714,10 +726,18 @@ __device__ __forceinline__ void chain_chunk(const double* __restrict__ R, double
 // ring, 46 KB for luma): shorter per-chunk latency, for small launches whose
 // few workgroups are latency-bound; big launches keep the serial one (36 KB,
 // four workgroups per CU).
-template <int BH, bool LU, bool YP = false, bool OV = false>
+// LF (luma, serial schedule): the map is not stored; it goes into an LDS tile,
+// and in the next chain phase wave 1 (idle there) folds it into NumPy's leaf
+// sums, one lane per (row, accumulator) -- k_ss_rows' scheme: whole leaves
+// inside a map row summed here, the elements of row-crossing leaves and of the
+// partial buffer written raw for k_ss_rgbsum.
+template <int BH, bool LU, bool YP = false, bool OV = false, bool LF = false>
 __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu(LU && !OV ? 4 : (LU ? 3 : 5)))) k_ss_band(SsimBatch B) {
+  static_assert(!LF || (LU && !YP && !OV && BH * 8 == 64), "leaf folding: the serial luma band, one wave of (row, accumulator) lanes");
   constexpr int RING = sb_ring<OV>();
   __shared__ BandLds<BH, LU, OV> L;
+  __shared__ double MT[LF ? BH : 1][LF ? SB_CW : 1];  // LF: the chunk's map values
+  __shared__ double FIN[LF ? BH : 1][8];              // LF: each row's leaf accumulators, final
   const int band = blockIdx.x, c = LU ? 3 : blockIdx.y, item = blockIdx.z;
   const int H = B.H, W = B.W;
   const int i0 = 3 + BH * band;
@@ -834,6 +854,54 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
     const int cq = t / BH, crow = t % BH;
     const bool chain_lane = t < 5 * BH && crow < nr;
     double s = 0.0;
+    // LF leaf lanes (wave 1): map row i0 + lrow - 3, accumulator lkq; its
+    // stream elements [rs, rs + cw), whole leaves in [hs, te) (recomputed per
+    // chunk: only the accumulator stays live across the loop)
+    const bool leaf_wave = LF && t >= 64 && t < 128;
+    double acc = 0.0;
+    auto leaf_pass = [&](int k) {
+      // (the lane's constants are re-derived here from an opaque copy of its
+      // index: hoisted out of the chunk loop they held registers all along)
+      int tl = t;
+      asm volatile("" : "+v"(tl));
+      const int lrow = ((tl - 64) >> 3) & 7, lkq = tl & 7;
+      const bool lrowok = lrow < nr;
+      const long long r = i0 + lrow - 3;
+      const long long rs = r * cw;
+      const long long hs = (rs + 127) & ~127LL, te = min((rs + cw) & ~127LL, B.efull);
+      double* const lfb = B.lf + (size_t)item * B.lf_pitch;
+      const int jc = k * SB_CW;
+      const long long eb = rs + (jc - 3);  // element of column jc
+      const int jj0 = (int)((lkq - eb) & 7LL);
+#pragma unroll
+      for (int i = 0; i < SB_CW / 8; ++i) {
+        const int jj = jj0 + 8 * i, j = jc + jj;
+        if (lrowok && j >= 3 && j < jend) {
+          const long long e = eb + jj;
+          const double m = MT[lrow][jj];
+          if (e >= hs && e < te) {  // NumPy's leaf: accumulator e mod 8, in element order
+            const int p = (int)(e & 127LL);
+            acc = p < 8 ? m : acc + m;
+            if (p >= 120) FIN[lrow][lkq] = acc;
+          } else if (e >= B.efull) {
+            lfb[B.lf_rawp + (e - B.efull)] = m;
+          } else {  // a row-crossing leaf (slot: the row it ends in; narrow maps a slot per leaf)
+            const long long slot = cw >= 128 ? (e < hs ? r : r + 1) : (e >> 7);
+            lfb[B.lf_raws + slot * 128 + (e & 127LL)] = m;
+          }
+        }
+      }
+      // a leaf of this row ends in this chunk: its eight accumulators summed in
+      // NumPy's order, ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+      const long long elo = eb + max(0, 3 - jc), ehi = eb + min(SB_CW, jend - jc);
+      const long long e127 = elo | 127LL;
+      const bool done = lrowok && e127 < ehi && e127 >= hs && e127 < te;
+      double x = FIN[lrow][lkq];
+      x = x + __shfl_xor(x, 1, 64);
+      x = x + __shfl_xor(x, 2, 64);
+      x = x + __shfl_xor(x, 4, 64);
+      if (done && lkq == 0) lfb[e127 >> 7] = x;
+    };
     // one chunk: cur holds chunk k + 1's loaded inputs (committed beside the
     // chain), then receives chunk k + 3's
     auto step = [&](int k, StageRegs<BH, LU, YP>& cur) {
@@ -856,6 +924,8 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
         else
           chain_chunk<0, false, RING>(Rg, o, s, nj);
       }
+      if constexpr (LF)
+        if (leaf_wave && k > 0) leaf_pass(k - 1);  // chunk k - 1's map (the tile is rewritten after the barrier)
       stage_commit<BH, LU, YP>(c, k + 1, nchunks, P, cur, L);  // chunk k's fill has read the buffer
       __syncthreads();
       // chunk k + 1's fill, chunk k's map, chunk k + 3's loads
@@ -884,12 +954,10 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
           const double a1 = __builtin_fma(2.0, pxy, B.c1), a2 = __builtin_fma(2.0, vxy, B.c2);  // (map2: exact doubling)
           const double b1 = ux * ux + uy * uy + B.c1, b2 = vx + vy + B.c2;
           const double d = b1 * b2;
-#ifdef JDS_SSIM_PROBE_NOSMAP  // tools: timing probe only (wrong values): the map computed, not stored
-          const double mv = div_map(a1 * a2, d);
-          if (mv == -7.25) smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = mv;
-#else
-          smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
-#endif
+          if constexpr (LF)
+            MT[row][jj] = div_map(a1 * a2, d);
+          else
+            smap[(size_t)(i0 + row - 3) * cw + (j - 3)] = div_map(a1 * a2, d);
         }
       }
       stage_issue<BH, LU, YP>(B, c, pr.a, pr.b, Xp, ck, band, k + 3, nchunks, P, cur);
@@ -899,6 +967,8 @@ __global__ void __launch_bounds__(SB_THREADS) __attribute__((amdgpu_waves_per_eu
       step(k, RB);
       if (k + 1 < nchunks) step(k + 1, RA);
     }
+    if constexpr (LF)
+      if (leaf_wave) leaf_pass(nchunks - 1);
   }
 }
 
@@ -937,13 +1007,14 @@ struct RgbBatch {
   int nfull, mpart;       // full 8192-element buffers of a map stream; elements of the last, partial one
   long long ns, efull;    // ns = (H - 6) * cw; efull = 8192 * nfull
   double c1, c2, cov_norm;
-  double* lsum;           // [item][3][lsum_pitch]: sums of the leaves inside one map row
-  double* raws;           // [item][3][raws_pitch]: elements of row-crossing leaves, 128 per slot
-  double* rawp;           // [item][3][8192]: the partial buffer's elements
-  double* chunks;         // [item][3][nfull + 1]: buffer sums
-  double* out;            // [item][out_stride]: ssim R, G, B
+  double* lsum;           // [item][nchan][lsum_pitch]: sums of the leaves inside one map row
+  double* raws;           // [item][nchan][raws_pitch]: elements of row-crossing leaves, 128 per slot
+  double* rawp;           // [item][nchan][rawp_pitch]: the partial buffer's elements
+  double* chunks;         // [item][nchan][chunks_pitch]: buffer sums
+  double* out;            // [item][out_stride]: ssim R, G, B (nchan 3) or Y (nchan 1, ch_out 3)
   int out_stride;
-  long long lsum_pitch, raws_pitch;
+  long long lsum_pitch, raws_pitch, rawp_pitch, chunks_pitch;
+  int nchan, ch_out;      // maps per item: 3 (k_ss_rows) or 1 (k_ss_band's leaf-folded luma); first out slot
   PwTree tree;            // the partial buffer's pairwise tree
 };
 
@@ -990,7 +1061,7 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
   const size_t ic = (size_t)item * 3 + ch;
   double* lsum = B.lsum + ic * B.lsum_pitch;
   double* raws = B.raws + ic * B.raws_pitch;
-  double* rawp = B.rawp + ic * SB_NP_BUF;
+  double* rawp = B.rawp + ic * B.rawp_pitch;
   const int nchunks = (W + SR_CW - 1) / SR_CW;
 
   // staging item of thread t (t < 2 SR_RG SR_PG): image si, row group sg
@@ -1185,7 +1256,8 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
   }
 }
 
-// The R, G, B maps' buffer sums: grid (nfull + 1, 3, items), 64 lanes.  A full
+// The R, G, B maps' (or the leaf-folded luma map's) buffer sums: grid (nfull +
+// 1, nchan, items), 64 lanes.  A full
 // buffer's 64 leaves: a lane's leaf from lsum, or, if it crosses a row
 // boundary, summed here from its raw elements (NumPy's leaf order); then the
 // perfect binary tree by a shuffle butterfly.  The partial buffer: the host's
@@ -1193,8 +1265,8 @@ __global__ void __launch_bounds__(SR_THREADS) __attribute__((amdgpu_waves_per_eu
 __global__ void __launch_bounds__(64) k_ss_rgbsum(RgbBatch B) {
   __shared__ double lsh[2 * PW_MAXN];
   const int b = blockIdx.x, ch = blockIdx.y, item = blockIdx.z, t = threadIdx.x;
-  const size_t ic = (size_t)item * 3 + ch;
-  double* out = B.chunks + ic * (B.nfull + 1) + b;
+  const size_t ic = (size_t)item * B.nchan + ch;
+  double* out = B.chunks + ic * B.chunks_pitch + b;
   auto leaf = [](const double* v, int n) {  // pairwise_sum of n <= 128 elements
     if (n < 8) {
       double a = 0.0;
@@ -1222,7 +1294,7 @@ __global__ void __launch_bounds__(64) k_ss_rgbsum(RgbBatch B) {
     if (t == 0) *out = p;
   } else if (B.mpart > 0) {
     const PwTree& T = B.tree;
-    const double* v = B.rawp + ic * SB_NP_BUF;
+    const double* v = B.rawp + ic * B.rawp_pitch;
     for (int l = t; l < T.nl; l += 64) lsh[l] = leaf(v + T.off[l], T.n[l]);
     __syncthreads();
     for (int h = 0; h < T.nh; ++h) {
@@ -1233,15 +1305,15 @@ __global__ void __launch_bounds__(64) k_ss_rgbsum(RgbBatch B) {
   }
 }
 
-// buffer sums left to right from 0.0, / ns: grid (3, items)
+// buffer sums left to right from 0.0, / ns: grid (nchan, items)
 __global__ void __launch_bounds__(64) k_ss_rgbfinal(RgbBatch B) {
   const int ch = blockIdx.x, item = blockIdx.y;
   if (threadIdx.x != 0) return;
   const int nb = B.nfull + (B.mpart > 0 ? 1 : 0);
-  const double* cs = B.chunks + ((size_t)item * 3 + ch) * (B.nfull + 1);
+  const double* cs = B.chunks + ((size_t)item * B.nchan + ch) * B.chunks_pitch;
   double acc = 0.0;
   for (int k = 0; k < nb; ++k) acc = acc + cs[k];
-  B.out[(size_t)item * B.out_stride + ch] = acc / (double)B.ns;
+  B.out[(size_t)item * B.out_stride + B.ch_out + ch] = acc / (double)B.ns;
 }
 
 // ---------------------------------------------------------- NumPy means --
@@ -1468,6 +1540,28 @@ static long long ck_pitch_of(int H, int W) { return (5LL * ssim_bands(H) * W + 6
 
 int ssim_batch_max_items() { return SB_MAX_ITEMS; }
 
+// k_ss_rows' raw slots per (item, channel), 128 doubles each
+static long long rgb_raws_pitch(int H, int W) {
+  const int cw = W - 6;
+  const long long ns = (long long)(H - 6) * cw;
+  return (cw >= 128 ? (long long)(H - 5) : (ns + 127) / 128 + 1) * 128;
+}
+
+// the leaf-folded luma map's doubles per item (k_ss_band<.., LF>): leaf sums
+// [nfull * 64], row-crossing leaves (raw slots), the partial buffer [8192];
+// offsets of the last two
+struct LfLayout {
+  long long raws, rawp, pitch;
+};
+static LfLayout lf_layout(int H, int W) {
+  const long long nfull = (long long)(H - 6) * (W - 6) / SB_NP_BUF;
+  LfLayout l;
+  l.raws = nfull * 64;
+  l.rawp = l.raws + rgb_raws_pitch(H, W);
+  l.pitch = (l.rawp + SB_NP_BUF + 63) & ~63LL;
+  return l;
+}
+
 // whether a launch of `items` pairs keeps fp64 luma planes (small launches:
 // k_ss_yplanes for the per-quantity chains; larger ones form the luma from
 // the bytes wherever they need it)
@@ -1478,16 +1572,13 @@ bool ssim_batch_planes(int items) { return items < SB_YCHK_COL_ITEMS; }
 size_t ssim_batch_scratch_doubles(int H, int W, bool rgb, bool planes) {
   const size_t n = (size_t)H * W;
   const size_t nch = (n + SB_NP_BUF - 1) / SB_NP_BUF;  // n > ns
-  return (planes ? 2 * (size_t)n_pitch_of(H, W) : 0) + (size_t)ck_pitch_of(H, W) +
-         (rgb ? 4 : 1) * (size_t)ns_pitch_of(H, W) + 5 * nch;
+  // (launches without the R, G, B bands and without planes fold the luma map
+  // into leaf sums instead of storing it)
+  const size_t maps = rgb ? 4 * (size_t)ns_pitch_of(H, W)
+                          : (planes || !SB_LEAF_FOLD ? (size_t)ns_pitch_of(H, W) : (size_t)lf_layout(H, W).pitch);
+  return (planes ? 2 * (size_t)n_pitch_of(H, W) : 0) + (size_t)ck_pitch_of(H, W) + maps + 5 * nch;
 }
 
-// k_ss_rows' raw slots per (item, channel), 128 doubles each
-static long long rgb_raws_pitch(int H, int W) {
-  const int cw = W - 6;
-  const long long ns = (long long)(H - 6) * cw;
-  return (cw >= 128 ? (long long)(H - 5) : (ns + 127) / 128 + 1) * 128;
-}
 
 // scratch doubles per item of the R, G, B path (k_ss_rows, k_ss_rgbsum)
 size_t ssim_rgb_scratch_doubles(int H, int W) {
@@ -1518,6 +1609,10 @@ hipError_t launch_ssim_rgb(const void* pairs_dev, int items, int H, int W, doubl
   R.cov_norm = 49.0 / 48.0;
   R.lsum_pitch = (long long)R.nfull * 64;
   R.raws_pitch = rgb_raws_pitch(H, W);
+  R.rawp_pitch = SB_NP_BUF;
+  R.chunks_pitch = R.nfull + 1;
+  R.nchan = 3;
+  R.ch_out = 0;
   R.lsum = scratch;
   R.raws = R.lsum + (size_t)items * 3 * R.lsum_pitch;
   R.rawp = R.raws + (size_t)items * 3 * R.raws_pitch;
@@ -1565,8 +1660,15 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
   B.yplanes = planes ? scratch : nullptr;
   B.ck = scratch + (planes ? (size_t)items * 2 * B.n_pitch : 0);
   B.ck_pitch = ck_pitch_of(H, W);
-  B.smap = B.ck + (size_t)items * B.ck_pitch;
-  B.chunks = B.smap + (size_t)items * B.smap_ch * B.ns_pitch;
+  const bool lf = SB_LEAF_FOLD && !planes && !rgb;  // the luma map folded into leaf sums (k_ss_band<.., LF>)
+  const LfLayout lo = lf_layout(H, W);
+  B.smap = lf ? nullptr : B.ck + (size_t)items * B.ck_pitch;
+  B.lf = lf ? B.ck + (size_t)items * B.ck_pitch : nullptr;
+  B.lf_pitch = lo.pitch;
+  B.lf_raws = lo.raws;
+  B.lf_rawp = lo.rawp;
+  B.efull = (B.ns / SB_NP_BUF) * SB_NP_BUF;
+  B.chunks = lf ? B.lf + (size_t)items * lo.pitch : B.smap + (size_t)items * B.smap_ch * B.ns_pitch;
   B.out = out;
   B.out_stride = out_stride;
   B.sse = sse;
@@ -1588,17 +1690,43 @@ hipError_t launch_psnr_ssim_batch(const void* pairs_dev, int items, int H, int W
                        dim3(256), 0, s, B);
     hipLaunchKernelGGL(k_ss_ychkq<SB_BH>, dim3((W + 63) / 64, 5, items), dim3(64), 0, s, B);
   }
+  if (lf) {
+    hipLaunchKernelGGL((k_ss_band<SB_BH, true, false, false, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
+    hipLaunchKernelGGL(k_ss_chunks, dim3(B.nch_y, 1, items), dim3(SB_THREADS), 0, s, B, 4);  // luma MSE
+    // the luma map's buffer sums from its leaf sums and raw elements
+    RgbBatch R{};
+    R.pairs = B.pairs;
+    R.H = H;
+    R.W = W;
+    R.cw = W - 6;
+    R.ns = B.ns;
+    R.nfull = (int)(B.ns / SB_NP_BUF);
+    R.efull = B.efull;
+    R.mpart = (int)(B.ns - B.efull);
+    R.lsum = B.lf;
+    R.raws = B.lf + lo.raws;
+    R.rawp = B.lf + lo.rawp;
+    R.chunks = B.chunks;  // (the luma map's slots, [item][5][nch] at channel 3)
+    R.lsum_pitch = R.raws_pitch = R.rawp_pitch = lo.pitch;
+    R.chunks_pitch = 5LL * nch;
+    R.nchan = 1;
+    R.ch_out = 3;
+    R.out = out;
+    R.out_stride = out_stride;
+    pw_tree(R.mpart, &R.tree);
+    R.chunks += 3 * nch;  // channel 3's row of the item's [5][nch] block
+    hipLaunchKernelGGL(k_ss_rgbsum, dim3(R.nfull + 1, 1, items), dim3(64), 0, s, R);
+    hipLaunchKernelGGL(k_ss_rgbfinal, dim3(1, items), dim3(64), 0, s, R);
+    hipLaunchKernelGGL(k_ss_final, dim3(1, items), dim3(256), 0, s, B, 4);  // the luma MSE
+    return hipGetLastError();
+  }
   if (!planes && !rgb)
     hipLaunchKernelGGL((k_ss_band<SB_BH, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   else if (!planes)
     hipLaunchKernelGGL((k_ss_band<SB_BH, true, false, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
   else
     hipLaunchKernelGGL((k_ss_band<SB_BH, true, true, true>), dim3(B.NB, 1, items), dim3(SB_THREADS), 0, s, B);
-#ifdef JDS_SSIM_PROBE_NOSMAP
-  hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 1, items), dim3(SB_THREADS), 0, s, B, 4);
-#else
   hipLaunchKernelGGL(k_ss_chunks, dim3(nch, 2, items), dim3(SB_THREADS), 0, s, B, 3);  // luma map, luma MSE
-#endif
   if (rgb && (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_ss_final, dim3(rgb ? 5 : 2, items), dim3(256), 0, s, B, rgb ? 0 : 3);
   return hipGetLastError();
