@@ -510,6 +510,21 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
       const int nx = g.W - x0 < 8 ? g.W - x0 : 8;
       uint8_t* o = out_f + ((size_t)y * g.W + x0) * 3;
       const bool wide = nx == 8 && ((((uintptr_t)o) & 7u) == 0);
+      // SSE runs: the input row requested before the colour work, so its latency
+      // hides under it (sweep step 3.758 -> 3.731 ms, tools/r6_ww.sh)
+      uint32_t in[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+      if constexpr (XTRA > 0) {
+        const uint8_t* src = in_f + ((size_t)y * g.W + x0) * 3;
+        if (wide) {
+          const uint2* s2 = reinterpret_cast<const uint2*>(src);
+          const uint2 a = s2[0], b2 = s2[1], c = s2[2];
+          in[0] = a.x; in[1] = a.y; in[2] = b2.x; in[3] = b2.y; in[4] = c.x; in[5] = c.y;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 24; ++k)
+            if (k < 3 * nx) in[k >> 2] |= (uint32_t)src[k] << (8 * (k & 3));
+        }
+      }
       uint32_t pk[6];
       // the row's smallest / largest fraction word
       uint32_t r_min = 0xffffffffu, r_max = 0u;
@@ -549,19 +564,8 @@ __device__ __forceinline__ bool inv_fast_tile(InvShared<MODE, XTRA>& sh, const G
           if (b < 3 * nx) o[b] = (uint8_t)(pk[b >> 2] >> (8 * (b & 3)));
       }
       if constexpr (XTRA > 0) {
-        // reference PSNR inputs (utils/metrics.py:11-20): exact integer SSE,
-        // fp64 luma of both uint8 images (jds_inv.hip k_inv2's XTRA = 1 terms)
-        uint32_t in[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-        const uint8_t* src = in_f + ((size_t)y * g.W + x0) * 3;
-        if (wide) {
-          const uint2* s2 = reinterpret_cast<const uint2*>(src);
-          const uint2 a = s2[0], b2 = s2[1], c = s2[2];
-          in[0] = a.x; in[1] = a.y; in[2] = b2.x; in[3] = b2.y; in[4] = c.x; in[5] = c.y;
-        } else {
-#pragma unroll
-          for (int k = 0; k < 24; ++k)
-            if (k < 3 * nx) in[k >> 2] |= (uint32_t)src[k] << (8 * (k & 3));
-        }
+        // reference PSNR inputs (utils/metrics.py:11-20): exact integer SSE and
+        // the luma SSE as one exact integer per pixel (luma_sse_e6)
         auto byte_of = [](const uint32_t (&w)[6], int b) { return (int)((w[b >> 2] >> (8 * (b & 3))) & 255u); };
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
