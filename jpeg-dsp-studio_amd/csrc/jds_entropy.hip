@@ -286,7 +286,10 @@ constexpr int ES_SW = 8;
 constexpr int ES_HI = 64 - ES_DENSE;     // positions of the nonzero loop
 static_assert(ES_HI <= 32, "es_hi_stash's nonzero mask is one 32-bit word (ES_DENSE = 24 dropped positions 56-63)");
 constexpr int ES_MAXW = 53;              // words per block at most (1660 bits + the partial word): the spill area
-constexpr int ES_WAVES = 4;
+#ifndef JDS_ES_WAVES  // tools: A/B builds of the walk's waves per workgroup
+#define JDS_ES_WAVES 4
+#endif
+constexpr int ES_WAVES = JDS_ES_WAVES;
 
 // Append the L (< 32) bits of symL (left-aligned, zero below) to the pending
 // word acc (n bits, left-aligned with zeros below: an append is one shift and
@@ -909,6 +912,7 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
   auto* ffs = (unsigned long long*)buf[4];
   auto* ffx = (unsigned long long*)buf[5];
   const unsigned wg = (unsigned)((nseg + ES_WAVES - 1) / ES_WAVES);
+  const unsigned wg4 = (unsigned)((nseg + 3) / 4);  // k_ent_place / k_ent_emit3: four segment waves per workgroup
   const EsTab* est = reinterpret_cast<const EsTab*>((const char*)tab_dev + sizeof(EntTab));
   hipLaunchKernelGGL(k_ent_walk, dim3(wg), dim3(64 * ES_WAVES), 0, s, e, nseg, coeffs, est, ovf, nbits, agg, badseg,
                      ffs);
@@ -922,7 +926,7 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
                        nullptr, nullptr, 0ll, nullptr, nullptr);
     kmark(s, "k_ent_fscan<0>");
   }
-  hipLaunchKernelGGL(k_ent_place, dim3(wg), dim3(256), 0, s, e, nseg, ovf, nbits, agg, segoff, desc, raw, ffs, info,
+  hipLaunchKernelGGL(k_ent_place, dim3(wg4), dim3(256), 0, s, e, nseg, ovf, nbits, agg, segoff, desc, raw, ffs, info,
                      scan_bits);
   kmark(s, "k_ent_place");
   if ((err = hipGetLastError()) != hipSuccess) return err;
@@ -932,7 +936,7 @@ static hipError_t launch_entropy_fused(const Geo& g, int n, const int16_t* coeff
   hipLaunchKernelGGL(k_ent_fscan<true>, dim3(n), dim3(1024), 0, s, e, ffs, ffx, fftot, desc, info, outoff, hdr_dev,
                      out, stride, lengths, badseg);
   kmark(s, "k_ent_fscan<1>");
-  hipLaunchKernelGGL(k_ent_emit3, dim3(wg), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
+  hipLaunchKernelGGL(k_ent_emit3, dim3(wg4), dim3(256), 0, s, e, nseg, desc, info, raw, outoff, out, stride);
   kmark(s, "k_ent_emit3");
   return hipGetLastError();
 }
